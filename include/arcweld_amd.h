@@ -1,0 +1,188 @@
+/* arcweld_amd.h -- C ABI of the MI355X (gfx950) HIP kernels behind the VQ-VAE + Transformer training path.
+ *
+ * The reference (tmdt-buw/VQ-VAE-Transformer-Arc-Welding) is pure Python on stock PyTorch ops; it has no FFI.
+ * Its drop-in boundary is the nn.Module surface.  This library sits BELOW that
+ * surface: each entry point replaces the ATen work of one reference call site, cited per function.
+ *
+ * Conventions (all entry points):
+ *   - plain device pointers + sizes/leading dimensions (in elements); caller owns every buffer;
+ *   - `stream` is a hipStream_t passed as void*; nothing synchronises the host;
+ *   - return 0 (AW_OK) or a negative status; aw_last_error() returns a thread-local message;
+ *   - no allocation inside (graph-capture safe); accumulators that must start at zero are documented.
+ */
+#ifndef ARCWELD_AMD_H
+#define ARCWELD_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum { AW_OK = 0, AW_ERR_ARG = -1, AW_ERR_LAUNCH = -2 };
+enum { AW_F32 = 0, AW_BF16 = 1 };
+enum { AW_ACT_GELU_ERF = 0, AW_ACT_GELU_TANH = 1 };
+
+const char* aw_last_error(void);
+int aw_version(void);
+
+/* ------------------------------------------------------------------------------------------------ GEMM
+ * C[M,N] = epilogue( alpha * op(A)[M,K] . op(B)[K,N] )  on MFMA (bf16 16x16x32 or exact-f32 16x16x4).
+ * Replaces every conv1d / conv_transpose1d / addmm / mm of the hot path (SURVEY.md section 2 ATen table):
+ *   model/vq_vae_patch_embedd.py:11,27,30,65,68,81,87,143 and model/transformer_block.py:30,32,78-79,
+ *   model/transformer_decoder.py:29 -- forward, input-gradient and weight-gradient forms.
+ * Operand storage (dtype = a_dtype for A and B; AW_F32 or AW_BF16):
+ *   a_trans = 0: A[m*lda + k]        a_trans = 1: A[k*lda + m]
+ *   b_trans = 0: B[n*ldb + k]        b_trans = 1: B[k*ldb + n]      (weights [out][in] are b_trans = 0)
+ * Implicit k=3/pad=1 convolution along windows of `conv_seg` rows (conv_cin > 0):
+ *   conv_operand = 0 (A, a_trans = 0): K = 3*conv_cin, A[m][j*cin+i] = src[(m + conv_dir*(j-1))*lda + i],
+ *                  zero where the shifted row leaves its window;
+ *   conv_operand = 1 (B, b_trans = 1): N = 3*conv_cin, B[k][j*cin+i] = src[(k + (j-1))*ldb + i], same mask.
+ * Epilogue, per element (row r, col c), in this order:
+ *   v = alpha*acc;  v += bias[c];  v *= act'(pre[r*ld_pre + c]);  v *= dropout(drop_seed, r*N+c, drop_p);
+ *   v += resid[r*ld_resid + c];  v += beta * C_old (C must be f32 when beta != 0);  C[r*ldc + c] = v (c_dtype)
+ *   C2 (c2_mode): 1 = act(v), 2 = v, 3 = v * dropout(drop2_seed, r*N+c, drop2_p); stored as c2_dtype
+ *   colstats (f64, 2*stats_mod): += v and v*v into slot (c % stats_mod)      (BatchNorm batch statistics)
+ *   a_rowsum (f32, M): += sum_k A[m][k]                                      (bias gradients, fused)
+ */
+typedef struct {
+  int M, N, K;
+  int a_dtype;
+  const void* A; int64_t lda; int a_trans;
+  const void* B; int64_t ldb; int b_trans;
+  int conv_cin, conv_seg, conv_dir, conv_operand;
+  float alpha, beta;
+  const float* bias;
+  int act;                       /* AW_ACT_GELU_ERF or AW_ACT_GELU_TANH, for act' and C2 mode 1 */
+  const float* pre; int64_t ld_pre;
+  const float* resid; int64_t ld_resid;
+  float drop_p; uint64_t drop_seed;
+  void* C; int64_t ldc; int c_dtype;
+  void* C2; int64_t ldc2; int c2_mode; int c2_dtype;
+  float drop2_p; uint64_t drop2_seed;
+  double* colstats; int stats_mod;
+  float* a_rowsum;
+} aw_gemm_args;
+
+int aw_gemm(const aw_gemm_args* args, void* stream);
+
+/* -------------------------------------------------------------------------------- vector quantizer
+ * VectorQuantizer.forward (model/vector_quantizer.py:76-119), fp32, codebook staged in LDS, no MFMA:
+ *   dist = fl(fl(|z|^2 + |e_k|^2) - 2 * (k-ordered fmaf chain z.e_k)), argmin with first-index ties,
+ *   z_q_ste = z + (e_idx - z), idx (int64), counts[k] += 1, sqerr[0] += sum (e_idx - z)^2 (f64).
+ * counts (K floats) and sqerr (1 double) must be zero on entry.  D in {16,32,64,128,256}.
+ */
+int aw_vq_forward(const float* z, const float* E, int64_t N, int K, int D,
+                  float* zq, int64_t* idx, float* counts, double* sqerr, void* stream);
+/* loss = m + beta*m with m = sqerr/(N*D) (vector_quantizer.py:107-108); perplexity = exp(-sum p log(p+1e-10)),
+ * p = counts/N (:114-115).  out2 = {loss, perplexity}. */
+int aw_vq_finalize(const float* counts, const double* sqerr, int64_t N, int K, int D, float beta,
+                   float* out2, void* stream);
+/* Backward of the STE + loss: dz = g_zq + g_loss*2(z - z_q)/(N*D);  dE[idx] += g_loss*2*beta*(z_q - z)/(N*D).
+ * g_zq may be NULL (treated as 0); g_loss is a device scalar.  dE is accumulated (not overwritten). */
+int aw_vq_backward(const float* z, const float* E, const int64_t* idx, const float* g_zq, const float* g_loss,
+                   int64_t N, int K, int D, float beta, float* dz, float* dE, void* stream);
+/* min_encodings one-hot (N,K) f32 (vector_quantizer.py:98-100). */
+int aw_vq_onehot(const int64_t* idx, int64_t N, int K, float* onehot, void* stream);
+/* Gather E[idx] -> out (N, D) (get_embedding_from_one_hot, vector_quantizer.py:121-131). */
+int aw_vq_gather(const float* E, const int64_t* idx, int64_t N, int D, float* out, void* stream);
+
+/* --------------------------------------------------------------------------- VQ-VAE layout kernels
+ * Patchify (model/vq_vae_patch_embedd.py:13-17): x (B, L, C) -> patches (B*S, ldp) with token t covering the
+ * channel-major flat window [t*P, (t+1)*P); columns P..ldp-1 are zero.  S = L*C/P. */
+int aw_patchify(const float* x, int64_t B, int L, int C, int P, void* patches, int64_t ldp, int dtype,
+                void* stream);
+/* Weight relayouts (+cast) for the GEMM operand forms; out dtype = `dtype`.
+ * mode 0: conv (O,I,k) tap t -> [O][I]                        (centre tap of the per-token encoder convs)
+ * mode 1: conv (O,I,3)     -> [O][3*I], col j*I+i              (decoder conv forward, b_trans=0)
+ * mode 2: conv (O,I,3)     -> [3*O][I], row j*O+o = W[o][:,j]  (decoder conv input-gradient, b_trans=1)
+ * mode 3: convT (I,O,k)    -> [k*O][I], row j*O+o              (un-patch ConvT forward b_trans=0 / dgrad b_trans=1)
+ * mode 4: conv (O,I,k)     -> [O][ldo] zero padded, col i*k+j  (patch embed, 1 input channel)
+ * `ldo` is the output row length (ignored except for mode 4). */
+int aw_weight_relayout(const float* W, int O, int I, int k, int tap, int mode, void* out, int64_t ldo,
+                       int dtype, void* stream);
+/* Inverse relayout of weight GRADIENTS, accumulated (+=) into the reference-layout gradient:
+ * mode 0: g[O][I] -> G[o][i][tap];  mode 1: g[O][3I] -> G[o][i][j];  mode 3: g[kO][I] -> G[i][o][j];
+ * mode 4: g[O][ldo] -> G[o][0][j]. */
+int aw_weight_grad_scatter(const float* g, int O, int I, int k, int tap, int mode, int64_t ldg, float* G,
+                           void* stream);
+/* Elementwise cast/copy: out[i] = in[i] (f32 -> dtype). */
+int aw_cast(const float* in, int64_t n, void* out, int dtype, void* stream);
+
+/* Un-patch head forward (vq_vae_patch_embedd.py:27-30,52-57 + autencoder_lightning_base.py:82):
+ * y (R = B*Q rows of H, f32, BN input) -> BN(train stats from colstats or eval running stats) -> GELU(erf)
+ * -> ConvT(H->1, k5, s5) -> x_hat (B, 200, 2) interleaved; sqerr[0] += sum (x_hat - x)^2 (f64, zero on entry).
+ * stats (f32 4*H): mean, invstd, gamma, beta as produced by aw_bn_finalize. */
+int aw_unpatch_head_fwd(const float* y, int64_t R, int H, int Q, const float* stats, const float* w2,
+                        const float* b2, const float* x, float* x_hat, double* sqerr, void* stream);
+/* BatchNorm finalize: colstats (f64 sum, sumsq over n rows) -> stats {mean, invstd, gamma, beta};
+ * training: running_mean/var momentum update (unbiased var), *nbt += 1.  eval (training == 0): uses running. */
+int aw_bn_finalize(const double* colstats, int64_t n, int H, const float* gamma, const float* beta,
+                   float* running_mean, float* running_var, int64_t* nbt, float eps, float momentum,
+                   int training, float* stats, void* stream);
+/* Un-patch head backward.  g_xhat = 2(x_hat - x)/numel * g_recon (device scalar).
+ * pass 1: per-channel sums sum_g, sum_gxhat (f64 2H, zero on entry), grads of w2 (H*5) and b2 (1) accumulated;
+ * pass 2: g_y (R x H, gy_dtype) = BN backward (batch stats) of g * act'(.), and db_y (bias-of-y gradient,
+ *         H f32, accumulated, channel sums of g_y). */
+int aw_unpatch_head_bwd1(const float* y, int64_t R, int H, int Q, const float* stats, const float* w2,
+                         const float* x_hat, const float* x, const float* g_recon, double* gsums, float* gw2,
+                         float* gb2, float* ggamma, float* gbeta, int training, void* stream);
+int aw_unpatch_head_bwd2(const float* y, int64_t R, int H, int Q, const float* stats, const float* w2,
+                         const float* x_hat, const float* x, const float* g_recon, const double* gsums,
+                         int training, void* g_y, int gy_dtype, float* db_y, int k1, void* stream);
+
+/* loss = a[0] + b[0] (both device scalars) -> out[0]; also used for the autograd scalar plumbing. */
+int aw_scalar_add(const float* a, const float* b, float* out, void* stream);
+/* recon = sqerr/numel as f32 -> out */
+int aw_mse_finalize(const double* sqerr, int64_t numel, float* out, void* stream);
+
+/* ------------------------------------------------------------------------------------- optimizer
+ * Multi-tensor RAdam over one flat parameter buffer (torch.optim.RAdam semantics, L2 weight decay):
+ * segments [seg_off[s], seg_off[s]+seg_len[s]) (sorted, within [0,total)) with weight decay seg_wd[s]; seg_active[s]==0
+ * are skipped (grad None: model/transformer_decoder.py heads under find_unused_parameters).
+ * scalars come from host (step count, lr, betas, eps); `gscale` is a device scalar multiplying the gradient
+ * first (clip coefficient; NULL = 1). */
+int aw_radam_step(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, const int64_t* seg_off,
+                  const int64_t* seg_len, const float* seg_wd, const int* seg_active, int nseg, int64_t total, int64_t step,
+                  float lr, float beta1, float beta2, float eps, const float* gscale, void* stream);
+/* Global L2 norm of the active segments of `grad` -> out_norm (f32 device scalar) and the clip coefficient
+ * min(max_norm/(norm+1e-6), 1) -> out_coef (Lightning gradient_clip_val -> clip_grad_norm_).  ws: f64[1]. */
+int aw_grad_norm_clip(const float* grad, const int64_t* seg_off, const int64_t* seg_len, const int* seg_active,
+                      int nseg, float max_norm, double* ws, float* out_norm, float* out_coef, void* stream);
+/* x[i] *= s (device scalar), over n elements. */
+int aw_scale(float* x, int64_t n, const float* s, void* stream);
+
+/* ------------------------------------------------------------------------------------ transformer
+ * LayerNorm (model/transformer_block.py:71,73; transformer_decoder.py:28), eps, over the last dim D.
+ * y = (x-mean)*rstd*w + b (y_dtype); mean/rstd saved (f32, R each). */
+int aw_layernorm_fwd(const float* x, int64_t R, int D, const float* w, const float* b, float eps, void* y,
+                     int y_dtype, float* mean, float* rstd, void* stream);
+/* dx (+= if accumulate) and dw/db (accumulated, f32) */
+int aw_layernorm_bwd(const float* x, const float* dy, int64_t R, int D, const float* w, const float* mean,
+                     const float* rstd, float* dx, int accumulate, float* dw, float* db, void* stream);
+/* Token embedding + sinusoidal PE (model/embedding.py:57-59): x[b,t,:] = Wtok[ids[b,t]] + pe[t] */
+int aw_embed_fwd(const int64_t* ids, int64_t B, int T, int D, const float* wtok, const float* pe, float* x,
+                 void* stream);
+int aw_embed_bwd(const int64_t* ids, int64_t B, int T, int D, const float* dx, float* dwtok, void* stream);
+/* Causal self-attention core (model/transformer_block.py:44-60) on the packed qkv projection
+ * (B*T, 3*d, dtype), heads of hs = d/n_head: y (B*T, d, dtype) = softmax(q k^T / sqrt(hs), causal) v;
+ * lse (B*n_head*T f32) saved for the backward (flash-style, T x T never materialised). */
+int aw_attn_fwd(const void* qkv, int64_t B, int T, int n_head, int d, int dtype, void* y, float* lse,
+                void* stream);
+/* dqkv (B*T, 3d, dtype) from dy (B*T, d, dtype), recomputing P from lse; ws: f32 B*n_head*T (delta). */
+int aw_attn_bwd(const void* qkv, const void* y, const void* dy, const float* lse, int64_t B, int T, int n_head,
+                int d, int dtype, void* dqkv, float* ws, void* stream);
+/* Cross entropy with ignore_index (transformer_decoder.py:226-230): logits (R, V) f32 with row stride ldl;
+ * loss_sum (f64, zero on entry) += sum over kept rows of (lse - logit[y]); count (f64) += kept rows.
+ * The backward writes dlogits = (softmax - onehot) * g / count (g device scalar) into dlogits (dtype). */
+int aw_ce_fwd(const float* logits, int64_t R, int V, int64_t ldl, const int64_t* y, int ignore_index,
+              double* loss_sum, double* count, float* lse, void* stream);
+int aw_ce_bwd(const float* logits, int64_t R, int V, int64_t ldl, const int64_t* y, int ignore_index,
+              const float* lse, const double* count, const float* g, void* dlogits, int64_t ldd, int dtype,
+              void* stream);
+int aw_ce_finalize(const double* loss_sum, const double* count, float* out, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ARCWELD_AMD_H */

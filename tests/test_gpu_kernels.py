@@ -1,0 +1,193 @@
+"""Kernel-level parity on the MI355X: every GEMM form / epilogue against a plain PyTorch fp32 reference of the
+same op, and the VQ kernel against the reference's own golden indices (bit-exact) and the CPU oracle."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from conftest import golden
+from oracle import gen
+from oracle import vqvae as ov
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+
+
+@pytest.fixture(scope="module")
+def K():
+    from arcweld import kernels
+    return kernels
+
+
+def _rand(shape, seed, dtype=torch.float32, scale=1.0):
+    return torch.tensor(gen.normal(seed, shape, scale)).to(DEV, dtype)
+
+
+def _tol(dtype, K):
+    return (2e-5 * np.sqrt(K / 64), 1e-5) if dtype == torch.float32 else (2e-2, 1e-2)
+
+
+def _padded(rows, cols, seed, dtype):
+    """(rows, cols) view of a (rows, roundup(cols, 8)) buffer: 16-B aligned rows, ragged logical width."""
+    ld = (cols + 7) // 8 * 8
+    return _rand((rows, ld), seed, dtype)[:, :cols]
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("a_trans,b_trans", [(0, 0), (0, 1), (1, 0), (1, 1)])
+@pytest.mark.parametrize("M,N,Kd", [(256, 128, 64), (300, 200, 72), (17, 514, 512), (1000, 64, 48), (64, 96, 514)])
+def test_gemm_layouts(K, dtype, a_trans, b_trans, M, N, Kd):
+    A = _padded(Kd, M, 1, dtype) if a_trans else _padded(M, Kd, 1, dtype)
+    B = _padded(Kd, N, 2, dtype) if b_trans else _padded(N, Kd, 2, dtype)
+    C = torch.empty(M, N, device=DEV)
+    K.gemm(A, B, M, N, Kd, a_trans=a_trans, b_trans=b_trans, C=C)
+    Af = A.float().cpu()
+    Bf = B.float().cpu()
+    ref = (Af.t() if a_trans else Af) @ (Bf if b_trans else Bf.t())
+    rtol, atol = _tol(dtype, Kd)
+    torch.testing.assert_close(C.cpu(), ref, rtol=rtol, atol=atol * np.sqrt(Kd))
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_gemm_epilogue_chain(K, dtype):
+    M, N, Kd = 384, 256, 128
+    A = _rand((M, Kd), 3, dtype)
+    W = _rand((N, Kd), 4, dtype, 0.1)
+    bias = _rand((N,), 5)
+    pre = _rand((M, N), 6)
+    resid = _rand((M, N), 7)
+    C = torch.empty(M, N, device=DEV)
+    C2 = torch.empty(M, N, device=DEV, dtype=dtype)
+    stats = torch.zeros(2 * 64, device=DEV, dtype=torch.float64)
+    rows = torch.zeros(M, device=DEV)
+    K.gemm(A, W, M, N, Kd, C=C, C2=C2, c2_mode=1, bias=bias, pre=pre, resid=resid, colstats=stats, stats_mod=64,
+           a_rowsum=rows)
+    acc = A.float().cpu() @ W.float().cpu().t()
+    pre_c = pre.cpu()
+    gp = 0.5 * (1 + torch.erf(pre_c / np.sqrt(2))) + pre_c * torch.exp(-0.5 * pre_c ** 2) / np.sqrt(2 * np.pi)
+    v = (acc + bias.cpu()) * gp + resid.cpu()
+    rtol, atol = _tol(dtype, Kd)
+    torch.testing.assert_close(C.cpu(), v, rtol=rtol, atol=atol * 10)
+    torch.testing.assert_close(C2.float().cpu(), F.gelu(v), rtol=2e-2 if dtype != torch.float32 else 1e-5,
+                               atol=atol * 10)
+    st = stats.cpu()
+    vv = C.cpu().double()
+    # fp32 per-wave partials, f64 across waves
+    torch.testing.assert_close(st[:64], vv.view(M, N // 64, 64).sum((0, 1)), rtol=2e-5, atol=1e-3)
+    torch.testing.assert_close(st[64:], (vv ** 2).view(M, N // 64, 64).sum((0, 1)), rtol=2e-5, atol=1e-3)
+    torch.testing.assert_close(rows.cpu(), A.float().cpu().sum(1), rtol=1e-5, atol=1e-4)
+
+
+def test_gemm_beta_and_dropout(K):
+    M, N, Kd = 256, 128, 64
+    A = _rand((M, Kd), 8)
+    W = _rand((N, Kd), 9)
+    C = _rand((M, N), 10)
+    C0 = C.cpu().clone()
+    K.gemm(A, W, M, N, Kd, C=C, beta=1.0, alpha=0.5)
+    torch.testing.assert_close(C.cpu(), C0 + 0.5 * (A.cpu() @ W.cpu().t()), rtol=1e-5, atol=1e-4)
+    D = torch.empty(M, N, device=DEV)
+    K.gemm(A, W, M, N, Kd, C=D, drop=(0.25, 1234))
+    ref = A.cpu() @ W.cpu().t()
+    d = D.cpu()
+    zero = d == 0
+    assert 0.2 < zero.float().mean().item() < 0.3
+    torch.testing.assert_close(d[~zero], ref[~zero] / 0.75, rtol=1e-5, atol=1e-4)
+    D2 = torch.empty(M, N, device=DEV)
+    K.gemm(A, W, M, N, Kd, C=D2, drop=(0.25, 1234))
+    assert torch.equal(D.cpu(), D2.cpu())          # counter-based mask: reproducible for the backward
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_gemm_implicit_conv3(K, dtype):
+    """Decoder conv (k=3, pad=1 per window of S tokens): forward, input-gradient and weight-gradient forms."""
+    Bw, S, Cin, Cout = 6, 16, 64, 96
+    M = Bw * S
+    x = _rand((M, Cin), 11, dtype)
+    W = torch.tensor(gen.normal(12, (Cout, Cin, 3), 0.1))
+    dev_dtype = dtype
+    Wk = torch.empty(Cout, 3 * Cin, device=DEV, dtype=dev_dtype)
+    K.weight_relayout(W.to(DEV), Cout, Cin, 3, 0, 1, Wk)
+    y = torch.empty(M, Cout, device=DEV)
+    K.gemm(x, Wk, M, Cout, 3 * Cin, conv=(Cin, S, 1, 0), C=y)
+    xr = x.float().cpu().view(Bw, S, Cin).transpose(1, 2)
+    Wr = W.to(dtype).float()
+    ref = F.conv1d(xr, Wr, padding=1).transpose(1, 2).reshape(M, Cout)
+    rtol, atol = _tol(dtype, 3 * Cin)
+    torch.testing.assert_close(y.cpu(), ref, rtol=rtol, atol=atol * 10)
+    # input gradient: g_in = conv_transpose of g_out
+    g = _rand((M, Cout), 13, dtype)
+    Wd = torch.empty(3 * Cout, Cin, device=DEV, dtype=dev_dtype)
+    K.weight_relayout(W.to(DEV), Cout, Cin, 3, 0, 2, Wd)
+    gin = torch.empty(M, Cin, device=DEV)
+    K.gemm(g, Wd, M, Cin, 3 * Cout, b_trans=True, conv=(Cout, S, -1, 0), C=gin)
+    xr2 = xr.clone().requires_grad_(True)
+    out = F.conv1d(xr2, Wr.clone().requires_grad_(True), padding=1)
+    gr = g.float().cpu().view(Bw, S, Cout).transpose(1, 2)
+    out.backward(gr)
+    torch.testing.assert_close(gin.cpu(), xr2.grad.transpose(1, 2).reshape(M, Cin), rtol=rtol, atol=atol * 10)
+    # weight gradient: dWk[o][(j,i)] = sum_m g[m][o] x[m+j-1][i]
+    dWk = torch.empty(Cout, 3 * Cin, device=DEV)
+    K.gemm(g, x, Cout, 3 * Cin, M, a_trans=True, b_trans=True, conv=(Cin, S, 1, 1), C=dWk)
+    G = torch.zeros(Cout, Cin, 3, device=DEV)
+    K.weight_grad_scatter(dWk, Cout, Cin, 3, 0, 1, G)
+    Wg = Wr.clone().requires_grad_(True)
+    F.conv1d(xr, Wg, padding=1).backward(gr)
+    torch.testing.assert_close(G.cpu(), Wg.grad, rtol=rtol, atol=atol * 30)
+
+
+@pytest.mark.parametrize("tag,Kc,D,N,eseed,estd", [
+    ("K512_D64_init", 512, 64, 16384, 201, None),
+    ("K512_D64_trained", 512, 64, 16384, 202, 0.08),
+    ("K8192_D256_trained", 8192, 256, 4096, 203, 0.05),
+])
+def test_vq_indices_bit_exact_vs_reference(K, tag, Kc, D, N, eseed, estd):
+    g = golden("vq_idx.npz")
+    z = gen.normal(210 + Kc, (N, D), 0.08)
+    E = gen.uniform(eseed, (Kc, D), -1.0 / Kc, 1.0 / Kc) if estd is None else gen.normal(eseed, (Kc, D), estd)
+    zd, Ed = torch.tensor(z, device=DEV), torch.tensor(E, device=DEV)
+    zq = torch.empty_like(zd)
+    idx = torch.empty(N, dtype=torch.int64, device=DEV)
+    counts = torch.zeros(Kc, device=DEV)
+    sq = torch.zeros(1, dtype=torch.float64, device=DEV)
+    K.vq_forward(zd, Ed, zq, idx, counts, sq)
+    ref = g[f"idx_{tag}"].astype(np.int64)
+    got = idx.cpu().numpy()
+    gap = g[f"gap_{tag}"]
+    bad = np.nonzero(got != ref)[0]
+    assert bad.size == 0, f"{bad.size} index mismatches; top-2 gaps there: {gap[bad][:8]}"
+    out2 = torch.empty(2, device=DEV)
+    K.vq_finalize(counts, sq, N, Kc, D, 0.25, out2)
+    np.testing.assert_allclose(out2[0].item(), g[f"loss_{tag}"], rtol=1e-5)
+    np.testing.assert_allclose(out2[1].item(), g[f"perplexity_{tag}"], rtol=1e-5)
+    np.testing.assert_array_equal(counts.cpu().numpy(), np.bincount(ref, minlength=Kc).astype(np.float32))
+
+
+def test_vq_small_forward_backward_vs_reference(K):
+    g = golden("vq_small.npz")
+    E = torch.tensor(gen.uniform(101, (64, 16), -0.5, 0.5), device=DEV)
+    z = torch.tensor(gen.normal(102, (16 * 16, 16), 0.5), device=DEV)
+    g_zq = torch.tensor(gen.normal(103, (16 * 16, 16), 1.0), device=DEV)
+    N = z.shape[0]
+    zq = torch.empty_like(z)
+    idx = torch.empty(N, dtype=torch.int64, device=DEV)
+    counts = torch.zeros(64, device=DEV)
+    sq = torch.zeros(1, dtype=torch.float64, device=DEV)
+    K.vq_forward(z, E, zq, idx, counts, sq)
+    out2 = torch.empty(2, device=DEV)
+    K.vq_finalize(counts, sq, N, 64, 16, 0.25, out2)
+    assert np.array_equal(idx.cpu().numpy(), g["idx"].reshape(-1))
+    np.testing.assert_allclose(zq.cpu().numpy().reshape(g["z_q"].shape), g["z_q"], rtol=0, atol=1e-7)
+    np.testing.assert_allclose(out2[0].item(), g["loss"], rtol=1e-6)
+    np.testing.assert_allclose(out2[1].item(), g["perplexity"], rtol=1e-6)
+    dz = torch.empty_like(z)
+    dE = torch.zeros_like(E)
+    gl = torch.tensor([float(g["g_loss"])], device=DEV)
+    K.vq_backward(z, E, idx, g_zq, gl, 0.25, dz, dE)
+    np.testing.assert_allclose(dz.cpu().numpy().reshape(g["dz"].shape), g["dz"], rtol=1e-5, atol=1e-7)
+    np.testing.assert_allclose(dE.cpu().numpy(), g["dE"], rtol=1e-4, atol=1e-7)
+    oh = torch.empty(N, 64, device=DEV)
+    K.vq_onehot(idx, 64, oh)
+    np.testing.assert_array_equal(oh.cpu().numpy().argmax(1), g["idx"].reshape(-1))
+    assert oh.sum().item() == N

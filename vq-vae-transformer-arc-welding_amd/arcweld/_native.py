@@ -1,0 +1,134 @@
+"""ctypes binding of the HIP C ABI (include/arcweld_amd.h).
+
+The library is loaded AFTER ``import torch`` so that its ``libamdhip64.so.7`` dependency resolves (by SONAME) to
+the HIP runtime torch already loaded: device pointers, streams and the caching allocator are then shared.
+There is no fallback: if the library is missing or a call fails, an exception is raised.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch  # noqa: F401  (must precede the library load, see module docstring)
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG_DIR, "lib", "libarcweld_amd.so")
+HEADER = os.path.join(os.path.dirname(PKG_DIR), "include", "arcweld_amd.h")
+
+AW_F32, AW_BF16 = 0, 1
+AW_ACT_GELU_ERF, AW_ACT_GELU_TANH = 0, 1
+
+c_i64 = ctypes.c_int64
+c_int = ctypes.c_int
+c_f = ctypes.c_float
+c_p = ctypes.c_void_p
+
+
+class GemmArgs(ctypes.Structure):
+    _fields_ = [
+        ("M", c_int), ("N", c_int), ("K", c_int),
+        ("a_dtype", c_int),
+        ("A", c_p), ("lda", c_i64), ("a_trans", c_int),
+        ("B", c_p), ("ldb", c_i64), ("b_trans", c_int),
+        ("conv_cin", c_int), ("conv_seg", c_int), ("conv_dir", c_int), ("conv_operand", c_int),
+        ("alpha", c_f), ("beta", c_f),
+        ("bias", c_p),
+        ("act", c_int),
+        ("pre", c_p), ("ld_pre", c_i64),
+        ("resid", c_p), ("ld_resid", c_i64),
+        ("drop_p", c_f), ("drop_seed", ctypes.c_uint64),
+        ("C", c_p), ("ldc", c_i64), ("c_dtype", c_int),
+        ("C2", c_p), ("ldc2", c_i64), ("c2_mode", c_int), ("c2_dtype", c_int),
+        ("drop2_p", c_f), ("drop2_seed", ctypes.c_uint64),
+        ("colstats", c_p), ("stats_mod", c_int),
+        ("a_rowsum", c_p),
+    ]
+
+
+# name -> argtypes (every entry returns int status except aw_last_error)
+SIGNATURES = {
+    "aw_version": [],
+    "aw_gemm": [ctypes.POINTER(GemmArgs), c_p],
+    "aw_vq_forward": [c_p, c_p, c_i64, c_int, c_int, c_p, c_p, c_p, c_p, c_p],
+    "aw_vq_finalize": [c_p, c_p, c_i64, c_int, c_int, c_f, c_p, c_p],
+    "aw_vq_backward": [c_p, c_p, c_p, c_p, c_p, c_i64, c_int, c_int, c_f, c_p, c_p, c_p],
+    "aw_vq_onehot": [c_p, c_i64, c_int, c_p, c_p],
+    "aw_vq_gather": [c_p, c_p, c_i64, c_int, c_p, c_p],
+    "aw_patchify": [c_p, c_i64, c_int, c_int, c_int, c_p, c_i64, c_int, c_p],
+    "aw_weight_relayout": [c_p, c_int, c_int, c_int, c_int, c_int, c_p, c_i64, c_int, c_p],
+    "aw_weight_grad_scatter": [c_p, c_int, c_int, c_int, c_int, c_int, c_i64, c_p, c_p],
+    "aw_cast": [c_p, c_i64, c_p, c_int, c_p],
+    "aw_unpatch_head_fwd": [c_p, c_i64, c_int, c_int, c_p, c_p, c_p, c_p, c_p, c_p, c_p],
+    "aw_bn_finalize": [c_p, c_i64, c_int, c_p, c_p, c_p, c_p, c_p, c_f, c_f, c_int, c_p, c_p],
+    "aw_unpatch_head_bwd1": [c_p, c_i64, c_int, c_int, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_int, c_p],
+    "aw_unpatch_head_bwd2": [c_p, c_i64, c_int, c_int, c_p, c_p, c_p, c_p, c_p, c_p, c_int, c_p, c_int, c_p, c_int,
+                             c_p],
+    "aw_scalar_add": [c_p, c_p, c_p, c_p],
+    "aw_mse_finalize": [c_p, c_i64, c_p, c_p],
+    "aw_radam_step": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_int, c_i64, c_i64, c_f, c_f, c_f, c_f, c_p, c_p],
+    "aw_grad_norm_clip": [c_p, c_p, c_p, c_p, c_int, c_f, c_p, c_p, c_p, c_p],
+    "aw_scale": [c_p, c_i64, c_p, c_p],
+    "aw_layernorm_fwd": [c_p, c_i64, c_int, c_p, c_p, c_f, c_p, c_int, c_p, c_p, c_p],
+    "aw_layernorm_bwd": [c_p, c_p, c_i64, c_int, c_p, c_p, c_p, c_p, c_int, c_p, c_p, c_p],
+    "aw_embed_fwd": [c_p, c_i64, c_int, c_int, c_p, c_p, c_p, c_p],
+    "aw_embed_bwd": [c_p, c_i64, c_int, c_int, c_p, c_p, c_p],
+    "aw_attn_fwd": [c_p, c_i64, c_int, c_int, c_int, c_int, c_p, c_p, c_p],
+    "aw_attn_bwd": [c_p, c_p, c_p, c_p, c_i64, c_int, c_int, c_int, c_int, c_p, c_p, c_p],
+    "aw_ce_fwd": [c_p, c_i64, c_int, c_i64, c_p, c_int, c_p, c_p, c_p, c_p],
+    "aw_ce_bwd": [c_p, c_i64, c_int, c_i64, c_p, c_int, c_p, c_p, c_p, c_p, c_i64, c_int, c_p],
+    "aw_ce_finalize": [c_p, c_p, c_p, c_p],
+}
+
+_lib = None
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+def load(path: str = LIB_PATH):
+    """Load (once) and return the ctypes library with typed entry points."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise NativeError(f"HIP library not built: {path} is missing (run `python -c 'import __graft_entry__ as g; "
+                          f"g.build()'` or `make -C vq-vae-transformer-arc-welding_amd/csrc`)")
+    lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+    lib.aw_last_error.restype = ctypes.c_char_p
+    lib.aw_last_error.argtypes = []
+    for name, argtypes in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = c_int
+        fn.argtypes = argtypes
+    _lib = lib
+    return lib
+
+
+def call(name: str, *args) -> None:
+    lib = load()
+    status = getattr(lib, name)(*args)
+    if status != 0:
+        raise NativeError(f"{name} failed ({status}): {lib.aw_last_error().decode(errors='replace')}")
+
+
+def stream_ptr(stream=None) -> int:
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return s.cuda_stream
+
+
+def ptr(t):
+    """Raw device pointer of a tensor (None -> NULL).  CPU tensors are rejected: no host fallback exists."""
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise NativeError("arcweld HIP kernels need device tensors (got a CPU tensor); there is no CPU fallback")
+    return t.data_ptr()
+
+
+def dtype_code(dt: torch.dtype) -> int:
+    if dt == torch.float32:
+        return AW_F32
+    if dt == torch.bfloat16:
+        return AW_BF16
+    raise NativeError(f"unsupported operand dtype {dt}")

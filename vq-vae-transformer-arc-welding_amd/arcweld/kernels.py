@@ -1,0 +1,200 @@
+"""Typed wrappers over the C ABI (one function per entry point of include/arcweld_amd.h).
+
+Every wrapper takes torch DEVICE tensors, derives sizes/leading dimensions from their strides, launches on the
+current torch stream and raises on a non-zero status.  No wrapper has a CPU path.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _native as nat
+from ._native import AW_ACT_GELU_ERF, AW_ACT_GELU_TANH, AW_BF16, AW_F32, GemmArgs, call, dtype_code, ptr, stream_ptr
+
+__all__ = ["gemm", "AW_ACT_GELU_ERF", "AW_ACT_GELU_TANH", "AW_BF16", "AW_F32"]
+
+
+def _ld(t):
+    if t is None:
+        return 0
+    if t.dim() == 1:
+        return t.shape[0]
+    if t.stride(-1) != 1:
+        raise nat.NativeError("operand rows must be contiguous (stride(-1) == 1)")
+    return t.stride(0)
+
+
+def gemm(A, B, M, N, K, *, a_trans=False, b_trans=False, conv=None, alpha=1.0, beta=0.0, bias=None,
+         act=AW_ACT_GELU_ERF, pre=None, resid=None, drop=(0.0, 0), C=None, C2=None, c2_mode=0, drop2=(0.0, 0),
+         colstats=None, stats_mod=0, a_rowsum=None, stream=None):
+    """C = epilogue(alpha * op(A) @ op(B)); see aw_gemm in include/arcweld_amd.h for the exact semantics.
+
+    conv = (cin, seg, dir, operand) selects the implicit k=3 convolution form."""
+    if A.dtype != B.dtype:
+        raise nat.NativeError(f"gemm operands must share a dtype ({A.dtype} vs {B.dtype})")
+    a = GemmArgs()
+    a.M, a.N, a.K = int(M), int(N), int(K)
+    a.a_dtype = dtype_code(A.dtype)
+    a.A, a.lda, a.a_trans = ptr(A), _ld(A), int(bool(a_trans))
+    a.B, a.ldb, a.b_trans = ptr(B), _ld(B), int(bool(b_trans))
+    if conv is not None:
+        a.conv_cin, a.conv_seg, a.conv_dir, a.conv_operand = (int(v) for v in conv)
+    a.alpha, a.beta = float(alpha), float(beta)
+    a.bias = ptr(bias)
+    a.act = int(act)
+    a.pre, a.ld_pre = ptr(pre), _ld(pre)
+    a.resid, a.ld_resid = ptr(resid), _ld(resid)
+    a.drop_p, a.drop_seed = float(drop[0]), int(drop[1]) & 0xFFFFFFFFFFFFFFFF
+    if C is not None:
+        a.C, a.ldc, a.c_dtype = ptr(C), _ld(C), dtype_code(C.dtype)
+    if C2 is not None:
+        a.C2, a.ldc2, a.c2_dtype = ptr(C2), _ld(C2), dtype_code(C2.dtype)
+    a.c2_mode = int(c2_mode)
+    a.drop2_p, a.drop2_seed = float(drop2[0]), int(drop2[1]) & 0xFFFFFFFFFFFFFFFF
+    if colstats is not None:
+        if colstats.dtype != torch.float64:
+            raise nat.NativeError("colstats must be float64")
+        a.colstats, a.stats_mod = ptr(colstats), int(stats_mod)
+    a.a_rowsum = ptr(a_rowsum)
+    call("aw_gemm", ctypes.byref(a), stream_ptr(stream))
+    return C
+
+
+# ------------------------------------------------------------------------------------------------ VQ
+def vq_forward(z2d, E, zq, idx, counts, sqerr, stream=None):
+    N, D = z2d.shape
+    call("aw_vq_forward", ptr(z2d), ptr(E), N, E.shape[0], D, ptr(zq), ptr(idx), ptr(counts), ptr(sqerr),
+         stream_ptr(stream))
+
+
+def vq_finalize(counts, sqerr, N, K, D, beta, out2, stream=None):
+    call("aw_vq_finalize", ptr(counts), ptr(sqerr), N, K, D, float(beta), ptr(out2), stream_ptr(stream))
+
+
+def vq_backward(z2d, E, idx, g_zq, g_loss, beta, dz, dE, stream=None):
+    N, D = z2d.shape
+    call("aw_vq_backward", ptr(z2d), ptr(E), ptr(idx), ptr(g_zq), ptr(g_loss), N, E.shape[0], D, float(beta),
+         ptr(dz), ptr(dE), stream_ptr(stream))
+
+
+def vq_onehot(idx, K, out, stream=None):
+    call("aw_vq_onehot", ptr(idx), idx.numel(), K, ptr(out), stream_ptr(stream))
+
+
+def vq_gather(E, idx, out, stream=None):
+    call("aw_vq_gather", ptr(E), ptr(idx), idx.numel(), E.shape[1], ptr(out), stream_ptr(stream))
+
+
+# ------------------------------------------------------------------------------------------ layouts
+def patchify(x, P, out, stream=None):
+    B, L, C = x.shape
+    call("aw_patchify", ptr(x), B, L, C, P, ptr(out), out.stride(0), dtype_code(out.dtype), stream_ptr(stream))
+
+
+def weight_relayout(W, O, I, k, tap, mode, out, ldo=0, stream=None):
+    call("aw_weight_relayout", ptr(W), O, I, k, tap, mode, ptr(out), ldo, dtype_code(out.dtype), stream_ptr(stream))
+
+
+def weight_grad_scatter(g, O, I, k, tap, mode, G, stream=None):
+    call("aw_weight_grad_scatter", ptr(g), O, I, k, tap, mode, g.stride(0), ptr(G), stream_ptr(stream))
+
+
+def cast(x, out, stream=None):
+    call("aw_cast", ptr(x), x.numel(), ptr(out), dtype_code(out.dtype), stream_ptr(stream))
+
+
+def bn_finalize(colstats, n, H, gamma, beta, rm, rv, nbt, eps, momentum, training, stats, stream=None):
+    call("aw_bn_finalize", ptr(colstats), n, H, ptr(gamma), ptr(beta), ptr(rm), ptr(rv), ptr(nbt), float(eps),
+         float(momentum), int(training), ptr(stats), stream_ptr(stream))
+
+
+def unpatch_head_fwd(y, Q, stats, w2, b2, x, x_hat, sqerr, stream=None):
+    R, H = y.shape
+    call("aw_unpatch_head_fwd", ptr(y), R, H, Q, ptr(stats), ptr(w2), ptr(b2), ptr(x), ptr(x_hat), ptr(sqerr),
+         stream_ptr(stream))
+
+
+def unpatch_head_bwd1(y, Q, stats, w2, x_hat, x, g_recon, gsums, gw2, gb2, ggamma, gbeta, training, stream=None):
+    R, H = y.shape
+    call("aw_unpatch_head_bwd1", ptr(y), R, H, Q, ptr(stats), ptr(w2), ptr(x_hat), ptr(x), ptr(g_recon), ptr(gsums),
+         ptr(gw2), ptr(gb2), ptr(ggamma), ptr(gbeta), int(training), stream_ptr(stream))
+
+
+def unpatch_head_bwd2(y, Q, stats, w2, x_hat, x, g_recon, gsums, training, g_y, db_y, k1, stream=None):
+    R, H = y.shape
+    call("aw_unpatch_head_bwd2", ptr(y), R, H, Q, ptr(stats), ptr(w2), ptr(x_hat), ptr(x), ptr(g_recon), ptr(gsums),
+         int(training), ptr(g_y), dtype_code(g_y.dtype), ptr(db_y), k1, stream_ptr(stream))
+
+
+def scalar_add(a, b, out, stream=None):
+    call("aw_scalar_add", ptr(a), ptr(b), ptr(out), stream_ptr(stream))
+
+
+def mse_finalize(sqerr, numel, out, stream=None):
+    call("aw_mse_finalize", ptr(sqerr), int(numel), ptr(out), stream_ptr(stream))
+
+
+# ------------------------------------------------------------------------------------------ optimizer
+def radam_step(param, grad, m, v, seg_off, seg_len, seg_wd, seg_active, nseg, total, step, lr, beta1, beta2, eps,
+               gscale=None, stream=None):
+    call("aw_radam_step", ptr(param), ptr(grad), ptr(m), ptr(v), ptr(seg_off), ptr(seg_len), ptr(seg_wd),
+         ptr(seg_active), int(nseg), int(total), int(step), float(lr), float(beta1), float(beta2), float(eps),
+         ptr(gscale), stream_ptr(stream))
+
+
+def grad_norm_clip(grad, seg_off, seg_len, seg_active, nseg, max_norm, ws, out_norm, out_coef, stream=None):
+    call("aw_grad_norm_clip", ptr(grad), ptr(seg_off), ptr(seg_len), ptr(seg_active), int(nseg), float(max_norm),
+         ptr(ws), ptr(out_norm), ptr(out_coef), stream_ptr(stream))
+
+
+def scale_(x, s, stream=None):
+    call("aw_scale", ptr(x), x.numel(), ptr(s), stream_ptr(stream))
+
+
+# ---------------------------------------------------------------------------------------- transformer
+def layernorm_fwd(x, w, b, eps, y, mean, rstd, stream=None):
+    R, D = x.shape
+    call("aw_layernorm_fwd", ptr(x), R, D, ptr(w), ptr(b), float(eps), ptr(y), dtype_code(y.dtype), ptr(mean),
+         ptr(rstd), stream_ptr(stream))
+
+
+def layernorm_bwd(x, dy, w, mean, rstd, dx, accumulate, dw, db, stream=None):
+    R, D = x.shape
+    call("aw_layernorm_bwd", ptr(x), ptr(dy), R, D, ptr(w), ptr(mean), ptr(rstd), ptr(dx), int(accumulate), ptr(dw),
+         ptr(db), stream_ptr(stream))
+
+
+def embed_fwd(ids, wtok, pe, x, stream=None):
+    B, T = ids.shape
+    call("aw_embed_fwd", ptr(ids), B, T, wtok.shape[1], ptr(wtok), ptr(pe), ptr(x), stream_ptr(stream))
+
+
+def embed_bwd(ids, dx, dwtok, stream=None):
+    B, T = ids.shape
+    call("aw_embed_bwd", ptr(ids), B, T, dwtok.shape[1], ptr(dx), ptr(dwtok), stream_ptr(stream))
+
+
+def attn_fwd(qkv, B, T, n_head, d, y, lse, stream=None):
+    call("aw_attn_fwd", ptr(qkv), B, T, n_head, d, dtype_code(qkv.dtype), ptr(y), ptr(lse), stream_ptr(stream))
+
+
+def attn_bwd(qkv, y, dy, lse, B, T, n_head, d, dqkv, ws, stream=None):
+    call("aw_attn_bwd", ptr(qkv), ptr(y), ptr(dy), ptr(lse), B, T, n_head, d, dtype_code(qkv.dtype), ptr(dqkv),
+         ptr(ws), stream_ptr(stream))
+
+
+def ce_fwd(logits, V, y, ignore_index, loss_sum, count, lse, stream=None):
+    R = y.numel()
+    call("aw_ce_fwd", ptr(logits), R, V, logits.stride(0), ptr(y), int(ignore_index), ptr(loss_sum), ptr(count),
+         ptr(lse), stream_ptr(stream))
+
+
+def ce_bwd(logits, V, y, ignore_index, lse, count, g, dlogits, stream=None):
+    R = y.numel()
+    call("aw_ce_bwd", ptr(logits), R, V, logits.stride(0), ptr(y), int(ignore_index), ptr(lse), ptr(count), ptr(g),
+         ptr(dlogits), dlogits.stride(0), dtype_code(dlogits.dtype), stream_ptr(stream))
+
+
+def ce_finalize(loss_sum, count, out, stream=None):
+    call("aw_ce_finalize", ptr(loss_sum), ptr(count), ptr(out), stream_ptr(stream))

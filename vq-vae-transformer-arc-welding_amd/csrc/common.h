@@ -1,0 +1,102 @@
+// Shared device helpers for the arc-welding VQ-VAE / Transformer HIP kernels (gfx950 / CDNA4 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+#include <stdio.h>
+
+#include "../../include/arcweld_amd.h"
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(2))) float f32x2;
+typedef __bf16 bf16;
+
+// ---------------------------------------------------------------- error plumbing (host side)
+namespace aw {
+void set_error(const char* fmt, ...);
+int check_launch(const char* what);
+}  // namespace aw
+
+#define AW_REQUIRE(cond, ...)                 \
+  do {                                        \
+    if (!(cond)) {                            \
+      aw::set_error(__VA_ARGS__);             \
+      return AW_ERR_ARG;                      \
+    }                                         \
+  } while (0)
+
+// ---------------------------------------------------------------- numerics
+#define AW_INV_SQRT2 0.70710678118654752440f
+#define AW_INV_SQRT2PI 0.39894228040143267794f
+
+// GELU with the exact erf form (torch nn.GELU() default; model/vq_vae_patch_embedd.py:62,65 and
+// model/transformer_decoder.py:34).
+__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * AW_INV_SQRT2)); }
+__device__ __forceinline__ float gelu_erf_grad(float x) {
+  return 0.5f * (1.0f + erff(x * AW_INV_SQRT2)) + x * AW_INV_SQRT2PI * __expf(-0.5f * x * x);
+}
+// GELU tanh form (model/transformer_block.py:8-15).
+#define AW_SQRT_2_OVER_PI 0.79788456080286535588f
+__device__ __forceinline__ float gelu_tanh(float x) {
+  float u = AW_SQRT_2_OVER_PI * (x + 0.044715f * x * x * x);
+  return 0.5f * x * (1.0f + tanhf(u));
+}
+__device__ __forceinline__ float gelu_tanh_grad(float x) {
+  float u = AW_SQRT_2_OVER_PI * (x + 0.044715f * x * x * x);
+  float t = tanhf(u);
+  float du = AW_SQRT_2_OVER_PI * (1.0f + 3.0f * 0.044715f * x * x);
+  return 0.5f * (1.0f + t) + 0.5f * x * (1.0f - t * t) * du;
+}
+
+// ---------------------------------------------------------------- counter-based RNG (dropout masks)
+// keep(e) for element e of a launch with seed s: splitmix64 finaliser of s + (e+1)*golden, top 24 bits
+// as a uniform in [0,1).  Forward and backward regenerate the identical mask from (seed, element).
+__device__ __forceinline__ float aw_uniform(uint64_t seed, uint64_t e) {
+  uint64_t z = seed + (e + 1ull) * 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return (float)(z >> 40) * (1.0f / 16777216.0f);
+}
+__device__ __forceinline__ float aw_dropout_scale(uint64_t seed, uint64_t e, float p) {
+  if (p <= 0.f) return 1.f;
+  return aw_uniform(seed, e) < p ? 0.f : 1.f / (1.f - p);
+}
+
+// ---------------------------------------------------------------- typed load/store helpers
+template <typename T> __device__ __forceinline__ float to_f32(T v);
+template <> __device__ __forceinline__ float to_f32<float>(float v) { return v; }
+template <> __device__ __forceinline__ float to_f32<bf16>(bf16 v) { return (float)v; }
+template <typename T> __device__ __forceinline__ T from_f32(float v);
+template <> __device__ __forceinline__ float from_f32<float>(float v) { return v; }
+template <> __device__ __forceinline__ bf16 from_f32<bf16>(float v) { return (bf16)v; }
+
+__device__ __forceinline__ float load_as_f32(const void* p, int dtype, int64_t i) {
+  return dtype == AW_BF16 ? (float)((const bf16*)p)[i] : ((const float*)p)[i];
+}
+__device__ __forceinline__ void store_from_f32(void* p, int dtype, int64_t i, float v) {
+  if (dtype == AW_BF16)
+    ((bf16*)p)[i] = (bf16)v;
+  else
+    ((float*)p)[i] = v;
+}
+
+// ---------------------------------------------------------------- wave reductions (wave64)
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+static inline int aw_cdiv(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }

@@ -1,0 +1,147 @@
+// Multi-tensor RAdam + global-norm clip over one flat parameter/gradient buffer (gfx950).
+// torch.optim.RAdam semantics (L2 weight decay added to the gradient, lerp first moment, rectification
+// once rho_t > 5) as configured by model/autencoder_lightning_base.py:122-124 and
+// model/transformer_decoder.py:64-114; clip = Lightning gradient_clip_val -> clip_grad_norm_ (L2).
+#include <math.h>
+
+#include "common.h"
+
+namespace {
+
+constexpr int MAXSEG_LDS = 1024;
+
+struct RAdamScalars {
+  float lr, beta1, beta2, eps;
+  float bc1, sqrt_bc2, rect;
+  int rectified;
+};
+
+__device__ __forceinline__ int find_seg(const int64_t* off, int nseg, int64_t e) {
+  int lo = 0, hi = nseg - 1;
+  while (lo < hi) {  // last segment with off <= e
+    int mid = (lo + hi + 1) >> 1;
+    if (off[mid] <= e) lo = mid;
+    else hi = mid - 1;
+  }
+  return lo;
+}
+
+__global__ __launch_bounds__(256) void radam_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                    float* __restrict__ m, float* __restrict__ v,
+                                                    const int64_t* __restrict__ seg_off,
+                                                    const int64_t* __restrict__ seg_len,
+                                                    const float* __restrict__ seg_wd, const int* __restrict__ seg_active,
+                                                    int nseg, int64_t total, RAdamScalars S,
+                                                    const float* __restrict__ gscale) {
+  __shared__ int64_t s_off[MAXSEG_LDS];
+  for (int i = threadIdx.x; i < nseg; i += blockDim.x) s_off[i] = seg_off[i];
+  __syncthreads();
+  const float gs = gscale ? gscale[0] : 1.0f;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int s = find_seg(s_off, nseg, e);
+    if (e >= s_off[s] + seg_len[s] || !seg_active[s]) continue;
+    float gr = gs == 1.0f ? g[e] : g[e] * gs;
+    float pv = p[e];
+    const float wd = seg_wd[s];
+    if (wd != 0.f) gr = gr + wd * pv;
+    float mv = m[e];
+    mv = mv + (1.0f - S.beta1) * (gr - mv);  // exp_avg.lerp_(grad, 1-beta1)
+    float vv = v[e] * S.beta2 + (1.0f - S.beta2) * (gr * gr);
+    m[e] = mv;
+    v[e] = vv;
+    const float mhat = mv / S.bc1;
+    if (S.rectified) {
+      const float adaptive = S.sqrt_bc2 / (sqrtf(vv) + S.eps);
+      pv = pv - ((mhat * S.lr) * adaptive) * S.rect;
+    } else {
+      pv = pv - mhat * S.lr;
+    }
+    p[e] = pv;
+  }
+}
+
+__global__ __launch_bounds__(256) void sumsq_kernel(const float* __restrict__ g, const int64_t* __restrict__ seg_off,
+                                                    const int64_t* __restrict__ seg_len,
+                                                    const int* __restrict__ seg_active, int nseg, double* ws) {
+  double acc = 0.0;
+  for (int s = 0; s < nseg; ++s) {
+    if (!seg_active[s]) continue;
+    const float* gp = g + seg_off[s];
+    const int64_t n = seg_len[s];
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+      const float x = gp[i];
+      acc += (double)(x * x);
+    }
+  }
+  __shared__ double red[4];
+  acc = wave_sum_d(acc);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicAdd(ws, red[0] + red[1] + red[2] + red[3]);
+}
+
+__global__ void clip_coef_kernel(const double* ws, float max_norm, float* out_norm, float* out_coef) {
+  const float norm = (float)sqrt(ws[0]);
+  out_norm[0] = norm;
+  float c = max_norm / (norm + 1e-6f);
+  out_coef[0] = c < 1.0f ? c : 1.0f;
+}
+
+__global__ void scale_kernel(float* x, int64_t n, const float* s) {
+  const float c = s[0];
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    x[i] *= c;
+}
+
+}  // namespace
+
+extern "C" int aw_radam_step(float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
+                             const int64_t* seg_off, const int64_t* seg_len, const float* seg_wd, const int* seg_active,
+                             int nseg, int64_t total, int64_t step, float lr, float beta1, float beta2, float eps,
+                             const float* gscale, void* stream) {
+  AW_REQUIRE(param && grad && exp_avg && exp_avg_sq && seg_off && seg_len && seg_wd && seg_active,
+             "aw_radam_step: null pointer");
+  AW_REQUIRE(nseg > 0 && nseg <= MAXSEG_LDS, "aw_radam_step: nseg must be in [1, %d]", MAXSEG_LDS);
+  AW_REQUIRE(step >= 1 && total >= 0, "aw_radam_step: step counts from 1");
+  // host-side scalars in double, as torch's _single_tensor_radam computes them (python floats)
+  const double b1 = beta1, b2 = beta2, t = (double)step;
+  const double bc1 = 1.0 - pow(b1, t), bc2 = 1.0 - pow(b2, t);
+  const double rho_inf = 2.0 / (1.0 - b2) - 1.0;
+  const double rho_t = rho_inf - 2.0 * t * pow(b2, t) / bc2;
+  RAdamScalars S;
+  S.lr = lr;
+  S.beta1 = beta1;
+  S.beta2 = beta2;
+  S.eps = eps;
+  S.bc1 = (float)bc1;
+  S.sqrt_bc2 = (float)sqrt(bc2);
+  S.rectified = rho_t > 5.0;
+  S.rect = S.rectified ? (float)sqrt((rho_t - 4) * (rho_t - 2) * rho_inf / ((rho_inf - 4) * (rho_inf - 2) * rho_t)) : 1.f;
+  if (total == 0) return AW_OK;
+  int64_t g = (total + 255) / 256;
+  if (g > 4096) g = 4096;
+  hipLaunchKernelGGL(radam_kernel, dim3((int)g), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), param, grad,
+                     exp_avg, exp_avg_sq, seg_off, seg_len, seg_wd, seg_active, nseg, total, S, gscale);
+  return aw::check_launch("aw_radam_step");
+}
+
+extern "C" int aw_grad_norm_clip(const float* grad, const int64_t* seg_off, const int64_t* seg_len,
+                                 const int* seg_active, int nseg, float max_norm, double* ws, float* out_norm,
+                                 float* out_coef, void* stream) {
+  AW_REQUIRE(grad && seg_off && seg_len && seg_active && ws && out_norm && out_coef && nseg > 0,
+             "aw_grad_norm_clip: bad args");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (hipMemsetAsync(ws, 0, sizeof(double), s) != hipSuccess) return aw::check_launch("aw_grad_norm_clip memset");
+  hipLaunchKernelGGL(sumsq_kernel, dim3(1024), dim3(256), 0, s, grad, seg_off, seg_len, seg_active, nseg, ws);
+  hipLaunchKernelGGL(clip_coef_kernel, dim3(1), dim3(1), 0, s, ws, max_norm, out_norm, out_coef);
+  return aw::check_launch("aw_grad_norm_clip");
+}
+
+extern "C" int aw_scale(float* x, int64_t n, const float* sc, void* stream) {
+  AW_REQUIRE(x && sc && n >= 0, "aw_scale: bad args");
+  if (n == 0) return AW_OK;
+  int64_t g = (n + 255) / 256;
+  if (g > 4096) g = 4096;
+  hipLaunchKernelGGL(scale_kernel, dim3((int)g), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), x, n, sc);
+  return aw::check_launch("aw_scale");
+}

@@ -1,0 +1,517 @@
+// Latent-Transformer kernels (model/transformer_block.py, model/transformer_decoder.py, model/embedding.py)
+// for gfx950: LayerNorm, token+position embedding, causal attention (flash-style: the T x T score matrix is
+// never materialised, softmax statistics are kept per query row and the backward recomputes P from the
+// saved log-sum-exp), and cross-entropy with ignore_index.
+#include "common.h"
+
+namespace {
+
+// ---------------------------------------------------------------- LayerNorm (one wave per row)
+template <typename T>
+__global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ x, int64_t R, int D,
+                                                     const float* __restrict__ w, const float* __restrict__ b,
+                                                     float eps, T* __restrict__ y, float* __restrict__ mean,
+                                                     float* __restrict__ rstd) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  if (r >= R) return;
+  const float* xr = x + r * D;
+  float s = 0.f;
+  for (int i = lane; i < D; i += 64) s += xr[i];
+  const float mu = wave_sum(s) / (float)D;
+  float v = 0.f;
+  for (int i = lane; i < D; i += 64) {
+    const float d = xr[i] - mu;
+    v += d * d;
+  }
+  const float rs = rsqrtf(wave_sum(v) / (float)D + eps);
+  for (int i = lane; i < D; i += 64) y[r * D + i] = from_f32<T>((xr[i] - mu) * rs * w[i] + b[i]);
+  if (lane == 0) {
+    mean[r] = mu;
+    rstd[r] = rs;
+  }
+}
+
+__global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ x, const float* __restrict__ dy,
+                                                     int64_t R, int D, const float* __restrict__ w,
+                                                     const float* __restrict__ mean, const float* __restrict__ rstd,
+                                                     float* __restrict__ dx, int accumulate, float* __restrict__ dw,
+                                                     float* __restrict__ db) {
+  extern __shared__ float red[];  // 2*D
+  for (int i = threadIdx.x; i < 2 * D; i += blockDim.x) red[i] = 0.f;
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t r = wave; r < R; r += nw) {
+    const float mu = mean[r], rs = rstd[r];
+    const float* xr = x + r * D;
+    const float* dyr = dy + r * D;
+    float s1 = 0.f, s2 = 0.f;
+    for (int i = lane; i < D; i += 64) {
+      const float xh = (xr[i] - mu) * rs;
+      const float g = dyr[i] * w[i];
+      s1 += g;
+      s2 += g * xh;
+      atomicAdd(&red[i], dyr[i] * xh);
+      atomicAdd(&red[D + i], dyr[i]);
+    }
+    s1 = wave_sum(s1) / (float)D;
+    s2 = wave_sum(s2) / (float)D;
+    for (int i = lane; i < D; i += 64) {
+      const float xh = (xr[i] - mu) * rs;
+      const float g = dyr[i] * w[i];
+      const float v = rs * (g - s1 - xh * s2);
+      if (accumulate) dx[r * D + i] += v;
+      else dx[r * D + i] = v;
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < D; i += blockDim.x) {
+    atomicAdd(dw + i, red[i]);
+    atomicAdd(db + i, red[D + i]);
+  }
+}
+
+// ---------------------------------------------------------------- embedding (model/embedding.py:57-59)
+__global__ void embed_fwd_kernel(const int64_t* __restrict__ ids, int64_t B, int T, int D,
+                                 const float* __restrict__ wtok, const float* __restrict__ pe, float* __restrict__ x) {
+  const int64_t n = B * T * D;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = e / D;
+    const int i = (int)(e - r * D);
+    const int t = (int)(r % T);
+    x[e] = wtok[ids[r] * D + i] + pe[(int64_t)t * D + i];
+  }
+}
+
+__global__ void embed_bwd_kernel(const int64_t* __restrict__ ids, int64_t B, int T, int D, const float* __restrict__ dx,
+                                 float* __restrict__ dw) {
+  const int64_t n = B * T * D;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = e / D;
+    atomicAdd(dw + ids[r] * D + (e - r * D), dx[e]);
+  }
+}
+
+// ---------------------------------------------------------------- causal attention
+// Two lanes per query (or key) row, each holding half of the head dimension (HS/2 values); partial dot
+// products are combined with one xor-1 shuffle.  Key/value (resp. query) tiles of 32 rows are staged in LDS
+// and read as broadcasts.  64 rows per 128-thread workgroup; grid = (ceil(T/64), n_head, B).
+constexpr int ATT_ROWS = 64;
+constexpr int ATT_TILE = 32;
+
+template <typename T, int HS>
+__global__ __launch_bounds__(128) void attn_fwd_kernel(const T* __restrict__ qkv, int T_, int nh, int d,
+                                                       T* __restrict__ y, float* __restrict__ lse, float scale) {
+  constexpr int H2 = HS / 2;
+  __shared__ float Ks[ATT_TILE][HS + 1];
+  __shared__ float Vs[ATT_TILE][HS + 1];
+  const int b = blockIdx.z, h = blockIdx.y;
+  const int tid = threadIdx.x, half = tid & 1;
+  const int qi = blockIdx.x * ATT_ROWS + (tid >> 1);
+  const int64_t ld = 3 * (int64_t)d;
+  const T* base = qkv + (int64_t)b * T_ * ld;
+  const bool valid = qi < T_;
+  float q[H2], o[H2];
+#pragma unroll
+  for (int e = 0; e < H2; ++e) {
+    q[e] = valid ? to_f32<T>(base[(int64_t)qi * ld + h * HS + half * H2 + e]) * scale : 0.f;
+    o[e] = 0.f;
+  }
+  float m = -__builtin_huge_valf(), l = 0.f;
+  const int kend = min(T_, (blockIdx.x + 1) * ATT_ROWS);  // keys beyond the block's last query are masked
+  for (int k0 = 0; k0 < kend; k0 += ATT_TILE) {
+    __syncthreads();
+    for (int i = tid; i < ATT_TILE * HS; i += 128) {
+      const int kr = i / HS, e = i - kr * HS;
+      const int kk = k0 + kr;
+      float kv = 0.f, vv = 0.f;
+      if (kk < T_) {
+        kv = to_f32<T>(base[(int64_t)kk * ld + d + h * HS + e]);
+        vv = to_f32<T>(base[(int64_t)kk * ld + 2 * d + h * HS + e]);
+      }
+      Ks[kr][e] = kv;
+      Vs[kr][e] = vv;
+    }
+    __syncthreads();
+    float s[ATT_TILE];
+    float tmax = -__builtin_huge_valf();
+#pragma unroll
+    for (int j = 0; j < ATT_TILE; ++j) {
+      float a = 0.f;
+#pragma unroll
+      for (int e = 0; e < H2; ++e) a = fmaf(q[e], Ks[j][half * H2 + e], a);
+      a += __shfl_xor(a, 1, 64);
+      const bool ok = (k0 + j) <= qi && (k0 + j) < T_;
+      s[j] = ok ? a : -__builtin_huge_valf();
+      tmax = fmaxf(tmax, s[j]);
+    }
+    const float mn = fmaxf(m, tmax);
+    if (mn == -__builtin_huge_valf()) continue;  // nothing visible yet (padded row)
+    const float corr = __expf(m - mn);
+    l *= corr;
+#pragma unroll
+    for (int e = 0; e < H2; ++e) o[e] *= corr;
+#pragma unroll
+    for (int j = 0; j < ATT_TILE; ++j) {
+      const float pj = __expf(s[j] - mn);
+      l += pj;
+#pragma unroll
+      for (int e = 0; e < H2; ++e) o[e] = fmaf(pj, Vs[j][half * H2 + e], o[e]);
+    }
+    m = mn;
+  }
+  if (!valid) return;
+  const float inv = 1.f / l;
+  T* yr = y + ((int64_t)b * T_ + qi) * d + h * HS + half * H2;
+#pragma unroll
+  for (int e = 0; e < H2; ++e) yr[e] = from_f32<T>(o[e] * inv);
+  if (half == 0) lse[((int64_t)b * nh + h) * T_ + qi] = m + logf(l);
+}
+
+// delta_i = sum_e dy_i,e * y_i,e   (per (b, h, i))
+template <typename T, int HS>
+__global__ void attn_delta_kernel(const T* __restrict__ y, const T* __restrict__ dy, int64_t B, int T_, int nh, int d,
+                                  float* __restrict__ delta) {
+  const int64_t n = B * nh * T_;
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t bh = r / T_;
+    const int t = (int)(r - bh * T_);
+    const int64_t b = bh / nh;
+    const int h = (int)(bh - b * nh);
+    const int64_t off = (b * T_ + t) * d + h * HS;
+    float s = 0.f;
+#pragma unroll 8
+    for (int e = 0; e < HS; ++e) s += to_f32<T>(dy[off + e]) * to_f32<T>(y[off + e]);
+    delta[r] = s;
+  }
+}
+
+// dq_i = scale * sum_{j<=i} P_ij (dP_ij - delta_i) k_j     (query-stationary)
+template <typename T, int HS>
+__global__ __launch_bounds__(128) void attn_bwd_dq_kernel(const T* __restrict__ qkv, const T* __restrict__ dy,
+                                                          const float* __restrict__ lse,
+                                                          const float* __restrict__ delta, int T_, int nh, int d,
+                                                          T* __restrict__ dqkv, float scale) {
+  constexpr int H2 = HS / 2;
+  __shared__ float Ks[ATT_TILE][HS + 1];
+  __shared__ float Vs[ATT_TILE][HS + 1];
+  const int b = blockIdx.z, h = blockIdx.y;
+  const int tid = threadIdx.x, half = tid & 1;
+  const int qi = blockIdx.x * ATT_ROWS + (tid >> 1);
+  const int64_t ld = 3 * (int64_t)d;
+  const T* base = qkv + (int64_t)b * T_ * ld;
+  const bool valid = qi < T_;
+  float q[H2], g[H2], dq[H2];
+  const int64_t yo = ((int64_t)b * T_ + (valid ? qi : 0)) * d + h * HS + half * H2;
+#pragma unroll
+  for (int e = 0; e < H2; ++e) {
+    q[e] = valid ? to_f32<T>(base[(int64_t)qi * ld + h * HS + half * H2 + e]) * scale : 0.f;
+    g[e] = valid ? to_f32<T>(dy[yo + e]) : 0.f;
+    dq[e] = 0.f;
+  }
+  const int64_t st = ((int64_t)b * nh + h) * T_ + (valid ? qi : 0);
+  const float L = valid ? lse[st] : 0.f, Dl = valid ? delta[st] : 0.f;
+  const int kend = min(T_, (blockIdx.x + 1) * ATT_ROWS);
+  for (int k0 = 0; k0 < kend; k0 += ATT_TILE) {
+    __syncthreads();
+    for (int i = tid; i < ATT_TILE * HS; i += 128) {
+      const int kr = i / HS, e = i - kr * HS;
+      const int kk = k0 + kr;
+      float kv = 0.f, vv = 0.f;
+      if (kk < T_) {
+        kv = to_f32<T>(base[(int64_t)kk * ld + d + h * HS + e]);
+        vv = to_f32<T>(base[(int64_t)kk * ld + 2 * d + h * HS + e]);
+      }
+      Ks[kr][e] = kv;
+      Vs[kr][e] = vv;
+    }
+    __syncthreads();
+#pragma unroll 4
+    for (int j = 0; j < ATT_TILE; ++j) {
+      float a = 0.f, dp = 0.f;
+#pragma unroll
+      for (int e = 0; e < H2; ++e) {
+        a = fmaf(q[e], Ks[j][half * H2 + e], a);
+        dp = fmaf(g[e], Vs[j][half * H2 + e], dp);
+      }
+      a += __shfl_xor(a, 1, 64);
+      dp += __shfl_xor(dp, 1, 64);
+      const bool ok = valid && (k0 + j) <= qi && (k0 + j) < T_;
+      const float p = ok ? __expf(a - L) : 0.f;
+      const float ds = p * (dp - Dl);
+#pragma unroll
+      for (int e = 0; e < H2; ++e) dq[e] = fmaf(ds, Ks[j][half * H2 + e], dq[e]);
+    }
+  }
+  if (!valid) return;
+  T* out = dqkv + ((int64_t)b * T_ + qi) * ld + h * HS + half * H2;
+#pragma unroll
+  for (int e = 0; e < H2; ++e) out[e] = from_f32<T>(dq[e] * scale);
+}
+
+// dk_j = scale * sum_{i>=j} dS_ij q_i ;  dv_j = sum_{i>=j} P_ij dy_i      (key-stationary)
+template <typename T, int HS>
+__global__ __launch_bounds__(128) void attn_bwd_dkv_kernel(const T* __restrict__ qkv, const T* __restrict__ dy,
+                                                           const float* __restrict__ lse,
+                                                           const float* __restrict__ delta, int T_, int nh, int d,
+                                                           T* __restrict__ dqkv, float scale) {
+  constexpr int H2 = HS / 2;
+  __shared__ float Qs[ATT_TILE][HS + 1];
+  __shared__ float Gs[ATT_TILE][HS + 1];
+  __shared__ float Ls[ATT_TILE], Ds[ATT_TILE];
+  const int b = blockIdx.z, h = blockIdx.y;
+  const int tid = threadIdx.x, half = tid & 1;
+  const int kj = blockIdx.x * ATT_ROWS + (tid >> 1);
+  const int64_t ld = 3 * (int64_t)d;
+  const T* base = qkv + (int64_t)b * T_ * ld;
+  const bool valid = kj < T_;
+  float k[H2], v[H2], dk[H2], dv[H2];
+#pragma unroll
+  for (int e = 0; e < H2; ++e) {
+    k[e] = valid ? to_f32<T>(base[(int64_t)kj * ld + d + h * HS + half * H2 + e]) : 0.f;
+    v[e] = valid ? to_f32<T>(base[(int64_t)kj * ld + 2 * d + h * HS + half * H2 + e]) : 0.f;
+    dk[e] = dv[e] = 0.f;
+  }
+  const int qstart = blockIdx.x * ATT_ROWS;  // queries before the block's first key see none of its keys
+  for (int q0 = (qstart / ATT_TILE) * ATT_TILE; q0 < T_; q0 += ATT_TILE) {
+    __syncthreads();
+    for (int i = tid; i < ATT_TILE * HS; i += 128) {
+      const int qr = i / HS, e = i - qr * HS;
+      const int qq = q0 + qr;
+      float qv = 0.f, gv = 0.f;
+      if (qq < T_) {
+        qv = to_f32<T>(base[(int64_t)qq * ld + h * HS + e]) * scale;
+        gv = to_f32<T>(dy[((int64_t)b * T_ + qq) * d + h * HS + e]);
+      }
+      Qs[qr][e] = qv;
+      Gs[qr][e] = gv;
+    }
+    for (int i = tid; i < ATT_TILE; i += 128) {
+      const int qq = q0 + i;
+      const int64_t st = ((int64_t)b * nh + h) * T_ + qq;
+      Ls[i] = qq < T_ ? lse[st] : 0.f;
+      Ds[i] = qq < T_ ? delta[st] : 0.f;
+    }
+    __syncthreads();
+#pragma unroll 4
+    for (int i = 0; i < ATT_TILE; ++i) {
+      float a = 0.f, dp = 0.f;
+#pragma unroll
+      for (int e = 0; e < H2; ++e) {
+        a = fmaf(Qs[i][half * H2 + e], k[e], a);
+        dp = fmaf(Gs[i][half * H2 + e], v[e], dp);
+      }
+      a += __shfl_xor(a, 1, 64);
+      dp += __shfl_xor(dp, 1, 64);
+      const int qq = q0 + i;
+      const bool ok = valid && qq >= kj && qq < T_;
+      const float p = ok ? __expf(a - Ls[i]) : 0.f;
+      const float ds = p * (dp - Ds[i]);
+#pragma unroll
+      for (int e = 0; e < H2; ++e) {
+        dv[e] = fmaf(p, Gs[i][half * H2 + e], dv[e]);
+        dk[e] = fmaf(ds, Qs[i][half * H2 + e], dk[e]);  // Qs already carries the scale
+      }
+    }
+  }
+  if (!valid) return;
+  T* out = dqkv + ((int64_t)b * T_ + kj) * ld + h * HS + half * H2;
+#pragma unroll
+  for (int e = 0; e < H2; ++e) {
+    out[d + e] = from_f32<T>(dk[e]);
+    out[2 * d + e] = from_f32<T>(dv[e]);
+  }
+}
+
+// ---------------------------------------------------------------- cross entropy (one wave per row)
+__global__ __launch_bounds__(256) void ce_fwd_kernel(const float* __restrict__ logits, int64_t R, int V, int64_t ldl,
+                                                     const int64_t* __restrict__ y, int ignore, double* loss_sum,
+                                                     double* count, float* __restrict__ lse) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  if (r >= R) return;
+  const float* lr = logits + r * ldl;
+  float mx = -__builtin_huge_valf();
+  for (int i = lane; i < V; i += 64) mx = fmaxf(mx, lr[i]);
+  mx = wave_max(mx);
+  float s = 0.f;
+  for (int i = lane; i < V; i += 64) s += __expf(lr[i] - mx);
+  s = wave_sum(s);
+  const float L = mx + logf(s);
+  if (lane == 0) {
+    lse[r] = L;
+    const int64_t t = y[r];
+    if (t != ignore) {
+      atomicAdd(loss_sum, (double)(L - lr[t]));
+      atomicAdd(count, 1.0);
+    }
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void ce_bwd_kernel(const float* __restrict__ logits, int64_t R, int V, int64_t ldl,
+                                                     const int64_t* __restrict__ y, int ignore,
+                                                     const float* __restrict__ lse, const double* __restrict__ count,
+                                                     const float* __restrict__ g, T* __restrict__ dl, int64_t ldd) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  if (r >= R) return;
+  const int64_t t = y[r];
+  const float c = t == ignore ? 0.f : g[0] / (float)count[0];
+  const float L = lse[r];
+  for (int i = lane; i < V; i += 64) {
+    const float p = __expf(logits[r * ldl + i] - L);
+    dl[r * ldd + i] = from_f32<T>(c * (p - (i == t ? 1.f : 0.f)));
+  }
+}
+
+__global__ void ce_finalize_kernel(const double* s, const double* c, float* out) { out[0] = (float)(s[0] / c[0]); }
+
+int gridcap(int64_t n, int threads = 256, int cap = 8192) {
+  int64_t g = (n + threads - 1) / threads;
+  return (int)(g < 1 ? 1 : (g > cap ? cap : g));
+}
+
+}  // namespace
+
+extern "C" int aw_layernorm_fwd(const float* x, int64_t R, int D, const float* w, const float* b, float eps, void* y,
+                                int y_dtype, float* mean, float* rstd, void* stream) {
+  AW_REQUIRE(x && w && b && y && mean && rstd && R >= 0 && D > 0, "aw_layernorm_fwd: bad args");
+  if (R == 0) return AW_OK;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  dim3 grid(aw_cdiv(R, 4));
+  if (y_dtype == AW_BF16)
+    hipLaunchKernelGGL(ln_fwd_kernel<bf16>, grid, dim3(256), 0, s, x, R, D, w, b, eps, (bf16*)y, mean, rstd);
+  else
+    hipLaunchKernelGGL(ln_fwd_kernel<float>, grid, dim3(256), 0, s, x, R, D, w, b, eps, (float*)y, mean, rstd);
+  return aw::check_launch("aw_layernorm_fwd");
+}
+
+extern "C" int aw_layernorm_bwd(const float* x, const float* dy, int64_t R, int D, const float* w, const float* mean,
+                                const float* rstd, float* dx, int accumulate, float* dw, float* db, void* stream) {
+  AW_REQUIRE(x && dy && w && mean && rstd && dx && dw && db && R >= 0 && D > 0 && D <= 8192,
+             "aw_layernorm_bwd: bad args");
+  if (R == 0) return AW_OK;
+  hipLaunchKernelGGL(ln_bwd_kernel, dim3(gridcap(R * 64, 256, 512)), dim3(256), 2 * D * sizeof(float),
+                     reinterpret_cast<hipStream_t>(stream), x, dy, R, D, w, mean, rstd, dx, accumulate, dw, db);
+  return aw::check_launch("aw_layernorm_bwd");
+}
+
+extern "C" int aw_embed_fwd(const int64_t* ids, int64_t B, int T, int D, const float* wtok, const float* pe, float* x,
+                            void* stream) {
+  AW_REQUIRE(ids && wtok && pe && x && B >= 0 && T > 0 && D > 0, "aw_embed_fwd: bad args");
+  if (B == 0) return AW_OK;
+  hipLaunchKernelGGL(embed_fwd_kernel, dim3(gridcap(B * T * D)), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                     ids, B, T, D, wtok, pe, x);
+  return aw::check_launch("aw_embed_fwd");
+}
+
+extern "C" int aw_embed_bwd(const int64_t* ids, int64_t B, int T, int D, const float* dx, float* dwtok, void* stream) {
+  AW_REQUIRE(ids && dx && dwtok && B >= 0 && T > 0 && D > 0, "aw_embed_bwd: bad args");
+  if (B == 0) return AW_OK;
+  hipLaunchKernelGGL(embed_bwd_kernel, dim3(gridcap(B * T * D)), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                     ids, B, T, D, dx, dwtok);
+  return aw::check_launch("aw_embed_bwd");
+}
+
+#define AW_ATT_DISPATCH(KERNEL, HSV, ...)                                                        \
+  do {                                                                                           \
+    if (dtype == AW_BF16) hipLaunchKernelGGL((KERNEL<bf16, HSV>), __VA_ARGS__);                  \
+    else hipLaunchKernelGGL((KERNEL<float, HSV>), __VA_ARGS__);                                  \
+  } while (0)
+
+extern "C" int aw_attn_fwd(const void* qkv, int64_t B, int T, int n_head, int d, int dtype, void* y, float* lse,
+                           void* stream) {
+  AW_REQUIRE(qkv && y && lse && B >= 0 && T > 0 && n_head > 0 && d % n_head == 0, "aw_attn_fwd: bad args");
+  const int hs = d / n_head;
+  AW_REQUIRE(hs == 16 || hs == 32 || hs == 64 || hs == 128, "aw_attn_fwd: head size %d unsupported", hs);
+  if (B == 0) return AW_OK;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  dim3 grid(aw_cdiv(T, ATT_ROWS), n_head, (unsigned)B);
+  const float scale = 1.0f / sqrtf((float)hs);
+#define AW_F(HSV)                                                                                          \
+  if (dtype == AW_BF16)                                                                                    \
+    hipLaunchKernelGGL((attn_fwd_kernel<bf16, HSV>), grid, dim3(128), 0, s, (const bf16*)qkv, T, n_head, d, \
+                       (bf16*)y, lse, scale);                                                              \
+  else                                                                                                     \
+    hipLaunchKernelGGL((attn_fwd_kernel<float, HSV>), grid, dim3(128), 0, s, (const float*)qkv, T, n_head, d, \
+                       (float*)y, lse, scale);
+  switch (hs) {
+    case 16: AW_F(16) break;
+    case 32: AW_F(32) break;
+    case 64: AW_F(64) break;
+    default: AW_F(128) break;
+  }
+#undef AW_F
+  return aw::check_launch("aw_attn_fwd");
+}
+
+extern "C" int aw_attn_bwd(const void* qkv, const void* y, const void* dy, const float* lse, int64_t B, int T,
+                           int n_head, int d, int dtype, void* dqkv, float* ws, void* stream) {
+  AW_REQUIRE(qkv && y && dy && lse && dqkv && ws && B >= 0 && T > 0 && n_head > 0 && d % n_head == 0,
+             "aw_attn_bwd: bad args");
+  const int hs = d / n_head;
+  AW_REQUIRE(hs == 16 || hs == 32 || hs == 64 || hs == 128, "aw_attn_bwd: head size %d unsupported", hs);
+  if (B == 0) return AW_OK;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  dim3 grid(aw_cdiv(T, ATT_ROWS), n_head, (unsigned)B);
+  const float scale = 1.0f / sqrtf((float)hs);
+  const int64_t nrows = B * n_head * T;
+#define AW_B(HSV)                                                                                                  \
+  if (dtype == AW_BF16) {                                                                                          \
+    hipLaunchKernelGGL((attn_delta_kernel<bf16, HSV>), dim3(gridcap(nrows)), dim3(256), 0, s, (const bf16*)y,       \
+                       (const bf16*)dy, B, T, n_head, d, ws);                                                      \
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<bf16, HSV>), grid, dim3(128), 0, s, (const bf16*)qkv, (const bf16*)dy,   \
+                       lse, ws, T, n_head, d, (bf16*)dqkv, scale);                                                 \
+    hipLaunchKernelGGL((attn_bwd_dkv_kernel<bf16, HSV>), grid, dim3(128), 0, s, (const bf16*)qkv, (const bf16*)dy,  \
+                       lse, ws, T, n_head, d, (bf16*)dqkv, scale);                                                 \
+  } else {                                                                                                         \
+    hipLaunchKernelGGL((attn_delta_kernel<float, HSV>), dim3(gridcap(nrows)), dim3(256), 0, s, (const float*)y,     \
+                       (const float*)dy, B, T, n_head, d, ws);                                                     \
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<float, HSV>), grid, dim3(128), 0, s, (const float*)qkv,                  \
+                       (const float*)dy, lse, ws, T, n_head, d, (float*)dqkv, scale);                              \
+    hipLaunchKernelGGL((attn_bwd_dkv_kernel<float, HSV>), grid, dim3(128), 0, s, (const float*)qkv,                 \
+                       (const float*)dy, lse, ws, T, n_head, d, (float*)dqkv, scale);                              \
+  }
+  switch (hs) {
+    case 16: AW_B(16) break;
+    case 32: AW_B(32) break;
+    case 64: AW_B(64) break;
+    default: AW_B(128) break;
+  }
+#undef AW_B
+  return aw::check_launch("aw_attn_bwd");
+}
+
+extern "C" int aw_ce_fwd(const float* logits, int64_t R, int V, int64_t ldl, const int64_t* y, int ignore_index,
+                         double* loss_sum, double* count, float* lse, void* stream) {
+  AW_REQUIRE(logits && y && loss_sum && count && lse && R >= 0 && V > 0 && ldl >= V, "aw_ce_fwd: bad args");
+  if (R == 0) return AW_OK;
+  hipLaunchKernelGGL(ce_fwd_kernel, dim3(aw_cdiv(R, 4)), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), logits, R,
+                     V, ldl, y, ignore_index, loss_sum, count, lse);
+  return aw::check_launch("aw_ce_fwd");
+}
+
+extern "C" int aw_ce_bwd(const float* logits, int64_t R, int V, int64_t ldl, const int64_t* y, int ignore_index,
+                         const float* lse, const double* count, const float* g, void* dlogits, int64_t ldd, int dtype,
+                         void* stream) {
+  AW_REQUIRE(logits && y && lse && count && g && dlogits && R >= 0 && V > 0 && ldd >= V, "aw_ce_bwd: bad args");
+  if (R == 0) return AW_OK;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (dtype == AW_BF16)
+    hipLaunchKernelGGL(ce_bwd_kernel<bf16>, dim3(aw_cdiv(R, 4)), dim3(256), 0, s, logits, R, V, ldl, y, ignore_index,
+                       lse, count, g, (bf16*)dlogits, ldd);
+  else
+    hipLaunchKernelGGL(ce_bwd_kernel<float>, dim3(aw_cdiv(R, 4)), dim3(256), 0, s, logits, R, V, ldl, y, ignore_index,
+                       lse, count, g, (float*)dlogits, ldd);
+  return aw::check_launch("aw_ce_bwd");
+}
+
+extern "C" int aw_ce_finalize(const double* loss_sum, const double* count, float* out, void* stream) {
+  AW_REQUIRE(loss_sum && count && out, "aw_ce_finalize: bad args");
+  hipLaunchKernelGGL(ce_finalize_kernel, dim3(1), dim3(1), 0, reinterpret_cast<hipStream_t>(stream), loss_sum, count,
+                     out);
+  return aw::check_launch("aw_ce_finalize");
+}

@@ -1,0 +1,445 @@
+// VQ-VAE-Patch layout and un-patch head kernels (model/vq_vae_patch_embedd.py) for gfx950.
+// HBM-bound byte/elementwise work: coalesced float4 traffic, one wave per row where a row reduction is needed.
+#include "common.h"
+
+namespace {
+
+// ---------------------------------------------------------------- patchify (vq_vae_patch_embedd.py:13-17)
+template <typename T>
+__global__ void patchify_kernel(const float* __restrict__ x, int64_t B, int L, int C, int P, T* __restrict__ out,
+                                int64_t ldp) {
+  const int S = L * C / P;
+  const int64_t n = B * S * ldp;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t tok = i / ldp;
+    const int j = (int)(i - tok * ldp);
+    float v = 0.f;
+    if (j < P) {
+      const int64_t b = tok / S;
+      const int t = (int)(tok - b * S);
+      const int f = t * P + j;          // channel-major flat index within the window
+      const int c = f / L, l = f - c * L;
+      v = x[(b * L + l) * C + c];
+    }
+    out[i] = from_f32<T>(v);
+  }
+}
+
+// ---------------------------------------------------------------- weight relayouts (+cast)
+template <typename T>
+__global__ void relayout_kernel(const float* __restrict__ W, int O, int I, int k, int tap, int mode,
+                                T* __restrict__ out, int64_t ldo) {
+  int64_t n;
+  switch (mode) {
+    case 0: n = (int64_t)O * I; break;
+    case 1: n = (int64_t)O * 3 * I; break;
+    case 2: n = (int64_t)3 * O * I; break;
+    case 3: n = (int64_t)k * O * I; break;  // W is (I, O, k) here: "O" = out channels of the ConvT
+    default: n = (int64_t)O * ldo; break;
+  }
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
+    float v = 0.f;
+    if (mode == 0) {
+      const int64_t o = e / I, i = e - o * I;
+      v = W[(o * I + i) * k + tap];
+    } else if (mode == 1) {
+      const int64_t o = e / (3 * I), r = e - o * 3 * I;
+      const int64_t j = r / I, i = r - j * I;
+      v = W[(o * I + i) * 3 + j];
+    } else if (mode == 2) {
+      const int64_t jo = e / I, i = e - jo * I;
+      const int64_t j = jo / O, o = jo - j * O;
+      v = W[(o * I + i) * 3 + j];
+    } else if (mode == 3) {
+      const int64_t jo = e / I, i = e - jo * I;
+      const int64_t j = jo / O, o = jo - j * O;
+      v = W[(i * O + o) * k + j];
+    } else {
+      const int64_t o = e / ldo, j = e - o * ldo;
+      v = j < k ? W[o * k + j] : 0.f;
+    }
+    out[e] = from_f32<T>(v);
+  }
+}
+
+__global__ void grad_scatter_kernel(const float* __restrict__ g, int O, int I, int k, int tap, int mode, int64_t ldg,
+                                    float* __restrict__ G) {
+  int64_t n;
+  switch (mode) {
+    case 0: n = (int64_t)O * I; break;
+    case 1: n = (int64_t)O * 3 * I; break;
+    case 3: n = (int64_t)k * O * I; break;
+    default: n = (int64_t)O * k; break;
+  }
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
+    if (mode == 0) {
+      const int64_t o = e / I, i = e - o * I;
+      G[(o * I + i) * k + tap] += g[o * ldg + i];
+    } else if (mode == 1) {
+      const int64_t o = e / (3 * I), r = e - o * 3 * I;
+      const int64_t j = r / I, i = r - j * I;
+      G[(o * I + i) * 3 + j] += g[o * ldg + r];
+    } else if (mode == 3) {
+      const int64_t jo = e / I, i = e - jo * I;
+      const int64_t j = jo / O, o = jo - j * O;
+      G[(i * O + o) * k + j] += g[jo * ldg + i];
+    } else {
+      const int64_t o = e / k, j = e - o * k;
+      G[o * k + j] += g[o * ldg + j];
+    }
+  }
+}
+
+template <typename T>
+__global__ void cast_kernel(const float* __restrict__ in, int64_t n, T* __restrict__ out) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = from_f32<T>(in[i]);
+}
+
+// ---------------------------------------------------------------- BatchNorm finalize
+__global__ void bn_finalize_kernel(const double* __restrict__ cs, int64_t n, int H, const float* gamma,
+                                   const float* beta, float* rm, float* rv, int64_t* nbt, float eps, float mom,
+                                   int training, float* stats) {
+  const int o = blockIdx.x * blockDim.x + threadIdx.x;
+  if (o >= H) return;
+  float mean, invstd;
+  if (training) {
+    const double m = cs[o] / (double)n;
+    double var = cs[H + o] / (double)n - m * m;
+    if (var < 0) var = 0;
+    mean = (float)m;
+    invstd = (float)(1.0 / sqrt(var + (double)eps));
+    if (rm) rm[o] = (1.f - mom) * rm[o] + mom * mean;
+    if (rv) rv[o] = (1.f - mom) * rv[o] + mom * (float)(var * (double)n / (double)(n > 1 ? n - 1 : 1));
+    if (o == 0 && nbt) nbt[0] += 1;
+  } else {
+    mean = rm[o];
+    invstd = 1.0f / sqrtf(rv[o] + eps);
+  }
+  stats[o] = mean;
+  stats[H + o] = invstd;
+  stats[2 * H + o] = gamma ? gamma[o] : 1.f;
+  stats[3 * H + o] = beta ? beta[o] : 0.f;
+}
+
+// ---------------------------------------------------------------- un-patch head forward
+// one wave per row (position); lane handles channels o = 4*lane + 256*it (float4)
+constexpr int HEAD_MAXV = 4;  // float4 slots per lane -> H <= 1024
+
+__global__ __launch_bounds__(256) void head_fwd_kernel(const float* __restrict__ y, int64_t R, int H, int Q,
+                                                       const float* __restrict__ st, const float* __restrict__ w2,
+                                                       const float* __restrict__ b2, const float* __restrict__ x,
+                                                       float* __restrict__ x_hat, double* __restrict__ sqerr) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  double se = 0.0;
+  for (int64_t r = wave; r < R; r += nw) {
+    float part[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int o4 = lane * 4; o4 < H; o4 += 256) {
+      const float4 v = *reinterpret_cast<const float4*>(y + r * H + o4);
+      const float vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int o = o4 + e;
+        const float bn = (vv[e] - st[o]) * st[H + o] * st[2 * H + o] + st[3 * H + o];
+        const float a = gelu_erf(bn);
+#pragma unroll
+        for (int j = 0; j < 5; ++j) part[j] = fmaf(a, w2[o * 5 + j], part[j]);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 5; ++j) part[j] = wave_sum(part[j]);
+    if (lane < 5) {
+      float pj = part[0];
+#pragma unroll
+      for (int j = 1; j < 5; ++j)
+        if (lane == j) pj = part[j];
+      const int64_t b = r / Q;
+      const int q = (int)(r - b * Q);
+      const int64_t f = b * (int64_t)Q * 5 + q * 5 + lane;
+      const float xh = pj + b2[0];
+      x_hat[f] = xh;
+      const float d = xh - x[f];
+      se += (double)d * d;
+    }
+  }
+  se = wave_sum_d(se);
+  if (lane == 0) atomicAdd(sqerr, se);
+}
+
+// ---------------------------------------------------------------- un-patch head backward
+// pass 1: per-channel sums for the BN backward + ConvT2 weight/bias grads + gamma/beta grads.
+__global__ __launch_bounds__(256) void head_bwd1_kernel(const float* __restrict__ y, int64_t R, int H, int Q,
+                                                        const float* __restrict__ st, const float* __restrict__ w2,
+                                                        const float* __restrict__ x_hat, const float* __restrict__ x,
+                                                        const float* __restrict__ g_recon, double* __restrict__ gsums,
+                                                        float* __restrict__ gw2, float* __restrict__ gb2,
+                                                        float* __restrict__ ggamma, float* __restrict__ gbeta) {
+  extern __shared__ float red[];  // 7*H floats: gw2 (5H), sum g (H), sum g*xn (H)
+  for (int i = threadIdx.x; i < 7 * H; i += blockDim.x) red[i] = 0.f;
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  const float c = 2.0f / (float)(R * 5) * g_recon[0];  // numel = B*Q*5
+  float accw[HEAD_MAXV][4][5];
+  float accg[HEAD_MAXV][4], accgx[HEAD_MAXV][4];
+#pragma unroll
+  for (int s = 0; s < HEAD_MAXV; ++s)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      accg[s][e] = accgx[s][e] = 0.f;
+#pragma unroll
+      for (int j = 0; j < 5; ++j) accw[s][e][j] = 0.f;
+    }
+  float gbsum = 0.f;
+  for (int64_t r = wave; r < R; r += nw) {
+    const int64_t b = r / Q;
+    const int q = (int)(r - b * Q);
+    const int64_t f0 = b * (int64_t)Q * 5 + q * 5;
+    float go[5];
+#pragma unroll
+    for (int j = 0; j < 5; ++j) go[j] = c * (x_hat[f0 + j] - x[f0 + j]);
+    if (lane == 0) gbsum += go[0] + go[1] + go[2] + go[3] + go[4];
+#pragma unroll
+    for (int s = 0; s < HEAD_MAXV; ++s) {
+      const int o4 = lane * 4 + 256 * s;
+      if (o4 >= H) break;
+      const float4 v = *reinterpret_cast<const float4*>(y + r * H + o4);
+      const float vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int o = o4 + e;
+        const float xn = (vv[e] - st[o]) * st[H + o];
+        const float bn = xn * st[2 * H + o] + st[3 * H + o];
+        const float a = gelu_erf(bn);
+        float ga = 0.f;
+#pragma unroll
+        for (int j = 0; j < 5; ++j) {
+          ga = fmaf(go[j], w2[o * 5 + j], ga);
+          accw[s][e][j] = fmaf(a, go[j], accw[s][e][j]);
+        }
+        const float gbn = ga * gelu_erf_grad(bn);
+        accg[s][e] += gbn;
+        accgx[s][e] = fmaf(gbn, xn, accgx[s][e]);
+      }
+    }
+  }
+#pragma unroll
+  for (int s = 0; s < HEAD_MAXV; ++s) {
+    const int o4 = lane * 4 + 256 * s;
+    if (o4 >= H) break;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int o = o4 + e;
+#pragma unroll
+      for (int j = 0; j < 5; ++j) atomicAdd(&red[o * 5 + j], accw[s][e][j]);
+      atomicAdd(&red[5 * H + o], accg[s][e]);
+      atomicAdd(&red[6 * H + o], accgx[s][e]);
+    }
+  }
+  if (lane == 0) atomicAdd(gb2, gbsum);
+  __syncthreads();
+  for (int i = threadIdx.x; i < 5 * H; i += blockDim.x) atomicAdd(gw2 + i, red[i]);
+  for (int o = threadIdx.x; o < H; o += blockDim.x) {
+    atomicAdd(gsums + o, (double)red[5 * H + o]);
+    atomicAdd(gsums + H + o, (double)red[6 * H + o]);
+    if (gbeta) atomicAdd(gbeta + o, red[5 * H + o]);
+    if (ggamma) atomicAdd(ggamma + o, red[6 * H + o]);
+  }
+}
+
+// pass 2: g_y = BN backward of g*gelu'(bn); db_y = channel sums of g_y.
+template <typename T>
+__global__ __launch_bounds__(256) void head_bwd2_kernel(const float* __restrict__ y, int64_t R, int H, int Q,
+                                                        const float* __restrict__ st, const float* __restrict__ w2,
+                                                        const float* __restrict__ x_hat, const float* __restrict__ x,
+                                                        const float* __restrict__ g_recon,
+                                                        const double* __restrict__ gsums, int training,
+                                                        T* __restrict__ gy, float* __restrict__ dby) {
+  extern __shared__ float red[];  // H
+  for (int i = threadIdx.x; i < H; i += blockDim.x) red[i] = 0.f;
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  const float c = 2.0f / (float)(R * 5) * g_recon[0];
+  const float invn = 1.0f / (float)R;
+  float accd[HEAD_MAXV][4];
+#pragma unroll
+  for (int s = 0; s < HEAD_MAXV; ++s)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) accd[s][e] = 0.f;
+  for (int64_t r = wave; r < R; r += nw) {
+    const int64_t b = r / Q;
+    const int q = (int)(r - b * Q);
+    const int64_t f0 = b * (int64_t)Q * 5 + q * 5;
+    float go[5];
+#pragma unroll
+    for (int j = 0; j < 5; ++j) go[j] = c * (x_hat[f0 + j] - x[f0 + j]);
+#pragma unroll
+    for (int s = 0; s < HEAD_MAXV; ++s) {
+      const int o4 = lane * 4 + 256 * s;
+      if (o4 >= H) break;
+      const float4 v = *reinterpret_cast<const float4*>(y + r * H + o4);
+      const float vv[4] = {v.x, v.y, v.z, v.w};
+      T outv[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int o = o4 + e;
+        const float xn = (vv[e] - st[o]) * st[H + o];
+        const float bn = xn * st[2 * H + o] + st[3 * H + o];
+        float ga = 0.f;
+#pragma unroll
+        for (int j = 0; j < 5; ++j) ga = fmaf(go[j], w2[o * 5 + j], ga);
+        const float gbn = ga * gelu_erf_grad(bn);
+        float g;
+        if (training) {
+          const float sg = (float)gsums[o] * invn, sgx = (float)gsums[H + o] * invn;
+          g = st[2 * H + o] * st[H + o] * (gbn - sg - xn * sgx);
+        } else {
+          g = st[2 * H + o] * st[H + o] * gbn;
+        }
+        accd[s][e] += g;
+        outv[e] = from_f32<T>(g);
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) gy[r * H + o4 + e] = outv[e];
+    }
+  }
+#pragma unroll
+  for (int s = 0; s < HEAD_MAXV; ++s) {
+    const int o4 = lane * 4 + 256 * s;
+    if (o4 >= H) break;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) atomicAdd(&red[o4 + e], accd[s][e]);
+  }
+  __syncthreads();
+  for (int o = threadIdx.x; o < H; o += blockDim.x) atomicAdd(dby + o, red[o]);
+}
+
+__global__ void scalar_add_kernel(const float* a, const float* b, float* out) { out[0] = a[0] + b[0]; }
+__global__ void mse_finalize_kernel(const double* s, int64_t n, float* out) { out[0] = (float)(s[0] / (double)n); }
+
+int grid_for(int64_t n, int threads = 256, int cap = 8192) {
+  int64_t g = (n + threads - 1) / threads;
+  if (g > cap) g = cap;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+}  // namespace
+
+extern "C" int aw_patchify(const float* x, int64_t B, int L, int C, int P, void* patches, int64_t ldp, int dtype,
+                           void* stream) {
+  AW_REQUIRE(x && patches && B >= 0 && L > 0 && C > 0 && P > 0 && ldp >= P, "aw_patchify: bad args");
+  AW_REQUIRE((L * C) % P == 0, "aw_patchify: L*C must be a multiple of P");
+  if (B == 0) return AW_OK;
+  const int64_t n = B * (L * C / P) * ldp;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (dtype == AW_BF16)
+    hipLaunchKernelGGL(patchify_kernel<bf16>, dim3(grid_for(n)), dim3(256), 0, s, x, B, L, C, P, (bf16*)patches, ldp);
+  else
+    hipLaunchKernelGGL(patchify_kernel<float>, dim3(grid_for(n)), dim3(256), 0, s, x, B, L, C, P, (float*)patches, ldp);
+  return aw::check_launch("aw_patchify");
+}
+
+extern "C" int aw_weight_relayout(const float* W, int O, int I, int k, int tap, int mode, void* out, int64_t ldo,
+                                  int dtype, void* stream) {
+  AW_REQUIRE(W && out && O > 0 && I > 0 && k > 0 && mode >= 0 && mode <= 4, "aw_weight_relayout: bad args");
+  AW_REQUIRE(!(mode == 4 && ldo < k), "aw_weight_relayout: ldo < k");
+  int64_t n = mode == 4 ? (int64_t)O * ldo : (int64_t)O * I * (mode == 0 ? 1 : (mode == 3 ? k : 3));
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (dtype == AW_BF16)
+    hipLaunchKernelGGL(relayout_kernel<bf16>, dim3(grid_for(n)), dim3(256), 0, s, W, O, I, k, tap, mode, (bf16*)out, ldo);
+  else
+    hipLaunchKernelGGL(relayout_kernel<float>, dim3(grid_for(n)), dim3(256), 0, s, W, O, I, k, tap, mode, (float*)out, ldo);
+  return aw::check_launch("aw_weight_relayout");
+}
+
+extern "C" int aw_weight_grad_scatter(const float* g, int O, int I, int k, int tap, int mode, int64_t ldg, float* G,
+                                      void* stream) {
+  AW_REQUIRE(g && G && O > 0 && I > 0 && k > 0 && (mode == 0 || mode == 1 || mode == 3 || mode == 4),
+             "aw_weight_grad_scatter: bad args");
+  int64_t n = mode == 4 ? (int64_t)O * k : (int64_t)O * I * (mode == 0 ? 1 : (mode == 3 ? k : 3));
+  hipLaunchKernelGGL(grad_scatter_kernel, dim3(grid_for(n)), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), g, O,
+                     I, k, tap, mode, ldg, G);
+  return aw::check_launch("aw_weight_grad_scatter");
+}
+
+extern "C" int aw_cast(const float* in, int64_t n, void* out, int dtype, void* stream) {
+  AW_REQUIRE(in && out && n >= 0, "aw_cast: bad args");
+  if (n == 0) return AW_OK;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (dtype == AW_BF16)
+    hipLaunchKernelGGL(cast_kernel<bf16>, dim3(grid_for(n)), dim3(256), 0, s, in, n, (bf16*)out);
+  else
+    hipLaunchKernelGGL(cast_kernel<float>, dim3(grid_for(n)), dim3(256), 0, s, in, n, (float*)out);
+  return aw::check_launch("aw_cast");
+}
+
+extern "C" int aw_bn_finalize(const double* colstats, int64_t n, int H, const float* gamma, const float* beta,
+                              float* running_mean, float* running_var, int64_t* nbt, float eps, float momentum,
+                              int training, float* stats, void* stream) {
+  AW_REQUIRE(stats && H > 0, "aw_bn_finalize: bad args");
+  AW_REQUIRE(!training || (colstats && n > 0), "aw_bn_finalize: training needs colstats");
+  AW_REQUIRE(training || (running_mean && running_var), "aw_bn_finalize: eval needs running stats");
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3(aw_cdiv(H, 256)), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                     colstats, n, H, gamma, beta, running_mean, running_var, nbt, eps, momentum, training, stats);
+  return aw::check_launch("aw_bn_finalize");
+}
+
+extern "C" int aw_unpatch_head_fwd(const float* y, int64_t R, int H, int Q, const float* stats, const float* w2,
+                                   const float* b2, const float* x, float* x_hat, double* sqerr, void* stream) {
+  AW_REQUIRE(y && stats && w2 && b2 && x && x_hat && sqerr && R >= 0 && Q > 0 && H > 0, "aw_unpatch_head_fwd: bad args");
+  AW_REQUIRE(H % 4 == 0 && H <= 256 * HEAD_MAXV, "aw_unpatch_head_fwd: H must be a multiple of 4 and <= 1024");
+  AW_REQUIRE(R % Q == 0, "aw_unpatch_head_fwd: rows must be whole windows");
+  if (R == 0) return AW_OK;
+  hipLaunchKernelGGL(head_fwd_kernel, dim3(grid_for(R * 64, 256, 2048)), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), y, R, H, Q, stats, w2, b2, x, x_hat, sqerr);
+  return aw::check_launch("aw_unpatch_head_fwd");
+}
+
+extern "C" int aw_unpatch_head_bwd1(const float* y, int64_t R, int H, int Q, const float* stats, const float* w2,
+                                    const float* x_hat, const float* x, const float* g_recon, double* gsums, float* gw2,
+                                    float* gb2, float* ggamma, float* gbeta, int training, void* stream) {
+  (void)training;
+  AW_REQUIRE(y && stats && w2 && x_hat && x && g_recon && gsums && gw2 && gb2, "aw_unpatch_head_bwd1: null pointer");
+  AW_REQUIRE(H % 4 == 0 && H <= 256 * HEAD_MAXV && R % Q == 0, "aw_unpatch_head_bwd1: bad shape");
+  if (R == 0) return AW_OK;
+  hipLaunchKernelGGL(head_bwd1_kernel, dim3(grid_for(R * 64, 256, 256)), dim3(256), 7 * H * sizeof(float),
+                     reinterpret_cast<hipStream_t>(stream), y, R, H, Q, stats, w2, x_hat, x, g_recon, gsums, gw2, gb2,
+                     ggamma, gbeta);
+  return aw::check_launch("aw_unpatch_head_bwd1");
+}
+
+extern "C" int aw_unpatch_head_bwd2(const float* y, int64_t R, int H, int Q, const float* stats, const float* w2,
+                                    const float* x_hat, const float* x, const float* g_recon, const double* gsums,
+                                    int training, void* g_y, int gy_dtype, float* db_y, int k1, void* stream) {
+  (void)k1;
+  AW_REQUIRE(y && stats && w2 && x_hat && x && g_recon && gsums && g_y && db_y, "aw_unpatch_head_bwd2: null pointer");
+  AW_REQUIRE(H % 4 == 0 && H <= 256 * HEAD_MAXV && R % Q == 0, "aw_unpatch_head_bwd2: bad shape");
+  if (R == 0) return AW_OK;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  dim3 grid(grid_for(R * 64, 256, 1024));
+  if (gy_dtype == AW_BF16)
+    hipLaunchKernelGGL(head_bwd2_kernel<bf16>, grid, dim3(256), H * sizeof(float), s, y, R, H, Q, stats, w2, x_hat, x,
+                       g_recon, gsums, training, (bf16*)g_y, db_y);
+  else
+    hipLaunchKernelGGL(head_bwd2_kernel<float>, grid, dim3(256), H * sizeof(float), s, y, R, H, Q, stats, w2, x_hat, x,
+                       g_recon, gsums, training, (float*)g_y, db_y);
+  return aw::check_launch("aw_unpatch_head_bwd2");
+}
+
+extern "C" int aw_scalar_add(const float* a, const float* b, float* out, void* stream) {
+  AW_REQUIRE(a && b && out, "aw_scalar_add: null pointer");
+  hipLaunchKernelGGL(scalar_add_kernel, dim3(1), dim3(1), 0, reinterpret_cast<hipStream_t>(stream), a, b, out);
+  return aw::check_launch("aw_scalar_add");
+}
+
+extern "C" int aw_mse_finalize(const double* sqerr, int64_t numel, float* out, void* stream) {
+  AW_REQUIRE(sqerr && out && numel > 0, "aw_mse_finalize: bad args");
+  hipLaunchKernelGGL(mse_finalize_kernel, dim3(1), dim3(1), 0, reinterpret_cast<hipStream_t>(stream), sqerr, numel, out);
+  return aw::check_launch("aw_mse_finalize");
+}
