@@ -39,7 +39,7 @@ int aw_version(void);
  *                  zero where the shifted row leaves its window;
  *   conv_operand = 1 (B, b_trans = 1): N = 3*conv_cin, B[k][j*cin+i] = src[(k + (j-1))*ldb + i], same mask.
  * Epilogue, per element (row r, col c), in this order:
- *   v = alpha*acc;  v += bias[c];  v *= act'(pre[r*ld_pre + c]);  v *= dropout(drop_seed, r*N+c, drop_p);
+ *   v = alpha*acc;  v += bias[c] (bias[c % bias_mod] if bias_mod > 0);  v *= act'(pre[r*ld_pre + c]);  v *= dropout(drop_seed, r*N+c, drop_p);
  *   v += resid[r*ld_resid + c];  v += beta * C_old (C must be f32 when beta != 0);  C[r*ldc + c] = v (c_dtype)
  *   C2 (c2_mode): 1 = act(v), 2 = v, 3 = v * dropout(drop2_seed, r*N+c, drop2_p); stored as c2_dtype
  *   colstats (f64, 2*stats_mod): += v and v*v into slot (c % stats_mod)      (BatchNorm batch statistics)
@@ -62,6 +62,7 @@ typedef struct {
   float drop2_p; uint64_t drop2_seed;
   double* colstats; int stats_mod;
   float* a_rowsum;
+  int bias_mod;                  /* > 0: bias index is c % bias_mod (ConvT bias shared by the k taps) */
 } aw_gemm_args;
 
 int aw_gemm(const aw_gemm_args* args, void* stream);
@@ -75,9 +76,9 @@ int aw_gemm(const aw_gemm_args* args, void* stream);
 int aw_vq_forward(const float* z, const float* E, int64_t N, int K, int D,
                   float* zq, int64_t* idx, float* counts, double* sqerr, void* stream);
 /* loss = m + beta*m with m = sqerr/(N*D) (vector_quantizer.py:107-108); perplexity = exp(-sum p log(p+1e-10)),
- * p = counts/N (:114-115).  out2 = {loss, perplexity}. */
+ * p = counts/N (:114-115).  Each output is one f32 device scalar. */
 int aw_vq_finalize(const float* counts, const double* sqerr, int64_t N, int K, int D, float beta,
-                   float* out2, void* stream);
+                   float* loss, float* perplexity, void* stream);
 /* Backward of the STE + loss: dz = g_zq + g_loss*2(z - z_q)/(N*D);  dE[idx] += g_loss*2*beta*(z_q - z)/(N*D).
  * g_zq may be NULL (treated as 0); g_loss is a device scalar.  dE is accumulated (not overwritten). */
 int aw_vq_backward(const float* z, const float* E, const int64_t* idx, const float* g_zq, const float* g_loss,
@@ -109,27 +110,31 @@ int aw_weight_grad_scatter(const float* g, int O, int I, int k, int tap, int mod
 /* Elementwise cast/copy: out[i] = in[i] (f32 -> dtype). */
 int aw_cast(const float* in, int64_t n, void* out, int dtype, void* stream);
 
-/* Un-patch head forward (vq_vae_patch_embedd.py:27-30,52-57 + autencoder_lightning_base.py:82):
- * y (R = B*Q rows of H, f32, BN input) -> BN(train stats from colstats or eval running stats) -> GELU(erf)
- * -> ConvT(H->1, k5, s5) -> x_hat (B, 200, 2) interleaved; sqerr[0] += sum (x_hat - x)^2 (f64, zero on entry).
- * stats (f32 4*H): mean, invstd, gamma, beta as produced by aw_bn_finalize. */
+/* Un-patch head forward (vq_vae_patch_embedd.py:27-30,52-57):
+ * y (R = B*Q rows of H, f32, BN input) -> BN(stats) -> GELU(erf) -> ConvT(H->1, k5, s5) -> x_hat (B, 200, 2)
+ * interleaved (flat position 5q+j of window b).  stats (f32 4*H): mean, invstd, gamma, beta (aw_bn_finalize). */
 int aw_unpatch_head_fwd(const float* y, int64_t R, int H, int Q, const float* stats, const float* w2,
-                        const float* b2, const float* x, float* x_hat, double* sqerr, void* stream);
+                        const float* b2, float* x_hat, void* stream);
 /* BatchNorm finalize: colstats (f64 sum, sumsq over n rows) -> stats {mean, invstd, gamma, beta};
  * training: running_mean/var momentum update (unbiased var), *nbt += 1.  eval (training == 0): uses running. */
 int aw_bn_finalize(const double* colstats, int64_t n, int H, const float* gamma, const float* beta,
                    float* running_mean, float* running_var, int64_t* nbt, float eps, float momentum,
                    int training, float* stats, void* stream);
-/* Un-patch head backward.  g_xhat = 2(x_hat - x)/numel * g_recon (device scalar).
- * pass 1: per-channel sums sum_g, sum_gxhat (f64 2H, zero on entry), grads of w2 (H*5) and b2 (1) accumulated;
- * pass 2: g_y (R x H, gy_dtype) = BN backward (batch stats) of g * act'(.), and db_y (bias-of-y gradient,
- *         H f32, accumulated, channel sums of g_y). */
+/* Un-patch head backward from g_xhat (same layout as x_hat).
+ * pass 1: per-channel sums sum_g, sum_g*xhat (f64 2H, zero on entry); grads of w2 (H*5), b2 (1), gamma, beta
+ *         accumulated (+=).
+ * pass 2: g_y (R x H, gy_dtype) = BatchNorm backward (batch stats if training, else running) of g*gelu'(.),
+ *         db_y (H f32, +=) = channel sums of g_y (gradient of the ConvT bias feeding the BN). */
 int aw_unpatch_head_bwd1(const float* y, int64_t R, int H, int Q, const float* stats, const float* w2,
-                         const float* x_hat, const float* x, const float* g_recon, double* gsums, float* gw2,
-                         float* gb2, float* ggamma, float* gbeta, int training, void* stream);
+                         const float* g_xhat, double* gsums, float* gw2, float* gb2, float* ggamma, float* gbeta,
+                         void* stream);
 int aw_unpatch_head_bwd2(const float* y, int64_t R, int H, int Q, const float* stats, const float* w2,
-                         const float* x_hat, const float* x, const float* g_recon, const double* gsums,
-                         int training, void* g_y, int gy_dtype, float* db_y, int k1, void* stream);
+                         const float* g_xhat, const double* gsums, int training, void* g_y, int gy_dtype, float* db_y,
+                         void* stream);
+/* Mean-squared error (F.mse_loss, autencoder_lightning_base.py:82): sqerr[0] (f64, zero on entry) += sum (a-b)^2;
+ * backward: ga = 2(a-b)/n * g (device scalar g). */
+int aw_mse_fwd(const float* a, const float* b, int64_t n, double* sqerr, void* stream);
+int aw_mse_bwd(const float* a, const float* b, int64_t n, const float* g, float* ga, void* stream);
 
 /* loss = a[0] + b[0] (both device scalars) -> out[0]; also used for the autograd scalar plumbing. */
 int aw_scalar_add(const float* a, const float* b, float* out, void* stream);

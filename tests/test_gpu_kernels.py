@@ -158,7 +158,7 @@ def test_vq_indices_bit_exact_vs_reference(K, tag, Kc, D, N, eseed, estd):
     bad = np.nonzero(got != ref)[0]
     assert bad.size == 0, f"{bad.size} index mismatches; top-2 gaps there: {gap[bad][:8]}"
     out2 = torch.empty(2, device=DEV)
-    K.vq_finalize(counts, sq, N, Kc, D, 0.25, out2)
+    K.vq_finalize(counts, sq, N, Kc, D, 0.25, out2[0:1], out2[1:2])
     np.testing.assert_allclose(out2[0].item(), g[f"loss_{tag}"], rtol=1e-5)
     np.testing.assert_allclose(out2[1].item(), g[f"perplexity_{tag}"], rtol=1e-5)
     np.testing.assert_array_equal(counts.cpu().numpy(), np.bincount(ref, minlength=Kc).astype(np.float32))
@@ -176,7 +176,7 @@ def test_vq_small_forward_backward_vs_reference(K):
     sq = torch.zeros(1, dtype=torch.float64, device=DEV)
     K.vq_forward(z, E, zq, idx, counts, sq)
     out2 = torch.empty(2, device=DEV)
-    K.vq_finalize(counts, sq, N, 64, 16, 0.25, out2)
+    K.vq_finalize(counts, sq, N, 64, 16, 0.25, out2[0:1], out2[1:2])
     assert np.array_equal(idx.cpu().numpy(), g["idx"].reshape(-1))
     np.testing.assert_allclose(zq.cpu().numpy().reshape(g["z_q"].shape), g["z_q"], rtol=0, atol=1e-7)
     np.testing.assert_allclose(out2[0].item(), g["loss"], rtol=1e-6)

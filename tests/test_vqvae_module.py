@@ -1,0 +1,143 @@
+"""VQVAEPatch drop-in: module surface on CPU; fused HIP forward/backward against the reference's golden
+fixtures on the GPU (fp32 parity mode: torch.set_float32_matmul_precision('highest') -> exact-f32 MFMA)."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden
+from oracle import gen
+from oracle import vqvae as ov
+
+CASES = {
+    "vqvae_small.npz": (dict(hidden_dim=64, num_embeddings=64, embedding_dim=16, n_resblocks=2, patch_size=25), 8,
+                        301, 302),
+    "vqvae_small_p10.npz": (dict(hidden_dim=64, num_embeddings=64, embedding_dim=16, n_resblocks=1, patch_size=10), 4,
+                            305, 306),
+    "vqvae_small_p50.npz": (dict(hidden_dim=64, num_embeddings=64, embedding_dim=16, n_resblocks=1, patch_size=50), 4,
+                            307, 308),
+}
+
+
+def make_model(kw, wseed, device="cpu", batch_norm=False, dropout=0.0):
+    from model.vq_vae_patch_embedd import VQVAEPatch
+    m = VQVAEPatch(input_dim=2, learning_rate=1e-3, dropout_p=dropout, batch_norm=batch_norm, **kw)
+    cfg = ov.VQVAEConfig(batch_norm=batch_norm, **kw)
+    sd = ov.det_state_dict(cfg, wseed)
+    m.load_state_dict({k: torch.tensor(v) for k, v in sd.items()})
+    return m.to(device)
+
+
+@pytest.mark.parametrize("kw", [dict(hidden_dim=512, num_embeddings=512, embedding_dim=64, n_resblocks=8, patch_size=25),
+                                dict(hidden_dim=64, num_embeddings=64, embedding_dim=16, n_resblocks=2, patch_size=10,
+                                     batch_norm=True)])
+def test_state_dict_layout_matches_reference(kw):
+    from model.vq_vae_patch_embedd import VQVAEPatch
+    bn = kw.pop("batch_norm", False)
+    m = VQVAEPatch(input_dim=2, learning_rate=1e-3, batch_norm=bn, **kw)
+    ref = ov.reference_state_dict_shapes(ov.VQVAEConfig(batch_norm=bn, **kw))
+    got = {k: tuple(v.shape) for k, v in m.state_dict().items()}
+    assert got == {k: tuple(s) for k, s in ref.items()}
+    assert m.enc_out_len == 200 // kw["patch_size"] * 2
+    assert m.hparams["hidden_dim"] == kw["hidden_dim"] and m.hparams["patch_size"] == kw["patch_size"]
+
+
+def test_unsupported_patch_size_raises():
+    from model.vq_vae_patch_embedd import VQVAEPatch
+    with pytest.raises(NotImplementedError):
+        VQVAEPatch(hidden_dim=8, input_dim=2, num_embeddings=4, embedding_dim=4, n_resblocks=1, learning_rate=1e-3,
+                   patch_size=20)
+
+
+@pytest.fixture
+def fp32_parity():
+    old = torch.get_float32_matmul_precision()
+    torch.set_float32_matmul_precision("highest")
+    yield
+    torch.set_float32_matmul_precision(old)
+
+
+def _check_grads(m, g, rtol=1e-3):
+    for name, p in m.named_parameters():
+        ref = g["grad/" + name]
+        got = p.grad.detach().cpu().numpy()
+        scale = np.abs(ref).max() + 1e-12
+        np.testing.assert_allclose(got, ref, rtol=rtol, atol=2e-4 * scale + 1e-7, err_msg=name)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fname", list(CASES))
+def test_vqvae_train_step_parity_fp32(fname, fp32_parity):
+    from arcweld.functional import mse_loss
+    kw, B, wseed, xseed = CASES[fname]
+    g = golden(fname)
+    m = make_model(kw, wseed, "cuda")
+    m.train()
+    x = torch.tensor(gen.windows(xseed, B), device="cuda")
+    emb, x_hat, perp = m(x)
+    recon = mse_loss(x_hat, x)
+    loss = recon + emb
+    loss.backward()
+    idx = m._last_indices.cpu().numpy()
+    assert np.array_equal(idx, g["idx"]), f"{(idx != g['idx']).sum()} index mismatches"
+    np.testing.assert_allclose(x_hat.detach().cpu().numpy(), g["x_hat"], rtol=1e-4, atol=1e-4)
+    for k, v in (("emb_loss", emb), ("perplexity", perp), ("recon", recon), ("loss", loss)):
+        np.testing.assert_allclose(v.item(), g[k], rtol=1e-4, err_msg=k)
+    _check_grads(m, g)
+    sd = m.state_dict()
+    for k in g.files:
+        if k.startswith("state/") and "running" in k:
+            np.testing.assert_allclose(sd[k[6:]].cpu().numpy(), g[k], rtol=1e-4, atol=1e-5, err_msg=k)
+    assert int(sd["reverse_patch_embed.proj.1.num_batches_tracked"]) == 1
+    m.eval()
+    with torch.no_grad():
+        e2, xh2, _ = m(x)
+    np.testing.assert_allclose(xh2.cpu().numpy(), g["eval_x_hat"], rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.gpu
+def test_vqvae_full_size_parity_fp32(fp32_parity):
+    from arcweld.functional import mse_loss
+    g = golden("vqvae_full_b4.npz")
+    kw = dict(hidden_dim=512, num_embeddings=512, embedding_dim=64, n_resblocks=8, patch_size=25)
+    m = make_model(kw, 309, "cuda")
+    x = torch.tensor(gen.windows(310, 4), device="cuda")
+    emb, x_hat, perp = m(x)
+    loss = mse_loss(x_hat, x) + emb
+    loss.backward()
+    assert np.array_equal(m._last_indices.cpu().numpy(), g["idx"])
+    np.testing.assert_allclose(x_hat.detach().cpu().numpy(), g["x_hat"], rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(loss.item(), g["loss"], rtol=1e-4)
+    for name, p in m.named_parameters():
+        gn = np.linalg.norm(p.grad.detach().cpu().numpy().astype(np.float64))
+        np.testing.assert_allclose(gn, g["gnorm/" + name], rtol=2e-3, atol=1e-6, err_msg=name)
+
+
+@pytest.mark.gpu
+def test_vqvae_bf16_mode_tracks_fp32():
+    """bf16 MFMA operands (fp32 accumulate): reconstruction within bf16 tolerance of the fp32 golden."""
+    torch.set_float32_matmul_precision("medium")
+    try:
+        kw, B, wseed, xseed = CASES["vqvae_small.npz"]
+        g = golden("vqvae_small.npz")
+        m = make_model(kw, wseed, "cuda")
+        x = torch.tensor(gen.windows(xseed, B), device="cuda")
+        emb, x_hat, perp = m(x)
+        err = np.abs(x_hat.detach().cpu().numpy() - g["x_hat"]).max()
+        assert err < 5e-2 * np.abs(g["x_hat"]).max(), err
+    finally:
+        torch.set_float32_matmul_precision("highest")
+
+
+@pytest.mark.gpu
+def test_vqvae_dropout_train_step_runs_and_is_seeded():
+    kw, B, wseed, xseed = CASES["vqvae_small.npz"]
+    m = make_model(kw, wseed, "cuda", dropout=0.1)
+    x = torch.tensor(gen.windows(xseed, B), device="cuda")
+    torch.manual_seed(3)
+    m._step_seed = 0
+    _, a, _ = m(x)
+    m._step_seed = 0
+    _, b, _ = m(x)
+    assert torch.equal(a, b)
+    _, c, _ = m(x)
+    assert not torch.equal(a, c)

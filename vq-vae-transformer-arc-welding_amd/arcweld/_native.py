@@ -42,6 +42,7 @@ class GemmArgs(ctypes.Structure):
         ("drop2_p", c_f), ("drop2_seed", ctypes.c_uint64),
         ("colstats", c_p), ("stats_mod", c_int),
         ("a_rowsum", c_p),
+        ("bias_mod", c_int),
     ]
 
 
@@ -50,7 +51,7 @@ SIGNATURES = {
     "aw_version": [],
     "aw_gemm": [ctypes.POINTER(GemmArgs), c_p],
     "aw_vq_forward": [c_p, c_p, c_i64, c_int, c_int, c_p, c_p, c_p, c_p, c_p],
-    "aw_vq_finalize": [c_p, c_p, c_i64, c_int, c_int, c_f, c_p, c_p],
+    "aw_vq_finalize": [c_p, c_p, c_i64, c_int, c_int, c_f, c_p, c_p, c_p],
     "aw_vq_backward": [c_p, c_p, c_p, c_p, c_p, c_i64, c_int, c_int, c_f, c_p, c_p, c_p],
     "aw_vq_onehot": [c_p, c_i64, c_int, c_p, c_p],
     "aw_vq_gather": [c_p, c_p, c_i64, c_int, c_p, c_p],
@@ -58,11 +59,12 @@ SIGNATURES = {
     "aw_weight_relayout": [c_p, c_int, c_int, c_int, c_int, c_int, c_p, c_i64, c_int, c_p],
     "aw_weight_grad_scatter": [c_p, c_int, c_int, c_int, c_int, c_int, c_i64, c_p, c_p],
     "aw_cast": [c_p, c_i64, c_p, c_int, c_p],
-    "aw_unpatch_head_fwd": [c_p, c_i64, c_int, c_int, c_p, c_p, c_p, c_p, c_p, c_p, c_p],
+    "aw_unpatch_head_fwd": [c_p, c_i64, c_int, c_int, c_p, c_p, c_p, c_p, c_p],
     "aw_bn_finalize": [c_p, c_i64, c_int, c_p, c_p, c_p, c_p, c_p, c_f, c_f, c_int, c_p, c_p],
-    "aw_unpatch_head_bwd1": [c_p, c_i64, c_int, c_int, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_int, c_p],
-    "aw_unpatch_head_bwd2": [c_p, c_i64, c_int, c_int, c_p, c_p, c_p, c_p, c_p, c_p, c_int, c_p, c_int, c_p, c_int,
-                             c_p],
+    "aw_unpatch_head_bwd1": [c_p, c_i64, c_int, c_int, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p],
+    "aw_unpatch_head_bwd2": [c_p, c_i64, c_int, c_int, c_p, c_p, c_p, c_p, c_int, c_p, c_int, c_p, c_p],
+    "aw_mse_fwd": [c_p, c_p, c_i64, c_p, c_p],
+    "aw_mse_bwd": [c_p, c_p, c_i64, c_p, c_p, c_p],
     "aw_scalar_add": [c_p, c_p, c_p, c_p],
     "aw_mse_finalize": [c_p, c_i64, c_p, c_p],
     "aw_radam_step": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_int, c_i64, c_i64, c_f, c_f, c_f, c_f, c_p, c_p],

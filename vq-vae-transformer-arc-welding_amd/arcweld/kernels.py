@@ -27,7 +27,7 @@ def _ld(t):
 
 def gemm(A, B, M, N, K, *, a_trans=False, b_trans=False, conv=None, alpha=1.0, beta=0.0, bias=None,
          act=AW_ACT_GELU_ERF, pre=None, resid=None, drop=(0.0, 0), C=None, C2=None, c2_mode=0, drop2=(0.0, 0),
-         colstats=None, stats_mod=0, a_rowsum=None, stream=None):
+         colstats=None, stats_mod=0, a_rowsum=None, bias_mod=0, stream=None):
     """C = epilogue(alpha * op(A) @ op(B)); see aw_gemm in include/arcweld_amd.h for the exact semantics.
 
     conv = (cin, seg, dir, operand) selects the implicit k=3 convolution form."""
@@ -57,6 +57,7 @@ def gemm(A, B, M, N, K, *, a_trans=False, b_trans=False, conv=None, alpha=1.0, b
             raise nat.NativeError("colstats must be float64")
         a.colstats, a.stats_mod = ptr(colstats), int(stats_mod)
     a.a_rowsum = ptr(a_rowsum)
+    a.bias_mod = int(bias_mod)
     call("aw_gemm", ctypes.byref(a), stream_ptr(stream))
     return C
 
@@ -68,8 +69,9 @@ def vq_forward(z2d, E, zq, idx, counts, sqerr, stream=None):
          stream_ptr(stream))
 
 
-def vq_finalize(counts, sqerr, N, K, D, beta, out2, stream=None):
-    call("aw_vq_finalize", ptr(counts), ptr(sqerr), N, K, D, float(beta), ptr(out2), stream_ptr(stream))
+def vq_finalize(counts, sqerr, N, K, D, beta, loss, perplexity, stream=None):
+    call("aw_vq_finalize", ptr(counts), ptr(sqerr), N, K, D, float(beta), ptr(loss), ptr(perplexity),
+         stream_ptr(stream))
 
 
 def vq_backward(z2d, E, idx, g_zq, g_loss, beta, dz, dE, stream=None):
@@ -109,22 +111,29 @@ def bn_finalize(colstats, n, H, gamma, beta, rm, rv, nbt, eps, momentum, trainin
          float(momentum), int(training), ptr(stats), stream_ptr(stream))
 
 
-def unpatch_head_fwd(y, Q, stats, w2, b2, x, x_hat, sqerr, stream=None):
+def unpatch_head_fwd(y, Q, stats, w2, b2, x_hat, stream=None):
     R, H = y.shape
-    call("aw_unpatch_head_fwd", ptr(y), R, H, Q, ptr(stats), ptr(w2), ptr(b2), ptr(x), ptr(x_hat), ptr(sqerr),
-         stream_ptr(stream))
+    call("aw_unpatch_head_fwd", ptr(y), R, H, Q, ptr(stats), ptr(w2), ptr(b2), ptr(x_hat), stream_ptr(stream))
 
 
-def unpatch_head_bwd1(y, Q, stats, w2, x_hat, x, g_recon, gsums, gw2, gb2, ggamma, gbeta, training, stream=None):
+def unpatch_head_bwd1(y, Q, stats, w2, g_xhat, gsums, gw2, gb2, ggamma, gbeta, stream=None):
     R, H = y.shape
-    call("aw_unpatch_head_bwd1", ptr(y), R, H, Q, ptr(stats), ptr(w2), ptr(x_hat), ptr(x), ptr(g_recon), ptr(gsums),
-         ptr(gw2), ptr(gb2), ptr(ggamma), ptr(gbeta), int(training), stream_ptr(stream))
+    call("aw_unpatch_head_bwd1", ptr(y), R, H, Q, ptr(stats), ptr(w2), ptr(g_xhat), ptr(gsums), ptr(gw2), ptr(gb2),
+         ptr(ggamma), ptr(gbeta), stream_ptr(stream))
 
 
-def unpatch_head_bwd2(y, Q, stats, w2, x_hat, x, g_recon, gsums, training, g_y, db_y, k1, stream=None):
+def unpatch_head_bwd2(y, Q, stats, w2, g_xhat, gsums, training, g_y, db_y, stream=None):
     R, H = y.shape
-    call("aw_unpatch_head_bwd2", ptr(y), R, H, Q, ptr(stats), ptr(w2), ptr(x_hat), ptr(x), ptr(g_recon), ptr(gsums),
-         int(training), ptr(g_y), dtype_code(g_y.dtype), ptr(db_y), k1, stream_ptr(stream))
+    call("aw_unpatch_head_bwd2", ptr(y), R, H, Q, ptr(stats), ptr(w2), ptr(g_xhat), ptr(gsums), int(training),
+         ptr(g_y), dtype_code(g_y.dtype), ptr(db_y), stream_ptr(stream))
+
+
+def mse_fwd(a, b, sqerr, stream=None):
+    call("aw_mse_fwd", ptr(a), ptr(b), a.numel(), ptr(sqerr), stream_ptr(stream))
+
+
+def mse_bwd(a, b, g, ga, stream=None):
+    call("aw_mse_bwd", ptr(a), ptr(b), a.numel(), ptr(g), ptr(ga), stream_ptr(stream))
 
 
 def scalar_add(a, b, out, stream=None):

@@ -1,0 +1,325 @@
+"""Fused VQ-VAE-Patch training path on the HIP kernels (model/vq_vae_patch_embedd.py:117-167).
+
+Activations are TOKEN-MAJOR: a batch of B windows is N = B*S token rows of H channels, row = b*S + t, with the
+reference's channel-major patch order (tokens 0..S/2-1 voltage, S/2..S-1 current).  Every dense contraction is
+one ``aw_gemm`` launch:
+
+  patch embed   (N x ldp) . Wp^T            -> x0 (f32) + gelu(x0) (operand dtype)
+  enc ResBlock  a0 . W1c^T -> h, gelu(h);  a1 . W2c^T + b, dropout, + x  -> x', gelu(x')   (centre taps only)
+  sep conv      x_R . Ws^T                  -> z (f32)
+  VQ            aw_vq_forward (fp32, bit-exact argmin)
+  dec 1x1       zq . Wd0^T                  -> y0, gelu(y0)
+  dec ResBlock  implicit k=3 conv GEMMs (K = 3H, rows shifted within each window)
+  ConvT(H->H)   y_R . Wt1r^T (N = k1*H)     -> Y (f32) + BatchNorm column statistics in the epilogue
+  head          BN -> GELU -> ConvT(H->1) -> x_hat, one wave per position
+
+The backward mirrors it (input-gradient GEMMs with the GELU' and dropout masks fused in the epilogues,
+weight-gradient GEMMs with the bias gradient fused as an A-row-sum).  Operand dtype follows
+``torch.get_float32_matmul_precision()`` unless the module overrides it: 'highest' -> exact fp32 MFMA
+(parity mode), 'high'/'medium' -> bf16 MFMA with fp32 accumulation (the reference scripts set 'medium',
+train_reconstruction_embedding.py:253).
+"""
+from __future__ import annotations
+
+import torch
+
+from . import kernels as K
+
+F32 = torch.float32
+
+
+def operand_dtype(override=None):
+    if override is not None:
+        return override
+    return F32 if torch.get_float32_matmul_precision() == "highest" else torch.bfloat16
+
+
+def _mix(seed: int, salt: int) -> int:
+    z = (seed * 0x9E3779B97F4A7C15 + salt * 0xBF58476D1CE4E5B9 + 0x94D049BB133111EB) & 0xFFFFFFFFFFFFFFFF
+    z ^= z >> 31
+    z = (z * 0xD6E8FEB86659FD93) & 0xFFFFFFFFFFFFFFFF
+    return z ^ (z >> 32)
+
+
+class VQVAEShapes:
+    def __init__(self, m, B):
+        self.B = B
+        self.H, self.D, self.K = m.hidden_dim, m.embedding_dim, m.num_embeddings
+        self.R = m.n_resblocks
+        self.P, self.L, self.C = m.patch_size, m.seq_len, m.input_dim
+        self.S = self.L * self.C // self.P
+        self.N = B * self.S
+        self.k1 = m.reverse_patch_embed.k1
+        self.Q = self.S * self.k1
+        self.ldp = (self.P + 7) // 8 * 8
+
+
+def _params(m):
+    """Reference-layout parameter tensors of a VQVAEPatch, by role."""
+    enc = [(blk.block[1], blk.block[4]) for blk in m.encoder[0].shared_conv]
+    dec = [(blk.block[1], blk.block[4]) for blk in m.decoder[1].shared_conv]
+    rp = m.reverse_patch_embed.proj
+    return dict(pe=m.patch_embed.proj, enc=enc, sep=m.encoder[1].shared_conv, E=m.vector_quantization.embedding.weight,
+                dec0=m.decoder[0], dec=dec, t1=rp[0], bn=rp[1], t2=rp[3])
+
+
+class Saved:
+    pass
+
+
+def forward(m, x, training: bool, need_backward: bool, dtype=None, seed: int = 0):
+    """Returns (emb_loss (), x_hat (B, L, C), perplexity (), indices (N,), saved-or-None)."""
+    T = operand_dtype(dtype)
+    if x.dtype != F32 or x.dim() != 3:
+        raise ValueError("VQVAEPatch expects float32 windows of shape (B, seq_len, input_dim)")
+    x = x.contiguous()
+    sh = VQVAEShapes(m, x.shape[0])
+    H, D, N, S, R, P, k1 = sh.H, sh.D, sh.N, sh.S, sh.R, sh.P, sh.k1
+    if x.shape[1] != sh.L or x.shape[2] != sh.C:
+        raise ValueError(f"expected windows (B, {sh.L}, {sh.C}), got {tuple(x.shape)}")
+    pr = _params(m)
+    dev = x.device
+    p_drop = float(m.dropout_p) if training else 0.0
+    e = lambda *s, dt=F32: torch.empty(*s, device=dev, dtype=dt)  # noqa: E731
+    sv = Saved()
+    sv.sh, sv.T, sv.p_drop, sv.training = sh, T, p_drop, training
+    sv.enc_seed = [_mix(seed, 100 + r) for r in range(R)]
+    sv.dec_seed = [_mix(seed, 200 + r) for r in range(R)]
+
+    # ---- operand copies of the weights (relayout + cast)
+    Wp = e(H, sh.ldp, dt=T)
+    K.weight_relayout(pr["pe"].weight, H, 1, P, 0, 4, Wp, ldo=sh.ldp)
+    enc_w = []
+    for c1, c2 in pr["enc"]:
+        w1, w2 = e(H, H, dt=T), e(H, H, dt=T)
+        K.weight_relayout(c1.weight, H, H, 3, 1, 0, w1)
+        K.weight_relayout(c2.weight, H, H, 3, 1, 0, w2)
+        enc_w.append((w1, w2))
+    Ws = e(D, H, dt=T)
+    K.weight_relayout(pr["sep"].weight, D, H, 1, 0, 0, Ws)
+    Wd0 = e(H, D, dt=T)
+    K.weight_relayout(pr["dec0"].weight, H, D, 1, 0, 0, Wd0)
+    dec_w = []
+    for c1, c2 in pr["dec"]:
+        w1, w2 = e(H, 3 * H, dt=T), e(H, 3 * H, dt=T)
+        K.weight_relayout(c1.weight, H, H, 3, 0, 1, w1)
+        K.weight_relayout(c2.weight, H, H, 3, 0, 1, w2)
+        dec_w.append((w1, w2))
+    Wt1 = e(k1 * H, H, dt=T)
+    K.weight_relayout(pr["t1"].weight, H, H, k1, 0, 3, Wt1)
+
+    # ---- patch embed
+    patches = e(N, sh.ldp, dt=T)
+    K.patchify(x, P, patches)
+    x0, a0 = e(N, H), e(N, H, dt=T)
+    K.gemm(patches, Wp, N, H, sh.ldp, bias=pr["pe"].bias, C=x0, C2=a0, c2_mode=1)
+
+    # ---- encoder ResBlocks (per-token: centre taps)
+    xs, a0s, hs, a1s = [x0], [a0], [], []
+    for r, (c1, c2) in enumerate(pr["enc"]):
+        h, a1 = e(N, H), e(N, H, dt=T)
+        K.gemm(a0s[r], enc_w[r][0], N, H, H, bias=c1.bias, C=h, C2=a1, c2_mode=1)
+        if r < R - 1:
+            xn, an = e(N, H), e(N, H, dt=T)
+            K.gemm(a1, enc_w[r][1], N, H, H, bias=c2.bias, drop=(p_drop, sv.enc_seed[r]), resid=xs[r], C=xn, C2=an,
+                   c2_mode=1)
+        else:  # last block: only the operand copy of x_R is consumed (sep conv)
+            xn, an = None, e(N, H, dt=T)
+            K.gemm(a1, enc_w[r][1], N, H, H, bias=c2.bias, drop=(p_drop, sv.enc_seed[r]), resid=xs[r], C=an)
+        xs.append(xn)
+        a0s.append(an)
+        hs.append(h)
+        a1s.append(a1)
+    xR_T = a0s[R] if R > 0 else (x0 if T == F32 else _cast(x0, T))
+
+    # ---- SepCNNBlock -> z (B, S, D)
+    z = e(N, D)
+    K.gemm(xR_T, Ws, N, D, H, bias=pr["sep"].bias, C=z)
+
+    # ---- vector quantizer
+    Kc = sh.K
+    zq = e(N, D)
+    idx = e(N, dt=torch.int64)
+    counts = torch.zeros(Kc, device=dev)
+    sq = torch.zeros(1, device=dev, dtype=torch.float64)
+    K.vq_forward(z, pr["E"], zq, idx, counts, sq)
+    emb_loss, perplexity = e(()), e(())
+    K.vq_finalize(counts, sq, N, Kc, D, m.vector_quantization.beta, emb_loss, perplexity)
+    zq_T = zq if T == F32 else _cast(zq, T)
+
+    # ---- decoder: 1x1 conv + ResBlocks with k=3 convs along the window
+    y0, ya0 = e(N, H), e(N, H, dt=T)
+    K.gemm(zq_T, Wd0, N, H, D, bias=pr["dec0"].bias, C=y0, C2=ya0, c2_mode=1)
+    conv = (H, S, 1, 0)
+    ys, ya0s, dhs, da1s = [y0], [ya0], [], []
+    for r, (c1, c2) in enumerate(pr["dec"]):
+        h, a1 = e(N, H), e(N, H, dt=T)
+        K.gemm(ya0s[r], dec_w[r][0], N, H, 3 * H, conv=conv, bias=c1.bias, C=h, C2=a1, c2_mode=1)
+        if r < R - 1:
+            yn, an = e(N, H), e(N, H, dt=T)
+            K.gemm(a1, dec_w[r][1], N, H, 3 * H, conv=conv, bias=c2.bias, drop=(p_drop, sv.dec_seed[r]), resid=ys[r],
+                   C=yn, C2=an, c2_mode=1)
+        else:
+            yn, an = None, e(N, H, dt=T)
+            K.gemm(a1, dec_w[r][1], N, H, 3 * H, conv=conv, bias=c2.bias, drop=(p_drop, sv.dec_seed[r]), resid=ys[r],
+                   C=an)
+        ys.append(yn)
+        ya0s.append(an)
+        dhs.append(h)
+        da1s.append(a1)
+    yR_T = ya0s[R] if R > 0 else (y0 if T == F32 else _cast(y0, T))
+
+    # ---- un-patch: ConvT(H->H, k1) with BN statistics in the epilogue, then the fused head
+    bn = pr["bn"]
+    Y = e(N, k1 * H)
+    colstats = torch.zeros(2 * H, device=dev, dtype=torch.float64) if training else None
+    K.gemm(yR_T, Wt1, N, k1 * H, H, bias=pr["t1"].bias, bias_mod=H, C=Y, colstats=colstats, stats_mod=H)
+    stats = e(4 * H)
+    K.bn_finalize(colstats, N * k1, H, bn.weight, bn.bias, bn.running_mean if training else bn.running_mean,
+                  bn.running_var, bn.num_batches_tracked if training else None, bn.eps,
+                  bn.momentum if bn.momentum is not None else 0.1, training, stats)
+    x_hat = e(sh.B, sh.L, sh.C)
+    Y2 = Y.view(N * k1, H)
+    K.unpatch_head_fwd(Y2, sh.Q, stats, pr["t2"].weight.view(H, 5), pr["t2"].bias, x_hat)
+
+    if not need_backward:
+        return emb_loss, x_hat, perplexity, idx, None
+    sv.patches, sv.xs, sv.a0s, sv.hs, sv.a1s, sv.xR_T = patches, xs, a0s, hs, a1s, xR_T
+    sv.z, sv.idx, sv.zq_T = z, idx, zq_T
+    sv.ys, sv.ya0s, sv.dhs, sv.da1s, sv.yR_T = ys, ya0s, dhs, da1s, yR_T
+    sv.Y2, sv.stats = Y2, stats
+    sv.enc_w, sv.Ws, sv.Wd0, sv.Wt1 = enc_w, Ws, Wd0, Wt1
+    return emb_loss, x_hat, perplexity, idx, sv
+
+
+def _cast(t, T):
+    out = torch.empty(t.shape, device=t.device, dtype=T)
+    K.cast(t, out)
+    return out
+
+
+def backward(m, sv, g_emb, g_xhat, slot):
+    """Accumulate parameter gradients into ``slot(param)`` (f32 tensors shaped like the parameter)."""
+    sh, T, p_drop = sv.sh, sv.T, sv.p_drop
+    H, D, N, S, R, P, k1 = sh.H, sh.D, sh.N, sh.S, sh.R, sh.P, sh.k1
+    pr = _params(m)
+    dev = g_xhat.device
+    e = lambda *s, dt=F32: torch.empty(*s, device=dev, dtype=dt)  # noqa: E731
+    g_xhat = g_xhat.contiguous()
+    bn = pr["bn"]
+
+    # ---- head + BN backward
+    gsums = torch.zeros(2 * H, device=dev, dtype=torch.float64)
+    K.unpatch_head_bwd1(sv.Y2, sh.Q, sv.stats, pr["t2"].weight.view(H, 5), g_xhat, gsums,
+                        slot(pr["t2"].weight).view(H, 5), slot(pr["t2"].bias), slot(bn.weight), slot(bn.bias))
+    gY = e(N * k1, H, dt=T)
+    K.unpatch_head_bwd2(sv.Y2, sh.Q, sv.stats, pr["t2"].weight.view(H, 5), g_xhat, gsums, sv.training, gY,
+                        slot(pr["t1"].bias))
+    gY2 = gY.view(N, k1 * H)
+    # ConvT1 weight gradient [k1*H][H] -> (H_in, H_out, k1)
+    tmp = e(k1 * H, H)
+    K.gemm(gY2, sv.yR_T, k1 * H, H, N, a_trans=True, b_trans=True, C=tmp)
+    K.weight_grad_scatter(tmp, H, H, k1, 0, 3, slot(pr["t1"].weight))
+    # ConvT1 input gradient -> grad of the decoder output, plus the dropout-masked operand for its last block
+    gy, go = e(N, H), e(N, H, dt=T)
+    last = R - 1
+    K.gemm(gY2, sv.Wt1, N, H, k1 * H, b_trans=True, C=gy, C2=go, c2_mode=3 if R > 0 else 2,
+           drop2=(p_drop, sv.dec_seed[last] if R > 0 else 0))
+
+    # ---- decoder ResBlocks (reverse)
+    dconv_in = (H, S, -1, 0)
+    wconv = (H, S, 1, 1)
+    for r in reversed(range(R)):
+        c1, c2 = pr["dec"][r]
+        W1d, W2d = e(3 * H, H, dt=T), e(3 * H, H, dt=T)
+        K.weight_relayout(c1.weight, H, H, 3, 0, 2, W1d)
+        K.weight_relayout(c2.weight, H, H, 3, 0, 2, W2d)
+        gh = e(N, H, dt=T)
+        K.gemm(go, W2d, N, H, 3 * H, b_trans=True, conv=dconv_in, pre=sv.dhs[r], C=gh)
+        tmp = e(H, 3 * H)
+        K.gemm(go, sv.da1s[r], H, 3 * H, N, a_trans=True, b_trans=True, conv=wconv, C=tmp, a_rowsum=slot(c2.bias))
+        K.weight_grad_scatter(tmp, H, H, 3, 0, 1, slot(c2.weight))
+        gyn, gon = e(N, H), e(N, H, dt=T)
+        K.gemm(gh, W1d, N, H, 3 * H, b_trans=True, conv=dconv_in, pre=sv.ys[r], resid=gy, C=gyn, C2=gon,
+               c2_mode=3 if r > 0 else 2, drop2=(p_drop, sv.dec_seed[r - 1] if r > 0 else 0))
+        tmp = e(H, 3 * H)
+        K.gemm(gh, sv.ya0s[r], H, 3 * H, N, a_trans=True, b_trans=True, conv=wconv, C=tmp, a_rowsum=slot(c1.bias))
+        K.weight_grad_scatter(tmp, H, H, 3, 0, 1, slot(c1.weight))
+        gy, go = gyn, gon
+
+    # ---- decoder 1x1 conv (weight (H, D, 1) is a contiguous [H][D] matrix)
+    K.gemm(go, sv.zq_T, H, D, N, a_trans=True, b_trans=True, C=slot(pr["dec0"].weight).view(H, D), beta=1.0,
+           a_rowsum=slot(pr["dec0"].bias))
+    gzq = e(N, D)
+    K.gemm(go, sv.Wd0, N, D, H, b_trans=True, C=gzq)
+
+    # ---- vector quantizer (straight-through + codebook/commitment loss)
+    dz = e(N, D)
+    K.vq_backward(sv.z, pr["E"], sv.idx, gzq, g_emb, m.vector_quantization.beta, dz, slot(pr["E"]))
+    dz_T = dz if T == F32 else _cast(dz, T)
+
+    # ---- SepCNNBlock
+    K.gemm(dz_T, sv.xR_T, D, H, N, a_trans=True, b_trans=True, C=slot(pr["sep"].weight).view(D, H), beta=1.0,
+           a_rowsum=slot(pr["sep"].bias))
+    gx, gxo = e(N, H), e(N, H, dt=T)
+    K.gemm(dz_T, sv.Ws, N, H, D, b_trans=True, C=gx, C2=gxo, c2_mode=3 if R > 0 else 2,
+           drop2=(p_drop, sv.enc_seed[R - 1] if R > 0 else 0))
+
+    # ---- encoder ResBlocks (reverse)
+    for r in reversed(range(R)):
+        c1, c2 = pr["enc"][r]
+        w1, w2 = sv.enc_w[r]
+        gh = e(N, H, dt=T)
+        K.gemm(gxo, w2, N, H, H, b_trans=True, pre=sv.hs[r], C=gh)
+        tmp = e(H, H)
+        K.gemm(gxo, sv.a1s[r], H, H, N, a_trans=True, b_trans=True, C=tmp, a_rowsum=slot(c2.bias))
+        K.weight_grad_scatter(tmp, H, H, 3, 1, 0, slot(c2.weight))
+        gxn, gxon = e(N, H), e(N, H, dt=T)
+        K.gemm(gh, w1, N, H, H, b_trans=True, pre=sv.xs[r], resid=gx, C=gxn, C2=gxon, c2_mode=3 if r > 0 else 2,
+               drop2=(p_drop, sv.enc_seed[r - 1] if r > 0 else 0))
+        tmp = e(H, H)
+        K.gemm(gh, sv.a0s[r], H, H, N, a_trans=True, b_trans=True, C=tmp, a_rowsum=slot(c1.bias))
+        K.weight_grad_scatter(tmp, H, H, 3, 1, 0, slot(c1.weight))
+        gx, gxo = gxn, gxon
+
+    # ---- patch embed weight/bias
+    tmp = e(H, sh.ldp)
+    K.gemm(gxo, sv.patches, H, sh.ldp, N, a_trans=True, b_trans=True, C=tmp, a_rowsum=slot(pr["pe"].bias))
+    K.weight_grad_scatter(tmp, H, 1, P, 0, 4, slot(pr["pe"].weight))
+
+
+class VQVAEPatchFunction(torch.autograd.Function):
+    """autograd boundary of the fused path: inputs (x, *params) -> (emb_loss, x_hat, perplexity)."""
+
+    @staticmethod
+    def forward(ctx, m, x, seed, *params):
+        training = m.training
+        need = torch.is_grad_enabled() or any(p.requires_grad for p in params)
+        emb, x_hat, perp, idx, sv = forward(m, x, training, need_backward=True, seed=seed)
+        ctx.m, ctx.sv, ctx.params = m, sv, params
+        ctx.mark_non_differentiable(perp)
+        m._last_indices = idx
+        return emb, x_hat, perp
+
+    @staticmethod
+    def backward(ctx, g_emb, g_xhat, g_perp):
+        m, sv = ctx.m, ctx.sv
+        sink = getattr(m, "_grad_sink", None)
+        grads = {}
+
+        def slot(p):
+            if sink is not None and p in sink:
+                return sink[p]
+            g = grads.get(p)
+            if g is None:
+                g = torch.zeros_like(p, dtype=F32)
+                grads[p] = g
+            return g
+
+        if g_emb is None:
+            g_emb = torch.zeros(1, device=g_xhat.device)
+        if g_xhat is None:
+            g_xhat = torch.zeros(sv.sh.B, sv.sh.L, sv.sh.C, device=g_emb.device)
+        backward(m, sv, g_emb.reshape(1).contiguous(), g_xhat, slot)
+        ctx.sv = None
+        return (None, None, None) + tuple(grads.get(p) for p in ctx.params)

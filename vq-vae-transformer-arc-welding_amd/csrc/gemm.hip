@@ -252,7 +252,7 @@ __global__ __launch_bounds__(NTHREADS) void gemm_kernel(GemmP P) {
   for (int j = 0; j < 4; ++j) {
     const int col = n0 + wn * 64 + j * 16 + cq;
     const bool col_ok = col < N;
-    const float bias = (p.bias && col_ok) ? p.bias[col] : 0.f;
+    const float bias = (p.bias && col_ok) ? p.bias[p.bias_mod > 0 ? col % p.bias_mod : col] : 0.f;
     float csum = 0.f, csq = 0.f;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {

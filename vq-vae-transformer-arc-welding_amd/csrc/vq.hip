@@ -128,7 +128,7 @@ __global__ __launch_bounds__(VQ_THREADS) void vq_fwd_kernel(const float* __restr
 }
 
 __global__ void vq_finalize_kernel(const float* counts, const double* sqerr, int64_t N, int K, int D, float beta,
-                                   float* out2) {
+                                   float* loss, float* perp) {
   __shared__ float part[256];
   const float invN = 1.0f / (float)N;
   float s = 0.f;
@@ -144,8 +144,8 @@ __global__ void vq_finalize_kernel(const float* counts, const double* sqerr, int
   }
   if (threadIdx.x == 0) {
     const float m = (float)(sqerr[0] / ((double)N * (double)D));
-    out2[0] = m + beta * m;
-    out2[1] = expf(-part[0]);
+    loss[0] = m + beta * m;
+    perp[0] = expf(-part[0]);
   }
 }
 
@@ -201,10 +201,10 @@ extern "C" int aw_vq_forward(const float* z, const float* E, int64_t N, int K, i
 }
 
 extern "C" int aw_vq_finalize(const float* counts, const double* sqerr, int64_t N, int K, int D, float beta,
-                              float* out2, void* stream) {
-  AW_REQUIRE(counts && sqerr && out2 && N > 0 && K > 0 && D > 0, "aw_vq_finalize: bad args");
+                              float* loss, float* perplexity, void* stream) {
+  AW_REQUIRE(counts && sqerr && loss && perplexity && N > 0 && K > 0 && D > 0, "aw_vq_finalize: bad args");
   hipLaunchKernelGGL(vq_finalize_kernel, dim3(1), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), counts, sqerr,
-                     N, K, D, beta, out2);
+                     N, K, D, beta, loss, perplexity);
   return aw::check_launch("aw_vq_finalize");
 }
 

@@ -128,12 +128,10 @@ constexpr int HEAD_MAXV = 4;  // float4 slots per lane -> H <= 1024
 
 __global__ __launch_bounds__(256) void head_fwd_kernel(const float* __restrict__ y, int64_t R, int H, int Q,
                                                        const float* __restrict__ st, const float* __restrict__ w2,
-                                                       const float* __restrict__ b2, const float* __restrict__ x,
-                                                       float* __restrict__ x_hat, double* __restrict__ sqerr) {
+                                                       const float* __restrict__ b2, float* __restrict__ x_hat) {
   const int lane = threadIdx.x & 63;
   const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  double se = 0.0;
   for (int64_t r = wave; r < R; r += nw) {
     float part[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
     for (int o4 = lane * 4; o4 < H; o4 += 256) {
@@ -158,22 +156,16 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(const float* __restrict__
       const int64_t b = r / Q;
       const int q = (int)(r - b * Q);
       const int64_t f = b * (int64_t)Q * 5 + q * 5 + lane;
-      const float xh = pj + b2[0];
-      x_hat[f] = xh;
-      const float d = xh - x[f];
-      se += (double)d * d;
+      x_hat[f] = pj + b2[0];
     }
   }
-  se = wave_sum_d(se);
-  if (lane == 0) atomicAdd(sqerr, se);
 }
 
 // ---------------------------------------------------------------- un-patch head backward
 // pass 1: per-channel sums for the BN backward + ConvT2 weight/bias grads + gamma/beta grads.
 __global__ __launch_bounds__(256) void head_bwd1_kernel(const float* __restrict__ y, int64_t R, int H, int Q,
                                                         const float* __restrict__ st, const float* __restrict__ w2,
-                                                        const float* __restrict__ x_hat, const float* __restrict__ x,
-                                                        const float* __restrict__ g_recon, double* __restrict__ gsums,
+                                                        const float* __restrict__ gx, double* __restrict__ gsums,
                                                         float* __restrict__ gw2, float* __restrict__ gb2,
                                                         float* __restrict__ ggamma, float* __restrict__ gbeta) {
   extern __shared__ float red[];  // 7*H floats: gw2 (5H), sum g (H), sum g*xn (H)
@@ -182,7 +174,6 @@ __global__ __launch_bounds__(256) void head_bwd1_kernel(const float* __restrict_
   const int lane = threadIdx.x & 63;
   const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  const float c = 2.0f / (float)(R * 5) * g_recon[0];  // numel = B*Q*5
   float accw[HEAD_MAXV][4][5];
   float accg[HEAD_MAXV][4], accgx[HEAD_MAXV][4];
 #pragma unroll
@@ -200,7 +191,7 @@ __global__ __launch_bounds__(256) void head_bwd1_kernel(const float* __restrict_
     const int64_t f0 = b * (int64_t)Q * 5 + q * 5;
     float go[5];
 #pragma unroll
-    for (int j = 0; j < 5; ++j) go[j] = c * (x_hat[f0 + j] - x[f0 + j]);
+    for (int j = 0; j < 5; ++j) go[j] = gx[f0 + j];
     if (lane == 0) gbsum += go[0] + go[1] + go[2] + go[3] + go[4];
 #pragma unroll
     for (int s = 0; s < HEAD_MAXV; ++s) {
@@ -254,8 +245,7 @@ __global__ __launch_bounds__(256) void head_bwd1_kernel(const float* __restrict_
 template <typename T>
 __global__ __launch_bounds__(256) void head_bwd2_kernel(const float* __restrict__ y, int64_t R, int H, int Q,
                                                         const float* __restrict__ st, const float* __restrict__ w2,
-                                                        const float* __restrict__ x_hat, const float* __restrict__ x,
-                                                        const float* __restrict__ g_recon,
+                                                        const float* __restrict__ gx,
                                                         const double* __restrict__ gsums, int training,
                                                         T* __restrict__ gy, float* __restrict__ dby) {
   extern __shared__ float red[];  // H
@@ -264,7 +254,6 @@ __global__ __launch_bounds__(256) void head_bwd2_kernel(const float* __restrict_
   const int lane = threadIdx.x & 63;
   const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  const float c = 2.0f / (float)(R * 5) * g_recon[0];
   const float invn = 1.0f / (float)R;
   float accd[HEAD_MAXV][4];
 #pragma unroll
@@ -277,7 +266,7 @@ __global__ __launch_bounds__(256) void head_bwd2_kernel(const float* __restrict_
     const int64_t f0 = b * (int64_t)Q * 5 + q * 5;
     float go[5];
 #pragma unroll
-    for (int j = 0; j < 5; ++j) go[j] = c * (x_hat[f0 + j] - x[f0 + j]);
+    for (int j = 0; j < 5; ++j) go[j] = gx[f0 + j];
 #pragma unroll
     for (int s = 0; s < HEAD_MAXV; ++s) {
       const int o4 = lane * 4 + 256 * s;
@@ -317,6 +306,27 @@ __global__ __launch_bounds__(256) void head_bwd2_kernel(const float* __restrict_
   }
   __syncthreads();
   for (int o = threadIdx.x; o < H; o += blockDim.x) atomicAdd(dby + o, red[o]);
+}
+
+__global__ __launch_bounds__(256) void mse_fwd_kernel(const float* __restrict__ a, const float* __restrict__ b,
+                                                      int64_t n, double* sqerr) {
+  double acc = 0.0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const float d = a[i] - b[i];
+    acc += (double)(d * d);
+  }
+  __shared__ double red[4];
+  acc = wave_sum_d(acc);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicAdd(sqerr, red[0] + red[1] + red[2] + red[3]);
+}
+
+__global__ void mse_bwd_kernel(const float* __restrict__ a, const float* __restrict__ b, int64_t n,
+                               const float* __restrict__ g, float* __restrict__ ga) {
+  const float c = 2.0f / (float)n * g[0];
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    ga[i] = c * (a[i] - b[i]);
 }
 
 __global__ void scalar_add_kernel(const float* a, const float* b, float* out) { out[0] = a[0] + b[0]; }
@@ -391,45 +401,59 @@ extern "C" int aw_bn_finalize(const double* colstats, int64_t n, int H, const fl
 }
 
 extern "C" int aw_unpatch_head_fwd(const float* y, int64_t R, int H, int Q, const float* stats, const float* w2,
-                                   const float* b2, const float* x, float* x_hat, double* sqerr, void* stream) {
-  AW_REQUIRE(y && stats && w2 && b2 && x && x_hat && sqerr && R >= 0 && Q > 0 && H > 0, "aw_unpatch_head_fwd: bad args");
+                                   const float* b2, float* x_hat, void* stream) {
+  AW_REQUIRE(y && stats && w2 && b2 && x_hat && R >= 0 && Q > 0 && H > 0, "aw_unpatch_head_fwd: bad args");
   AW_REQUIRE(H % 4 == 0 && H <= 256 * HEAD_MAXV, "aw_unpatch_head_fwd: H must be a multiple of 4 and <= 1024");
   AW_REQUIRE(R % Q == 0, "aw_unpatch_head_fwd: rows must be whole windows");
   if (R == 0) return AW_OK;
   hipLaunchKernelGGL(head_fwd_kernel, dim3(grid_for(R * 64, 256, 2048)), dim3(256), 0,
-                     reinterpret_cast<hipStream_t>(stream), y, R, H, Q, stats, w2, b2, x, x_hat, sqerr);
+                     reinterpret_cast<hipStream_t>(stream), y, R, H, Q, stats, w2, b2, x_hat);
   return aw::check_launch("aw_unpatch_head_fwd");
 }
 
 extern "C" int aw_unpatch_head_bwd1(const float* y, int64_t R, int H, int Q, const float* stats, const float* w2,
-                                    const float* x_hat, const float* x, const float* g_recon, double* gsums, float* gw2,
-                                    float* gb2, float* ggamma, float* gbeta, int training, void* stream) {
-  (void)training;
-  AW_REQUIRE(y && stats && w2 && x_hat && x && g_recon && gsums && gw2 && gb2, "aw_unpatch_head_bwd1: null pointer");
+                                    const float* g_xhat, double* gsums, float* gw2, float* gb2, float* ggamma,
+                                    float* gbeta, void* stream) {
+  AW_REQUIRE(y && stats && w2 && g_xhat && gsums && gw2 && gb2, "aw_unpatch_head_bwd1: null pointer");
   AW_REQUIRE(H % 4 == 0 && H <= 256 * HEAD_MAXV && R % Q == 0, "aw_unpatch_head_bwd1: bad shape");
   if (R == 0) return AW_OK;
   hipLaunchKernelGGL(head_bwd1_kernel, dim3(grid_for(R * 64, 256, 256)), dim3(256), 7 * H * sizeof(float),
-                     reinterpret_cast<hipStream_t>(stream), y, R, H, Q, stats, w2, x_hat, x, g_recon, gsums, gw2, gb2,
-                     ggamma, gbeta);
+                     reinterpret_cast<hipStream_t>(stream), y, R, H, Q, stats, w2, g_xhat, gsums, gw2, gb2, ggamma,
+                     gbeta);
   return aw::check_launch("aw_unpatch_head_bwd1");
 }
 
 extern "C" int aw_unpatch_head_bwd2(const float* y, int64_t R, int H, int Q, const float* stats, const float* w2,
-                                    const float* x_hat, const float* x, const float* g_recon, const double* gsums,
-                                    int training, void* g_y, int gy_dtype, float* db_y, int k1, void* stream) {
-  (void)k1;
-  AW_REQUIRE(y && stats && w2 && x_hat && x && g_recon && gsums && g_y && db_y, "aw_unpatch_head_bwd2: null pointer");
+                                    const float* g_xhat, const double* gsums, int training, void* g_y, int gy_dtype,
+                                    float* db_y, void* stream) {
+  AW_REQUIRE(y && stats && w2 && g_xhat && gsums && g_y && db_y, "aw_unpatch_head_bwd2: null pointer");
   AW_REQUIRE(H % 4 == 0 && H <= 256 * HEAD_MAXV && R % Q == 0, "aw_unpatch_head_bwd2: bad shape");
   if (R == 0) return AW_OK;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   dim3 grid(grid_for(R * 64, 256, 1024));
   if (gy_dtype == AW_BF16)
-    hipLaunchKernelGGL(head_bwd2_kernel<bf16>, grid, dim3(256), H * sizeof(float), s, y, R, H, Q, stats, w2, x_hat, x,
-                       g_recon, gsums, training, (bf16*)g_y, db_y);
+    hipLaunchKernelGGL(head_bwd2_kernel<bf16>, grid, dim3(256), H * sizeof(float), s, y, R, H, Q, stats, w2, g_xhat,
+                       gsums, training, (bf16*)g_y, db_y);
   else
-    hipLaunchKernelGGL(head_bwd2_kernel<float>, grid, dim3(256), H * sizeof(float), s, y, R, H, Q, stats, w2, x_hat, x,
-                       g_recon, gsums, training, (float*)g_y, db_y);
+    hipLaunchKernelGGL(head_bwd2_kernel<float>, grid, dim3(256), H * sizeof(float), s, y, R, H, Q, stats, w2, g_xhat,
+                       gsums, training, (float*)g_y, db_y);
   return aw::check_launch("aw_unpatch_head_bwd2");
+}
+
+extern "C" int aw_mse_fwd(const float* a, const float* b, int64_t n, double* sqerr, void* stream) {
+  AW_REQUIRE(a && b && sqerr && n >= 0, "aw_mse_fwd: bad args");
+  if (n == 0) return AW_OK;
+  hipLaunchKernelGGL(mse_fwd_kernel, dim3(grid_for(n, 256, 1024)), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                     a, b, n, sqerr);
+  return aw::check_launch("aw_mse_fwd");
+}
+
+extern "C" int aw_mse_bwd(const float* a, const float* b, int64_t n, const float* g, float* ga, void* stream) {
+  AW_REQUIRE(a && b && g && ga && n >= 0, "aw_mse_bwd: bad args");
+  if (n == 0) return AW_OK;
+  hipLaunchKernelGGL(mse_bwd_kernel, dim3(grid_for(n, 256, 4096)), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                     a, b, n, g, ga);
+  return aw::check_launch("aw_mse_bwd");
 }
 
 extern "C" int aw_scalar_add(const float* a, const float* b, float* out, void* stream) {
