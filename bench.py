@@ -1,0 +1,172 @@
+"""Benchmark: welding windows/sec of the VQ-VAE-Patch reconstruction TRAIN step (BASELINE.json configs[1]:
+batch 1024 windows of 200x2 per GPU, codebook 512x64, H=512, 8 ResBlocks, patch 25, dropout 0.1, bf16 MFMA
+operands with fp32 accumulation / fp32 master weights).
+
+One step = forward + backward of loss = mse(x_hat, x) + vq_loss, global-norm clip 0.7 and the RAdam update
+(train_reconstruction_embedding.py:190-199) over one batch of synthetic standardised windows that is resident
+in HBM before the timed region.  Multi-GPU: one process per GPU (torch.distributed.run), RCCL all-reduce of the
+flat gradient buffer every step, per-rank batch fixed (weak scaling).
+
+Prints ONE JSON line (rank 0) with the roofline of the dominant kernel (the MFMA GEMM family, timed live with
+HIP events on its launch stream over the timed region) and a CPU baseline (the oracle port on the host cores,
+bounded sample, rank 0 at N=1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "vq-vae-transformer-arc-welding_amd"))
+sys.path.insert(0, REPO)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "welding windows/sec (train) VQ-VAE+8-blk Transformer at 1/2/4/8 MI355X"
+BF16_PEAK_TFLOPS = 2500.0     # MI355X dense bf16 MFMA (MI355X_MICROARCH.md: ~2.5 PF dense)
+HBM_PEAK_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=1024, help="windows per GPU")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--no-profile", action="store_true", help="skip the live per-GEMM event timing")
+    return ap.parse_args()
+
+
+def build_model(dev):
+    from model.vq_vae_patch_embedd import VQVAEPatch
+    torch.manual_seed(1)
+    m = VQVAEPatch(hidden_dim=512, input_dim=2, num_embeddings=512, embedding_dim=64, n_resblocks=8,
+                   learning_rate=1e-3, dropout_p=0.1, patch_size=25, seq_len=200, batch_norm=False)
+    return m.to(dev).train()
+
+
+def cpu_baseline(seconds):
+    """Oracle port (oracle/vqvae.py, torch CPU fp32, all host threads) on a bounded sample of the same workload:
+    full-size model, B=32 windows per step, fwd+bwd+RAdam; windows/s."""
+    import numpy as np
+    from oracle import gen
+    from oracle import optim as oo
+    from oracle import vqvae as ov
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    cfg = ov.VQVAEConfig(dropout_p=0.0)
+    sd = ov.det_state_dict(cfg, 1)
+    names = [k for k in sd if not (k.endswith("running_mean") or k.endswith("running_var") or
+                                   k.endswith("num_batches_tracked"))]
+    st = oo.RAdamState([sd[k].shape for k in names])
+    B = 32
+    x = gen.windows(0, B)
+    steps, t0 = 0, None
+    while True:
+        out, grads, state = ov.vqvae_train_step_grads(sd, x, cfg)
+        gl = [grads[k].copy() for k in names]
+        oo.clip_grad_norm(gl, 0.7)
+        ps = [sd[k] for k in names]
+        oo.radam_step(ps, gl, st, 1e-3, (0.9, 0.999), 1e-8, [0.0] * len(ps))
+        if t0 is None:            # first step is warm-up
+            t0 = time.time()
+            continue
+        steps += 1
+        if time.time() - t0 > seconds:
+            break
+    el = time.time() - t0
+    return {"value": round(B * steps / el, 2), "unit": "windows/s", "cores": threads, "kind": "port",
+            "sample": f"oracle/vqvae.py full-size VQ-VAE (H512 R8 K512xD64) fp32 train step, B={B} windows, "
+                      f"{steps} timed steps ({el:.1f} s) after 1 warm-up, torch CPU {threads} threads"}
+
+
+def main():
+    args = parse()
+    distributed = int(os.environ.get("WORLD_SIZE", "1")) > 1
+    if distributed:
+        dist.init_process_group("nccl")
+        rank, world = dist.get_rank(), dist.get_world_size()
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+    else:
+        rank, world, local = 0, 1, 0
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    torch.set_float32_matmul_precision("medium")    # as train_reconstruction_embedding.py:253 -> bf16 MFMA
+
+    from arcweld import kernels
+    from arcweld.trainer import Trainer
+
+    model = build_model(dev)
+    trainer = Trainer(gradient_clip_val=0.7)
+    trainer.setup_optimizer(model)
+    scale = 1.0 / world
+    gen_ = torch.Generator(device=dev)
+    gen_.manual_seed(1000 + rank)
+    batches = [torch.randn(args.batch, 200, 2, device=dev, generator=gen_) for _ in range(4)]
+
+    def step(i):
+        trainer.micro_step(model, batches[i % len(batches)], i, scale)
+        trainer.optimizer_step(model)
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    if distributed:
+        dist.barrier()
+    torch.cuda.synchronize()
+    if not args.no_profile:
+        kernels.PROFILE = []
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(i)
+    torch.cuda.synchronize()
+    if distributed:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    prof = kernels.PROFILE
+    kernels.PROFILE = None
+    t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+    if distributed:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+    value = world * args.batch * args.steps / elapsed
+
+    roofline = None
+    if prof:
+        ms = sum(e0.elapsed_time(e1) for e0, e1, _ in prof)
+        flops = sum(f for _, _, f in prof)
+        n = len(prof)
+        achieved = flops / (ms * 1e-3) / 1e12
+        roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
+                    "frac": round(achieved / BF16_PEAK_TFLOPS, 4), "traffic": None,
+                    "kernel": "gemm_kernel<bf16> (aw_gemm)", "launches_per_step": n // args.steps,
+                    "avg_launch_us": round(ms * 1e3 / n, 2), "avg_algorithmic_gflop_per_launch": round(flops / n / 1e9, 4),
+                    "gemm_share_of_step": round(ms / (elapsed * 1e3), 4)}
+
+    if rank == 0:
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            cpu = cpu_baseline(args.cpu_seconds)
+        line = {"metric": METRIC, "value": round(value, 2), "unit": "windows/s", "n_gpus": world,
+                "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed * 1e3 / args.steps, 3),
+                "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+                "data": "synthetic N(0,1) standardised 200x2 welding windows, random-init weights",
+                "config": {"workload": "VQ-VAE-Patch reconstruction train step (configs[1])",
+                           "global_batch": world * args.batch, "per_gpu_batch": args.batch, "seq_len": 200,
+                           "codebook": "512x64", "hidden": 512, "n_resblocks": 8, "patch": 25,
+                           "parallelism": f"dp{world}", "clip": 0.7, "optimizer": "RAdam(lr 1e-3)"},
+                "roofline": roofline, "cpu_baseline": cpu}
+        print(json.dumps(line), flush=True)
+    if distributed:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -25,9 +25,25 @@ def _ld(t):
     return t.stride(0)
 
 
+# Optional live profiler: when set to a list, every gemm() appends (start_event, end_event, algorithmic_flops)
+# recorded on the launch stream (bench.py uses it for the roofline of the GEMM kernel over the timed region).
+PROFILE = None
+
+
+def _algorithmic_flops(M, N, Kd, conv, flops):
+    """2*M*N*K counting only taps that touch real input: the implicit k=3 conv loses one tap at each window
+    edge (K_eff = cin*(3 - 2/seg)); callers with zero-padded operands (patch embed) pass `flops` explicitly."""
+    if flops is not None:
+        return float(flops)
+    if conv is not None:
+        seg = conv[1]
+        return 2.0 * M * N * (Kd / 3.0) * (3.0 - 2.0 / seg)
+    return 2.0 * M * N * Kd
+
+
 def gemm(A, B, M, N, K, *, a_trans=False, b_trans=False, conv=None, alpha=1.0, beta=0.0, bias=None,
          act=AW_ACT_GELU_ERF, pre=None, resid=None, drop=(0.0, 0), C=None, C2=None, c2_mode=0, drop2=(0.0, 0),
-         colstats=None, stats_mod=0, a_rowsum=None, bias_mod=0, stream=None):
+         colstats=None, stats_mod=0, a_rowsum=None, bias_mod=0, stream=None, flops=None):
     """C = epilogue(alpha * op(A) @ op(B)); see aw_gemm in include/arcweld_amd.h for the exact semantics.
 
     conv = (cin, seg, dir, operand) selects the implicit k=3 convolution form."""
@@ -58,7 +74,15 @@ def gemm(A, B, M, N, K, *, a_trans=False, b_trans=False, conv=None, alpha=1.0, b
         a.colstats, a.stats_mod = ptr(colstats), int(stats_mod)
     a.a_rowsum = ptr(a_rowsum)
     a.bias_mod = int(bias_mod)
-    call("aw_gemm", ctypes.byref(a), stream_ptr(stream))
+    if PROFILE is None:
+        call("aw_gemm", ctypes.byref(a), stream_ptr(stream))
+        return C
+    s = stream if stream is not None else torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(s)
+    call("aw_gemm", ctypes.byref(a), s.cuda_stream)
+    e1.record(s)
+    PROFILE.append((e0, e1, _algorithmic_flops(M, N, K, conv, flops)))
     return C
 
 

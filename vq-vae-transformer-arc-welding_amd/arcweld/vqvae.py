@@ -112,7 +112,7 @@ def forward(m, x, training: bool, need_backward: bool, dtype=None, seed: int = 0
     patches = e(N, sh.ldp, dt=T)
     K.patchify(x, P, patches)
     x0, a0 = e(N, H), e(N, H, dt=T)
-    K.gemm(patches, Wp, N, H, sh.ldp, bias=pr["pe"].bias, C=x0, C2=a0, c2_mode=1)
+    K.gemm(patches, Wp, N, H, sh.ldp, bias=pr["pe"].bias, C=x0, C2=a0, c2_mode=1, flops=2 * N * H * P)
 
     # ---- encoder ResBlocks (per-token: centre taps)
     xs, a0s, hs, a1s = [x0], [a0], [], []
@@ -284,7 +284,8 @@ def backward(m, sv, g_emb, g_xhat, slot):
 
     # ---- patch embed weight/bias
     tmp = e(H, sh.ldp)
-    K.gemm(gxo, sv.patches, H, sh.ldp, N, a_trans=True, b_trans=True, C=tmp, a_rowsum=slot(pr["pe"].bias))
+    K.gemm(gxo, sv.patches, H, sh.ldp, N, a_trans=True, b_trans=True, C=tmp, a_rowsum=slot(pr["pe"].bias),
+           flops=2 * N * H * P)
     K.weight_grad_scatter(tmp, H, 1, P, 0, 4, slot(pr["pe"].weight))
 
 

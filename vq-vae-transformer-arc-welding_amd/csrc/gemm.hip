@@ -1,142 +1,170 @@
 // MFMA GEMM family for gfx950 (CDNA4): one kernel body for every dense contraction of the hot path.
 //
-// Tile 128x128 per 256-thread workgroup (4 waves as 2x2, each wave 64x64 = 4x4 fragments of 16x16).
-// K is staged through LDS 64 bytes per row per step (32 bf16 or 16 f32), register-staged double buffer,
-// one barrier per K step.  Operands are re-laid into a K-contiguous LDS image whatever their global layout,
-// so one fragment path serves forward (A.W^T), input-gradient (dY.W) and weight-gradient (dY^T.X) forms and
-// the implicit k=3 convolution (row-shifted A or B loads, zero outside each window).
+// Tile 128x128 per 256-thread workgroup (4 waves as 2x2, each wave 64x64 = 4x4 fragments of 16x16),
+// K staged through LDS 64 bytes per row per step (32 bf16 / 16 f32), register-staged double buffer, one barrier
+// per K step.  Operand layouts are compile-time template parameters:
+//   K-contiguous operand ([rows][K], e.g. activations in forward, weights [out][in]) -> LDS image [row][k],
+//       fragments by one ds_read_b128;
+//   row-contiguous operand ([K][rows], e.g. activations as the weight-gradient reduction operand) -> LDS image
+//       [k][row] written with one ds_write_b128 per staged chunk; bf16 fragments come from two
+//       ds_read_b64_tr_b16 hardware-transposed reads (gfx950), f32 fragments from four ds_read_b32.
+// Implicit k=3/pad=1 convolution (decoder ResBlocks) = row-shifted loads with a per-window zero mask.
 //   bf16: v_mfma_f32_16x16x32_bf16 (fp32 accumulate)      f32: v_mfma_f32_16x16x4_f32 (exact f32)
-// Fused epilogue: bias, act' (GELU backward), dropout (counter-based mask), residual add, beta*C,
-// second output (act / copy / dropout-masked copy), BatchNorm column statistics, and a fused A-row-sum
-// (bias gradients in weight-gradient GEMMs).
+// Split-K (grid.y) with fp32 atomics serves the weight-gradient shapes (M x N = 512 x 512 .. 2560 x 512,
+// K = tokens), whose tile count alone would leave most of the 256 CUs idle.
+// Fused epilogue (non-split): bias, act' (GELU backward), dropout (counter-based mask), residual add,
+// beta*C, second output (act / copy / dropout-masked copy), BatchNorm column statistics; and a fused A-row-sum
+// (bias gradients) from the staged A tiles in every mode.
 #include "common.h"
 
 namespace {
 
 constexpr int BM = 128, BN = 128, NTHREADS = 256;
-constexpr int ROWB = 64;          // bytes of K per LDS row per step
-constexpr int PITCHB = ROWB + 16; // padded LDS row pitch in bytes
-
-struct GemmP {
-  aw_gemm_args a;
-  int tiles_m, tiles_n, nblocks;
-};
+constexpr int ROWB = 64;                 // bytes of K per operand row per step
+constexpr int KPB = ROWB + 16;           // pitch of the [row][k] image (bytes)
+constexpr int STAGE_OP = 10240;          // bytes reserved per operand per stage (>= 128*KPB, >= BK*MPB)
+constexpr int CPITCH = BN + 4;           // f32 pitch of the epilogue tile
+constexpr int SMEM = (BM * CPITCH * 4 > 4 * STAGE_OP) ? BM * CPITCH * 4 : 4 * STAGE_OP;
 
 template <typename T> struct TT;
 template <> struct TT<bf16> {
-  static constexpr int EPC = 8;                 // elements per 16-byte chunk
-  static constexpr int BK = ROWB / 2;           // 32
+  static constexpr int EPC = 8, BK = 32;
+  static constexpr int MPB = 128 * 2 + 16;   // pitch of the [k][row] image: 272 B
 };
 template <> struct TT<float> {
-  static constexpr int EPC = 4;
-  static constexpr int BK = ROWB / 4;           // 16
+  static constexpr int EPC = 4, BK = 16;
+  static constexpr int MPB = 128 * 4 + 16;   // 528 B
+};
+static_assert(128 * KPB <= STAGE_OP && 32 * TT<bf16>::MPB <= STAGE_OP && 16 * TT<float>::MPB <= STAGE_OP, "LDS");
+
+struct GemmP {
+  aw_gemm_args a;
+  int tiles_n, nblocks, splits, ksplit;
 };
 
-// One 16-byte chunk of an operand tile, loaded to registers (register staging).
-struct Chunk {
-  uint4 v;
+enum { CONV_NONE = 0, CONV_ROWSHIFT = 1, CONV_KSHIFT = 2 };
+
+// ---------------------------------------------------------------- operand staging (global -> regs -> LDS)
+template <typename T, bool TR, int CONV, bool RAGGED>
+struct Stager {
+  static constexpr int EPC = TT<T>::EPC, BK = TT<T>::BK, MPB = TT<T>::MPB;
+  static constexpr int CPR = 128 / EPC;   // chunks per k-row of a row-contiguous tile
+  const T* base;
+  int64_t ld;
+  int rows_total, row0, kend, cin, seg, dir;
+  uint4 v[2];
+
+  __device__ __forceinline__ void load(int k0, int tid) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int c = tid + i * NTHREADS;
+      uint4 out = make_uint4(0, 0, 0, 0);
+      if constexpr (!TR) {
+        const int row = row0 + (c >> 2);
+        const int k = k0 + (c & 3) * EPC;
+        bool ok = row < rows_total && k < kend;
+        int64_t src = row;
+        int kk = k;
+        if constexpr (CONV == CONV_ROWSHIFT) {
+          const int j = k / cin;
+          kk = k - j * cin;
+          const int s = dir * (j - 1);
+          const int t = row % seg;
+          ok = ok && (t + s >= 0) && (t + s < seg);
+          src = row + s;
+        }
+        if (ok) {
+          const T* p = base + src * ld + kk;
+          if constexpr (RAGGED) {
+            if (k + EPC > kend) {
+              T tmp[EPC];
+#pragma unroll
+              for (int e = 0; e < EPC; ++e) tmp[e] = (k + e < kend) ? p[e] : from_f32<T>(0.f);
+              memcpy(&out, tmp, 16);
+            } else {
+              out = *reinterpret_cast<const uint4*>(p);
+            }
+          } else {
+            out = *reinterpret_cast<const uint4*>(p);
+          }
+        }
+      } else {
+        const int k = k0 + c / CPR;
+        const int m = row0 + (c % CPR) * EPC;
+        bool ok = k < kend && m < rows_total;
+        int64_t srck = k;
+        int mm = m;
+        if constexpr (CONV == CONV_KSHIFT) {
+          const int j = m / cin;
+          mm = m - j * cin;
+          const int s = j - 1;
+          const int t = k % seg;
+          ok = ok && (t + s >= 0) && (t + s < seg);
+          srck = k + s;
+        }
+        if (ok) {
+          const T* p = base + srck * ld + mm;
+          if constexpr (RAGGED) {
+            if (m + EPC > rows_total) {
+              T tmp[EPC];
+#pragma unroll
+              for (int e = 0; e < EPC; ++e) tmp[e] = (m + e < rows_total) ? p[e] : from_f32<T>(0.f);
+              memcpy(&out, tmp, 16);
+            } else {
+              out = *reinterpret_cast<const uint4*>(p);
+            }
+          } else {
+            out = *reinterpret_cast<const uint4*>(p);
+          }
+        }
+      }
+      v[i] = out;
+    }
+  }
+
+  __device__ __forceinline__ void store(char* lds, int tid) const {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int c = tid + i * NTHREADS;
+      if constexpr (!TR)
+        *reinterpret_cast<uint4*>(lds + (c >> 2) * KPB + (c & 3) * 16) = v[i];
+      else
+        *reinterpret_cast<uint4*>(lds + (c / CPR) * MPB + (c % CPR) * 16) = v[i];
+    }
+  }
 };
 
-// Load a 16-byte chunk of row-contiguous data at (row, k..k+EPC) -- row-major along K ("k-contiguous").
-// Returns zero for out-of-range rows / k and for window-masked implicit-conv rows.
-template <typename T>
-__device__ __forceinline__ uint4 load_kcontig(const T* base, int64_t ld, int row, int rows_total, int k, int K,
-                                              int conv_cin, int conv_seg, int conv_dir) {
-  constexpr int EPC = TT<T>::EPC;
-  uint4 out = make_uint4(0, 0, 0, 0);
-  if (row >= rows_total || k >= K) return out;
-  int64_t src_row = row;
-  int kk = k;
-  if (conv_cin > 0) {
-    int j = k / conv_cin;
-    kk = k - j * conv_cin;
-    int s = conv_dir * (j - 1);
-    int t = row % conv_seg;
-    if (t + s < 0 || t + s >= conv_seg) return out;
-    src_row = row + s;
-  }
-  const T* p = base + src_row * ld + kk;
-  if (k + EPC <= K) {
-    out = *reinterpret_cast<const uint4*>(p);
+// ---------------------------------------------------------------- fragments
+typedef short v4i16 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
+
+// Fragment of the 16 rows [rbase, rbase+16) x this lane's K slice, as 16 bytes.
+template <typename T, bool TR>
+__device__ __forceinline__ uint4 frag(const char* lds, int rbase, int lane) {
+  if constexpr (!TR) {
+    return *reinterpret_cast<const uint4*>(lds + (rbase + (lane & 15)) * KPB + (lane >> 4) * 16);
+  } else if constexpr (sizeof(T) == 2) {
+    // two 4(k) x 16(row) transposed reads: lane 4q+p addresses k-row q, rows 4p..4p+3 of the block;
+    // lane i receives row i, k-rows 0..3
+    constexpr int MPB = TT<T>::MPB;
+    const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+    const char* b0 = lds + (8 * g + q) * MPB + (rbase + 4 * p) * 2;
+    const v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(uintptr_t)(b0));
+    const v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(uintptr_t)(b0 + 4 * MPB));
+    uint4 out;
+    memcpy(&out, &lo, 8);
+    memcpy(reinterpret_cast<char*>(&out) + 8, &hi, 8);
+    return out;
   } else {
-    T tmp[EPC];
+    constexpr int MPB = TT<T>::MPB;
+    const int g = lane >> 4, i = lane & 15;
+    const char* b0 = lds + 4 * g * MPB + (rbase + i) * 4;
+    float f[4];
 #pragma unroll
-    for (int e = 0; e < EPC; ++e) tmp[e] = (k + e < K) ? p[e] : from_f32<T>(0.f);
-    memcpy(&out, tmp, 16);
-  }
-  return out;
-}
-
-// Load a 16-byte chunk of "m-contiguous" data: elements (k, m..m+EPC) of storage [k][m] (ld along k).
-// Optional implicit-conv shift along k (rows) with the tap taken from the column index (B operand, wgrad).
-template <typename T>
-__device__ __forceinline__ uint4 load_mcontig(const T* base, int64_t ld, int k, int K, int m, int Mtot,
-                                              int conv_cin, int conv_seg) {
-  constexpr int EPC = TT<T>::EPC;
-  uint4 out = make_uint4(0, 0, 0, 0);
-  if (k >= K || m >= Mtot) return out;
-  int64_t src_k = k;
-  int mm = m;
-  if (conv_cin > 0) {
-    int j = m / conv_cin;
-    mm = m - j * conv_cin;
-    int s = j - 1;
-    int t = k % conv_seg;
-    if (t + s < 0 || t + s >= conv_seg) return out;
-    src_k = k + s;
-  }
-  const T* p = base + src_k * ld + mm;
-  if (m + EPC <= Mtot) {
-    out = *reinterpret_cast<const uint4*>(p);
-  } else {
-    T tmp[EPC];
-#pragma unroll
-    for (int e = 0; e < EPC; ++e) tmp[e] = (m + e < Mtot) ? p[e] : from_f32<T>(0.f);
-    memcpy(&out, tmp, 16);
-  }
-  return out;
-}
-
-// Stage one operand tile (128 rows x BK) into registers: 2 chunks per thread.
-template <typename T>
-__device__ __forceinline__ void stage_load(Chunk (&c)[2], const T* base, int64_t ld, int trans, int row0,
-                                           int rows_total, int k0, int K, int conv_cin, int conv_seg,
-                                           int conv_dir, int tid) {
-  constexpr int EPC = TT<T>::EPC;
-  constexpr int BK = TT<T>::BK;
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    int ci = tid + i * NTHREADS;
-    if (!trans) {  // k-contiguous: 4 chunks per row
-      int r = ci >> 2, kc = ci & 3;
-      c[i].v = load_kcontig<T>(base, ld, row0 + r, rows_total, k0 + kc * EPC, K, conv_cin, conv_seg, conv_dir);
-    } else {       // row-contiguous: 128/EPC chunks per k-row
-      constexpr int CPR = 128 / EPC;
-      int kr = ci / CPR, mc = ci % CPR;
-      c[i].v = load_mcontig<T>(base, ld, k0 + kr, K, row0 + mc * EPC, rows_total, conv_cin, conv_seg);
-    }
-  }
-  (void)BK;
-}
-
-template <typename T>
-__device__ __forceinline__ void stage_store(const Chunk (&c)[2], char* lds, int trans, int tid) {
-  constexpr int EPC = TT<T>::EPC;
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    int ci = tid + i * NTHREADS;
-    if (!trans) {
-      int r = ci >> 2, kc = ci & 3;
-      *reinterpret_cast<uint4*>(lds + r * PITCHB + kc * 16) = c[i].v;
-    } else {
-      constexpr int CPR = 128 / EPC;
-      int kr = ci / CPR, mc = ci % CPR;
-      T tmp[EPC];
-      memcpy(tmp, &c[i].v, 16);
-#pragma unroll
-      for (int e = 0; e < EPC; ++e)
-        *reinterpret_cast<T*>(lds + (mc * EPC + e) * PITCHB + kr * (int)sizeof(T)) = tmp[e];
-    }
+    for (int s = 0; s < 4; ++s) f[s] = *reinterpret_cast<const float*>(b0 + s * MPB);
+    uint4 out;
+    memcpy(&out, f, 16);
+    return out;
   }
 }
 
@@ -166,19 +194,35 @@ __device__ __forceinline__ float act_bwd(int act, float x) {
 
 // Bijective XCD-aware remap: consecutive logical tiles land on the same XCD (blocks b and b+8 share one).
 __device__ __forceinline__ int xcd_remap(int bid, int nblocks) {
-  int q = nblocks / 8, r = nblocks % 8;
-  int xcd = bid % 8, slot = bid / 8;
+  const int q = nblocks / 8, r = nblocks % 8;
+  const int xcd = bid % 8, slot = bid / 8;
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + slot;
 }
 
-template <typename T>
-__global__ __launch_bounds__(NTHREADS) void gemm_kernel(GemmP P) {
+// sum over this thread's half of the staged A K-slice (fused bias gradient of weight-gradient GEMMs)
+template <typename T, bool TR>
+__device__ __forceinline__ float a_row_partial(const char* lds, int tid) {
   constexpr int BK = TT<T>::BK;
-  constexpr int EPC = TT<T>::EPC;
+  const int r = tid >> 1, h = tid & 1;
+  float s = 0.f;
+  if constexpr (!TR) {
+    const T* rowp = reinterpret_cast<const T*>(lds + r * KPB) + h * (BK / 2);
+#pragma unroll
+    for (int e = 0; e < BK / 2; ++e) s += to_f32<T>(rowp[e]);
+  } else {
+    constexpr int MPB = TT<T>::MPB;
+#pragma unroll
+    for (int e = 0; e < BK / 2; ++e)
+      s += to_f32<T>(*reinterpret_cast<const T*>(lds + (h * (BK / 2) + e) * MPB + r * (int)sizeof(T)));
+  }
+  return s;
+}
+
+template <typename T, bool ATR, bool BTR, int ACONV, int BCONV, bool RAGGED>
+__global__ __launch_bounds__(NTHREADS, 2) void gemm_kernel(GemmP P) {
+  constexpr int BK = TT<T>::BK;
   const aw_gemm_args& p = P.a;
-  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * 128 * PITCHB];
-  // stage buffer b: A image at smem + b*STAGE, B image right after it
-  constexpr int STAGE = 2 * 128 * PITCHB;
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wid = tid >> 6;
@@ -186,12 +230,13 @@ __global__ __launch_bounds__(NTHREADS) void gemm_kernel(GemmP P) {
   const int tile = xcd_remap(blockIdx.x, P.nblocks);
   const int tm = tile / P.tiles_n, tn = tile % P.tiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
-  const int M = p.M, N = p.N, K = p.K;
+  const int M = p.M, N = p.N;
+  const int kbeg = blockIdx.y * P.ksplit;
+  const int kend = min(p.K, kbeg + P.ksplit);
 
-  const T* Ab = reinterpret_cast<const T*>(p.A);
-  const T* Bb = reinterpret_cast<const T*>(p.B);
-  const int a_conv = (p.conv_cin > 0 && p.conv_operand == 0) ? p.conv_cin : 0;
-  const int b_conv = (p.conv_cin > 0 && p.conv_operand == 1) ? p.conv_cin : 0;
+  Stager<T, ATR, ACONV, RAGGED> sa{reinterpret_cast<const T*>(p.A), p.lda, M, m0, kend, p.conv_cin, p.conv_seg,
+                                   p.conv_dir, {}};
+  Stager<T, BTR, BCONV, RAGGED> sb{reinterpret_cast<const T*>(p.B), p.ldb, N, n0, kend, p.conv_cin, p.conv_seg, 1, {}};
   const bool do_rowsum = p.a_rowsum != nullptr && tn == 0;
 
   f32x4 acc[4][4];
@@ -201,93 +246,135 @@ __global__ __launch_bounds__(NTHREADS) void gemm_kernel(GemmP P) {
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   float rowsum = 0.f;
 
-  const int nk = (K + BK - 1) / BK;
-  Chunk ca[2], cb[2];
-  stage_load<T>(ca, Ab, p.lda, p.a_trans, m0, M, 0, K, a_conv, p.conv_seg, p.conv_dir, tid);
-  stage_load<T>(cb, Bb, p.ldb, p.b_trans, n0, N, 0, K, b_conv, p.conv_seg, 1, tid);
-  stage_store<T>(ca, smem, p.a_trans, tid);
-  stage_store<T>(cb, smem + 128 * PITCHB, p.b_trans, tid);
+  const int nk = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
+  sa.load(kbeg, tid);
+  sb.load(kbeg, tid);
+  sa.store(smem, tid);
+  sb.store(smem + STAGE_OP, tid);
   __syncthreads();
 
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
     if (kt + 1 < nk) {
-      stage_load<T>(ca, Ab, p.lda, p.a_trans, m0, M, (kt + 1) * BK, K, a_conv, p.conv_seg, p.conv_dir, tid);
-      stage_load<T>(cb, Bb, p.ldb, p.b_trans, n0, N, (kt + 1) * BK, K, b_conv, p.conv_seg, 1, tid);
+      sa.load(kbeg + (kt + 1) * BK, tid);
+      sb.load(kbeg + (kt + 1) * BK, tid);
     }
-    const char* a_l = smem + cur * STAGE;
-    const char* b_l = a_l + 128 * PITCHB;
+    const char* a_l = smem + cur * 2 * STAGE_OP;
+    const char* b_l = a_l + STAGE_OP;
     uint4 af[4], bfr[4];
 #pragma unroll
     for (int f = 0; f < 4; ++f) {
-      af[f] = *reinterpret_cast<const uint4*>(a_l + (wm * 64 + f * 16 + (lane & 15)) * PITCHB + (lane >> 4) * 16);
-      bfr[f] = *reinterpret_cast<const uint4*>(b_l + (wn * 64 + f * 16 + (lane & 15)) * PITCHB + (lane >> 4) * 16);
+      af[f] = frag<T, ATR>(a_l, wm * 64 + f * 16, lane);
+      bfr[f] = frag<T, BTR>(b_l, wn * 64 + f * 16, lane);
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) Mfma<T>::run(acc[i][j], af[i], bfr[j]);
-    if (do_rowsum) {  // row r = tid>>1 sums half a K step
-      const T* rowp = reinterpret_cast<const T*>(a_l + (tid >> 1) * PITCHB) + (tid & 1) * (BK / 2);
-#pragma unroll
-      for (int e = 0; e < BK / 2; ++e) rowsum += to_f32<T>(rowp[e]);
-    }
+    if (do_rowsum) rowsum += a_row_partial<T, ATR>(a_l, tid);
     if (kt + 1 < nk) {
-      stage_store<T>(ca, smem + (cur ^ 1) * STAGE, p.a_trans, tid);
-      stage_store<T>(cb, smem + (cur ^ 1) * STAGE + 128 * PITCHB, p.b_trans, tid);
+      char* nxt = smem + (cur ^ 1) * 2 * STAGE_OP;
+      sa.store(nxt, tid);
+      sb.store(nxt + STAGE_OP, tid);
     }
     __syncthreads();
   }
-  (void)EPC;
 
   if (do_rowsum) {
     rowsum += __shfl_xor(rowsum, 1, 64);
-    int r = m0 + (tid >> 1);
+    const int r = m0 + (tid >> 1);
     if ((tid & 1) == 0 && r < M) atomicAdd(p.a_rowsum + r, rowsum);
   }
 
   // ---------------------------------------------------------------- epilogue
-  const int cq = lane & 15, rq = (lane >> 4) * 4;
+  // 1) accumulators -> LDS tile (static register indexing), 2) one element per thread per step with
+  //    consecutive threads on consecutive columns: every wave instruction touches 256 contiguous bytes.
+  float* Cs = reinterpret_cast<float*>(smem);
+  {
+    const int cq = lane & 15, rq = (lane >> 4) * 4;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int col = n0 + wn * 64 + j * 16 + cq;
-    const bool col_ok = col < N;
-    const float bias = (p.bias && col_ok) ? p.bias[p.bias_mod > 0 ? col % p.bias_mod : col] : 0.f;
-    float csum = 0.f, csq = 0.f;
+    for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+      for (int j = 0; j < 4; ++j)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = m0 + wm * 64 + i * 16 + rq + r;
-        if (!col_ok || row >= M) continue;
-        float v = p.alpha * acc[i][j][r] + bias;
-        if (p.pre) v *= act_bwd(p.act, p.pre[(int64_t)row * p.ld_pre + col]);
-        if (p.drop_p > 0.f) v *= aw_dropout_scale(p.drop_seed, (uint64_t)row * N + col, p.drop_p);
-        if (p.resid) v += p.resid[(int64_t)row * p.ld_resid + col];
-        if (p.beta != 0.f) v += p.beta * reinterpret_cast<const float*>(p.C)[(int64_t)row * p.ldc + col];
-        if (p.C) store_from_f32(p.C, p.c_dtype, (int64_t)row * p.ldc + col, v);
-        if (p.c2_mode) {
-          float w = v;
-          if (p.c2_mode == 1) w = act_fwd(p.act, v);
-          else if (p.c2_mode == 3) w = v * aw_dropout_scale(p.drop2_seed, (uint64_t)row * N + col, p.drop2_p);
-          store_from_f32(p.C2, p.c2_dtype, (int64_t)row * p.ldc2 + col, w);
-        }
-        csum += v;
-        csq += v * v;
+        for (int r = 0; r < 4; ++r)
+          Cs[(wm * 64 + i * 16 + rq + r) * CPITCH + wn * 64 + j * 16 + cq] = acc[i][j][r];
+  }
+  __syncthreads();
+  const int lc = tid & 127;
+  const int col = n0 + lc;
+  const bool col_ok = col < N;
+  const int rows_here = min(BM, M - m0);
+  if (P.splits > 1) {  // split-K: plain accumulate into f32 C
+    if (!col_ok) return;
+    float* C = reinterpret_cast<float*>(p.C);
+    for (int lr = tid >> 7; lr < rows_here; lr += 2)
+      atomicAdd(C + (int64_t)(m0 + lr) * p.ldc + col, p.alpha * Cs[lr * CPITCH + lc]);
+    return;
+  }
+  const float bias = (p.bias && col_ok) ? p.bias[p.bias_mod > 0 ? col % p.bias_mod : col] : 0.f;
+  float csum = 0.f, csq = 0.f;
+  if (col_ok) {
+    for (int lr = tid >> 7; lr < rows_here; lr += 2) {
+      const int row = m0 + lr;
+      const int64_t e = (int64_t)row * p.ldc + col;
+      float v = p.alpha * Cs[lr * CPITCH + lc] + bias;
+      if (p.pre) v *= act_bwd(p.act, p.pre[(int64_t)row * p.ld_pre + col]);
+      if (p.drop_p > 0.f) v *= aw_dropout_scale(p.drop_seed, (uint64_t)row * N + col, p.drop_p);
+      if (p.resid) v += p.resid[(int64_t)row * p.ld_resid + col];
+      if (p.beta != 0.f) v += p.beta * reinterpret_cast<const float*>(p.C)[e];
+      if (p.C) store_from_f32(p.C, p.c_dtype, e, v);
+      if (p.c2_mode) {
+        float w = v;
+        if (p.c2_mode == 1) w = act_fwd(p.act, v);
+        else if (p.c2_mode == 3) w = v * aw_dropout_scale(p.drop2_seed, (uint64_t)row * N + col, p.drop2_p);
+        store_from_f32(p.C2, p.c2_dtype, (int64_t)row * p.ldc2 + col, w);
       }
+      csum += v;
+      csq += v * v;
     }
-    if (p.colstats) {
-      // reduce over the 4 row-quads of the wave (lanes with equal lane&15)
-      csum += __shfl_xor(csum, 16, 64);
-      csum += __shfl_xor(csum, 32, 64);
-      csq += __shfl_xor(csq, 16, 64);
-      csq += __shfl_xor(csq, 32, 64);
-      if (lane < 16 && col_ok) {
-        int s = col % p.stats_mod;
-        atomicAdd(p.colstats + s, (double)csum);
-        atomicAdd(p.colstats + p.stats_mod + s, (double)csq);
-      }
+  }
+  if (p.colstats) {  // BatchNorm batch statistics: pair the two threads of a column, one f64 atomic each
+    __syncthreads();
+    float* red = Cs;
+    if (tid >= 128) {
+      red[lc] = csum;
+      red[128 + lc] = csq;
     }
+    __syncthreads();
+    if (tid < 128 && col_ok) {
+      const int s = col % p.stats_mod;
+      atomicAdd(p.colstats + s, (double)(csum + red[lc]));
+      atomicAdd(p.colstats + p.stats_mod + s, (double)(csq + red[128 + lc]));
+    }
+  }
+}
+
+template <typename T, bool ATR, bool BTR, int ACONV, int BCONV>
+void launch(const GemmP& P, hipStream_t s, bool ragged) {
+  dim3 grid(P.nblocks, P.splits);
+  if (ragged)
+    hipLaunchKernelGGL((gemm_kernel<T, ATR, BTR, ACONV, BCONV, true>), grid, dim3(NTHREADS), 0, s, P);
+  else
+    hipLaunchKernelGGL((gemm_kernel<T, ATR, BTR, ACONV, BCONV, false>), grid, dim3(NTHREADS), 0, s, P);
+}
+
+template <typename T>
+void dispatch(const GemmP& P, hipStream_t s, bool ragged) {
+  const aw_gemm_args& a = P.a;
+  const bool conv = a.conv_cin > 0;
+  const bool aconv = conv && a.conv_operand == 0, bconv = conv && a.conv_operand == 1;
+  if (!a.a_trans && !a.b_trans) {
+    if (aconv) launch<T, false, false, CONV_ROWSHIFT, CONV_NONE>(P, s, ragged);
+    else launch<T, false, false, CONV_NONE, CONV_NONE>(P, s, ragged);
+  } else if (!a.a_trans && a.b_trans) {
+    if (aconv) launch<T, false, true, CONV_ROWSHIFT, CONV_NONE>(P, s, ragged);
+    else launch<T, false, true, CONV_NONE, CONV_NONE>(P, s, ragged);
+  } else if (a.a_trans && !a.b_trans) {
+    launch<T, true, false, CONV_NONE, CONV_NONE>(P, s, ragged);
+  } else {
+    if (bconv) launch<T, true, true, CONV_NONE, CONV_KSHIFT>(P, s, ragged);
+    else launch<T, true, true, CONV_NONE, CONV_NONE>(P, s, ragged);
   }
 }
 
@@ -303,6 +390,7 @@ extern "C" int aw_gemm(const aw_gemm_args* args, void* stream) {
   AW_REQUIRE(a.a_dtype == AW_F32 || a.a_dtype == AW_BF16, "aw_gemm: bad a_dtype %d", a.a_dtype);
   AW_REQUIRE(a.A && a.B, "aw_gemm: null operand");
   const int epc = a.a_dtype == AW_BF16 ? 8 : 4;
+  const int BK = a.a_dtype == AW_BF16 ? 32 : 16;
   AW_REQUIRE(((uintptr_t)a.A % 16) == 0 && ((uintptr_t)a.B % 16) == 0, "aw_gemm: operands must be 16-B aligned");
   AW_REQUIRE(a.lda % epc == 0 && a.ldb % epc == 0, "aw_gemm: lda/ldb must be multiples of %d elements", epc);
   if (a.conv_cin > 0) {
@@ -310,7 +398,8 @@ extern "C" int aw_gemm(const aw_gemm_args* args, void* stream) {
     if (a.conv_operand == 0)
       AW_REQUIRE(a.a_trans == 0 && a.K == 3 * a.conv_cin, "aw_gemm: A-conv needs a_trans=0 and K=3*cin");
     else
-      AW_REQUIRE(a.b_trans == 1 && a.N == 3 * a.conv_cin, "aw_gemm: B-conv needs b_trans=1 and N=3*cin");
+      AW_REQUIRE(a.a_trans == 1 && a.b_trans == 1 && a.N == 3 * a.conv_cin,
+                 "aw_gemm: B-conv needs a_trans=1, b_trans=1 and N=3*cin");
   }
   AW_REQUIRE(!(a.beta != 0.f && a.c_dtype != AW_F32), "aw_gemm: beta != 0 needs an f32 C");
   AW_REQUIRE(!(a.c2_mode && !a.C2), "aw_gemm: c2_mode without C2");
@@ -318,13 +407,31 @@ extern "C" int aw_gemm(const aw_gemm_args* args, void* stream) {
   if (a.M == 0 || a.N == 0) return AW_OK;
   GemmP P;
   P.a = a;
-  P.tiles_m = aw_cdiv(a.M, BM);
+  const int tiles_m = aw_cdiv(a.M, BM);
   P.tiles_n = aw_cdiv(a.N, BN);
-  P.nblocks = P.tiles_m * P.tiles_n;
+  P.nblocks = tiles_m * P.tiles_n;
+  // split-K for plain-accumulate shapes that cannot fill the chip with tiles alone
+  const bool plain = !a.bias && !a.pre && !a.resid && a.drop_p <= 0.f && !a.C2 && !a.colstats && a.C &&
+                     a.c_dtype == AW_F32 && (a.beta == 0.f || a.beta == 1.f) && a.alpha == 1.f;
+  int splits = 1;
+  if (plain && P.nblocks < 192 && a.K >= 64 * BK) {
+    splits = aw_cdiv(256, P.nblocks);
+    const int max_splits = a.K / (16 * BK);  // at least 16 K-steps per split
+    if (splits > max_splits) splits = max_splits;
+    if (splits < 1) splits = 1;
+  }
+  P.ksplit = splits > 1 ? aw_cdiv(aw_cdiv(a.K, splits), BK) * BK : (a.K > 0 ? a.K : 1);
+  P.splits = splits > 1 ? aw_cdiv(a.K, P.ksplit) : 1;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (P.splits > 1 && a.beta == 0.f) {
+    if (hipMemset2DAsync(a.C, a.ldc * sizeof(float), 0, a.N * sizeof(float), a.M, s) != hipSuccess)
+      return aw::check_launch("aw_gemm split-K zero");
+  }
+  // ragged: a contiguous extent that is not a whole number of 16-byte chunks
+  const bool ragged = (!a.a_trans ? (a.K % epc) : (a.M % epc)) != 0 || (!a.b_trans ? (a.K % epc) : (a.N % epc)) != 0;
   if (a.a_dtype == AW_BF16)
-    hipLaunchKernelGGL(gemm_kernel<bf16>, dim3(P.nblocks), dim3(NTHREADS), 0, s, P);
+    dispatch<bf16>(P, s, ragged);
   else
-    hipLaunchKernelGGL(gemm_kernel<float>, dim3(P.nblocks), dim3(NTHREADS), 0, s, P);
+    dispatch<float>(P, s, ragged);
   return aw::check_launch("aw_gemm");
 }
