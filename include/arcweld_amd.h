@@ -63,6 +63,11 @@ typedef struct {
   double* colstats; int stats_mod;
   float* a_rowsum;
   int bias_mod;                  /* > 0: bias index is c % bias_mod (ConvT bias shared by the k taps) */
+  /* accumulate = 1: C[r*ldc + colmap(c)] += alpha*acc with f32 atomics (split-K allowed; no other epilogue
+   * field may be set).  colmap(c) = (c % col_mod)*col_mul + c/col_mod + col_off  (col_mod > 0)
+   *                              =  c*col_mul + col_off                          (col_mod == 0)
+   * so weight gradients land directly in the reference layouts (conv (O,I,3) taps, ConvT (I,O,k)). */
+  int accumulate, col_mod, col_mul, col_off;
 } aw_gemm_args;
 
 int aw_gemm(const aw_gemm_args* args, void* stream);

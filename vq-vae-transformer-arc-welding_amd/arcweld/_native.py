@@ -43,6 +43,7 @@ class GemmArgs(ctypes.Structure):
         ("colstats", c_p), ("stats_mod", c_int),
         ("a_rowsum", c_p),
         ("bias_mod", c_int),
+        ("accumulate", c_int), ("col_mod", c_int), ("col_mul", c_int), ("col_off", c_int),
     ]
 
 

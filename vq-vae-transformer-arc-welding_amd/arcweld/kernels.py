@@ -43,7 +43,8 @@ def _algorithmic_flops(M, N, Kd, conv, flops):
 
 def gemm(A, B, M, N, K, *, a_trans=False, b_trans=False, conv=None, alpha=1.0, beta=0.0, bias=None,
          act=AW_ACT_GELU_ERF, pre=None, resid=None, drop=(0.0, 0), C=None, C2=None, c2_mode=0, drop2=(0.0, 0),
-         colstats=None, stats_mod=0, a_rowsum=None, bias_mod=0, stream=None, flops=None):
+         colstats=None, stats_mod=0, a_rowsum=None, bias_mod=0, accumulate=False, col_map=(0, 1, 0), stream=None,
+         flops=None):
     """C = epilogue(alpha * op(A) @ op(B)); see aw_gemm in include/arcweld_amd.h for the exact semantics.
 
     conv = (cin, seg, dir, operand) selects the implicit k=3 convolution form."""
@@ -74,6 +75,8 @@ def gemm(A, B, M, N, K, *, a_trans=False, b_trans=False, conv=None, alpha=1.0, b
         a.colstats, a.stats_mod = ptr(colstats), int(stats_mod)
     a.a_rowsum = ptr(a_rowsum)
     a.bias_mod = int(bias_mod)
+    a.accumulate = int(bool(accumulate))
+    a.col_mod, a.col_mul, a.col_off = (int(v) for v in col_map)
     if PROFILE is None:
         call("aw_gemm", ctypes.byref(a), stream_ptr(stream))
         return C

@@ -216,10 +216,9 @@ def backward(m, sv, g_emb, g_xhat, slot):
     K.unpatch_head_bwd2(sv.Y2, sh.Q, sv.stats, pr["t2"].weight.view(H, 5), g_xhat, gsums, sv.training, gY,
                         slot(pr["t1"].bias))
     gY2 = gY.view(N, k1 * H)
-    # ConvT1 weight gradient [k1*H][H] -> (H_in, H_out, k1)
-    tmp = e(k1 * H, H)
-    K.gemm(gY2, sv.yR_T, k1 * H, H, N, a_trans=True, b_trans=True, C=tmp)
-    K.weight_grad_scatter(tmp, H, H, k1, 0, 3, slot(pr["t1"].weight))
+    # ConvT1 weight gradient, computed as [i][(j,o)] and accumulated straight into the (H_in, H_out, k1) layout
+    K.gemm(sv.yR_T, gY2, H, k1 * H, N, a_trans=True, b_trans=True, C=slot(pr["t1"].weight).view(H, H * k1),
+           accumulate=True, col_map=(H, k1, 0))
     # ConvT1 input gradient -> grad of the decoder output, plus the dropout-masked operand for its last block
     gy, go = e(N, H), e(N, H, dt=T)
     last = R - 1
@@ -236,19 +235,17 @@ def backward(m, sv, g_emb, g_xhat, slot):
         K.weight_relayout(c2.weight, H, H, 3, 0, 2, W2d)
         gh = e(N, H, dt=T)
         K.gemm(go, W2d, N, H, 3 * H, b_trans=True, conv=dconv_in, pre=sv.dhs[r], C=gh)
-        tmp = e(H, 3 * H)
-        K.gemm(go, sv.da1s[r], H, 3 * H, N, a_trans=True, b_trans=True, conv=wconv, C=tmp, a_rowsum=slot(c2.bias))
-        K.weight_grad_scatter(tmp, H, H, 3, 0, 1, slot(c2.weight))
+        K.gemm(go, sv.da1s[r], H, 3 * H, N, a_trans=True, b_trans=True, conv=wconv,
+               C=slot(c2.weight).view(H, 3 * H), accumulate=True, col_map=(H, 3, 0), a_rowsum=slot(c2.bias))
         gyn, gon = e(N, H), e(N, H, dt=T)
         K.gemm(gh, W1d, N, H, 3 * H, b_trans=True, conv=dconv_in, pre=sv.ys[r], resid=gy, C=gyn, C2=gon,
                c2_mode=3 if r > 0 else 2, drop2=(p_drop, sv.dec_seed[r - 1] if r > 0 else 0))
-        tmp = e(H, 3 * H)
-        K.gemm(gh, sv.ya0s[r], H, 3 * H, N, a_trans=True, b_trans=True, conv=wconv, C=tmp, a_rowsum=slot(c1.bias))
-        K.weight_grad_scatter(tmp, H, H, 3, 0, 1, slot(c1.weight))
+        K.gemm(gh, sv.ya0s[r], H, 3 * H, N, a_trans=True, b_trans=True, conv=wconv,
+               C=slot(c1.weight).view(H, 3 * H), accumulate=True, col_map=(H, 3, 0), a_rowsum=slot(c1.bias))
         gy, go = gyn, gon
 
     # ---- decoder 1x1 conv (weight (H, D, 1) is a contiguous [H][D] matrix)
-    K.gemm(go, sv.zq_T, H, D, N, a_trans=True, b_trans=True, C=slot(pr["dec0"].weight).view(H, D), beta=1.0,
+    K.gemm(go, sv.zq_T, H, D, N, a_trans=True, b_trans=True, C=slot(pr["dec0"].weight).view(H, D), accumulate=True,
            a_rowsum=slot(pr["dec0"].bias))
     gzq = e(N, D)
     K.gemm(go, sv.Wd0, N, D, H, b_trans=True, C=gzq)
@@ -259,7 +256,7 @@ def backward(m, sv, g_emb, g_xhat, slot):
     dz_T = dz if T == F32 else _cast(dz, T)
 
     # ---- SepCNNBlock
-    K.gemm(dz_T, sv.xR_T, D, H, N, a_trans=True, b_trans=True, C=slot(pr["sep"].weight).view(D, H), beta=1.0,
+    K.gemm(dz_T, sv.xR_T, D, H, N, a_trans=True, b_trans=True, C=slot(pr["sep"].weight).view(D, H), accumulate=True,
            a_rowsum=slot(pr["sep"].bias))
     gx, gxo = e(N, H), e(N, H, dt=T)
     K.gemm(dz_T, sv.Ws, N, H, D, b_trans=True, C=gx, C2=gxo, c2_mode=3 if R > 0 else 2,
@@ -271,22 +268,18 @@ def backward(m, sv, g_emb, g_xhat, slot):
         w1, w2 = sv.enc_w[r]
         gh = e(N, H, dt=T)
         K.gemm(gxo, w2, N, H, H, b_trans=True, pre=sv.hs[r], C=gh)
-        tmp = e(H, H)
-        K.gemm(gxo, sv.a1s[r], H, H, N, a_trans=True, b_trans=True, C=tmp, a_rowsum=slot(c2.bias))
-        K.weight_grad_scatter(tmp, H, H, 3, 1, 0, slot(c2.weight))
+        K.gemm(gxo, sv.a1s[r], H, H, N, a_trans=True, b_trans=True, C=slot(c2.weight).view(H, 3 * H),
+               accumulate=True, col_map=(0, 3, 1), a_rowsum=slot(c2.bias))
         gxn, gxon = e(N, H), e(N, H, dt=T)
         K.gemm(gh, w1, N, H, H, b_trans=True, pre=sv.xs[r], resid=gx, C=gxn, C2=gxon, c2_mode=3 if r > 0 else 2,
                drop2=(p_drop, sv.enc_seed[r - 1] if r > 0 else 0))
-        tmp = e(H, H)
-        K.gemm(gh, sv.a0s[r], H, H, N, a_trans=True, b_trans=True, C=tmp, a_rowsum=slot(c1.bias))
-        K.weight_grad_scatter(tmp, H, H, 3, 1, 0, slot(c1.weight))
+        K.gemm(gh, sv.a0s[r], H, H, N, a_trans=True, b_trans=True, C=slot(c1.weight).view(H, 3 * H),
+               accumulate=True, col_map=(0, 3, 1), a_rowsum=slot(c1.bias))
         gx, gxo = gxn, gxon
 
     # ---- patch embed weight/bias
-    tmp = e(H, sh.ldp)
-    K.gemm(gxo, sv.patches, H, sh.ldp, N, a_trans=True, b_trans=True, C=tmp, a_rowsum=slot(pr["pe"].bias),
-           flops=2 * N * H * P)
-    K.weight_grad_scatter(tmp, H, 1, P, 0, 4, slot(pr["pe"].weight))
+    K.gemm(gxo, sv.patches, H, P, N, a_trans=True, b_trans=True, C=slot(pr["pe"].weight).view(H, P),
+           accumulate=True, a_rowsum=slot(pr["pe"].bias))
 
 
 class VQVAEPatchFunction(torch.autograd.Function):

@@ -40,6 +40,7 @@ static_assert(128 * KPB <= STAGE_OP && 32 * TT<bf16>::MPB <= STAGE_OP && 16 * TT
 struct GemmP {
   aw_gemm_args a;
   int tiles_n, nblocks, splits, ksplit;
+  int vec;   // every epilogue operand row is 16-B aligned: vectorised epilogue
 };
 
 enum { CONV_NONE = 0, CONV_ROWSHIFT = 1, CONV_KSHIFT = 2 };
@@ -192,6 +193,18 @@ __device__ __forceinline__ float act_bwd(int act, float x) {
   return act == AW_ACT_GELU_TANH ? gelu_tanh_grad(x) : gelu_erf_grad(x);
 }
 
+// 4 consecutive elements (16-B aligned for f32, 8-B for bf16)
+__device__ __forceinline__ void store4(void* base, int dtype, int64_t e, const float (&v)[4]) {
+  if (dtype == AW_BF16) {
+    bf16 h[4] = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+    uint2 u;
+    memcpy(&u, h, 8);
+    *reinterpret_cast<uint2*>(reinterpret_cast<bf16*>(base) + e) = u;
+  } else {
+    *reinterpret_cast<float4*>(reinterpret_cast<float*>(base) + e) = make_float4(v[0], v[1], v[2], v[3]);
+  }
+}
+
 // Bijective XCD-aware remap: consecutive logical tiles land on the same XCD (blocks b and b+8 share one).
 __device__ __forceinline__ int xcd_remap(int bid, int nblocks) {
   const int q = nblocks / 8, r = nblocks % 8;
@@ -301,51 +314,114 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_kernel(GemmP P) {
           Cs[(wm * 64 + i * 16 + rq + r) * CPITCH + wn * 64 + j * 16 + cq] = acc[i][j][r];
   }
   __syncthreads();
-  const int lc = tid & 127;
-  const int col = n0 + lc;
-  const bool col_ok = col < N;
   const int rows_here = min(BM, M - m0);
-  if (P.splits > 1) {  // split-K: plain accumulate into f32 C
-    if (!col_ok) return;
+  if (P.splits > 1 || p.accumulate) {  // accumulate into f32 C with atomics (consecutive lanes -> columns)
+    const int lc = tid & 127, col = n0 + lc;
+    if (col >= N) return;
+    const int64_t oc = p.col_mod > 0 ? (int64_t)(col % p.col_mod) * p.col_mul + col / p.col_mod + p.col_off
+                                     : (int64_t)col * (p.col_mul > 0 ? p.col_mul : 1) + p.col_off;
     float* C = reinterpret_cast<float*>(p.C);
     for (int lr = tid >> 7; lr < rows_here; lr += 2)
-      atomicAdd(C + (int64_t)(m0 + lr) * p.ldc + col, p.alpha * Cs[lr * CPITCH + lc]);
+      atomicAdd(C + (int64_t)(m0 + lr) * p.ldc + oc, p.alpha * Cs[lr * CPITCH + lc]);
     return;
   }
-  const float bias = (p.bias && col_ok) ? p.bias[p.bias_mod > 0 ? col % p.bias_mod : col] : 0.f;
-  float csum = 0.f, csq = 0.f;
-  if (col_ok) {
-    for (int lr = tid >> 7; lr < rows_here; lr += 2) {
-      const int row = m0 + lr;
-      const int64_t e = (int64_t)row * p.ldc + col;
-      float v = p.alpha * Cs[lr * CPITCH + lc] + bias;
-      if (p.pre) v *= act_bwd(p.act, p.pre[(int64_t)row * p.ld_pre + col]);
-      if (p.drop_p > 0.f) v *= aw_dropout_scale(p.drop_seed, (uint64_t)row * N + col, p.drop_p);
-      if (p.resid) v += p.resid[(int64_t)row * p.ld_resid + col];
-      if (p.beta != 0.f) v += p.beta * reinterpret_cast<const float*>(p.C)[e];
-      if (p.C) store_from_f32(p.C, p.c_dtype, e, v);
-      if (p.c2_mode) {
-        float w = v;
-        if (p.c2_mode == 1) w = act_fwd(p.act, v);
-        else if (p.c2_mode == 3) w = v * aw_dropout_scale(p.drop2_seed, (uint64_t)row * N + col, p.drop2_p);
-        store_from_f32(p.C2, p.c2_dtype, (int64_t)row * p.ldc2 + col, w);
+  // thread -> 4 consecutive columns (c4) x rows r0, r0+8, ...; 4 rows of loads in flight per thread
+  const int c4 = (tid & 31) * 4, r0 = tid >> 5;
+  const int col = n0 + c4;
+  const bool vec = P.vec && col + 4 <= N;
+  float bias[4], csum[4] = {0.f, 0.f, 0.f, 0.f}, csq[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int c = col + e;
+    bias[e] = (p.bias && c < N) ? p.bias[p.bias_mod > 0 ? c % p.bias_mod : c] : 0.f;
+  }
+  if (col < N) {
+    for (int lr0 = r0; lr0 < rows_here; lr0 += 32) {
+      float4 pre4[4], res4[4], old4[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {  // issue the operand loads of 4 rows first
+        const int lr = lr0 + 8 * u;
+        if (lr >= rows_here) break;
+        const int64_t row = m0 + lr;
+        if (vec) {
+          if (p.pre) pre4[u] = *reinterpret_cast<const float4*>(p.pre + row * p.ld_pre + col);
+          if (p.resid) res4[u] = *reinterpret_cast<const float4*>(p.resid + row * p.ld_resid + col);
+          if (p.beta != 0.f) old4[u] = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(p.C) + row * p.ldc + col);
+        } else {
+          float a[4] = {0.f, 0.f, 0.f, 0.f}, b[4] = {0.f, 0.f, 0.f, 0.f}, c[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            if (col + e >= N) break;
+            if (p.pre) a[e] = p.pre[row * p.ld_pre + col + e];
+            if (p.resid) b[e] = p.resid[row * p.ld_resid + col + e];
+            if (p.beta != 0.f) c[e] = reinterpret_cast<const float*>(p.C)[row * p.ldc + col + e];
+          }
+          pre4[u] = make_float4(a[0], a[1], a[2], a[3]);
+          res4[u] = make_float4(b[0], b[1], b[2], b[3]);
+          old4[u] = make_float4(c[0], c[1], c[2], c[3]);
+        }
       }
-      csum += v;
-      csq += v * v;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int lr = lr0 + 8 * u;
+        if (lr >= rows_here) break;
+        const int64_t row = m0 + lr;
+        const float4 a4 = *reinterpret_cast<const float4*>(Cs + lr * CPITCH + c4);
+        const float av[4] = {a4.x, a4.y, a4.z, a4.w};
+        const float pv[4] = {pre4[u].x, pre4[u].y, pre4[u].z, pre4[u].w};
+        const float rv[4] = {res4[u].x, res4[u].y, res4[u].z, res4[u].w};
+        const float ov[4] = {old4[u].x, old4[u].y, old4[u].z, old4[u].w};
+        float v[4], w[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float x = p.alpha * av[e] + bias[e];
+          if (p.pre) x *= act_bwd(p.act, pv[e]);
+          if (p.drop_p > 0.f) x *= aw_dropout_scale(p.drop_seed, (uint64_t)row * N + col + e, p.drop_p);
+          if (p.resid) x += rv[e];
+          if (p.beta != 0.f) x += p.beta * ov[e];
+          v[e] = x;
+          float y = x;
+          if (p.c2_mode == 1) y = act_fwd(p.act, x);
+          else if (p.c2_mode == 3) y = x * aw_dropout_scale(p.drop2_seed, (uint64_t)row * N + col + e, p.drop2_p);
+          w[e] = y;
+          if (col + e < N) {
+            csum[e] += x;
+            csq[e] += x * x;
+          }
+        }
+        if (vec) {
+          if (p.C) store4(p.C, p.c_dtype, row * p.ldc + col, v);
+          if (p.c2_mode) store4(p.C2, p.c2_dtype, row * p.ldc2 + col, w);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            if (col + e >= N) break;
+            if (p.C) store_from_f32(p.C, p.c_dtype, row * p.ldc + col + e, v[e]);
+            if (p.c2_mode) store_from_f32(p.C2, p.c2_dtype, row * p.ldc2 + col + e, w[e]);
+          }
+        }
+      }
     }
   }
-  if (p.colstats) {  // BatchNorm batch statistics: pair the two threads of a column, one f64 atomic each
+  if (p.colstats) {  // BatchNorm batch statistics: reduce the 8 row-groups of a column, one f64 atomic each
     __syncthreads();
-    float* red = Cs;
-    if (tid >= 128) {
-      red[lc] = csum;
-      red[128 + lc] = csq;
+    float* red = Cs;   // [8][2][128]
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      red[(r0 * 2 + 0) * 128 + c4 + e] = csum[e];
+      red[(r0 * 2 + 1) * 128 + c4 + e] = csq[e];
     }
     __syncthreads();
-    if (tid < 128 && col_ok) {
-      const int s = col % p.stats_mod;
-      atomicAdd(p.colstats + s, (double)(csum + red[lc]));
-      atomicAdd(p.colstats + p.stats_mod + s, (double)(csq + red[128 + lc]));
+    if (tid < 128 && n0 + tid < N) {
+      float a = 0.f, b = 0.f;
+#pragma unroll
+      for (int g = 0; g < 8; ++g) {
+        a += red[(g * 2 + 0) * 128 + tid];
+        b += red[(g * 2 + 1) * 128 + tid];
+      }
+      const int sl = (n0 + tid) % p.stats_mod;
+      atomicAdd(p.colstats + sl, (double)a);
+      atomicAdd(p.colstats + p.stats_mod + sl, (double)b);
     }
   }
 }
@@ -412,7 +488,9 @@ extern "C" int aw_gemm(const aw_gemm_args* args, void* stream) {
   P.nblocks = tiles_m * P.tiles_n;
   // split-K for plain-accumulate shapes that cannot fill the chip with tiles alone
   const bool plain = !a.bias && !a.pre && !a.resid && a.drop_p <= 0.f && !a.C2 && !a.colstats && a.C &&
-                     a.c_dtype == AW_F32 && (a.beta == 0.f || a.beta == 1.f) && a.alpha == 1.f;
+                     a.c_dtype == AW_F32 && (a.beta == 0.f || a.beta == 1.f || a.accumulate);
+  AW_REQUIRE(!a.accumulate || plain, "aw_gemm: accumulate mode allows no other epilogue field (f32 C only)");
+  AW_REQUIRE(!(a.accumulate && a.beta != 0.f), "aw_gemm: accumulate mode already adds into C (beta must be 0)");
   int splits = 1;
   if (plain && P.nblocks < 192 && a.K >= 64 * BK) {
     splits = aw_cdiv(256, P.nblocks);
@@ -423,9 +501,16 @@ extern "C" int aw_gemm(const aw_gemm_args* args, void* stream) {
   P.ksplit = splits > 1 ? aw_cdiv(aw_cdiv(a.K, splits), BK) * BK : (a.K > 0 ? a.K : 1);
   P.splits = splits > 1 ? aw_cdiv(a.K, P.ksplit) : 1;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  if (P.splits > 1 && a.beta == 0.f) {
+  if (P.splits > 1 && a.beta == 0.f && !a.accumulate) {
     if (hipMemset2DAsync(a.C, a.ldc * sizeof(float), 0, a.N * sizeof(float), a.M, s) != hipSuccess)
       return aw::check_launch("aw_gemm split-K zero");
+  }
+  {
+    auto al = [](const void* ptr, int64_t ld, int dt) {
+      return ptr == nullptr || (((uintptr_t)ptr % 16) == 0 && (ld * (dt == AW_BF16 ? 2 : 4)) % 16 == 0);
+    };
+    P.vec = al(a.C, a.ldc, a.c_dtype) && al(a.C2, a.ldc2, a.c2_dtype) && al(a.pre, a.ld_pre, AW_F32) &&
+            al(a.resid, a.ld_resid, AW_F32);
   }
   // ragged: a contiguous extent that is not a whole number of 16-byte chunks
   const bool ragged = (!a.a_trans ? (a.K % epc) : (a.M % epc)) != 0 || (!a.b_trans ? (a.K % epc) : (a.N % epc)) != 0;

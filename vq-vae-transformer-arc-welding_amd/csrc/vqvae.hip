@@ -122,47 +122,81 @@ __global__ void bn_finalize_kernel(const double* __restrict__ cs, int64_t n, int
   stats[3 * H + o] = beta ? beta[o] : 0.f;
 }
 
-// ---------------------------------------------------------------- un-patch head forward
-// one wave per row (position); lane handles channels o = 4*lane + 256*it (float4)
-constexpr int HEAD_MAXV = 4;  // float4 slots per lane -> H <= 1024
+// ---------------------------------------------------------------- un-patch head
+// One wave per position row; lane L owns channels o = 4L + 256s (s < NS): its BN statistics and ConvT2 taps
+// stay in registers for every row the wave visits, so the row loop is a pure float4 stream of y.
+constexpr int HEAD_MAXV = 4;  // NS <= 4 -> H <= 1024
 
+template <int NS>
+struct HeadParams {
+  float mean[NS][4], inv[NS][4], gam[NS][4], bet[NS][4], w[NS][4][5];
+  bool on[NS];
+  __device__ __forceinline__ void load(const float* st, const float* w2, int H, int lane) {
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const int o4 = lane * 4 + 256 * s;
+      on[s] = o4 < H;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int o = on[s] ? o4 + e : 0;
+        mean[s][e] = st[o];
+        inv[s][e] = st[H + o];
+        gam[s][e] = st[2 * H + o];
+        bet[s][e] = st[3 * H + o];
+#pragma unroll
+        for (int j = 0; j < 5; ++j) w[s][e][j] = on[s] ? w2[o * 5 + j] : 0.f;
+      }
+    }
+  }
+};
+
+__device__ __forceinline__ float pick5(const float (&v)[5], int lane) {
+  float r = v[0];
+#pragma unroll
+  for (int j = 1; j < 5; ++j)
+    if (lane == j) r = v[j];
+  return r;
+}
+
+template <int NS>
 __global__ __launch_bounds__(256) void head_fwd_kernel(const float* __restrict__ y, int64_t R, int H, int Q,
                                                        const float* __restrict__ st, const float* __restrict__ w2,
                                                        const float* __restrict__ b2, float* __restrict__ x_hat) {
   const int lane = threadIdx.x & 63;
   const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  HeadParams<NS> hp;
+  hp.load(st, w2, H, lane);
+  const float bias = b2[0];
   for (int64_t r = wave; r < R; r += nw) {
+    float4 v[NS];
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+      v[s] = hp.on[s] ? *reinterpret_cast<const float4*>(y + r * H + lane * 4 + 256 * s) : make_float4(0.f, 0.f, 0.f, 0.f);
     float part[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
-    for (int o4 = lane * 4; o4 < H; o4 += 256) {
-      const float4 v = *reinterpret_cast<const float4*>(y + r * H + o4);
-      const float vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      if (!hp.on[s]) continue;
+      const float vv[4] = {v[s].x, v[s].y, v[s].z, v[s].w};
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const int o = o4 + e;
-        const float bn = (vv[e] - st[o]) * st[H + o] * st[2 * H + o] + st[3 * H + o];
-        const float a = gelu_erf(bn);
+        const float a = gelu_erf((vv[e] - hp.mean[s][e]) * hp.inv[s][e] * hp.gam[s][e] + hp.bet[s][e]);
 #pragma unroll
-        for (int j = 0; j < 5; ++j) part[j] = fmaf(a, w2[o * 5 + j], part[j]);
+        for (int j = 0; j < 5; ++j) part[j] = fmaf(a, hp.w[s][e][j], part[j]);
       }
     }
 #pragma unroll
     for (int j = 0; j < 5; ++j) part[j] = wave_sum(part[j]);
     if (lane < 5) {
-      float pj = part[0];
-#pragma unroll
-      for (int j = 1; j < 5; ++j)
-        if (lane == j) pj = part[j];
       const int64_t b = r / Q;
       const int q = (int)(r - b * Q);
-      const int64_t f = b * (int64_t)Q * 5 + q * 5 + lane;
-      x_hat[f] = pj + b2[0];
+      x_hat[b * (int64_t)Q * 5 + q * 5 + lane] = pick5(part, lane) + bias;
     }
   }
 }
 
-// ---------------------------------------------------------------- un-patch head backward
 // pass 1: per-channel sums for the BN backward + ConvT2 weight/bias grads + gamma/beta grads.
+template <int NS>
 __global__ __launch_bounds__(256) void head_bwd1_kernel(const float* __restrict__ y, int64_t R, int H, int Q,
                                                         const float* __restrict__ st, const float* __restrict__ w2,
                                                         const float* __restrict__ gx, double* __restrict__ gsums,
@@ -174,10 +208,11 @@ __global__ __launch_bounds__(256) void head_bwd1_kernel(const float* __restrict_
   const int lane = threadIdx.x & 63;
   const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  float accw[HEAD_MAXV][4][5];
-  float accg[HEAD_MAXV][4], accgx[HEAD_MAXV][4];
+  HeadParams<NS> hp;
+  hp.load(st, w2, H, lane);
+  float accw[NS][4][5], accg[NS][4], accgx[NS][4];
 #pragma unroll
-  for (int s = 0; s < HEAD_MAXV; ++s)
+  for (int s = 0; s < NS; ++s)
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       accg[s][e] = accgx[s][e] = 0.f;
@@ -188,27 +223,25 @@ __global__ __launch_bounds__(256) void head_bwd1_kernel(const float* __restrict_
   for (int64_t r = wave; r < R; r += nw) {
     const int64_t b = r / Q;
     const int q = (int)(r - b * Q);
-    const int64_t f0 = b * (int64_t)Q * 5 + q * 5;
+    const float* gp = gx + b * (int64_t)Q * 5 + q * 5;
     float go[5];
 #pragma unroll
-    for (int j = 0; j < 5; ++j) go[j] = gx[f0 + j];
-    if (lane == 0) gbsum += go[0] + go[1] + go[2] + go[3] + go[4];
+    for (int j = 0; j < 5; ++j) go[j] = gp[j];
+    gbsum += go[0] + go[1] + go[2] + go[3] + go[4];
 #pragma unroll
-    for (int s = 0; s < HEAD_MAXV; ++s) {
-      const int o4 = lane * 4 + 256 * s;
-      if (o4 >= H) break;
-      const float4 v = *reinterpret_cast<const float4*>(y + r * H + o4);
+    for (int s = 0; s < NS; ++s) {
+      if (!hp.on[s]) continue;
+      const float4 v = *reinterpret_cast<const float4*>(y + r * H + lane * 4 + 256 * s);
       const float vv[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const int o = o4 + e;
-        const float xn = (vv[e] - st[o]) * st[H + o];
-        const float bn = xn * st[2 * H + o] + st[3 * H + o];
+        const float xn = (vv[e] - hp.mean[s][e]) * hp.inv[s][e];
+        const float bn = xn * hp.gam[s][e] + hp.bet[s][e];
         const float a = gelu_erf(bn);
         float ga = 0.f;
 #pragma unroll
         for (int j = 0; j < 5; ++j) {
-          ga = fmaf(go[j], w2[o * 5 + j], ga);
+          ga = fmaf(go[j], hp.w[s][e][j], ga);
           accw[s][e][j] = fmaf(a, go[j], accw[s][e][j]);
         }
         const float gbn = ga * gelu_erf_grad(bn);
@@ -218,12 +251,11 @@ __global__ __launch_bounds__(256) void head_bwd1_kernel(const float* __restrict_
     }
   }
 #pragma unroll
-  for (int s = 0; s < HEAD_MAXV; ++s) {
-    const int o4 = lane * 4 + 256 * s;
-    if (o4 >= H) break;
+  for (int s = 0; s < NS; ++s) {
+    if (!hp.on[s]) continue;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      const int o = o4 + e;
+      const int o = lane * 4 + 256 * s + e;
 #pragma unroll
       for (int j = 0; j < 5; ++j) atomicAdd(&red[o * 5 + j], accw[s][e][j]);
       atomicAdd(&red[5 * H + o], accg[s][e]);
@@ -242,7 +274,7 @@ __global__ __launch_bounds__(256) void head_bwd1_kernel(const float* __restrict_
 }
 
 // pass 2: g_y = BN backward of g*gelu'(bn); db_y = channel sums of g_y.
-template <typename T>
+template <typename T, int NS>
 __global__ __launch_bounds__(256) void head_bwd2_kernel(const float* __restrict__ y, int64_t R, int H, int Q,
                                                         const float* __restrict__ st, const float* __restrict__ w2,
                                                         const float* __restrict__ gx,
@@ -254,55 +286,60 @@ __global__ __launch_bounds__(256) void head_bwd2_kernel(const float* __restrict_
   const int lane = threadIdx.x & 63;
   const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  HeadParams<NS> hp;
+  hp.load(st, w2, H, lane);
   const float invn = 1.0f / (float)R;
-  float accd[HEAD_MAXV][4];
+  float sg[NS][4], sgx[NS][4], accd[NS][4];
 #pragma unroll
-  for (int s = 0; s < HEAD_MAXV; ++s)
+  for (int s = 0; s < NS; ++s)
 #pragma unroll
-    for (int e = 0; e < 4; ++e) accd[s][e] = 0.f;
+    for (int e = 0; e < 4; ++e) {
+      const int o = hp.on[s] ? lane * 4 + 256 * s + e : 0;
+      sg[s][e] = training ? (float)gsums[o] * invn : 0.f;
+      sgx[s][e] = training ? (float)gsums[H + o] * invn : 0.f;
+      accd[s][e] = 0.f;
+    }
   for (int64_t r = wave; r < R; r += nw) {
     const int64_t b = r / Q;
     const int q = (int)(r - b * Q);
-    const int64_t f0 = b * (int64_t)Q * 5 + q * 5;
+    const float* gp = gx + b * (int64_t)Q * 5 + q * 5;
     float go[5];
 #pragma unroll
-    for (int j = 0; j < 5; ++j) go[j] = gx[f0 + j];
+    for (int j = 0; j < 5; ++j) go[j] = gp[j];
 #pragma unroll
-    for (int s = 0; s < HEAD_MAXV; ++s) {
+    for (int s = 0; s < NS; ++s) {
+      if (!hp.on[s]) continue;
       const int o4 = lane * 4 + 256 * s;
-      if (o4 >= H) break;
       const float4 v = *reinterpret_cast<const float4*>(y + r * H + o4);
       const float vv[4] = {v.x, v.y, v.z, v.w};
-      T outv[4];
+      float g4[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const int o = o4 + e;
-        const float xn = (vv[e] - st[o]) * st[H + o];
-        const float bn = xn * st[2 * H + o] + st[3 * H + o];
+        const float xn = (vv[e] - hp.mean[s][e]) * hp.inv[s][e];
+        const float bn = xn * hp.gam[s][e] + hp.bet[s][e];
         float ga = 0.f;
 #pragma unroll
-        for (int j = 0; j < 5; ++j) ga = fmaf(go[j], w2[o * 5 + j], ga);
+        for (int j = 0; j < 5; ++j) ga = fmaf(go[j], hp.w[s][e][j], ga);
         const float gbn = ga * gelu_erf_grad(bn);
-        float g;
-        if (training) {
-          const float sg = (float)gsums[o] * invn, sgx = (float)gsums[H + o] * invn;
-          g = st[2 * H + o] * st[H + o] * (gbn - sg - xn * sgx);
-        } else {
-          g = st[2 * H + o] * st[H + o] * gbn;
-        }
+        const float g = hp.gam[s][e] * hp.inv[s][e] * (gbn - sg[s][e] - xn * sgx[s][e]);
         accd[s][e] += g;
-        outv[e] = from_f32<T>(g);
+        g4[e] = g;
       }
-#pragma unroll
-      for (int e = 0; e < 4; ++e) gy[r * H + o4 + e] = outv[e];
+      if constexpr (sizeof(T) == 2) {
+        bf16 h[4] = {(bf16)g4[0], (bf16)g4[1], (bf16)g4[2], (bf16)g4[3]};
+        uint2 u;
+        memcpy(&u, h, 8);
+        *reinterpret_cast<uint2*>(gy + r * H + o4) = u;
+      } else {
+        *reinterpret_cast<float4*>(gy + r * H + o4) = make_float4(g4[0], g4[1], g4[2], g4[3]);
+      }
     }
   }
 #pragma unroll
-  for (int s = 0; s < HEAD_MAXV; ++s) {
-    const int o4 = lane * 4 + 256 * s;
-    if (o4 >= H) break;
+  for (int s = 0; s < NS; ++s) {
+    if (!hp.on[s]) continue;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) atomicAdd(&red[o4 + e], accd[s][e]);
+    for (int e = 0; e < 4; ++e) atomicAdd(&red[lane * 4 + 256 * s + e], accd[s][e]);
   }
   __syncthreads();
   for (int o = threadIdx.x; o < H; o += blockDim.x) atomicAdd(dby + o, red[o]);
@@ -406,8 +443,14 @@ extern "C" int aw_unpatch_head_fwd(const float* y, int64_t R, int H, int Q, cons
   AW_REQUIRE(H % 4 == 0 && H <= 256 * HEAD_MAXV, "aw_unpatch_head_fwd: H must be a multiple of 4 and <= 1024");
   AW_REQUIRE(R % Q == 0, "aw_unpatch_head_fwd: rows must be whole windows");
   if (R == 0) return AW_OK;
-  hipLaunchKernelGGL(head_fwd_kernel, dim3(grid_for(R * 64, 256, 2048)), dim3(256), 0,
-                     reinterpret_cast<hipStream_t>(stream), y, R, H, Q, stats, w2, b2, x_hat);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  dim3 grid(grid_for(R * 64, 256, 2048));
+  switch ((H + 255) / 256) {
+    case 1: hipLaunchKernelGGL(head_fwd_kernel<1>, grid, dim3(256), 0, s, y, R, H, Q, stats, w2, b2, x_hat); break;
+    case 2: hipLaunchKernelGGL(head_fwd_kernel<2>, grid, dim3(256), 0, s, y, R, H, Q, stats, w2, b2, x_hat); break;
+    case 3: hipLaunchKernelGGL(head_fwd_kernel<3>, grid, dim3(256), 0, s, y, R, H, Q, stats, w2, b2, x_hat); break;
+    default: hipLaunchKernelGGL(head_fwd_kernel<4>, grid, dim3(256), 0, s, y, R, H, Q, stats, w2, b2, x_hat); break;
+  }
   return aw::check_launch("aw_unpatch_head_fwd");
 }
 
@@ -417,9 +460,19 @@ extern "C" int aw_unpatch_head_bwd1(const float* y, int64_t R, int H, int Q, con
   AW_REQUIRE(y && stats && w2 && g_xhat && gsums && gw2 && gb2, "aw_unpatch_head_bwd1: null pointer");
   AW_REQUIRE(H % 4 == 0 && H <= 256 * HEAD_MAXV && R % Q == 0, "aw_unpatch_head_bwd1: bad shape");
   if (R == 0) return AW_OK;
-  hipLaunchKernelGGL(head_bwd1_kernel, dim3(grid_for(R * 64, 256, 256)), dim3(256), 7 * H * sizeof(float),
-                     reinterpret_cast<hipStream_t>(stream), y, R, H, Q, stats, w2, g_xhat, gsums, gw2, gb2, ggamma,
-                     gbeta);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  dim3 grid(grid_for(R * 64, 256, 512));
+  const size_t sh = 7 * H * sizeof(float);
+#define AW_H1(NSV) \
+  hipLaunchKernelGGL(head_bwd1_kernel<NSV>, grid, dim3(256), sh, s, y, R, H, Q, stats, w2, g_xhat, gsums, gw2, gb2, \
+                     ggamma, gbeta)
+  switch ((H + 255) / 256) {
+    case 1: AW_H1(1); break;
+    case 2: AW_H1(2); break;
+    case 3: AW_H1(3); break;
+    default: AW_H1(4); break;
+  }
+#undef AW_H1
   return aw::check_launch("aw_unpatch_head_bwd1");
 }
 
@@ -431,12 +484,17 @@ extern "C" int aw_unpatch_head_bwd2(const float* y, int64_t R, int H, int Q, con
   if (R == 0) return AW_OK;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   dim3 grid(grid_for(R * 64, 256, 1024));
-  if (gy_dtype == AW_BF16)
-    hipLaunchKernelGGL(head_bwd2_kernel<bf16>, grid, dim3(256), H * sizeof(float), s, y, R, H, Q, stats, w2, g_xhat,
-                       gsums, training, (bf16*)g_y, db_y);
-  else
-    hipLaunchKernelGGL(head_bwd2_kernel<float>, grid, dim3(256), H * sizeof(float), s, y, R, H, Q, stats, w2, g_xhat,
-                       gsums, training, (float*)g_y, db_y);
+  const size_t sh = H * sizeof(float);
+#define AW_H2(TY, NSV) \
+  hipLaunchKernelGGL((head_bwd2_kernel<TY, NSV>), grid, dim3(256), sh, s, y, R, H, Q, stats, w2, g_xhat, gsums, \
+                     training, (TY*)g_y, db_y)
+  const int ns = (H + 255) / 256;
+  if (gy_dtype == AW_BF16) {
+    if (ns == 1) AW_H2(bf16, 1); else if (ns == 2) AW_H2(bf16, 2); else if (ns == 3) AW_H2(bf16, 3); else AW_H2(bf16, 4);
+  } else {
+    if (ns == 1) AW_H2(float, 1); else if (ns == 2) AW_H2(float, 2); else if (ns == 3) AW_H2(float, 3); else AW_H2(float, 4);
+  }
+#undef AW_H2
   return aw::check_launch("aw_unpatch_head_bwd2");
 }
 
