@@ -71,6 +71,11 @@ typedef struct {
 } aw_gemm_args;
 
 int aw_gemm(const aw_gemm_args* args, void* stream);
+/* Same, with a caller-provided f32 workspace: when the shape is split over K (small M*N, long K: the weight
+ * gradients), partial products go to plain-store slabs in `ws` and one reduce pass writes C (no atomics).
+ * aw_gemm_workspace returns the number of f32 elements needed (0: no split). */
+int64_t aw_gemm_workspace(const aw_gemm_args* args);
+int aw_gemm_ws(const aw_gemm_args* args, float* ws, int64_t ws_elems, void* stream);
 
 /* -------------------------------------------------------------------------------- vector quantizer
  * VectorQuantizer.forward (model/vector_quantizer.py:76-119), fp32, codebook staged in LDS, no MFMA:

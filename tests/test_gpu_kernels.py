@@ -191,3 +191,33 @@ def test_vq_small_forward_backward_vs_reference(K):
     K.vq_onehot(idx, 64, oh)
     np.testing.assert_array_equal(oh.cpu().numpy().argmax(1), g["idx"].reshape(-1))
     assert oh.sum().item() == N
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("use_ws", [True, False])
+def test_gemm_split_k_accumulate_colmap(K, dtype, use_ws):
+    """Weight-gradient form (A^T B, long K): split-K through slabs (workspace) or atomics, accumulated into a
+    strided reference layout via the column map (conv weight (O, I, 3): colmap(c) = (c % I)*3 + c // I)."""
+    import ctypes
+    from arcweld import _native as nat
+    M, I, Kd = 192, 96, 4096
+    N = 3 * I
+    A = _rand((Kd, M), 21, dtype)
+    B = _rand((Kd, N), 22, dtype)
+    G0 = _rand((M, I, 3), 23)
+    G = G0.clone()
+    if use_ws:
+        K.gemm(A, B, M, N, Kd, a_trans=True, b_trans=True, C=G.view(M, 3 * I), accumulate=True, col_map=(I, 3, 0))
+    else:  # force the atomic path: call the plain entry point (no workspace)
+        a = nat.GemmArgs()
+        a.M, a.N, a.K, a.a_dtype = M, N, Kd, nat.dtype_code(dtype)
+        a.A, a.lda, a.a_trans = A.data_ptr(), M, 1
+        a.B, a.ldb, a.b_trans = B.data_ptr(), N, 1
+        a.alpha = 1.0
+        a.C, a.ldc, a.c_dtype = G.data_ptr(), 3 * I, 0
+        a.accumulate, a.col_mod, a.col_mul, a.col_off = 1, I, 3, 0
+        nat.call("aw_gemm", ctypes.byref(a), torch.cuda.current_stream().cuda_stream)
+    prod = (A.float().cpu().t() @ B.float().cpu()).view(M, 3, I).permute(0, 2, 1)   # [o][i][j]
+    ref = G0.cpu() + prod
+    rtol, atol = _tol(dtype, Kd)
+    torch.testing.assert_close(G.cpu(), ref, rtol=rtol, atol=atol * np.sqrt(Kd) * 4)

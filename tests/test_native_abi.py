@@ -8,7 +8,7 @@ from conftest import REPO
 
 def _declared():
     src = open(os.path.join(REPO, "include", "arcweld_amd.h")).read()
-    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(aw_\w+)\s*\(", src, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|int64_t|const char\*)\s+(aw_\w+)\s*\(", src, re.M)))
 
 
 def test_header_declares_entry_points():

@@ -51,6 +51,8 @@ class GemmArgs(ctypes.Structure):
 SIGNATURES = {
     "aw_version": [],
     "aw_gemm": [ctypes.POINTER(GemmArgs), c_p],
+    "aw_gemm_ws": [ctypes.POINTER(GemmArgs), c_p, c_i64, c_p],
+    "aw_gemm_workspace": [ctypes.POINTER(GemmArgs)],
     "aw_vq_forward": [c_p, c_p, c_i64, c_int, c_int, c_p, c_p, c_p, c_p, c_p],
     "aw_vq_finalize": [c_p, c_p, c_i64, c_int, c_int, c_f, c_p, c_p, c_p],
     "aw_vq_backward": [c_p, c_p, c_p, c_p, c_p, c_i64, c_int, c_int, c_f, c_p, c_p, c_p],
@@ -82,6 +84,8 @@ SIGNATURES = {
     "aw_ce_finalize": [c_p, c_p, c_p, c_p],
 }
 
+RET_I64 = {"aw_gemm_workspace"}
+
 _lib = None
 
 
@@ -102,7 +106,7 @@ def load(path: str = LIB_PATH):
     lib.aw_last_error.argtypes = []
     for name, argtypes in SIGNATURES.items():
         fn = getattr(lib, name)
-        fn.restype = c_int
+        fn.restype = c_i64 if name in RET_I64 else c_int
         fn.argtypes = argtypes
     _lib = lib
     return lib

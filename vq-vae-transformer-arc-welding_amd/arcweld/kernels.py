@@ -77,13 +77,16 @@ def gemm(A, B, M, N, K, *, a_trans=False, b_trans=False, conv=None, alpha=1.0, b
     a.bias_mod = int(bias_mod)
     a.accumulate = int(bool(accumulate))
     a.col_mod, a.col_mul, a.col_off = (int(v) for v in col_map)
+    lib = nat.load()
+    wsn = lib.aw_gemm_workspace(ctypes.byref(a))
+    ws = torch.empty(wsn, device=A.device, dtype=torch.float32) if wsn > 0 else None
     if PROFILE is None:
-        call("aw_gemm", ctypes.byref(a), stream_ptr(stream))
+        call("aw_gemm_ws", ctypes.byref(a), ptr(ws), wsn, stream_ptr(stream))
         return C
     s = stream if stream is not None else torch.cuda.current_stream()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(s)
-    call("aw_gemm", ctypes.byref(a), s.cuda_stream)
+    call("aw_gemm_ws", ctypes.byref(a), ptr(ws), wsn, s.cuda_stream)
     e1.record(s)
     PROFILE.append((e0, e1, _algorithmic_flops(M, N, K, conv, flops)))
     return C

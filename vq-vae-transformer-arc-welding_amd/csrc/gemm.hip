@@ -41,6 +41,7 @@ struct GemmP {
   aw_gemm_args a;
   int tiles_n, nblocks, splits, ksplit;
   int vec;   // every epilogue operand row is 16-B aligned: vectorised epilogue
+  float* ws; // split-K partial slabs [splits][M][N] (NULL: fp32 atomics)
 };
 
 enum { CONV_NONE = 0, CONV_ROWSHIFT = 1, CONV_KSHIFT = 2 };
@@ -54,8 +55,30 @@ struct Stager {
   int64_t ld;
   int rows_total, row0, kend, cin, seg, dir;
   uint4 v[2];
+  // per-thread invariants of the implicit convolution (window position / tap of each chunk)
+  int wpos[2];    // ROWSHIFT: row % seg (fixed rows);  KSHIFT: (k0 + krow) % seg, advanced per K step
+  int tapoff[2];  // KSHIFT: row shift j-1 of the chunk's column tap
+  int colin[2];   // KSHIFT: column within the tap (m - j*cin)
+
+  __device__ __forceinline__ void init(int kbeg, int tid) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int c = tid + i * NTHREADS;
+      if constexpr (CONV == CONV_ROWSHIFT) {
+        wpos[i] = (row0 + (c >> 2)) % seg;
+      } else if constexpr (CONV == CONV_KSHIFT) {
+        const int m = row0 + (c % CPR) * EPC;
+        const int j = m / cin;
+        tapoff[i] = j - 1;
+        colin[i] = m - j * cin;
+        wpos[i] = (kbeg + c / CPR) % seg;
+      }
+    }
+  }
 
   __device__ __forceinline__ void load(int k0, int tid) {
+    // ROWSHIFT: cin % BK == 0, so the tap is uniform over the whole K step
+    const int jrow = (CONV == CONV_ROWSHIFT) ? k0 / cin : 0;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int c = tid + i * NTHREADS;
@@ -67,12 +90,10 @@ struct Stager {
         int64_t src = row;
         int kk = k;
         if constexpr (CONV == CONV_ROWSHIFT) {
-          const int j = k / cin;
-          kk = k - j * cin;
-          const int s = dir * (j - 1);
-          const int t = row % seg;
-          ok = ok && (t + s >= 0) && (t + s < seg);
-          src = row + s;
+          kk = k - jrow * cin;
+          const int sft = dir * (jrow - 1);
+          ok = ok && (wpos[i] + sft >= 0) && (wpos[i] + sft < seg);
+          src = row + sft;
         }
         if (ok) {
           const T* p = base + src * ld + kk;
@@ -96,12 +117,12 @@ struct Stager {
         int64_t srck = k;
         int mm = m;
         if constexpr (CONV == CONV_KSHIFT) {
-          const int j = m / cin;
-          mm = m - j * cin;
-          const int s = j - 1;
-          const int t = k % seg;
-          ok = ok && (t + s >= 0) && (t + s < seg);
-          srck = k + s;
+          mm = colin[i];
+          const int sft = tapoff[i];
+          ok = ok && (wpos[i] + sft >= 0) && (wpos[i] + sft < seg);
+          srck = k + sft;
+          wpos[i] += BK % seg;                 // advance the window position to the next K step
+          if (wpos[i] >= seg) wpos[i] -= seg;
         }
         if (ok) {
           const T* p = base + srck * ld + mm;
@@ -250,6 +271,8 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_kernel(GemmP P) {
   Stager<T, ATR, ACONV, RAGGED> sa{reinterpret_cast<const T*>(p.A), p.lda, M, m0, kend, p.conv_cin, p.conv_seg,
                                    p.conv_dir, {}};
   Stager<T, BTR, BCONV, RAGGED> sb{reinterpret_cast<const T*>(p.B), p.ldb, N, n0, kend, p.conv_cin, p.conv_seg, 1, {}};
+  sa.init(kbeg, tid);
+  sb.init(kbeg, tid);
   const bool do_rowsum = p.a_rowsum != nullptr && tn == 0;
 
   f32x4 acc[4][4];
@@ -315,6 +338,13 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_kernel(GemmP P) {
   }
   __syncthreads();
   const int rows_here = min(BM, M - m0);
+  if (P.splits > 1 && P.ws) {  // partial slab of this split: plain coalesced stores, reduced by gemm_reduce
+    const int lc = tid & 127, col = n0 + lc;
+    if (col >= N) return;
+    float* slab = P.ws + (int64_t)blockIdx.y * M * N;
+    for (int lr = tid >> 7; lr < rows_here; lr += 2) slab[(int64_t)(m0 + lr) * N + col] = Cs[lr * CPITCH + lc];
+    return;
+  }
   if (P.splits > 1 || p.accumulate) {  // accumulate into f32 C with atomics (consecutive lanes -> columns)
     const int lc = tid & 127, col = n0 + lc;
     if (col >= N) return;
@@ -426,6 +456,28 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_kernel(GemmP P) {
   }
 }
 
+// sum of the split-K slabs -> C (accumulate mode: += through the column map; else alpha*sum + beta*C)
+__global__ __launch_bounds__(256) void gemm_reduce_kernel(const float* __restrict__ ws, int splits, int M, int N,
+                                                          aw_gemm_args p) {
+  const int64_t n = (int64_t)M * N;
+  float* C = reinterpret_cast<float*>(p.C);
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
+    float acc = 0.f;
+    for (int s = 0; s < splits; ++s) acc += ws[s * n + e];
+    const int64_t r = e / N;
+    const int c = (int)(e - r * N);
+    if (p.accumulate) {
+      const int64_t oc = p.col_mod > 0 ? (int64_t)(c % p.col_mod) * p.col_mul + c / p.col_mod + p.col_off
+                                       : (int64_t)c * (p.col_mul > 0 ? p.col_mul : 1) + p.col_off;
+      C[r * p.ldc + oc] += p.alpha * acc;
+    } else {
+      float v = p.alpha * acc;
+      if (p.beta != 0.f) v += p.beta * C[r * p.ldc + c];
+      C[r * p.ldc + c] = v;
+    }
+  }
+}
+
 template <typename T, bool ATR, bool BTR, int ACONV, int BCONV>
 void launch(const GemmP& P, hipStream_t s, bool ragged) {
   dim3 grid(P.nblocks, P.splits);
@@ -456,7 +508,35 @@ void dispatch(const GemmP& P, hipStream_t s, bool ragged) {
 
 }  // namespace
 
-extern "C" int aw_gemm(const aw_gemm_args* args, void* stream) {
+// split-K choice shared by aw_gemm and aw_gemm_workspace
+static int choose_splits(const aw_gemm_args& a, int nblocks, int BK, int* ksplit) {
+  const bool plain = !a.bias && !a.pre && !a.resid && a.drop_p <= 0.f && !a.C2 && !a.colstats && a.C &&
+                     a.c_dtype == AW_F32 && (a.beta == 0.f || a.beta == 1.f || a.accumulate);
+  int splits = 1;
+  if (plain && nblocks < 192 && a.K >= 64 * BK) {
+    splits = aw_cdiv(256, nblocks);
+    const int max_splits = a.K / (16 * BK);  // at least 16 K-steps per split
+    if (splits > max_splits) splits = max_splits;
+    if (splits < 1) splits = 1;
+  }
+  *ksplit = splits > 1 ? aw_cdiv(aw_cdiv(a.K, splits), BK) * BK : (a.K > 0 ? a.K : 1);
+  return splits > 1 ? aw_cdiv(a.K, *ksplit) : 1;
+}
+
+extern "C" int64_t aw_gemm_workspace(const aw_gemm_args* a) {
+  if (!a || a->M <= 0 || a->N <= 0) return 0;
+  const int BK = a->a_dtype == AW_BF16 ? 32 : 16;
+  int ks;
+  const int nb = aw_cdiv(a->M, BM) * aw_cdiv(a->N, BN);
+  const int sp = choose_splits(*a, nb, BK, &ks);
+  return sp > 1 ? (int64_t)sp * a->M * a->N : 0;
+}
+
+extern "C" int aw_gemm_ws(const aw_gemm_args* args, float* ws, int64_t ws_elems, void* stream);
+
+extern "C" int aw_gemm(const aw_gemm_args* args, void* stream) { return aw_gemm_ws(args, nullptr, 0, stream); }
+
+extern "C" int aw_gemm_ws(const aw_gemm_args* args, float* ws, int64_t ws_elems, void* stream) {
   if (!args) {
     aw::set_error("aw_gemm: null args");
     return AW_ERR_ARG;
@@ -491,17 +571,12 @@ extern "C" int aw_gemm(const aw_gemm_args* args, void* stream) {
                      a.c_dtype == AW_F32 && (a.beta == 0.f || a.beta == 1.f || a.accumulate);
   AW_REQUIRE(!a.accumulate || plain, "aw_gemm: accumulate mode allows no other epilogue field (f32 C only)");
   AW_REQUIRE(!(a.accumulate && a.beta != 0.f), "aw_gemm: accumulate mode already adds into C (beta must be 0)");
-  int splits = 1;
-  if (plain && P.nblocks < 192 && a.K >= 64 * BK) {
-    splits = aw_cdiv(256, P.nblocks);
-    const int max_splits = a.K / (16 * BK);  // at least 16 K-steps per split
-    if (splits > max_splits) splits = max_splits;
-    if (splits < 1) splits = 1;
-  }
-  P.ksplit = splits > 1 ? aw_cdiv(aw_cdiv(a.K, splits), BK) * BK : (a.K > 0 ? a.K : 1);
-  P.splits = splits > 1 ? aw_cdiv(a.K, P.ksplit) : 1;
+  if (a.conv_cin > 0) AW_REQUIRE(a.conv_cin % BK == 0, "aw_gemm: conv_cin must be a multiple of %d", BK);
+  P.splits = choose_splits(a, P.nblocks, BK, &P.ksplit);
+  P.ws = nullptr;
+  if (P.splits > 1 && ws && ws_elems >= (int64_t)P.splits * a.M * a.N) P.ws = ws;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  if (P.splits > 1 && a.beta == 0.f && !a.accumulate) {
+  if (P.splits > 1 && !P.ws && a.beta == 0.f && !a.accumulate) {
     if (hipMemset2DAsync(a.C, a.ldc * sizeof(float), 0, a.N * sizeof(float), a.M, s) != hipSuccess)
       return aw::check_launch("aw_gemm split-K zero");
   }
@@ -518,5 +593,11 @@ extern "C" int aw_gemm(const aw_gemm_args* args, void* stream) {
     dispatch<bf16>(P, s, ragged);
   else
     dispatch<float>(P, s, ragged);
+  if (P.ws) {
+    const int64_t n = (int64_t)a.M * a.N;
+    int64_t g = (n + 255) / 256;
+    if (g > 2048) g = 2048;
+    hipLaunchKernelGGL(gemm_reduce_kernel, dim3((int)g), dim3(256), 0, s, P.ws, P.splits, a.M, a.N, a);
+  }
   return aw::check_launch("aw_gemm");
 }
