@@ -102,7 +102,7 @@ def test_gemm_beta_and_dropout(K):
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_gemm_implicit_conv3(K, dtype):
     """Decoder conv (k=3, pad=1 per window of S tokens): forward, input-gradient and weight-gradient forms."""
-    Bw, S, Cin, Cout = 6, 16, 64, 96
+    Bw, S, Cin, Cout = 6, 16, 64, 128
     M = Bw * S
     x = _rand((M, Cin), 11, dtype)
     W = torch.tensor(gen.normal(12, (Cout, Cin, 3), 0.1))

@@ -20,22 +20,32 @@
 namespace {
 
 constexpr int BM = 128, BN = 128, NTHREADS = 256;
-constexpr int ROWB = 64;                 // bytes of K per operand row per step
-constexpr int KPB = ROWB + 16;           // pitch of the [row][k] image (bytes)
-constexpr int STAGE_OP = 10240;          // bytes reserved per operand per stage (>= 128*KPB, >= BK*MPB)
+constexpr int ROWB = 128;                // bytes of K per operand row per step (K-contiguous image pitch)
+constexpr int STAGE_OP = 16384;          // bytes per operand per stage (both images are exactly 16 KiB)
 constexpr int CPITCH = BN + 4;           // f32 pitch of the epilogue tile
 constexpr int SMEM = (BM * CPITCH * 4 > 4 * STAGE_OP) ? BM * CPITCH * 4 : 4 * STAGE_OP;
+constexpr int NCH = STAGE_OP / 16 / NTHREADS;   // 16-B chunks per thread per operand per step (4)
 
 template <typename T> struct TT;
 template <> struct TT<bf16> {
-  static constexpr int EPC = 8, BK = 32;
-  static constexpr int MPB = 128 * 2 + 16;   // pitch of the [k][row] image: 272 B
+  static constexpr int EPC = 8, BK = 64;
+  static constexpr int MPB = 256;          // k-row of the row-contiguous image: 128 rows x 2 B
+  // rotation of k-row k (bytes): conflict-free ds_read_b64_tr_b16 for the 32-lane halves
+  __device__ static constexpr int rot(int k) { return 32 * ((k & 3) + 4 * ((k >> 3) & 1)); }
 };
 template <> struct TT<float> {
-  static constexpr int EPC = 4, BK = 16;
-  static constexpr int MPB = 128 * 4 + 16;   // 528 B
+  static constexpr int EPC = 4, BK = 32;
+  static constexpr int MPB = 512;          // 128 rows x 4 B
+  __device__ static constexpr int rot(int k) { return 64 * ((k >> 2) & 1); }
 };
-static_assert(128 * KPB <= STAGE_OP && 32 * TT<bf16>::MPB <= STAGE_OP && 16 * TT<float>::MPB <= STAGE_OP, "LDS");
+
+// K-contiguous image [row][128 B]: logical 16-B chunk c of row r lives at physical chunk c ^ ((r >> 1) & 7)
+// (conflict-free ds_read_b128 for the 16-row fragments; verified against the gfx950 lane groups).
+__device__ __forceinline__ int nt_off(int row, int chunk) { return row * ROWB + ((chunk ^ ((row >> 1) & 7)) << 4); }
+template <typename T>
+__device__ __forceinline__ int tr_off(int krow, int byte_in_row) {
+  return krow * TT<T>::MPB + ((byte_in_row + TT<T>::rot(krow)) & (TT<T>::MPB - 1));
+}
 
 struct GemmP {
   aw_gemm_args a;
@@ -49,23 +59,24 @@ enum { CONV_NONE = 0, CONV_ROWSHIFT = 1, CONV_KSHIFT = 2 };
 // ---------------------------------------------------------------- operand staging (global -> regs -> LDS)
 template <typename T, bool TR, int CONV, bool RAGGED>
 struct Stager {
-  static constexpr int EPC = TT<T>::EPC, BK = TT<T>::BK, MPB = TT<T>::MPB;
+  static constexpr int EPC = TT<T>::EPC, BK = TT<T>::BK;
   static constexpr int CPR = 128 / EPC;   // chunks per k-row of a row-contiguous tile
+  static constexpr int CPK = BK / EPC;    // chunks per row of a K-contiguous tile (8)
   const T* base;
   int64_t ld;
   int rows_total, row0, kend, cin, seg, dir;
-  uint4 v[2];
+  uint4 v[NCH];
   // per-thread invariants of the implicit convolution (window position / tap of each chunk)
-  int wpos[2];    // ROWSHIFT: row % seg (fixed rows);  KSHIFT: (k0 + krow) % seg, advanced per K step
-  int tapoff[2];  // KSHIFT: row shift j-1 of the chunk's column tap
-  int colin[2];   // KSHIFT: column within the tap (m - j*cin)
+  int wpos[NCH];    // ROWSHIFT: row % seg (fixed rows);  KSHIFT: (k0 + krow) % seg, advanced per K step
+  int tapoff[NCH];  // KSHIFT: row shift j-1 of the chunk's column tap
+  int colin[NCH];   // KSHIFT: column within the tap (m - j*cin)
 
   __device__ __forceinline__ void init(int kbeg, int tid) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < NCH; ++i) {
       const int c = tid + i * NTHREADS;
       if constexpr (CONV == CONV_ROWSHIFT) {
-        wpos[i] = (row0 + (c >> 2)) % seg;
+        wpos[i] = (row0 + c / CPK) % seg;
       } else if constexpr (CONV == CONV_KSHIFT) {
         const int m = row0 + (c % CPR) * EPC;
         const int j = m / cin;
@@ -80,12 +91,12 @@ struct Stager {
     // ROWSHIFT: cin % BK == 0, so the tap is uniform over the whole K step
     const int jrow = (CONV == CONV_ROWSHIFT) ? k0 / cin : 0;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < NCH; ++i) {
       const int c = tid + i * NTHREADS;
       uint4 out = make_uint4(0, 0, 0, 0);
       if constexpr (!TR) {
-        const int row = row0 + (c >> 2);
-        const int k = k0 + (c & 3) * EPC;
+        const int row = row0 + c / CPK;
+        const int k = k0 + (c % CPK) * EPC;
         bool ok = row < rows_total && k < kend;
         int64_t src = row;
         int kk = k;
@@ -146,12 +157,12 @@ struct Stager {
 
   __device__ __forceinline__ void store(char* lds, int tid) const {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < NCH; ++i) {
       const int c = tid + i * NTHREADS;
       if constexpr (!TR)
-        *reinterpret_cast<uint4*>(lds + (c >> 2) * KPB + (c & 3) * 16) = v[i];
+        *reinterpret_cast<uint4*>(lds + nt_off(c / CPK, c % CPK)) = v[i];
       else
-        *reinterpret_cast<uint4*>(lds + (c / CPR) * MPB + (c % CPR) * 16) = v[i];
+        *reinterpret_cast<uint4*>(lds + tr_off<T>(c / CPR, (c % CPR) * 16)) = v[i];
     }
   }
 };
@@ -160,30 +171,31 @@ struct Stager {
 typedef short v4i16 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
 
-// Fragment of the 16 rows [rbase, rbase+16) x this lane's K slice, as 16 bytes.
+// Fragment of the 16 rows [rbase, rbase+16) x this lane's K slice of MFMA sub-step u, as 16 bytes.
+// K order inside a sub-step is the same for A and B: lane group g holds k = 8g..8g+7 (bf16) /
+// k = 4g..4g+3 with one element per f32 MFMA (f32).
 template <typename T, bool TR>
-__device__ __forceinline__ uint4 frag(const char* lds, int rbase, int lane) {
+__device__ __forceinline__ uint4 frag(const char* lds, int rbase, int lane, int u) {
+  const int g = lane >> 4, i = lane & 15;
   if constexpr (!TR) {
-    return *reinterpret_cast<const uint4*>(lds + (rbase + (lane & 15)) * KPB + (lane >> 4) * 16);
+    return *reinterpret_cast<const uint4*>(lds + nt_off(rbase + i, 4 * u + g));
   } else if constexpr (sizeof(T) == 2) {
     // two 4(k) x 16(row) transposed reads: lane 4q+p addresses k-row q, rows 4p..4p+3 of the block;
     // lane i receives row i, k-rows 0..3
-    constexpr int MPB = TT<T>::MPB;
-    const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
-    const char* b0 = lds + (8 * g + q) * MPB + (rbase + 4 * p) * 2;
-    const v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(uintptr_t)(b0));
-    const v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(uintptr_t)(b0 + 4 * MPB));
+    const int q = i >> 2, p = i & 3;
+    const int k0 = 32 * u + 8 * g + q;
+    const v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (lds_v4i16*)(uintptr_t)(lds + tr_off<T>(k0, 2 * (rbase + 4 * p))));
+    const v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (lds_v4i16*)(uintptr_t)(lds + tr_off<T>(k0 + 4, 2 * (rbase + 4 * p))));
     uint4 out;
     memcpy(&out, &lo, 8);
     memcpy(reinterpret_cast<char*>(&out) + 8, &hi, 8);
     return out;
   } else {
-    constexpr int MPB = TT<T>::MPB;
-    const int g = lane >> 4, i = lane & 15;
-    const char* b0 = lds + 4 * g * MPB + (rbase + i) * 4;
     float f[4];
 #pragma unroll
-    for (int s = 0; s < 4; ++s) f[s] = *reinterpret_cast<const float*>(b0 + s * MPB);
+    for (int s = 0; s < 4; ++s) f[s] = *reinterpret_cast<const float*>(lds + tr_off<T>(16 * u + 4 * g + s, 4 * (rbase + i)));
     uint4 out;
     memcpy(&out, f, 16);
     return out;
@@ -236,18 +248,20 @@ __device__ __forceinline__ int xcd_remap(int bid, int nblocks) {
 // sum over this thread's half of the staged A K-slice (fused bias gradient of weight-gradient GEMMs)
 template <typename T, bool TR>
 __device__ __forceinline__ float a_row_partial(const char* lds, int tid) {
-  constexpr int BK = TT<T>::BK;
+  constexpr int BK = TT<T>::BK, EPC = TT<T>::EPC;
   const int r = tid >> 1, h = tid & 1;
   float s = 0.f;
   if constexpr (!TR) {
-    const T* rowp = reinterpret_cast<const T*>(lds + r * KPB) + h * (BK / 2);
 #pragma unroll
-    for (int e = 0; e < BK / 2; ++e) s += to_f32<T>(rowp[e]);
+    for (int cc = 0; cc < BK / EPC / 2; ++cc) {
+      const T* cp = reinterpret_cast<const T*>(lds + nt_off(r, h * (BK / EPC / 2) + cc));
+#pragma unroll
+      for (int e = 0; e < EPC; ++e) s += to_f32<T>(cp[e]);
+    }
   } else {
-    constexpr int MPB = TT<T>::MPB;
 #pragma unroll
     for (int e = 0; e < BK / 2; ++e)
-      s += to_f32<T>(*reinterpret_cast<const T*>(lds + (h * (BK / 2) + e) * MPB + r * (int)sizeof(T)));
+      s += to_f32<T>(*reinterpret_cast<const T*>(lds + tr_off<T>(h * (BK / 2) + e, r * (int)sizeof(T))));
   }
   return s;
 }
@@ -297,16 +311,19 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_kernel(GemmP P) {
     }
     const char* a_l = smem + cur * 2 * STAGE_OP;
     const char* b_l = a_l + STAGE_OP;
-    uint4 af[4], bfr[4];
 #pragma unroll
-    for (int f = 0; f < 4; ++f) {
-      af[f] = frag<T, ATR>(a_l, wm * 64 + f * 16, lane);
-      bfr[f] = frag<T, BTR>(b_l, wn * 64 + f * 16, lane);
+    for (int u = 0; u < 2; ++u) {
+      uint4 af[4], bfr[4];
+#pragma unroll
+      for (int f = 0; f < 4; ++f) {
+        af[f] = frag<T, ATR>(a_l, wm * 64 + f * 16, lane, u);
+        bfr[f] = frag<T, BTR>(b_l, wn * 64 + f * 16, lane, u);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) Mfma<T>::run(acc[i][j], af[i], bfr[j]);
     }
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) Mfma<T>::run(acc[i][j], af[i], bfr[j]);
     if (do_rowsum) rowsum += a_row_partial<T, ATR>(a_l, tid);
     if (kt + 1 < nk) {
       char* nxt = smem + (cur ^ 1) * 2 * STAGE_OP;
@@ -525,7 +542,7 @@ static int choose_splits(const aw_gemm_args& a, int nblocks, int BK, int* ksplit
 
 extern "C" int64_t aw_gemm_workspace(const aw_gemm_args* a) {
   if (!a || a->M <= 0 || a->N <= 0) return 0;
-  const int BK = a->a_dtype == AW_BF16 ? 32 : 16;
+  const int BK = a->a_dtype == AW_BF16 ? 64 : 32;
   int ks;
   const int nb = aw_cdiv(a->M, BM) * aw_cdiv(a->N, BN);
   const int sp = choose_splits(*a, nb, BK, &ks);
@@ -546,7 +563,7 @@ extern "C" int aw_gemm_ws(const aw_gemm_args* args, float* ws, int64_t ws_elems,
   AW_REQUIRE(a.a_dtype == AW_F32 || a.a_dtype == AW_BF16, "aw_gemm: bad a_dtype %d", a.a_dtype);
   AW_REQUIRE(a.A && a.B, "aw_gemm: null operand");
   const int epc = a.a_dtype == AW_BF16 ? 8 : 4;
-  const int BK = a.a_dtype == AW_BF16 ? 32 : 16;
+  const int BK = a.a_dtype == AW_BF16 ? 64 : 32;
   AW_REQUIRE(((uintptr_t)a.A % 16) == 0 && ((uintptr_t)a.B % 16) == 0, "aw_gemm: operands must be 16-B aligned");
   AW_REQUIRE(a.lda % epc == 0 && a.ldb % epc == 0, "aw_gemm: lda/ldb must be multiples of %d elements", epc);
   if (a.conv_cin > 0) {
