@@ -172,9 +172,19 @@ int aw_scale(float* x, int64_t n, const float* s, void* stream);
  * y = (x-mean)*rstd*w + b (y_dtype); mean/rstd saved (f32, R each). */
 int aw_layernorm_fwd(const float* x, int64_t R, int D, const float* w, const float* b, float eps, void* y,
                      int y_dtype, float* mean, float* rstd, void* stream);
-/* dx (+= if accumulate) and dw/db (accumulated, f32) */
+/* dx (+= if accumulate) and dw/db (accumulated, f32).  Optional second output dx2 (dx2_dtype) = the final dx
+ * times the dropout mask (drop_seed, r*D + c, drop_p) of the residual branch that produced x -- the operand of
+ * the preceding block's output-projection gradients (mask regenerated, never stored). */
 int aw_layernorm_bwd(const float* x, const float* dy, int64_t R, int D, const float* w, const float* mean,
-                     const float* rstd, float* dx, int accumulate, float* dw, float* db, void* stream);
+                     const float* rstd, float* dx, int accumulate, float* dw, float* db, void* dx2, int dx2_dtype,
+                     float drop_p, uint64_t drop_seed, void* stream);
+/* Classification head (transformer_decoder.py:126-129): s[r] = xf[r].w1 (+b1), g = GELU_erf(s),
+ * out[b][c] = sum_t g[b*T+t] W2[c][t] (+b2[c]).  b1/b2 may be NULL (class_h_bias=False). */
+int aw_class_head_fwd(const float* xf, int64_t B, int T, int D, const float* w1, const float* b1, const float* W2,
+                      const float* b2, float* s, float* out, void* stream);
+/* Backward: dxf (R x D, written), dw1 (D), db1 (1), dW2 (2 x T), db2 (2) accumulated (+=); NULL grads skipped. */
+int aw_class_head_bwd(const float* xf, const float* s, const float* dout, int64_t B, int T, int D, const float* w1,
+                      const float* W2, float* dxf, float* dw1, float* db1, float* dW2, float* db2, void* stream);
 /* Token embedding + sinusoidal PE (model/embedding.py:57-59): x[b,t,:] = Wtok[ids[b,t]] + pe[t] */
 int aw_embed_fwd(const int64_t* ids, int64_t B, int T, int D, const float* wtok, const float* pe, float* x,
                  void* stream);
@@ -189,7 +199,8 @@ int aw_attn_bwd(const void* qkv, const void* y, const void* dy, const float* lse
                 int d, int dtype, void* dqkv, float* ws, void* stream);
 /* Cross entropy with ignore_index (transformer_decoder.py:226-230): logits (R, V) f32 with row stride ldl;
  * loss_sum (f64, zero on entry) += sum over kept rows of (lse - logit[y]); count (f64) += kept rows.
- * The backward writes dlogits = (softmax - onehot) * g / count (g device scalar) into dlogits (dtype). */
+ * The backward writes dlogits = (softmax - onehot) * g / count (g device scalar) into dlogits (dtype) and zeros
+ * into its padding columns V..ldd-1. */
 int aw_ce_fwd(const float* logits, int64_t R, int V, int64_t ldl, const int64_t* y, int ignore_index,
               double* loss_sum, double* count, float* lse, void* stream);
 int aw_ce_bwd(const float* logits, int64_t R, int V, int64_t ldl, const int64_t* y, int ignore_index,

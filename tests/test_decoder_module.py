@@ -1,0 +1,203 @@
+"""MyTransformerDecoder drop-in: module surface / optimizer groups on CPU; the fused HIP forward/backward against
+the reference's golden fixtures on the GPU (fp32 parity mode -> exact-f32 MFMA; logits within 1e-4)."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden
+from oracle import decoder as od
+from oracle import gen
+
+SMALL = dict(d_model=64, n_classes=34, seq_len=33, n_blocks=2)
+FULL = dict(d_model=512, n_classes=514, seq_len=321, n_blocks=8)
+CASES = [("decoder_small.npz", SMALL, 4, 4, 401, 402, False),
+         ("decoder_small_bias.npz", SMALL, 4, 3, 403, 404, True)]
+
+
+def make_model(kw, n_head, wseed, bias=False, device="cpu", res_dropout=0.0):
+    from model.transformer_decoder import MyTransformerDecoder
+    m = MyTransformerDecoder(n_head=n_head, res_dropout=res_dropout, att_dropout=0.0, class_h_bias=bias, **kw)
+    sd = od.det_state_dict(wseed, class_h_bias=bias, **kw)
+    m.load_state_dict({k: torch.tensor(v) for k, v in sd.items()})
+    return m.to(device)
+
+
+def inputs(B, T, V, xseed, device="cpu"):
+    x = gen.randint(xseed, (B, T), 0, V)
+    y = gen.randint(xseed + 1, (B, T), 0, V)
+    y[:, -3:] = -1
+    cond = gen.randint(xseed + 2, (B,), 0, 2)
+    return tuple(torch.tensor(a, device=device) for a in (x, y, cond))
+
+
+@pytest.mark.parametrize("kw,bias", [(SMALL, False), (SMALL, True), (FULL, False)])
+def test_state_dict_layout_matches_reference(kw, bias):
+    from model.transformer_decoder import MyTransformerDecoder
+    m = MyTransformerDecoder(n_head=4, class_h_bias=bias, **kw)
+    ref = od.decoder_state_dict_shapes(class_h_bias=bias, **kw)
+    got = {k: tuple(v.shape) for k, v in m.state_dict().items()}
+    assert got == {k: tuple(s) for k, s in ref.items()}
+    assert m.hparams["d_model"] == kw["d_model"] and m.hparams["n_classes"] == kw["n_classes"]
+
+
+def test_optimizer_groups_match_reference():
+    """Linear weights decayed (0.1), biases / LayerNorm / Embedding not; betas (0.9, 0.95)."""
+    m = make_model(SMALL, 4, 401)
+    opt = m.configure_optimizers()
+    names = {id(p): n for n, p in m.named_parameters()}
+    decay = sorted(names[id(p)] for p in opt.param_groups[0]["params"])
+    no_decay = sorted(names[id(p)] for p in opt.param_groups[1]["params"])
+    assert opt.param_groups[0]["weight_decay"] == 0.1 and opt.param_groups[1]["weight_decay"] == 0.0
+    assert opt.param_groups[0]["betas"] == (0.9, 0.95)
+    assert all(n.endswith("weight") and "ln_" not in n and "embedding" not in n for n in decay)
+    assert "lm_head.weight" in decay and "transformer.h.0.mlp.c_fc.weight" in decay
+    assert "embedding.latent_embedding.weight" in no_decay and "transformer.ln_f.weight" in no_decay
+    assert len(decay) + len(no_decay) == len(names)
+
+
+def test_active_parameters_follow_task():
+    m = make_model(SMALL, 4, 401)
+    gen_names = {n for n, p in m.named_parameters() if any(p is q for q in m.active_parameters())}
+    assert "lm_head.weight" in gen_names and not any(n.startswith("class_head") for n in gen_names)
+    m.switch_to_classification()
+    cls_names = {n for n, p in m.named_parameters() if any(p is q for q in m.active_parameters())}
+    assert "lm_head.weight" not in cls_names and "class_head.linear_1.weight" in cls_names
+
+
+@pytest.fixture
+def fp32_parity():
+    old = torch.get_float32_matmul_precision()
+    torch.set_float32_matmul_precision("highest")
+    yield
+    torch.set_float32_matmul_precision(old)
+
+
+def _step(m, task, batch):
+    x, y, cond = batch
+    m.zero_grad(set_to_none=True)
+    if task == "gen":
+        m.switch_to_generate()
+        loss, logits, _ = m.step_task_gen((x, cond, y))
+    else:
+        m.switch_to_classification()
+        loss, logits, _ = m.step_task_class((x, cond, y))
+    loss.backward()
+    return loss, logits
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fname,kw,n_head,B,wseed,xseed,bias", CASES)
+def test_train_step_parity_fp32(fp32_parity, fname, kw, n_head, B, wseed, xseed, bias):
+    g = golden(fname)
+    m = make_model(kw, n_head, wseed, bias, "cuda").train()
+    batch = inputs(B, kw["seq_len"], kw["n_classes"], xseed, "cuda")
+    for t in ("gen", "cls"):
+        loss, logits = _step(m, t, batch)
+        np.testing.assert_allclose(logits.detach().cpu().numpy(), g[f"{t}/logits"], rtol=1e-4, atol=1e-4)
+        np.testing.assert_allclose(loss.item(), g[f"{t}/loss"], rtol=1e-5)
+        got = sorted(n for n, p in m.named_parameters() if p.grad is not None)
+        assert got == sorted(g[f"{t}/grad_names"].tolist())
+        for n, p in m.named_parameters():
+            if p.grad is None:
+                continue
+            ref = g[f"{t}/grad/{n}"]
+            np.testing.assert_allclose(p.grad.cpu().numpy(), ref, rtol=1e-3, atol=1e-4 * np.abs(ref).max() + 1e-7,
+                                       err_msg=f"{t} {n}")
+
+
+@pytest.mark.gpu
+def test_train_step_parity_full_size_fp32(fp32_parity):
+    g = golden("decoder_full_b2.npz")
+    m = make_model(FULL, 8, 405, device="cuda").train()
+    batch = inputs(2, 321, 514, 406, "cuda")
+    for t in ("gen", "cls"):
+        loss, logits = _step(m, t, batch)
+        lg = logits.detach().cpu().numpy()
+        if t == "gen":
+            np.testing.assert_allclose(lg[:, :, :32], g["gen/logits_slice"], rtol=1e-4, atol=1e-4)
+            np.testing.assert_allclose(lg[:, -1, :], g["gen/logits_lastrow"], rtol=1e-4, atol=1e-4)
+        else:
+            np.testing.assert_allclose(lg, g["cls/logits"], rtol=1e-4, atol=1e-4)
+        np.testing.assert_allclose(loss.item(), g[f"{t}/loss"], rtol=1e-5)
+        for n, p in m.named_parameters():
+            if p.grad is None:
+                continue
+            gn = np.linalg.norm(p.grad.double().cpu().numpy())
+            np.testing.assert_allclose(gn, g[f"{t}/gnorm/{n}"], rtol=2e-4, err_msg=f"{t} {n}")
+            sl = g[f"{t}/gslice/{n}"]
+            np.testing.assert_allclose(p.grad.reshape(-1)[:64].cpu().numpy(), sl, rtol=2e-3,
+                                       atol=2e-4 * np.abs(sl).max() + 1e-7, err_msg=f"{t} {n}")
+
+
+@pytest.mark.gpu
+def test_eval_forward_matches_train_forward_without_dropout(fp32_parity):
+    g = golden("decoder_small.npz")
+    m = make_model(SMALL, 4, 401, device="cuda").eval()
+    x, y, cond = inputs(4, 33, 34, 402, "cuda")
+    with torch.no_grad():
+        logits = m(x)
+        cls = m(x, generate=False)
+    np.testing.assert_allclose(logits.cpu().numpy(), g["gen/logits"], rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(cls.cpu().numpy(), g["cls/logits"], rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.gpu
+def test_bf16_tracks_fp32():
+    """'medium' precision (what train_transformer_mtasks.py sets) -> bf16 MFMA operands, fp32 accumulation."""
+    m = make_model(FULL, 8, 405, device="cuda").train()
+    batch = inputs(2, 321, 514, 406, "cuda")
+    old = torch.get_float32_matmul_precision()
+    try:
+        torch.set_float32_matmul_precision("highest")
+        l32, lg32 = _step(m, "gen", batch)
+        g32 = {n: p.grad.clone() for n, p in m.named_parameters() if p.grad is not None}
+        torch.set_float32_matmul_precision("medium")
+        l16, lg16 = _step(m, "gen", batch)
+    finally:
+        torch.set_float32_matmul_precision(old)
+    assert abs(l16.item() - l32.item()) < 2e-2 * abs(l32.item())
+    err = (lg16 - lg32).abs().max().item()
+    assert err < 5e-2 * lg32.abs().max().item() + 1e-2
+    for n, p in m.named_parameters():
+        if p.grad is None:
+            continue
+        rel = ((p.grad - g32[n]).norm() / (g32[n].norm() + 1e-12)).item()
+        assert rel < 5e-2, (n, rel)
+
+
+@pytest.mark.gpu
+def test_dropout_seeded_and_active():
+    m = make_model(SMALL, 4, 401, device="cuda", res_dropout=0.1).train()
+    x, y, cond = inputs(4, 33, 34, 402, "cuda")
+    torch.set_float32_matmul_precision("highest")
+    a = m(x).detach()
+    b = m(x).detach()
+    assert not torch.equal(a, b)                 # fresh mask per call
+    m.eval()
+    c = m(x).detach()
+    d = m(x).detach()
+    assert torch.equal(c, d)
+
+
+@pytest.mark.gpu
+def test_generate_greedy_matches_oracle_argmax(fp32_parity):
+    sd = od.det_state_dict(401, **SMALL)
+    m = make_model(SMALL, 4, 401, device="cuda").eval()
+    x0 = torch.tensor(gen.randint(9, (2, 3), 0, 34), device="cuda")
+    out = m.generate(x0)
+    assert out.shape == (2, 3 + 33)
+    # every greedy step picks the oracle's argmax of the last position (cropped context)
+    st = {k: torch.tensor(v) for k, v in sd.items()}
+    xs = out.cpu()
+    for t in range(3, 3 + 33):
+        ctx = xs[:, max(0, t - 33):t]
+        ref = od.decoder_forward(st, ctx, 4)[:, -1].argmax(-1)
+        assert torch.equal(ref, xs[:, t]), t
+
+
+@pytest.mark.gpu
+def test_sequence_longer_than_mask_raises():
+    m = make_model(SMALL, 4, 401, device="cuda").eval()
+    with pytest.raises(RuntimeError):
+        with torch.no_grad():
+            m(torch.zeros(1, 40, dtype=torch.long, device="cuda"))

@@ -74,7 +74,10 @@ SIGNATURES = {
     "aw_grad_norm_clip": [c_p, c_p, c_p, c_p, c_int, c_f, c_p, c_p, c_p, c_p],
     "aw_scale": [c_p, c_i64, c_p, c_p],
     "aw_layernorm_fwd": [c_p, c_i64, c_int, c_p, c_p, c_f, c_p, c_int, c_p, c_p, c_p],
-    "aw_layernorm_bwd": [c_p, c_p, c_i64, c_int, c_p, c_p, c_p, c_p, c_int, c_p, c_p, c_p],
+    "aw_layernorm_bwd": [c_p, c_p, c_i64, c_int, c_p, c_p, c_p, c_p, c_int, c_p, c_p, c_p, c_int, c_f,
+                         ctypes.c_uint64, c_p],
+    "aw_class_head_fwd": [c_p, c_i64, c_int, c_int, c_p, c_p, c_p, c_p, c_p, c_p, c_p],
+    "aw_class_head_bwd": [c_p, c_p, c_p, c_i64, c_int, c_int, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p],
     "aw_embed_fwd": [c_p, c_i64, c_int, c_int, c_p, c_p, c_p, c_p],
     "aw_embed_bwd": [c_p, c_i64, c_int, c_int, c_p, c_p, c_p],
     "aw_attn_fwd": [c_p, c_i64, c_int, c_int, c_int, c_int, c_p, c_p, c_p],

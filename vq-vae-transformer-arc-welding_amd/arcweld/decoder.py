@@ -1,0 +1,242 @@
+"""Fused latent-Transformer (MyTransformerDecoder) forward/backward on the HIP kernels.
+
+Reference: model/transformer_decoder.py:13-131 (+ model/transformer_block.py, model/embedding.py).
+Rows are the R = B*T tokens of a batch, row = b*T + t.  Per block:
+
+  a   = LN1(x)                       aw_layernorm_fwd (operand dtype)
+  qkv = a . Wqkv^T + b               aw_gemm                        [R][3d]
+  y   = causal attention(qkv)        aw_attn_fwd (flash-style, lse saved; the T x T matrix never exists)
+  x1  = x + drop(y . Wo^T + bo)      aw_gemm (bias + dropout + residual fused)
+  a2  = LN2(x1)
+  h   = a2 . Wfc^T + bfc             aw_gemm, C = h (f32, for GELU') and C2 = GELU_tanh(h) (operand dtype)
+  x2  = x1 + drop(g . Wp^T + bp)     aw_gemm
+
+Heads: lm_head (logits [R][V], ld padded to 8) + cross-entropy(ignore_index=-1), or the classification head
+(linear_1 -> GELU(erf) -> linear_2 over the sequence axis) + cross-entropy.  The backward mirrors the forward;
+dropout masks are regenerated from (seed, element), LayerNorm backward emits the masked operand of the preceding
+projection's gradient GEMMs directly.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import kernels as K
+from .vqvae import _mix, operand_dtype
+
+F32 = torch.float32
+
+
+def _pad8(n):
+    return (n + 7) // 8 * 8
+
+
+class DecSaved:
+    pass
+
+
+def _cast(t, T):
+    if t.dtype == T:
+        return t
+    out = torch.empty(t.shape, device=t.device, dtype=T)
+    K.cast(t, out)
+    return out
+
+
+def forward(m, ids, generate: bool, training: bool, need_backward: bool, seed: int = 0, dtype=None):
+    """ids (B, T) int64 -> logits (B, T, V) [generate] or (B, 2) [classify]."""
+    T_ = operand_dtype(dtype)
+    B, T = ids.shape
+    d = m.d_model
+    nh = m.n_head
+    R = B * T
+    dev = ids.device
+    V = m.n_classes
+    pe = m.embedding.positional_embedding.pe
+    if T > pe.shape[1]:
+        raise RuntimeError(f"The size of tensor a ({T}) must match the size of tensor b ({pe.shape[1]}) at "
+                           f"non-singleton dimension 1 (positional table capped at {pe.shape[1]} rows, "
+                           "model/embedding.py:49-50)")
+    if (not generate) and T != m.seq_len:
+        raise RuntimeError(f"classification head expects T == seq_len ({m.seq_len}), got {T}")
+    e = lambda *s, dt=F32: torch.empty(*s, device=dev, dtype=dt)  # noqa: E731
+    p_drop = float(m.res_dropout) if training else 0.0
+    sv = DecSaved()
+    sv.B, sv.T, sv.R, sv.d, sv.nh, sv.V, sv.Tdt, sv.generate = B, T, R, d, nh, V, T_, generate
+    sv.p_drop = p_drop
+    nb = len(m.transformer.h)
+    sv.seed_attn = [_mix(seed, 300 + i) for i in range(nb)]
+    sv.seed_mlp = [_mix(seed, 400 + i) for i in range(nb)]
+    ids = ids.contiguous()
+
+    x = e(R, d)
+    K.embed_fwd(ids, m.embedding.latent_embedding.weight, pe[0], x)
+    blocks = []
+    for i, blk in enumerate(m.transformer.h):
+        at, mlp = blk.attn, blk.mlp
+        Wqkv = _cast(at.c_attn.weight, T_)
+        Wo = _cast(at.c_proj.weight, T_)
+        Wfc = _cast(mlp.c_fc.weight, T_)
+        Wp = _cast(mlp.c_proj.weight, T_)
+        a, mu1, rs1 = e(R, d, dt=T_), e(R), e(R)
+        K.layernorm_fwd(x, blk.ln_1.weight, blk.ln_1.bias, blk.ln_1.eps, a, mu1, rs1)
+        qkv = e(R, 3 * d, dt=T_)
+        K.gemm(a, Wqkv, R, 3 * d, d, bias=at.c_attn.bias, C=qkv)
+        y, lse = e(R, d, dt=T_), e(B * nh * T)
+        K.attn_fwd(qkv, B, T, nh, d, y, lse)
+        x1 = e(R, d)
+        K.gemm(y, Wo, R, d, d, bias=at.c_proj.bias, drop=(p_drop, sv.seed_attn[i]), resid=x, C=x1)
+        a2, mu2, rs2 = e(R, d, dt=T_), e(R), e(R)
+        K.layernorm_fwd(x1, blk.ln_2.weight, blk.ln_2.bias, blk.ln_2.eps, a2, mu2, rs2)
+        h, g = e(R, 4 * d), e(R, 4 * d, dt=T_)
+        K.gemm(a2, Wfc, R, 4 * d, d, bias=mlp.c_fc.bias, act=K.AW_ACT_GELU_TANH, C=h, C2=g, c2_mode=1)
+        x2 = e(R, d)
+        K.gemm(g, Wp, R, d, 4 * d, bias=mlp.c_proj.bias, drop=(p_drop, sv.seed_mlp[i]), resid=x1, C=x2)
+        blocks.append(dict(x=x, a=a, mu1=mu1, rs1=rs1, qkv=qkv, y=y, lse=lse, x1=x1, a2=a2, mu2=mu2, rs2=rs2, h=h, g=g,
+                           Wqkv=Wqkv, Wo=Wo, Wfc=Wfc, Wp=Wp))
+        x = x2
+    lnf = m.transformer.ln_f
+    xf_dt = T_ if generate else F32
+    xf, muf, rsf = e(R, d, dt=xf_dt), e(R), e(R)
+    K.layernorm_fwd(x, lnf.weight, lnf.bias, lnf.eps, xf, muf, rsf)
+    sv.blocks, sv.x_last, sv.xf, sv.muf, sv.rsf = blocks, x, xf, muf, rsf
+    if generate:
+        Vp = _pad8(V)
+        Wlm = torch.zeros(Vp, d, device=dev, dtype=T_)        # padded rows stay zero (K padding of the dgrad)
+        K.cast(m.lm_head.weight, Wlm[:V])
+        logits_buf = e(R, Vp)
+        logits = logits_buf[:, :V]
+        K.gemm(xf, Wlm, R, V, d, C=logits)
+        sv.Wlm, sv.logits_buf, sv.Vp = Wlm, logits_buf, Vp
+        out = logits.view(B, T, V)
+    else:
+        ch = m.class_head
+        s, out = e(R), e(B, 2)
+        K.class_head_fwd(xf, B, T, ch.linear_1.weight, ch.linear_1.bias, ch.linear_2.weight, ch.linear_2.bias, s, out)
+        sv.s = s
+    return out, (sv if need_backward else None)
+
+
+def backward(m, sv, g_out, slot):
+    """g_out: gradient of the logits (B, T, V) f32 or of the class logits (B, 2)."""
+    B, T, R, d, nh, V, T_ = sv.B, sv.T, sv.R, sv.d, sv.nh, sv.V, sv.Tdt
+    dev = g_out.device
+    e = lambda *s, dt=F32: torch.empty(*s, device=dev, dtype=dt)  # noqa: E731
+    lnf = m.transformer.ln_f
+    nb = len(sv.blocks)
+    if sv.generate:
+        Vp = sv.Vp
+        gl = torch.zeros(R, Vp, device=dev, dtype=T_)
+        # strided cast into the zero-padded operand: GEMM epilogue with an empty contraction (v = 0 + resid)
+        K.gemm(gl, gl, R, V, 0, resid=g_out.reshape(R, V).contiguous(), C=gl[:, :V])
+        # lm_head weight gradient [V][d] and input gradient (K padded to Vp with zero rows/columns)
+        K.gemm(gl[:, :V], sv.xf, V, d, R, a_trans=True, b_trans=True, C=slot(m.lm_head.weight), accumulate=True)
+        gxf = e(R, d)
+        K.gemm(gl, sv.Wlm, R, d, Vp, b_trans=True, C=gxf)
+    else:
+        ch = m.class_head
+        gxf = e(R, d)
+        b1 = ch.linear_1.bias
+        b2 = ch.linear_2.bias
+        K.class_head_bwd(sv.xf, sv.s, g_out.contiguous(), B, T, ch.linear_1.weight, ch.linear_2.weight, gxf,
+                         slot(ch.linear_1.weight), slot(b1) if b1 is not None else None,
+                         slot(ch.linear_2.weight), slot(b2) if b2 is not None else None)
+    # ln_f backward -> residual-stream gradient gx (f32) + masked operand for the last block's MLP projection
+    gx = e(R, d)
+    go = e(R, d, dt=T_)
+    last = nb - 1
+    K.layernorm_bwd(sv.x_last, gxf, lnf.weight, sv.muf, sv.rsf, gx, False, slot(lnf.weight), slot(lnf.bias),
+                    dx2=go, drop=(sv.p_drop, sv.seed_mlp[last] if nb else 0))
+    for i in reversed(range(nb)):
+        blk = m.transformer.h[i]
+        at, mlp = blk.attn, blk.mlp
+        c = sv.blocks[i]
+        # ---- MLP
+        gh = e(R, 4 * d, dt=T_)
+        K.gemm(go, c["Wp"], R, 4 * d, d, b_trans=True, act=K.AW_ACT_GELU_TANH, pre=c["h"], C=gh)
+        K.gemm(go, c["g"], d, 4 * d, R, a_trans=True, b_trans=True, C=slot(mlp.c_proj.weight), accumulate=True,
+               a_rowsum=slot(mlp.c_proj.bias))
+        ga2 = e(R, d)
+        K.gemm(gh, c["Wfc"], R, d, 4 * d, b_trans=True, C=ga2)
+        K.gemm(gh, c["a2"], 4 * d, d, R, a_trans=True, b_trans=True, C=slot(mlp.c_fc.weight), accumulate=True,
+               a_rowsum=slot(mlp.c_fc.bias))
+        go2 = e(R, d, dt=T_)
+        K.layernorm_bwd(c["x1"], ga2, blk.ln_2.weight, c["mu2"], c["rs2"], gx, True, slot(blk.ln_2.weight),
+                        slot(blk.ln_2.bias), dx2=go2, drop=(sv.p_drop, sv.seed_attn[i]))
+        # ---- attention
+        gy = e(R, d, dt=T_)
+        K.gemm(go2, c["Wo"], R, d, d, b_trans=True, C=gy)
+        K.gemm(go2, c["y"], d, d, R, a_trans=True, b_trans=True, C=slot(at.c_proj.weight), accumulate=True,
+               a_rowsum=slot(at.c_proj.bias))
+        dqkv = e(R, 3 * d, dt=T_)
+        ws = e(B * nh * T)
+        K.attn_bwd(c["qkv"], c["y"], gy, c["lse"], B, T, nh, d, dqkv, ws)
+        K.gemm(dqkv, c["a"], 3 * d, d, R, a_trans=True, b_trans=True, C=slot(at.c_attn.weight), accumulate=True,
+               a_rowsum=slot(at.c_attn.bias))
+        ga = e(R, d)
+        K.gemm(dqkv, c["Wqkv"], R, d, 3 * d, b_trans=True, C=ga)
+        go = e(R, d, dt=T_) if i > 0 else None
+        K.layernorm_bwd(c["x"], ga, blk.ln_1.weight, c["mu1"], c["rs1"], gx, True, slot(blk.ln_1.weight),
+                        slot(blk.ln_1.bias), dx2=go, drop=(sv.p_drop, sv.seed_mlp[i - 1] if i > 0 else 0))
+    K.embed_bwd(sv_ids(sv), gx, slot(m.embedding.latent_embedding.weight))
+
+
+def sv_ids(sv):
+    return sv.ids
+
+
+class DecoderFunction(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, m, ids, generate, seed, *params):
+        out, sv = forward(m, ids, generate, m.training, need_backward=True, seed=seed)
+        sv.ids = ids.contiguous()
+        ctx.m, ctx.sv, ctx.params = m, sv, params
+        return out
+
+    @staticmethod
+    def backward(ctx, g_out):
+        m, sv = ctx.m, ctx.sv
+        sink = getattr(m, "_grad_sink", None)
+        grads = {}
+
+        def slot(p):
+            if sink is not None and p in sink:
+                return sink[p]
+            g = grads.get(p)
+            if g is None:
+                g = torch.zeros_like(p, dtype=F32)
+                grads[p] = g
+            return g
+
+        backward(m, sv, g_out.contiguous(), slot)
+        ctx.sv = None
+        return (None, None, None, None) + tuple(grads.get(p) for p in ctx.params)
+
+
+class _CrossEntropy(torch.autograd.Function):
+    """F.cross_entropy (mean over non-ignored rows) on the HIP kernels (transformer_decoder.py:226-230)."""
+
+    @staticmethod
+    def forward(ctx, logits2d, target, ignore_index):
+        R, V = logits2d.shape
+        lse = torch.empty(R, device=logits2d.device)
+        s = torch.zeros(2, device=logits2d.device, dtype=torch.float64)
+        K.ce_fwd(logits2d, V, target.contiguous(), ignore_index, s[0:1], s[1:2], lse)
+        out = torch.empty((), device=logits2d.device)
+        K.ce_finalize(s[0:1], s[1:2], out)
+        ctx.save_for_backward(logits2d, target, lse, s)
+        ctx.ignore = ignore_index
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        logits2d, target, lse, s = ctx.saved_tensors
+        R, V = logits2d.shape
+        dl = torch.empty(R, V, device=logits2d.device)
+        K.ce_bwd(logits2d, V, target.contiguous(), ctx.ignore, lse, s[1:2], g.reshape(1).contiguous(), dl)
+        return dl, None, None
+
+
+def cross_entropy(logits2d, target, ignore_index=-100):
+    if logits2d.stride(-1) != 1:
+        raise ValueError("logits rows must be contiguous")
+    return _CrossEntropy.apply(logits2d, target, ignore_index)

@@ -198,10 +198,21 @@ def layernorm_fwd(x, w, b, eps, y, mean, rstd, stream=None):
          ptr(rstd), stream_ptr(stream))
 
 
-def layernorm_bwd(x, dy, w, mean, rstd, dx, accumulate, dw, db, stream=None):
+def layernorm_bwd(x, dy, w, mean, rstd, dx, accumulate, dw, db, dx2=None, drop=(0.0, 0), stream=None):
     R, D = x.shape
     call("aw_layernorm_bwd", ptr(x), ptr(dy), R, D, ptr(w), ptr(mean), ptr(rstd), ptr(dx), int(accumulate), ptr(dw),
-         ptr(db), stream_ptr(stream))
+         ptr(db), ptr(dx2), dtype_code(dx2.dtype) if dx2 is not None else AW_F32, float(drop[0]),
+         int(drop[1]) & 0xFFFFFFFFFFFFFFFF, stream_ptr(stream))
+
+
+def class_head_fwd(xf, B, T, w1, b1, W2, b2, s, out, stream=None):
+    call("aw_class_head_fwd", ptr(xf), B, T, xf.shape[-1], ptr(w1), ptr(b1), ptr(W2), ptr(b2), ptr(s), ptr(out),
+         stream_ptr(stream))
+
+
+def class_head_bwd(xf, s, dout, B, T, w1, W2, dxf, dw1, db1, dW2, db2, stream=None):
+    call("aw_class_head_bwd", ptr(xf), ptr(s), ptr(dout), B, T, xf.shape[-1], ptr(w1), ptr(W2), ptr(dxf), ptr(dw1),
+         ptr(db1), ptr(dW2), ptr(db2), stream_ptr(stream))
 
 
 def embed_fwd(ids, wtok, pe, x, stream=None):

@@ -51,12 +51,18 @@ struct GemmP {
   aw_gemm_args a;
   int tiles_n, nblocks, splits, ksplit;
   int vec;   // every epilogue operand row is 16-B aligned: vectorised epilogue
+  int a_bytes, b_bytes;  // extents of A and B (buffer-descriptor ranges; < 2^31)
   float* ws; // split-K partial slabs [splits][M][N] (NULL: fp32 atomics)
 };
 
 enum { CONV_NONE = 0, CONV_ROWSHIFT = 1, CONV_KSHIFT = 2 };
 
 // ---------------------------------------------------------------- operand staging (global -> regs -> LDS)
+// Loads are raw buffer loads: an out-of-range byte offset returns zeros, which implements every mask
+// (M/N/K tails, implicit-conv window edges) without branches, so the compiler can keep two K steps of
+// loads in flight and wait with a counted vmcnt.
+constexpr int OOB = 0x7FFFFFF0;
+
 template <typename T, bool TR, int CONV, bool RAGGED>
 struct Stager {
   static constexpr int EPC = TT<T>::EPC, BK = TT<T>::BK;
@@ -65,13 +71,14 @@ struct Stager {
   const T* base;
   int64_t ld;
   int rows_total, row0, kend, cin, seg, dir;
-  uint4 v[NCH];
+  __amdgpu_buffer_rsrc_t rsrc;
   // per-thread invariants of the implicit convolution (window position / tap of each chunk)
   int wpos[NCH];    // ROWSHIFT: row % seg (fixed rows);  KSHIFT: (k0 + krow) % seg, advanced per K step
   int tapoff[NCH];  // KSHIFT: row shift j-1 of the chunk's column tap
   int colin[NCH];   // KSHIFT: column within the tap (m - j*cin)
 
-  __device__ __forceinline__ void init(int kbeg, int tid) {
+  __device__ __forceinline__ void init(int kbeg, int tid, int nbytes) {
+    rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, nbytes, 0x00020000);
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
       const int c = tid + i * NTHREADS;
@@ -87,46 +94,46 @@ struct Stager {
     }
   }
 
-  __device__ __forceinline__ void load(int k0, int tid) {
+  __device__ __forceinline__ uint4 bload(int off) const {
+    auto r = __builtin_amdgcn_raw_buffer_load_b128(rsrc, off, 0, 0);
+    uint4 u;
+    memcpy(&u, &r, 16);
+    return u;
+  }
+
+  __device__ __forceinline__ void load(int k0, int tid, uint4 (&v)[NCH]) {
     // ROWSHIFT: cin % BK == 0, so the tap is uniform over the whole K step
     const int jrow = (CONV == CONV_ROWSHIFT) ? k0 / cin : 0;
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
       const int c = tid + i * NTHREADS;
-      uint4 out = make_uint4(0, 0, 0, 0);
       if constexpr (!TR) {
         const int row = row0 + c / CPK;
         const int k = k0 + (c % CPK) * EPC;
         bool ok = row < rows_total && k < kend;
-        int64_t src = row;
-        int kk = k;
+        int src = row, kk = k;
         if constexpr (CONV == CONV_ROWSHIFT) {
           kk = k - jrow * cin;
           const int sft = dir * (jrow - 1);
           ok = ok && (wpos[i] + sft >= 0) && (wpos[i] + sft < seg);
           src = row + sft;
         }
-        if (ok) {
-          const T* p = base + src * ld + kk;
-          if constexpr (RAGGED) {
-            if (k + EPC > kend) {
-              T tmp[EPC];
+        if constexpr (RAGGED) {
+          if (ok && k + EPC > kend) {
+            const T* p = base + (int64_t)src * ld + kk;
+            T tmp[EPC];
 #pragma unroll
-              for (int e = 0; e < EPC; ++e) tmp[e] = (k + e < kend) ? p[e] : from_f32<T>(0.f);
-              memcpy(&out, tmp, 16);
-            } else {
-              out = *reinterpret_cast<const uint4*>(p);
-            }
-          } else {
-            out = *reinterpret_cast<const uint4*>(p);
+            for (int e = 0; e < EPC; ++e) tmp[e] = (k + e < kend) ? p[e] : from_f32<T>(0.f);
+            memcpy(&v[i], tmp, 16);
+            continue;
           }
         }
+        v[i] = bload(ok ? (int)(((int64_t)src * ld + kk) * (int)sizeof(T)) : OOB);
       } else {
         const int k = k0 + c / CPR;
         const int m = row0 + (c % CPR) * EPC;
         bool ok = k < kend && m < rows_total;
-        int64_t srck = k;
-        int mm = m;
+        int srck = k, mm = m;
         if constexpr (CONV == CONV_KSHIFT) {
           mm = colin[i];
           const int sft = tapoff[i];
@@ -135,27 +142,22 @@ struct Stager {
           wpos[i] += BK % seg;                 // advance the window position to the next K step
           if (wpos[i] >= seg) wpos[i] -= seg;
         }
-        if (ok) {
-          const T* p = base + srck * ld + mm;
-          if constexpr (RAGGED) {
-            if (m + EPC > rows_total) {
-              T tmp[EPC];
+        if constexpr (RAGGED) {
+          if (ok && m + EPC > rows_total) {
+            const T* p = base + (int64_t)srck * ld + mm;
+            T tmp[EPC];
 #pragma unroll
-              for (int e = 0; e < EPC; ++e) tmp[e] = (m + e < rows_total) ? p[e] : from_f32<T>(0.f);
-              memcpy(&out, tmp, 16);
-            } else {
-              out = *reinterpret_cast<const uint4*>(p);
-            }
-          } else {
-            out = *reinterpret_cast<const uint4*>(p);
+            for (int e = 0; e < EPC; ++e) tmp[e] = (m + e < rows_total) ? p[e] : from_f32<T>(0.f);
+            memcpy(&v[i], tmp, 16);
+            continue;
           }
         }
+        v[i] = bload(ok ? (int)(((int64_t)srck * ld + mm) * (int)sizeof(T)) : OOB);
       }
-      v[i] = out;
     }
   }
 
-  __device__ __forceinline__ void store(char* lds, int tid) const {
+  __device__ __forceinline__ void store(char* lds, int tid, const uint4 (&v)[NCH]) const {
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
       const int c = tid + i * NTHREADS;
@@ -267,7 +269,7 @@ __device__ __forceinline__ float a_row_partial(const char* lds, int tid) {
 }
 
 template <typename T, bool ATR, bool BTR, int ACONV, int BCONV, bool RAGGED>
-__global__ __launch_bounds__(NTHREADS, 2) void gemm_kernel(GemmP P) {
+__global__ __launch_bounds__(NTHREADS, RAGGED ? 1 : 2) void gemm_kernel(GemmP P) {
   constexpr int BK = TT<T>::BK;
   const aw_gemm_args& p = P.a;
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
@@ -283,10 +285,10 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_kernel(GemmP P) {
   const int kend = min(p.K, kbeg + P.ksplit);
 
   Stager<T, ATR, ACONV, RAGGED> sa{reinterpret_cast<const T*>(p.A), p.lda, M, m0, kend, p.conv_cin, p.conv_seg,
-                                   p.conv_dir, {}};
-  Stager<T, BTR, BCONV, RAGGED> sb{reinterpret_cast<const T*>(p.B), p.ldb, N, n0, kend, p.conv_cin, p.conv_seg, 1, {}};
-  sa.init(kbeg, tid);
-  sb.init(kbeg, tid);
+                                   p.conv_dir};
+  Stager<T, BTR, BCONV, RAGGED> sb{reinterpret_cast<const T*>(p.B), p.ldb, N, n0, kend, p.conv_cin, p.conv_seg, 1};
+  sa.init(kbeg, tid, P.a_bytes);
+  sb.init(kbeg, tid, P.b_bytes);
   const bool do_rowsum = p.a_rowsum != nullptr && tn == 0;
 
   f32x4 acc[4][4];
@@ -296,20 +298,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_kernel(GemmP P) {
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   float rowsum = 0.f;
 
-  const int nk = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
-  sa.load(kbeg, tid);
-  sb.load(kbeg, tid);
-  sa.store(smem, tid);
-  sb.store(smem + STAGE_OP, tid);
-  __syncthreads();
-
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) {
-      sa.load(kbeg + (kt + 1) * BK, tid);
-      sb.load(kbeg + (kt + 1) * BK, tid);
-    }
-    const char* a_l = smem + cur * 2 * STAGE_OP;
+  auto compute = [&](const char* a_l) {
     const char* b_l = a_l + STAGE_OP;
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
@@ -325,11 +314,34 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_kernel(GemmP P) {
         for (int j = 0; j < 4; ++j) Mfma<T>::run(acc[i][j], af[i], bfr[j]);
     }
     if (do_rowsum) rowsum += a_row_partial<T, ATR>(a_l, tid);
-    if (kt + 1 < nk) {
-      char* nxt = smem + (cur ^ 1) * 2 * STAGE_OP;
-      sa.store(nxt, tid);
-      sb.store(nxt + STAGE_OP, tid);
-    }
+  };
+
+  // Pipeline: LDS stage s holds K step t (t % 2 == s) while the registers of the other set carry the loads
+  // of step t+1 and the loads of step t+2 are issued at the top of step t: two steps of latency cover.
+  char* L0 = smem;
+  char* L1 = smem + 2 * STAGE_OP;
+  const int nk = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
+  uint4 ra0[NCH], rb0[NCH], ra1[NCH], rb1[NCH];
+  sa.load(kbeg, tid, ra0);
+  sb.load(kbeg, tid, rb0);
+  sa.load(kbeg + BK, tid, ra1);
+  sb.load(kbeg + BK, tid, rb1);
+  sa.store(L0, tid, ra0);
+  sb.store(L0 + STAGE_OP, tid, rb0);
+  __syncthreads();
+  for (int kt = 0; kt < nk; kt += 2) {
+    sa.load(kbeg + (kt + 2) * BK, tid, ra0);   // beyond kend: out-of-range -> zeros, never read
+    sb.load(kbeg + (kt + 2) * BK, tid, rb0);
+    compute(L0);
+    sa.store(L1, tid, ra1);
+    sb.store(L1 + STAGE_OP, tid, rb1);
+    __syncthreads();
+    if (kt + 1 >= nk) break;
+    sa.load(kbeg + (kt + 3) * BK, tid, ra1);
+    sb.load(kbeg + (kt + 3) * BK, tid, rb1);
+    compute(L1);
+    sa.store(L0, tid, ra0);
+    sb.store(L0 + STAGE_OP, tid, rb0);
     __syncthreads();
   }
 
@@ -603,6 +615,15 @@ extern "C" int aw_gemm_ws(const aw_gemm_args* args, float* ws, int64_t ws_elems,
     };
     P.vec = al(a.C, a.ldc, a.c_dtype) && al(a.C2, a.ldc2, a.c2_dtype) && al(a.pre, a.ld_pre, AW_F32) &&
             al(a.resid, a.ld_resid, AW_F32);
+  }
+  {
+    const int64_t es = a.a_dtype == AW_BF16 ? 2 : 4;
+    const int64_t ka = a.K > 0 ? a.K : 1;
+    const int64_t ea = (!a.a_trans ? ((int64_t)(a.M - 1) * a.lda + ka) : ((ka - 1) * a.lda + a.M)) * es;
+    const int64_t eb = (!a.b_trans ? ((int64_t)(a.N - 1) * a.ldb + ka) : ((ka - 1) * a.ldb + a.N)) * es;
+    AW_REQUIRE(ea < OOB && eb < OOB, "aw_gemm: operand extent >= 2 GiB is not supported");
+    P.a_bytes = (int)ea;
+    P.b_bytes = (int)eb;
   }
   // ragged: a contiguous extent that is not a whole number of 16-byte chunks
   const bool ragged = (!a.a_trans ? (a.K % epc) : (a.M % epc)) != 0 || (!a.b_trans ? (a.K % epc) : (a.N % epc)) != 0;

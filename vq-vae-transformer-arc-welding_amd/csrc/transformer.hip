@@ -32,11 +32,13 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ x
   }
 }
 
+template <typename T2>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ x, const float* __restrict__ dy,
                                                      int64_t R, int D, const float* __restrict__ w,
                                                      const float* __restrict__ mean, const float* __restrict__ rstd,
                                                      float* __restrict__ dx, int accumulate, float* __restrict__ dw,
-                                                     float* __restrict__ db) {
+                                                     float* __restrict__ db, T2* __restrict__ dx2, float drop_p,
+                                                     uint64_t drop_seed) {
   extern __shared__ float red[];  // 2*D
   for (int i = threadIdx.x; i < 2 * D; i += blockDim.x) red[i] = 0.f;
   __syncthreads();
@@ -61,9 +63,10 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ x
     for (int i = lane; i < D; i += 64) {
       const float xh = (xr[i] - mu) * rs;
       const float g = dyr[i] * w[i];
-      const float v = rs * (g - s1 - xh * s2);
-      if (accumulate) dx[r * D + i] += v;
-      else dx[r * D + i] = v;
+      float v = rs * (g - s1 - xh * s2);
+      if (accumulate) v += dx[r * D + i];
+      dx[r * D + i] = v;
+      if (dx2) dx2[r * D + i] = from_f32<T2>(v * aw_dropout_scale(drop_seed, (uint64_t)r * D + i, drop_p));
     }
   }
   __syncthreads();
@@ -365,6 +368,97 @@ __global__ __launch_bounds__(256) void ce_bwd_kernel(const float* __restrict__ l
     const float p = __expf(logits[r * ldl + i] - L);
     dl[r * ldd + i] = from_f32<T>(c * (p - (i == t ? 1.f : 0.f)));
   }
+  for (int i = V + lane; i < ldd; i += 64) dl[r * ldd + i] = from_f32<T>(0.f);
+}
+
+// ---------------------------------------------------------------- classification head
+__global__ __launch_bounds__(256) void class_s_kernel(const float* __restrict__ xf, int64_t R, int D,
+                                                      const float* __restrict__ w1, const float* __restrict__ b1,
+                                                      float* __restrict__ s) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  if (r >= R) return;
+  float a = 0.f;
+  for (int i = lane; i < D; i += 64) a = fmaf(xf[r * D + i], w1[i], a);
+  a = wave_sum(a);
+  if (lane == 0) s[r] = a + (b1 ? b1[0] : 0.f);
+}
+
+__global__ __launch_bounds__(64) void class_out_kernel(const float* __restrict__ s, int64_t B, int T,
+                                                       const float* __restrict__ W2, const float* __restrict__ b2,
+                                                       float* __restrict__ out) {
+  const int lane = threadIdx.x;
+  const int64_t b = blockIdx.x;
+  float a0 = 0.f, a1 = 0.f;
+  for (int t = lane; t < T; t += 64) {
+    const float g = gelu_erf(s[b * T + t]);
+    a0 = fmaf(g, W2[t], a0);
+    a1 = fmaf(g, W2[T + t], a1);
+  }
+  a0 = wave_sum(a0);
+  a1 = wave_sum(a1);
+  if (lane == 0) {
+    out[b * 2 + 0] = a0 + (b2 ? b2[0] : 0.f);
+    out[b * 2 + 1] = a1 + (b2 ? b2[1] : 0.f);
+  }
+}
+
+// per row r: ds = (sum_c dout[b][c] W2[c][t]) * gelu'(s); dxf[r] = ds * w1; dw1 += ds * xf[r]; db1 += ds
+__global__ __launch_bounds__(256) void class_bwd_rows_kernel(const float* __restrict__ xf, const float* __restrict__ s,
+                                                             const float* __restrict__ dout, int64_t R, int T, int D,
+                                                             const float* __restrict__ w1, const float* __restrict__ W2,
+                                                             float* __restrict__ dxf, float* __restrict__ dw1,
+                                                             float* __restrict__ db1) {
+  extern __shared__ float red[];  // D + 1
+  for (int i = threadIdx.x; i <= D; i += blockDim.x) red[i] = 0.f;
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  float dbsum = 0.f;
+  for (int64_t r = wave; r < R; r += nw) {
+    const int64_t b = r / T;
+    const int t = (int)(r - b * T);
+    const float dg = dout[b * 2] * W2[t] + dout[b * 2 + 1] * W2[T + t];
+    const float ds = dg * gelu_erf_grad(s[r]);
+    dbsum += ds;
+    for (int i = lane; i < D; i += 64) {
+      dxf[r * D + i] = ds * w1[i];
+      if (dw1) atomicAdd(&red[i], ds * xf[r * D + i]);
+    }
+  }
+  if (lane == 0) atomicAdd(&red[D], dbsum);
+  __syncthreads();
+  for (int i = threadIdx.x; i < D; i += blockDim.x)
+    if (dw1) atomicAdd(dw1 + i, red[i]);
+  if (threadIdx.x == 0 && db1) atomicAdd(db1, red[D]);
+}
+
+// dW2[c][t] += sum_b dout[b][c] g[b,t];  db2[c] += sum_b dout[b][c]
+__global__ void class_bwd_w2_kernel(const float* __restrict__ s, const float* __restrict__ dout, int64_t B, int T,
+                                    float* __restrict__ dW2, float* __restrict__ db2) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < T) {
+    float a0 = 0.f, a1 = 0.f;
+    for (int64_t b = 0; b < B; ++b) {
+      const float g = gelu_erf(s[b * T + t]);
+      a0 = fmaf(dout[b * 2], g, a0);
+      a1 = fmaf(dout[b * 2 + 1], g, a1);
+    }
+    if (dW2) {
+      dW2[t] += a0;
+      dW2[T + t] += a1;
+    }
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0 && db2) {
+    float c0 = 0.f, c1 = 0.f;
+    for (int64_t b = 0; b < B; ++b) {
+      c0 += dout[b * 2];
+      c1 += dout[b * 2 + 1];
+    }
+    db2[0] += c0;
+    db2[1] += c1;
+  }
 }
 
 __global__ void ce_finalize_kernel(const double* s, const double* c, float* out) { out[0] = (float)(s[0] / c[0]); }
@@ -390,12 +484,19 @@ extern "C" int aw_layernorm_fwd(const float* x, int64_t R, int D, const float* w
 }
 
 extern "C" int aw_layernorm_bwd(const float* x, const float* dy, int64_t R, int D, const float* w, const float* mean,
-                                const float* rstd, float* dx, int accumulate, float* dw, float* db, void* stream) {
+                                const float* rstd, float* dx, int accumulate, float* dw, float* db, void* dx2,
+                                int dx2_dtype, float drop_p, uint64_t drop_seed, void* stream) {
   AW_REQUIRE(x && dy && w && mean && rstd && dx && dw && db && R >= 0 && D > 0 && D <= 8192,
              "aw_layernorm_bwd: bad args");
   if (R == 0) return AW_OK;
-  hipLaunchKernelGGL(ln_bwd_kernel, dim3(gridcap(R * 64, 256, 512)), dim3(256), 2 * D * sizeof(float),
-                     reinterpret_cast<hipStream_t>(stream), x, dy, R, D, w, mean, rstd, dx, accumulate, dw, db);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  dim3 grid(gridcap(R * 64, 256, 512));
+  if (dx2_dtype == AW_BF16)
+    hipLaunchKernelGGL(ln_bwd_kernel<bf16>, grid, dim3(256), 2 * D * sizeof(float), s, x, dy, R, D, w, mean, rstd, dx,
+                       accumulate, dw, db, (bf16*)dx2, drop_p, drop_seed);
+  else
+    hipLaunchKernelGGL(ln_bwd_kernel<float>, grid, dim3(256), 2 * D * sizeof(float), s, x, dy, R, D, w, mean, rstd, dx,
+                       accumulate, dw, db, (float*)dx2, drop_p, drop_seed);
   return aw::check_launch("aw_layernorm_bwd");
 }
 
@@ -507,6 +608,30 @@ extern "C" int aw_ce_bwd(const float* logits, int64_t R, int V, int64_t ldl, con
     hipLaunchKernelGGL(ce_bwd_kernel<float>, dim3(aw_cdiv(R, 4)), dim3(256), 0, s, logits, R, V, ldl, y, ignore_index,
                        lse, count, g, (float*)dlogits, ldd);
   return aw::check_launch("aw_ce_bwd");
+}
+
+extern "C" int aw_class_head_fwd(const float* xf, int64_t B, int T, int D, const float* w1, const float* b1,
+                                 const float* W2, const float* b2, float* s, float* out, void* stream) {
+  AW_REQUIRE(xf && w1 && W2 && s && out && B >= 0 && T > 0 && D > 0, "aw_class_head_fwd: bad args");
+  if (B == 0) return AW_OK;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int64_t R = B * T;
+  hipLaunchKernelGGL(class_s_kernel, dim3(aw_cdiv(R, 4)), dim3(256), 0, st, xf, R, D, w1, b1, s);
+  hipLaunchKernelGGL(class_out_kernel, dim3((unsigned)B), dim3(64), 0, st, s, B, T, W2, b2, out);
+  return aw::check_launch("aw_class_head_fwd");
+}
+
+extern "C" int aw_class_head_bwd(const float* xf, const float* s, const float* dout, int64_t B, int T, int D,
+                                 const float* w1, const float* W2, float* dxf, float* dw1, float* db1, float* dW2,
+                                 float* db2, void* stream) {
+  AW_REQUIRE(xf && s && dout && w1 && W2 && dxf && B >= 0 && T > 0 && D > 0, "aw_class_head_bwd: bad args");
+  if (B == 0) return AW_OK;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int64_t R = B * T;
+  hipLaunchKernelGGL(class_bwd_rows_kernel, dim3(gridcap(R * 64, 256, 256)), dim3(256), (D + 1) * sizeof(float), st,
+                     xf, s, dout, R, T, D, w1, W2, dxf, dw1, db1);
+  hipLaunchKernelGGL(class_bwd_w2_kernel, dim3(aw_cdiv(T, 256)), dim3(256), 0, st, s, dout, B, T, dW2, db2);
+  return aw::check_launch("aw_class_head_bwd");
 }
 
 extern "C" int aw_ce_finalize(const double* loss_sum, const double* count, float* out, void* stream) {

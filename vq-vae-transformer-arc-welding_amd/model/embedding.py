@@ -1,0 +1,62 @@
+"""Token + positional embeddings -- drop-in for model/embedding.py of the reference (same buffers/parameters)."""
+import math
+
+import torch
+from torch import nn
+
+from arcweld import kernels as K
+
+
+class PositionalEmbedding(nn.Module):
+    """Fixed sinusoidal table (reference :6-24), buffer 'pe' of shape (1, max_len, d_model)."""
+
+    def __init__(self, d_model, max_len=5000):
+        super().__init__()
+        pe = torch.zeros(max_len, d_model).float()
+        pe.require_grad = False
+        position = torch.arange(0, max_len).float().unsqueeze(1)
+        div_term = (torch.arange(0, d_model, 2).float() * -(math.log(10000.0) / d_model)).exp()
+        pe[:, 0::2] = torch.sin(position * div_term)
+        pe[:, 1::2] = torch.cos(position * div_term)
+        self.register_buffer('pe', pe.unsqueeze(0))
+
+    def forward(self, x):
+        return self.pe[:, :x.size(1)]
+
+
+class LatentEmbeddingCond(nn.Module):
+    """Reference :27-43 (unused by the entry points); kept for state_dict/API compatibility."""
+
+    def __init__(self, input_size: int, d_model: int, cond_size: int) -> None:
+        super().__init__()
+        self.positional_embedding = PositionalEmbedding(d_model=d_model, max_len=input_size)
+        self.latent_embedding = nn.Embedding(num_embeddings=input_size, embedding_dim=d_model)
+        self.cond_embedding = nn.Embedding(num_embeddings=cond_size, embedding_dim=d_model)
+
+    def forward(self, x, cond):
+        raise NotImplementedError("LatentEmbeddingCond is unused by the reference entry points (out of scope)")
+
+
+class LatentEmbedding(nn.Module):
+    """latent_embedding(ids) + pe[:T] (reference :45-59); the PE table is capped at seq_len rows (default 512)."""
+
+    def __init__(self, input_size: int, d_model: int, seq_len: int = 512) -> None:
+        super().__init__()
+        self.positional_embedding = PositionalEmbedding(d_model=d_model, max_len=seq_len)
+        self.latent_embedding = nn.Embedding(num_embeddings=input_size, embedding_dim=d_model)
+        self.input_size = input_size
+        self.d_model = d_model
+        self.seq_len = seq_len
+
+    def forward(self, x):
+        if torch.is_grad_enabled() and self.latent_embedding.weight.requires_grad:
+            raise NotImplementedError("LatentEmbedding alone is inference-only on the HIP path; train through "
+                                      "MyTransformerDecoder.forward")
+        B, T = x.shape
+        if T > self.positional_embedding.pe.shape[1]:
+            raise RuntimeError(f"The size of tensor a ({T}) must match the size of tensor b "
+                               f"({self.positional_embedding.pe.shape[1]}) at non-singleton dimension 1")
+        out = torch.empty(B, T, self.d_model, device=x.device)
+        K.embed_fwd(x.contiguous(), self.latent_embedding.weight, self.positional_embedding.pe[0],
+                    out.view(B * T, self.d_model))
+        return out
