@@ -40,6 +40,10 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-profile", action="store_true", help="skip the live per-GEMM event timing")
+    ap.add_argument("--no-transformer", action="store_true",
+                    help="skip the secondary configs[2] line item (tokenize + 8-block Transformer train step)")
+    ap.add_argument("--seqs", type=int, default=51, help="Transformer sequences per GPU per step (configs[2])")
+    ap.add_argument("--n-cycles", type=int, default=20)
     return ap.parse_args()
 
 
@@ -49,6 +53,61 @@ def build_model(dev):
     m = VQVAEPatch(hidden_dim=512, input_dim=2, num_embeddings=512, embedding_dim=64, n_resblocks=8,
                    learning_rate=1e-3, dropout_p=0.1, patch_size=25, seq_len=200, batch_norm=False)
     return m.to(dev).train()
+
+
+def transformer_workload(dev, rank, world, args):
+    """configs[2]: per step the frozen VQ-VAE encoder tokenizes seqs x n_cycles windows (fused encoder + VQ, exact
+    fp32 operands), then one train step of the 8-block/8-head d512 decoder on the generation task
+    (T = 16*n_cycles + 1 = 321, V = 514, accumulate 1, clip 0.8, RAdam betas (0.9, 0.95) wd 0.1 on Linear weights).
+    Returns windows/s over all ranks and ms/step."""
+    from arcweld import tokenize
+    from arcweld.trainer import Trainer
+    from model.transformer_decoder import MyTransformerDecoder
+    vq = build_model(dev).eval()
+    nc = args.n_cycles
+    torch.manual_seed(2)
+    dec = MyTransformerDecoder(d_model=512, n_classes=514, seq_len=16 * nc + 1, n_blocks=8, n_head=8,
+                               res_dropout=0.1).to(dev).train()
+    tr = Trainer(gradient_clip_val=0.8)
+    tr.setup_optimizer(dec)
+    g = torch.Generator(device=dev)
+    g.manual_seed(2000 + rank)
+    wins = [torch.randn(args.seqs, 200 * nc, 2, device=dev, generator=g) for _ in range(2)]
+    cond = torch.zeros(args.seqs, dtype=torch.long, device=dev)
+
+    def step(i):
+        ids = tokenize.encode_ids(vq, wins[i % 2])
+        x, y, _ = tokenize.autoregressive_pairs(ids, start_token=512)
+        tr.micro_step(dec, (x, cond, y), i, 1.0 / world)
+        tr.optimizer_step(dec)
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    t = torch.tensor([el], device=dev, dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    el = float(t.item())
+    windows = world * args.seqs * nc * args.steps
+    flops_seq = 3 * (8 * (24 * 512 * 512 * (16 * nc + 1) + 2 * 512 * (16 * nc + 1) * (16 * nc + 2))
+                     + 2 * 512 * 514 * (16 * nc + 1))
+    return {"value": round(windows / el, 2), "unit": "windows/s", "ms_per_step": round(el * 1e3 / args.steps, 3),
+            "config": {"workload": "tokenize (frozen VQ-VAE encoder, fp32 exact) + Transformer train step "
+                                   "(configs[2])", "seqs_per_gpu": args.seqs, "n_cycles": nc, "T": 16 * nc + 1,
+                       "d_model": 512, "n_blocks": 8, "n_head": 8, "V": 514, "global_batch_windows": windows //
+                       args.steps},
+            "transformer_tflops": round(flops_seq * args.seqs * world * args.steps / el / 1e12, 2)}
 
 
 def cpu_baseline(seconds):
@@ -150,6 +209,10 @@ def main():
                     "avg_launch_us": round(ms * 1e3 / n, 2), "avg_algorithmic_gflop_per_launch": round(flops / n / 1e9, 4),
                     "gemm_share_of_step": round(ms / (elapsed * 1e3), 4)}
 
+    secondary = None
+    if not args.no_transformer:
+        secondary = transformer_workload(dev, rank, world, args)
+
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
@@ -162,7 +225,7 @@ def main():
                            "global_batch": world * args.batch, "per_gpu_batch": args.batch, "seq_len": 200,
                            "codebook": "512x64", "hidden": 512, "n_resblocks": 8, "patch": 25,
                            "parallelism": f"dp{world}", "clip": 0.7, "optimizer": "RAdam(lr 1e-3)"},
-                "roofline": roofline, "cpu_baseline": cpu}
+                "roofline": roofline, "cpu_baseline": cpu, "transformer": secondary}
         print(json.dumps(line), flush=True)
     if distributed:
         dist.destroy_process_group()

@@ -25,6 +25,8 @@ from __future__ import annotations
 
 import math
 
+import numpy as np
+
 import torch
 import torch.nn.functional as F
 
@@ -197,3 +199,29 @@ def reference_state_dict_shapes(cfg: VQVAEConfig):
 def det_state_dict(cfg: VQVAEConfig, base: int):
     from oracle import gen
     return {k: gen.param_value(base, k, s) for k, s in reference_state_dict_shapes(cfg).items()}
+
+
+def encode_ids(sd, x, cfg: VQVAEConfig, n_cycles: int):
+    """Frozen-encoder tokenization, restating the reference loop (latentspace_dataloader.py:154-161, 228-250):
+    for each window i: patch_embed -> encoder -> VQ idx (B*S,) -> (B, S); stack (n_cycles, B, S), swap to
+    (B, n_cycles, S) and flatten the trailing axes (:261).  x: (B, n_cycles*L, C) numpy f32 -> int64 (B, n_cycles*S).
+    Eval semantics: torch.no_grad, dropout off (encoder BN off, --batchnorm 0)."""
+    st = {k: torch.as_tensor(v) for k, v in sd.items()}
+    t_x = []
+    with torch.no_grad():
+        for i in range(n_cycles):
+            xi = torch.as_tensor(np.ascontiguousarray(x[:, i * cfg.L:(i + 1) * cfg.L, :]))
+            cap = {}
+            vqvae_forward(st, xi, cfg, train=False, capture=cap)
+            t_x.append(cap["idx"].numpy().reshape(xi.shape[0], -1))
+    return np.array(t_x).swapaxes(0, 1).reshape(x.shape[0], -1).astype(np.int64)
+
+
+def autoregressive_pairs(data):
+    """MyLatentAutoregressiveDataset (base_dataloader.py:84-97): start = max+1, end = max+2, classes = max+3;
+    x = [start, ids], y = [ids, end]."""
+    mx = int(np.max(data))
+    n = len(data)
+    x = np.concatenate([np.full((n, 1), mx + 1), data], axis=1)
+    y = np.concatenate([data, np.full((n, 1), mx + 2)], axis=1)
+    return x, y, mx + 3

@@ -53,7 +53,6 @@ class Trainer:
         self.max_epochs = max_epochs
         self.max_steps = max_steps
         self.logger = logger
-        self.callbacks = callbacks
         self.gradient_clip_val = gradient_clip_val
         self.accumulate = max(1, int(accumulate_grad_batches))
         self.log_every = log_every_n_steps
@@ -61,6 +60,11 @@ class Trainer:
         self.global_step = 0
         self.history = []
         self.optimizer = None
+        self.callbacks = [] if callbacks is None else (list(callbacks) if isinstance(callbacks, (list, tuple))
+                                                       else [callbacks])
+        self.logged_metrics = {}
+        self.should_stop = False
+        self.current_epoch = 0
 
     # ------------------------------------------------------------------------------ loop pieces
     def setup_optimizer(self, model):
@@ -92,48 +96,79 @@ class Trainer:
         opt.zero_grad()
         self.global_step += 1
 
-    def fit(self, model, datamodule=None, train_dataloaders=None):
+    def fit(self, model, datamodule=None, train_dataloaders=None, val_dataloaders=None):
         if datamodule is not None:
             datamodule.setup("fit")
             loader = datamodule.train_dataloader()
+            val_loader = datamodule.val_dataloader() if hasattr(datamodule, "val_dataloader") else None
         else:
-            loader = train_dataloaders
+            loader, val_loader = train_dataloaders, val_dataloaders
         model.train()
         model.trainer = self
         self.setup_optimizer(model)
+        self.should_stop = False
         dev = next(model.parameters()).device
         scale = 1.0 / (self.accumulate * world())
         t0 = time.time()
         for epoch in range(self.max_epochs):
+            self.current_epoch = epoch
             if hasattr(loader, "set_epoch"):
                 loader.set_epoch(epoch)
+            n = len(loader) if hasattr(loader, "__len__") else None
             for i, batch in enumerate(loader):
                 batch = _to_device(batch, dev)
                 loss = self.micro_step(model, batch, i, scale)
-                if (i + 1) % self.accumulate == 0:
+                # Lightning steps on every accumulate-th batch and on the last batch of the epoch
+                if (i + 1) % self.accumulate == 0 or (n is not None and i + 1 == n):
                     self.optimizer_step(model)
                     if self.global_step % self.log_every == 0:
                         self.history.append((self.global_step, float(loss.detach()), time.time() - t0))
                     if 0 < self.max_steps <= self.global_step:
                         break
-            if 0 < self.max_steps <= self.global_step:
+            if val_loader is not None:
+                metrics = self.evaluate(model, val_loader, "val")
+                self.logged_metrics.update(metrics)
+                if self.logger is not None and hasattr(self.logger, "log_metrics"):
+                    self.logger.log_metrics({"epoch": epoch, **metrics}, step=self.global_step)
+                for cb in self.callbacks:
+                    if hasattr(cb, "on_validation_end"):
+                        cb.on_validation_end(self, model, metrics)
+            if self.should_stop or 0 < self.max_steps <= self.global_step:
                 break
         model._grad_sink = None
         return self
 
     @torch.no_grad()
     def evaluate(self, model, loader, stage="val"):
+        """Runs validation_step/test_step over the loader; every logged scalar is averaged over the epoch
+        (weighted by batch size, Lightning's on_epoch reduction) and, under DDP, over ranks."""
         model.eval()
         dev = next(model.parameters()).device
-        tot, n = 0.0, 0
+        sums, total = {}, 0
         for i, batch in enumerate(loader):
             batch = _to_device(batch, dev)
-            out = (model.validation_step if stage == "val" else model.test_step)(batch, i)
-            loss = out["loss"] if isinstance(out, dict) else out
-            tot += float(loss)
-            n += 1
+            model._logged = {}
+            (model.validation_step if stage == "val" else model.test_step)(batch, i)
+            bs = len(batch[0]) if isinstance(batch, (list, tuple)) else len(batch)
+            for k, v in model.logged.items():
+                v = v.float() if isinstance(v, torch.Tensor) else torch.tensor(float(v), device=dev)
+                sums[k] = sums.get(k, 0.0) + v * bs
+            total += bs
         model.train()
-        return tot / max(n, 1)
+        if not sums:
+            return {}
+        keys = sorted(sums)
+        vec = torch.stack([sums[k] for k in keys] + [torch.tensor(float(total), device=dev)])
+        if world() > 1 and stage == "val":
+            dist.all_reduce(vec)
+        vec = vec.cpu()
+        return {k: float(vec[j] / vec[-1]) for j, k in enumerate(keys)}
+
+    def validate(self, model, datamodule=None, dataloaders=None):
+        if datamodule is not None:
+            datamodule.setup("fit")
+            dataloaders = datamodule.val_dataloader()
+        return self.evaluate(model, dataloaders, "val")
 
     def test(self, model, datamodule=None, dataloaders=None):
         if datamodule is not None:
@@ -141,7 +176,56 @@ class Trainer:
             loader = datamodule.test_dataloader()
         else:
             loader = dataloaders
-        return self.evaluate(model, loader, stage="test")
+        metrics = self.evaluate(model, loader, stage="test")
+        self.logged_metrics.update(metrics)
+        if self.logger is not None and hasattr(self.logger, "log_metrics"):
+            self.logger.log_metrics(metrics, step=self.global_step)
+        return [metrics]
+
+
+class EarlyStopping:
+    """lightning EarlyStopping(monitor, min_delta, patience, mode) evaluated at the end of each validation."""
+
+    def __init__(self, monitor, min_delta=0.0, patience=3, verbose=False, mode="min"):
+        self.monitor, self.min_delta, self.patience, self.mode = monitor, abs(min_delta), patience, mode
+        self.best, self.wait = None, 0
+
+    def on_validation_end(self, trainer, model, metrics):
+        if self.monitor not in metrics:
+            return
+        v = metrics[self.monitor]
+        better = (self.best is None or (v < self.best - self.min_delta if self.mode == "min"
+                                        else v > self.best + self.min_delta))
+        if better:
+            self.best, self.wait = v, 0
+        else:
+            self.wait += 1
+            if self.wait >= self.patience:
+                trainer.should_stop = True
+
+
+class ModelCheckpoint:
+    """Saves the best (by ``monitor``) and, with save_last, the last model as Lightning-layout checkpoints
+    (rank 0 only)."""
+
+    def __init__(self, dirpath, monitor=None, mode="min", filename="best", save_last=False):
+        self.dirpath, self.monitor, self.mode, self.filename, self.save_last = dirpath, monitor, mode, filename, \
+            save_last
+        self.best, self.best_model_path = None, None
+
+    def on_validation_end(self, trainer, model, metrics):
+        import os
+        if dist.is_available() and dist.is_initialized() and dist.get_rank() != 0:
+            return
+        os.makedirs(self.dirpath, exist_ok=True)
+        if self.monitor in metrics:
+            v = metrics[self.monitor]
+            if self.best is None or (v < self.best if self.mode == "min" else v > self.best):
+                self.best = v
+                self.best_model_path = os.path.join(self.dirpath, self.filename + ".ckpt")
+                model.save_checkpoint(self.best_model_path)
+        if self.save_last:
+            model.save_checkpoint(os.path.join(self.dirpath, "last.ckpt"))
 
 
 def _to_device(batch, dev):

@@ -192,6 +192,52 @@ def forward(m, x, training: bool, need_backward: bool, dtype=None, seed: int = 0
     return emb_loss, x_hat, perplexity, idx, sv
 
 
+@torch.no_grad()
+def encode(m, x, dtype=F32):
+    """Frozen-encoder tokenization: windows (W, L, C) f32 -> (codebook indices (W*S,) int64, z (W*S, D) f32).
+
+    patch embed -> encoder ResBlocks (eval: no dropout) -> sep conv -> VQ argmin; the decoder is never run
+    (latentspace_dataloader.py:154-161 calls only patch_embed/encoder/vector_quantization).  Operands default to
+    exact fp32 so the indices are the reference's bit for bit; ``dtype=torch.bfloat16`` trades that for speed.
+    """
+    T = operand_dtype(dtype)
+    if x.dtype != F32 or x.dim() != 3:
+        raise ValueError("expected float32 windows of shape (W, seq_len, input_dim)")
+    x = x.contiguous()
+    sh = VQVAEShapes(m, x.shape[0])
+    H, D, N, R, P = sh.H, sh.D, sh.N, sh.R, sh.P
+    if x.shape[1] != sh.L or x.shape[2] != sh.C:
+        raise ValueError(f"expected windows (W, {sh.L}, {sh.C}), got {tuple(x.shape)}")
+    pr = _params(m)
+    e = lambda *s, dt=F32: torch.empty(*s, device=x.device, dtype=dt)  # noqa: E731
+    Wp = e(H, sh.ldp, dt=T)
+    K.weight_relayout(pr["pe"].weight, H, 1, P, 0, 4, Wp, ldo=sh.ldp)
+    patches = e(N, sh.ldp, dt=T)
+    K.patchify(x, P, patches)
+    xr, a = e(N, H), e(N, H, dt=T)
+    K.gemm(patches, Wp, N, H, sh.ldp, bias=pr["pe"].bias, C=xr, C2=a, c2_mode=1, flops=2 * N * H * P)
+    w1, w2 = e(H, H, dt=T), e(H, H, dt=T)
+    h, a1 = e(N, H), e(N, H, dt=T)
+    for r, (c1, c2) in enumerate(pr["enc"]):
+        K.weight_relayout(c1.weight, H, H, 3, 1, 0, w1)
+        K.weight_relayout(c2.weight, H, H, 3, 1, 0, w2)
+        K.gemm(a, w1, N, H, H, bias=c1.bias, C=h, C2=a1, c2_mode=1)
+        if r < R - 1:   # x <- x + conv2(gelu(h)) in place (row-local epilogue), a <- gelu(x)
+            K.gemm(a1, w2, N, H, H, bias=c2.bias, resid=xr, C=xr, C2=a, c2_mode=1)
+        else:           # the sep conv consumes x_R itself (no GELU): write it in the operand dtype
+            K.gemm(a1, w2, N, H, H, bias=c2.bias, resid=xr, C=a)
+    xR_T = a if R > 0 else (xr if T == F32 else _cast(xr, T))
+    Ws = e(D, H, dt=T)
+    K.weight_relayout(pr["sep"].weight, D, H, 1, 0, 0, Ws)
+    z = e(N, D)
+    K.gemm(xR_T, Ws, N, D, H, bias=pr["sep"].bias, C=z)
+    zq, idx = e(N, D), e(N, dt=torch.int64)
+    counts = torch.zeros(sh.K, device=x.device)
+    sq = torch.zeros(1, device=x.device, dtype=torch.float64)
+    K.vq_forward(z, pr["E"], zq, idx, counts, sq)
+    return idx, z
+
+
 def _cast(t, T):
     out = torch.empty(t.shape, device=t.device, dtype=T)
     K.cast(t, out)
