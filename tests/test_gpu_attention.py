@@ -1,0 +1,78 @@
+"""Causal attention kernels (aw_attn_fwd / aw_attn_bwd) against a plain torch fp32 reference of
+CausalSelfAttention (model/transformer_block.py:37-63, attention dropout 0).  fp32 operands -> the VALU
+kernels (tolerance 1e-4); bf16 operands -> the MFMA kernels at head size 64 (VALU otherwise), compared on the
+same bf16-rounded inputs with bf16-output tolerance."""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def reference(qkv, B, T, nh, d, dy):
+    q, k, v = qkv.float().view(B, T, 3 * d).split(d, dim=2)
+    hs = d // nh
+    q = q.reshape(B, T, nh, hs).transpose(1, 2).requires_grad_()
+    k = k.reshape(B, T, nh, hs).transpose(1, 2).requires_grad_()
+    v = v.reshape(B, T, nh, hs).transpose(1, 2).requires_grad_()
+    att = (q @ k.transpose(-2, -1)) / math.sqrt(hs)
+    mask = torch.tril(torch.ones(T, T, device=qkv.device, dtype=torch.bool))
+    att = att.masked_fill(~mask, float("-inf"))
+    lse = torch.logsumexp(att, dim=-1)
+    y = (torch.softmax(att, dim=-1) @ v).transpose(1, 2).reshape(B * T, d)
+    y.backward(dy.float())
+    dq = q.grad.transpose(1, 2).reshape(B * T, d)
+    dk = k.grad.transpose(1, 2).reshape(B * T, d)
+    dv = v.grad.transpose(1, 2).reshape(B * T, d)
+    return y.detach(), lse.detach().reshape(-1), torch.cat([dq, dk, dv], dim=1)
+
+
+def run(qkv, B, T, nh, d, dy):
+    from arcweld import kernels as K
+    R = B * T
+    y = torch.empty(R, d, device="cuda", dtype=qkv.dtype)
+    lse = torch.empty(B * nh * T, device="cuda")
+    K.attn_fwd(qkv, B, T, nh, d, y, lse)
+    dqkv = torch.empty(R, 3 * d, device="cuda", dtype=qkv.dtype)
+    ws = torch.empty(B * nh * T, device="cuda")
+    K.attn_bwd(qkv, y, dy, lse, B, T, nh, d, dqkv, ws)
+    return y, lse, dqkv
+
+
+def _inputs(B, T, d, dtype, seed):
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    qkv = torch.randn(B * T, 3 * d, device="cuda", generator=g).to(dtype)
+    dy = torch.randn(B * T, d, device="cuda", generator=g).to(dtype)
+    return qkv, dy
+
+
+@pytest.mark.parametrize("T", [1, 33, 64, 65, 128, 200, 321])
+@pytest.mark.parametrize("hs", [16, 64])
+def test_attention_fp32(T, hs):
+    B, nh = 2, 2
+    d = hs * nh
+    qkv, dy = _inputs(B, T, d, torch.float32, T + hs)
+    y, lse, dqkv = run(qkv, B, T, nh, d, dy)
+    ry, rl, rg = reference(qkv, B, T, nh, d, dy)
+    torch.testing.assert_close(y, ry, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(lse, rl, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(dqkv, rg, rtol=1e-4, atol=2e-4)
+
+
+@pytest.mark.parametrize("T", [1, 17, 64, 65, 127, 128, 129, 200, 257, 321])
+@pytest.mark.parametrize("hs,nh", [(64, 2), (64, 8), (32, 4)])
+def test_attention_bf16(T, hs, nh):
+    B = 3
+    d = hs * nh
+    qkv, dy = _inputs(B, T, d, torch.bfloat16, 7 * T + hs)
+    y, lse, dqkv = run(qkv, B, T, nh, d, dy)
+    ry, rl, rg = reference(qkv, B, T, nh, d, dy)
+    torch.testing.assert_close(y.float(), ry, rtol=2e-2, atol=2e-2)
+    torch.testing.assert_close(lse, rl, rtol=1e-3, atol=1e-3)
+    err = (dqkv.float() - rg).abs().max().item()
+    assert err <= 3e-2 * rg.abs().max().item() + 2e-2, err
+    # relative Frobenius error of each of dq, dk, dv
+    for j in range(3):
+        a, r = dqkv.float()[:, j * d:(j + 1) * d], rg[:, j * d:(j + 1) * d]
+        assert (a - r).norm().item() <= 1e-2 * r.norm().item() + 1e-4, j   # dq is exactly 0 at T = 1

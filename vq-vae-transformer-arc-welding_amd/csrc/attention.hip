@@ -1,0 +1,414 @@
+// Causal self-attention on MFMA for bf16 operands, head size 64 (model/transformer_block.py:37-63 at the
+// transformer configs: d_model 512 / 8 heads).  Flash-style: the T x T matrices never reach HBM; the forward
+// keeps the running max / sum per query and saves lse = ln sum_j exp(q.k_j / sqrt(hs)); the backward recomputes
+// P from it.
+//
+// All products use v_mfma_f32_32x32x16_bf16.  Its 32x32 f32 result X has the COLUMN on the lane (r = lane & 31)
+// and rows 8*(i>>2) + 4*h + (i&3) in register i (h = lane >> 5), so a following MFMA that sums over X's row
+// index takes X straight from the registers as its B operand: k-step s of that product uses registers
+// 8s..8s+7, element j <-> row 16s + 8(j>>2) + 4h + (j&3) of X; its A operand supplies the same permuted k order,
+// read with ds_read_b64_tr_b16 (4 consecutive LDS rows per read).
+//
+//   forward (query on the lane):  S^T = K.Q^T       softmax over the rows (keys) -> P^T
+//                                 O^T += V^T.P^T    (V^T via transposed reads of the V tile)
+//   dQ      (query on the lane):  S^T = K.Q^T, dP^T = V.dO^T, dS^T = P^T (dP^T - delta)
+//                                 dQ^T += K^T.dS^T
+//   dK, dV  (key on the lane):    S = Q.K^T, dP = dO.V^T, dS = P (dP - delta)
+//                                 dV^T += dO^T.P,  dK^T += Q^T.dS
+//
+// Tiles of 64 rows x 64 head dims (128-byte rows) are staged in LDS in one image that serves both the 16-byte
+// row reads (A operands) and the transposed reads: 16-byte chunk c of row r lives at chunk c ^ f(r),
+// f(r) = ((r >> 1) & 1) << 2 | ((r >> 2) & 3) -- conflict-free for both kinds of read (checked against the
+// ds_read_b128 lane groups and the 32-lane halves of ds_read_b64_tr_b16).
+#include "common.h"
+
+namespace {
+
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+typedef short v4i16 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
+
+constexpr int HS = 64;       // head size served here
+constexpr int ROWB = 128;    // bytes per LDS row (64 bf16)
+constexpr int TILE = 64;     // rows per staged tile
+constexpr int WROWS = 32;    // rows (queries or keys) per wave
+constexpr int BLK = 128;     // rows per workgroup (4 waves)
+constexpr int IMG = TILE * ROWB;
+
+__device__ __forceinline__ int swz(int r) { return (((r >> 1) & 1) << 2) | ((r >> 2) & 3); }
+__device__ __forceinline__ int img_off(int r, int c) { return r * ROWB + ((c ^ swz(r)) << 4); }
+
+__device__ __forceinline__ f32x16 mfma32(const uint4& a, const uint4& b, const f32x16& c) {
+  bf16x8 av, bv;
+  memcpy(&av, &a, 16);
+  memcpy(&bv, &b, 16);
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bv, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ f32x16 zero16() {
+  f32x16 z;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) z[i] = 0.f;
+  return z;
+}
+
+// 16-byte A/B fragment of row `r` for k-step `ks` (head dims 16ks + 8h .. +7)
+__device__ __forceinline__ uint4 row_frag(const char* img, int r, int ks, int h) {
+  return *reinterpret_cast<const uint4*>(img + img_off(r, 2 * ks + h));
+}
+
+// Transposed fragment: A operand of a product summing over the tile's rows, k-step covering rows
+// rb + {0..3} and rb + 8 + {0..3} (rb = 16 s + 4 h), columns (head dims) 32 dt + (lane & 31).
+__device__ __forceinline__ uint4 tr_frag(const char* img, int rb, int dt, int lane) {
+  const int G = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const int col = 32 * dt + 16 * (G & 1) + 4 * p;       // head dim of the 4 elements this lane addresses
+  const int c = col >> 3, within = (col & 7) * 2;
+  const int r0 = rb + q, r1 = rb + 8 + q;
+  const v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(uintptr_t)(img + img_off(r0, c) + within));
+  const v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(uintptr_t)(img + img_off(r1, c) + within));
+  uint4 out;
+  memcpy(&out, &lo, 8);
+  memcpy(reinterpret_cast<char*>(&out) + 8, &hi, 8);
+  return out;
+}
+
+// Registers 8s..8s+7 of an accumulator as a bf16 B fragment
+__device__ __forceinline__ uint4 pack8(const f32x16& a, int s) {
+  bf16x8 v;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = (bf16)a[8 * s + j];
+  uint4 u;
+  memcpy(&u, &v, 16);
+  return u;
+}
+
+// Global -> registers for one 64-row tile (rows r0.., row stride ld elements, column offset col0); rows >= T
+// are zero.  Thread t carries chunks t and t + 256 of the 512.
+struct TileRegs {
+  uint4 v[2];
+};
+__device__ __forceinline__ void tile_load(TileRegs& tr, const bf16* src, int64_t ld, int col0, int r0, int T_,
+                                          int tid) {
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int c = tid + 256 * u, row = c >> 3, ch = c & 7;
+    const int gr = r0 + row;
+    tr.v[u] = gr < T_ ? *reinterpret_cast<const uint4*>(src + (int64_t)gr * ld + col0 + ch * 8) : make_uint4(0, 0, 0, 0);
+  }
+}
+__device__ __forceinline__ void tile_store(const TileRegs& tr, char* img, int tid) {
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int c = tid + 256 * u, row = c >> 3, ch = c & 7;
+    *reinterpret_cast<uint4*>(img + img_off(row, ch)) = tr.v[u];
+  }
+}
+
+__device__ __forceinline__ void store4_bf16(bf16* dst, const f32x16& a, int g4, float s) {
+  bf16 v[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) v[e] = (bf16)(a[4 * g4 + e] * s);
+  uint2 u;
+  memcpy(&u, v, 8);
+  *reinterpret_cast<uint2*>(dst) = u;
+}
+
+// ---------------------------------------------------------------- forward
+// grid (ceil(T/128), n_head, B), 256 threads; wave w owns queries qb*128 + 32w .. +31.
+__global__ __launch_bounds__(256) void attn_fwd_mfma_kernel(const bf16* __restrict__ qkv, int T_, int nh, int d,
+                                                            bf16* __restrict__ y, float* __restrict__ lse,
+                                                            float c2, float scale) {
+  __shared__ __attribute__((aligned(16))) char Ks[IMG];
+  __shared__ __attribute__((aligned(16))) char Vs[IMG];
+  const int nqb = (T_ + BLK - 1) / BLK;
+  const int qb = nqb - 1 - (int)blockIdx.x;  // longest key ranges first
+  const int h = blockIdx.y, b = blockIdx.z;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = lane & 31, hf = lane >> 5;
+  const int64_t ld = 3 * (int64_t)d;
+  const bf16* base = qkv + (int64_t)b * T_ * ld;
+  const int qw = qb * BLK + w * WROWS, q = qw + r;
+  const int qc = min(q, T_ - 1);
+  uint4 qf[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) qf[s] = *reinterpret_cast<const uint4*>(base + (int64_t)qc * ld + h * HS + 16 * s + 8 * hf);
+  f32x16 o[2] = {zero16(), zero16()};
+  float m = -__builtin_huge_valf(), l = 0.f;
+  const int kend = min(T_, qb * BLK + BLK);
+  const int nt = (kend + TILE - 1) / TILE;
+  TileRegs kr, vr;
+  tile_load(kr, base, ld, d + h * HS, 0, T_, tid);
+  tile_load(vr, base, ld, 2 * d + h * HS, 0, T_, tid);
+  for (int t = 0; t < nt; ++t) {
+    const int k0 = t * TILE;
+    __syncthreads();
+    tile_store(kr, Ks, tid);
+    tile_store(vr, Vs, tid);
+    __syncthreads();
+    if (t + 1 < nt) {
+      tile_load(kr, base, ld, d + h * HS, k0 + TILE, T_, tid);
+      tile_load(vr, base, ld, 2 * d + h * HS, k0 + TILE, T_, tid);
+    }
+    if (k0 > qw + WROWS - 1) continue;  // wave-uniform: the whole tile lies after this wave's queries
+    f32x16 s[2];
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      s[st] = zero16();
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) s[st] = mfma32(row_frag(Ks, 32 * st + r, ks, hf), qf[ks], s[st]);
+    }
+    const bool edge = (k0 + TILE - 1 > qw) || (k0 + TILE > T_);
+    float mx = -__builtin_huge_valf();
+#pragma unroll
+    for (int st = 0; st < 2; ++st)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        if (edge) {
+          const int key = k0 + 32 * st + 8 * (i >> 2) + 4 * hf + (i & 3);
+          if (key > q || key >= T_) s[st][i] = -__builtin_huge_valf();
+        }
+        mx = fmaxf(mx, s[st][i]);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float mn = fmaxf(m, mx);
+    const float alpha = exp2f((m - mn) * c2);
+    const float mc = mn * c2;
+    m = mn;
+    float ls = 0.f;
+#pragma unroll
+    for (int st = 0; st < 2; ++st)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const float p = exp2f(s[st][i] * c2 - mc);
+        s[st][i] = p;
+        ls += p;
+      }
+    l = l * alpha + ls;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) o[dt][i] *= alpha;
+#pragma unroll
+    for (int st = 0; st < 2; ++st)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const uint4 pb = pack8(s[st], s2);
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt) o[dt] = mfma32(tr_frag(Vs, 32 * st + 16 * s2 + 4 * hf, dt, lane), pb, o[dt]);
+      }
+  }
+  l += __shfl_xor(l, 32, 64);
+  if (q < T_) {
+    const float inv = 1.f / l;
+    bf16* yr = y + ((int64_t)b * T_ + q) * d + h * HS;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) store4_bf16(yr + 32 * dt + 8 * g4 + 4 * hf, o[dt], g4, inv);
+    if (hf == 0) lse[((int64_t)b * nh + h) * T_ + q] = m * scale + logf(l);
+  }
+}
+
+// ---------------------------------------------------------------- dQ (query-stationary)
+__global__ __launch_bounds__(256) void attn_dq_mfma_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ dy,
+                                                           const float* __restrict__ lse,
+                                                           const float* __restrict__ delta, int T_, int nh, int d,
+                                                           bf16* __restrict__ dqkv, float c2, float scale) {
+  __shared__ __attribute__((aligned(16))) char Ks[IMG];
+  __shared__ __attribute__((aligned(16))) char Vs[IMG];
+  const int nqb = (T_ + BLK - 1) / BLK;
+  const int qb = nqb - 1 - (int)blockIdx.x;
+  const int h = blockIdx.y, b = blockIdx.z;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = lane & 31, hf = lane >> 5;
+  const int64_t ld = 3 * (int64_t)d;
+  const bf16* base = qkv + (int64_t)b * T_ * ld;
+  const bf16* gbase = dy + (int64_t)b * T_ * d;
+  const int qw = qb * BLK + w * WROWS, q = qw + r;
+  const int qc = min(q, T_ - 1);
+  uint4 qf[4], gf[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    qf[s] = *reinterpret_cast<const uint4*>(base + (int64_t)qc * ld + h * HS + 16 * s + 8 * hf);
+    gf[s] = *reinterpret_cast<const uint4*>(gbase + (int64_t)qc * d + h * HS + 16 * s + 8 * hf);
+  }
+  const int64_t st_i = ((int64_t)b * nh + h) * T_ + qc;
+  const float L2 = lse[st_i] * 1.4426950408889634f, Dl = delta[st_i];
+  f32x16 acc[2] = {zero16(), zero16()};
+  const int kend = min(T_, qb * BLK + BLK);
+  const int nt = (kend + TILE - 1) / TILE;
+  TileRegs kr, vr;
+  tile_load(kr, base, ld, d + h * HS, 0, T_, tid);
+  tile_load(vr, base, ld, 2 * d + h * HS, 0, T_, tid);
+  for (int t = 0; t < nt; ++t) {
+    const int k0 = t * TILE;
+    __syncthreads();
+    tile_store(kr, Ks, tid);
+    tile_store(vr, Vs, tid);
+    __syncthreads();
+    if (t + 1 < nt) {
+      tile_load(kr, base, ld, d + h * HS, k0 + TILE, T_, tid);
+      tile_load(vr, base, ld, 2 * d + h * HS, k0 + TILE, T_, tid);
+    }
+    if (k0 > qw + WROWS - 1) continue;
+    const bool edge = (k0 + TILE - 1 > qw) || (k0 + TILE > T_);
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      f32x16 s = zero16(), dp = zero16();
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        s = mfma32(row_frag(Ks, 32 * st + r, ks, hf), qf[ks], s);
+        dp = mfma32(row_frag(Vs, 32 * st + r, ks, hf), gf[ks], dp);
+      }
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        float p = exp2f(s[i] * c2 - L2);
+        if (edge) {
+          const int key = k0 + 32 * st + 8 * (i >> 2) + 4 * hf + (i & 3);
+          if (key > q || key >= T_) p = 0.f;
+        }
+        s[i] = p * (dp[i] - Dl);
+      }
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const uint4 db = pack8(s, s2);
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt) acc[dt] = mfma32(tr_frag(Ks, 32 * st + 16 * s2 + 4 * hf, dt, lane), db, acc[dt]);
+      }
+    }
+  }
+  if (q < T_) {
+    bf16* out = dqkv + ((int64_t)b * T_ + q) * ld + h * HS;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) store4_bf16(out + 32 * dt + 8 * g4 + 4 * hf, acc[dt], g4, scale);
+  }
+}
+
+// ---------------------------------------------------------------- dK, dV (key-stationary)
+// grid (ceil(T/128), n_head, B); wave w owns keys kb*128 + 32w .. +31; query tiles from the block's first key on.
+__global__ __launch_bounds__(256) void attn_dkv_mfma_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ dy,
+                                                            const float* __restrict__ lse,
+                                                            const float* __restrict__ delta, int T_, int nh, int d,
+                                                            bf16* __restrict__ dqkv, float c2, float scale) {
+  __shared__ __attribute__((aligned(16))) char Qs[IMG];
+  __shared__ __attribute__((aligned(16))) char Gs[IMG];
+  __shared__ __attribute__((aligned(16))) float Ls[TILE];
+  __shared__ __attribute__((aligned(16))) float Ds[TILE];
+  const int kb = blockIdx.x;  // early key blocks see the most queries: launched first
+  const int h = blockIdx.y, b = blockIdx.z;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = lane & 31, hf = lane >> 5;
+  const int64_t ld = 3 * (int64_t)d;
+  const bf16* base = qkv + (int64_t)b * T_ * ld;
+  const bf16* gbase = dy + (int64_t)b * T_ * d;
+  const int kw = kb * BLK + w * WROWS, key = kw + r;
+  const int kc = min(key, T_ - 1);
+  uint4 kf[4], vf[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    kf[s] = *reinterpret_cast<const uint4*>(base + (int64_t)kc * ld + d + h * HS + 16 * s + 8 * hf);
+    vf[s] = *reinterpret_cast<const uint4*>(base + (int64_t)kc * ld + 2 * d + h * HS + 16 * s + 8 * hf);
+  }
+  f32x16 dk[2] = {zero16(), zero16()}, dv[2] = {zero16(), zero16()};
+  const int64_t sbase = ((int64_t)b * nh + h) * T_;
+  const int qstart = (kb * BLK / TILE) * TILE;
+  TileRegs qr, gr;
+  float lsv = 0.f, dsv = 0.f;
+  auto load = [&](int q0) {
+    tile_load(qr, base, ld, h * HS, q0, T_, tid);
+    tile_load(gr, gbase, d, h * HS, q0, T_, tid);
+    if (tid < TILE) {
+      const int qq = q0 + tid;
+      lsv = qq < T_ ? lse[sbase + qq] * 1.4426950408889634f : 0.f;
+      dsv = qq < T_ ? delta[sbase + qq] : 0.f;
+    }
+  };
+  load(qstart);
+  for (int q0 = qstart; q0 < T_; q0 += TILE) {
+    __syncthreads();
+    tile_store(qr, Qs, tid);
+    tile_store(gr, Gs, tid);
+    if (tid < TILE) {
+      Ls[tid] = lsv;
+      Ds[tid] = dsv;
+    }
+    __syncthreads();
+    if (q0 + TILE < T_) load(q0 + TILE);
+    if (q0 + TILE - 1 < kw) continue;  // every query of the tile precedes this wave's keys
+    const bool edge = (q0 < kw + WROWS - 1) || (q0 + TILE > T_);
+#pragma unroll
+    for (int qs = 0; qs < 2; ++qs) {
+      f32x16 s = zero16(), dp = zero16();
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        s = mfma32(row_frag(Qs, 32 * qs + r, ks, hf), kf[ks], s);
+        dp = mfma32(row_frag(Gs, 32 * qs + r, ks, hf), vf[ks], dp);
+      }
+      f32x16 p;
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int ql = 32 * qs + 8 * g4 + 4 * hf;  // first of this register group's 4 queries (tile-local)
+        const float4 L4 = *reinterpret_cast<const float4*>(Ls + ql);
+        const float4 D4 = *reinterpret_cast<const float4*>(Ds + ql);
+        const float Lv[4] = {L4.x, L4.y, L4.z, L4.w}, Dv[4] = {D4.x, D4.y, D4.z, D4.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int i = 4 * g4 + e;
+          float pv = exp2f(s[i] * c2 - Lv[e]);
+          if (edge) {
+            const int qq = q0 + ql + e;
+            if (qq < key || qq >= T_) pv = 0.f;
+          }
+          p[i] = pv;
+          s[i] = pv * (dp[i] - Dv[e]);
+        }
+      }
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const uint4 pb = pack8(p, s2), db = pack8(s, s2);
+        const int rb = 32 * qs + 16 * s2 + 4 * hf;
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt) {
+          dv[dt] = mfma32(tr_frag(Gs, rb, dt, lane), pb, dv[dt]);
+          dk[dt] = mfma32(tr_frag(Qs, rb, dt, lane), db, dk[dt]);
+        }
+      }
+    }
+  }
+  if (key < T_) {
+    bf16* out = dqkv + ((int64_t)b * T_ + key) * ld + h * HS;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        store4_bf16(out + d + 32 * dt + 8 * g4 + 4 * hf, dk[dt], g4, scale);
+        store4_bf16(out + 2 * d + 32 * dt + 8 * g4 + 4 * hf, dv[dt], g4, 1.f);
+      }
+  }
+}
+
+}  // namespace
+
+namespace aw {
+
+bool attn_mfma_supported(int dtype, int hs, int d) {
+  return dtype == AW_BF16 && hs == HS && d % 8 == 0;
+}
+
+void attn_fwd_mfma(const void* qkv, int64_t B, int T, int nh, int d, void* y, float* lse, hipStream_t s) {
+  const float scale = 1.0f / sqrtf((float)HS);
+  dim3 grid((T + BLK - 1) / BLK, nh, (unsigned)B);
+  hipLaunchKernelGGL(attn_fwd_mfma_kernel, grid, dim3(256), 0, s, (const bf16*)qkv, T, nh, d, (bf16*)y, lse,
+                     scale * 1.4426950408889634f, scale);
+}
+
+void attn_bwd_mfma(const void* qkv, const void* dy, const float* lse, const float* delta, int64_t B, int T, int nh,
+                   int d, void* dqkv, hipStream_t s) {
+  const float scale = 1.0f / sqrtf((float)HS);
+  dim3 grid((T + BLK - 1) / BLK, nh, (unsigned)B);
+  hipLaunchKernelGGL(attn_dq_mfma_kernel, grid, dim3(256), 0, s, (const bf16*)qkv, (const bf16*)dy, lse, delta, T,
+                     nh, d, (bf16*)dqkv, scale * 1.4426950408889634f, scale);
+  hipLaunchKernelGGL(attn_dkv_mfma_kernel, grid, dim3(256), 0, s, (const bf16*)qkv, (const bf16*)dy, lse, delta, T,
+                     nh, d, (bf16*)dqkv, scale * 1.4426950408889634f, scale);
+}
+
+}  // namespace aw

@@ -4,6 +4,13 @@
 // saved log-sum-exp), and cross-entropy with ignore_index.
 #include "common.h"
 
+namespace aw {  // attention.hip: MFMA path for bf16, head size 64
+bool attn_mfma_supported(int dtype, int hs, int d);
+void attn_fwd_mfma(const void* qkv, int64_t B, int T, int nh, int d, void* y, float* lse, hipStream_t s);
+void attn_bwd_mfma(const void* qkv, const void* dy, const float* lse, const float* delta, int64_t B, int T, int nh,
+                   int d, void* dqkv, hipStream_t s);
+}  // namespace aw
+
 namespace {
 
 // ---------------------------------------------------------------- LayerNorm (one wave per row)
@@ -530,6 +537,10 @@ extern "C" int aw_attn_fwd(const void* qkv, int64_t B, int T, int n_head, int d,
   AW_REQUIRE(hs == 16 || hs == 32 || hs == 64 || hs == 128, "aw_attn_fwd: head size %d unsupported", hs);
   if (B == 0) return AW_OK;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (aw::attn_mfma_supported(dtype, hs, d)) {
+    aw::attn_fwd_mfma(qkv, B, T, n_head, d, y, lse, s);
+    return aw::check_launch("aw_attn_fwd");
+  }
   dim3 grid(aw_cdiv(T, ATT_ROWS), n_head, (unsigned)B);
   const float scale = 1.0f / sqrtf((float)hs);
 #define AW_F(HSV)                                                                                          \
@@ -560,6 +571,12 @@ extern "C" int aw_attn_bwd(const void* qkv, const void* y, const void* dy, const
   dim3 grid(aw_cdiv(T, ATT_ROWS), n_head, (unsigned)B);
   const float scale = 1.0f / sqrtf((float)hs);
   const int64_t nrows = B * n_head * T;
+  if (aw::attn_mfma_supported(dtype, hs, d)) {
+    hipLaunchKernelGGL((attn_delta_kernel<bf16, 64>), dim3(gridcap(nrows)), dim3(256), 0, s, (const bf16*)y,
+                       (const bf16*)dy, B, T, n_head, d, ws);
+    aw::attn_bwd_mfma(qkv, dy, lse, ws, B, T, n_head, d, dqkv, s);
+    return aw::check_launch("aw_attn_bwd");
+  }
 #define AW_B(HSV)                                                                                                  \
   if (dtype == AW_BF16) {                                                                                          \
     hipLaunchKernelGGL((attn_delta_kernel<bf16, HSV>), dim3(gridcap(nrows)), dim3(256), 0, s, (const bf16*)y,       \
