@@ -68,6 +68,9 @@ typedef struct {
    *                              =  c*col_mul + col_off                          (col_mod == 0)
    * so weight gradients land directly in the reference layouts (conv (O,I,3) taps, ConvT (I,O,k)). */
   int accumulate, col_mod, col_mul, col_off;
+  /* seed_ptr != NULL: the dropout seeds become mix(drop_seed, *seed_ptr) and mix(drop2_seed, *seed_ptr), with
+   * *seed_ptr read on the device (a per-step counter, so one captured HIP graph replays with fresh masks). */
+  const uint64_t* seed_ptr;
 } aw_gemm_args;
 
 int aw_gemm(const aw_gemm_args* args, void* stream);
@@ -159,7 +162,12 @@ int aw_mse_finalize(const double* sqerr, int64_t numel, float* out, void* stream
  * first (clip coefficient; NULL = 1). */
 int aw_radam_step(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, const int64_t* seg_off,
                   const int64_t* seg_len, const float* seg_wd, const int* seg_active, int nseg, int64_t total, int64_t step,
-                  float lr, float beta1, float beta2, float eps, const float* gscale, void* stream);
+                  float lr, float beta1, float beta2, float eps, const float* gscale, const int64_t* step_ptr,
+                  void* stream);
+/* Device step counter / RNG counter: *counter += v (one thread; graph-capture safe).  With step_ptr != NULL,
+ * aw_radam_step reads the step number from the device (the host `step` is ignored) and derives the bias
+ * corrections and rectification there, in double precision like torch's python-float scalars. */
+int aw_counter_add(int64_t* counter, int64_t v, void* stream);
 /* Global L2 norm of the active segments of `grad` -> out_norm (f32 device scalar) and the clip coefficient
  * min(max_norm/(norm+1e-6), 1) -> out_coef (Lightning gradient_clip_val -> clip_grad_norm_).  ws: f64[1]. */
 int aw_grad_norm_clip(const float* grad, const int64_t* seg_off, const int64_t* seg_len, const int* seg_active,
@@ -177,7 +185,7 @@ int aw_layernorm_fwd(const float* x, int64_t R, int D, const float* w, const flo
  * the preceding block's output-projection gradients (mask regenerated, never stored). */
 int aw_layernorm_bwd(const float* x, const float* dy, int64_t R, int D, const float* w, const float* mean,
                      const float* rstd, float* dx, int accumulate, float* dw, float* db, void* dx2, int dx2_dtype,
-                     float drop_p, uint64_t drop_seed, void* stream);
+                     float drop_p, uint64_t drop_seed, const uint64_t* seed_ptr, void* stream);
 /* Classification head (transformer_decoder.py:126-129): s[r] = xf[r].w1 (+b1), g = GELU_erf(s),
  * out[b][c] = sum_t g[b*T+t] W2[c][t] (+b2[c]).  b1/b2 may be NULL (class_h_bias=False). */
 int aw_class_head_fwd(const float* xf, int64_t B, int T, int D, const float* w1, const float* b1, const float* W2,

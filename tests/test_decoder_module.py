@@ -166,13 +166,14 @@ def test_bf16_tracks_fp32():
 
 
 @pytest.mark.gpu
-def test_dropout_seeded_and_active():
+def test_dropout_seeded_and_active(fp32_parity):
     m = make_model(SMALL, 4, 401, device="cuda", res_dropout=0.1).train()
     x, y, cond = inputs(4, 33, 34, 402, "cuda")
-    torch.set_float32_matmul_precision("highest")
     a = m(x).detach()
     b = m(x).detach()
     assert not torch.equal(a, b)                 # fresh mask per call
+    m._rng_counter.zero_()
+    assert torch.equal(m(x).detach(), a)         # the per-call part of the seed is the device counter
     m.eval()
     c = m(x).detach()
     d = m(x).detach()

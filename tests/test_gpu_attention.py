@@ -76,3 +76,38 @@ def test_attention_bf16(T, hs, nh):
     for j in range(3):
         a, r = dqkv.float()[:, j * d:(j + 1) * d], rg[:, j * d:(j + 1) * d]
         assert (a - r).norm().item() <= 1e-2 * r.norm().item() + 1e-4, j   # dq is exactly 0 at T = 1
+
+
+@pytest.mark.parametrize("D", [64, 512])
+@pytest.mark.parametrize("out_dtype", [torch.float32, torch.bfloat16])
+def test_layernorm_fwd_bwd(D, out_dtype):
+    """aw_layernorm_fwd / aw_layernorm_bwd (vectorised at D % 256 == 0) vs torch layer_norm in fp32, including
+    the accumulate-into-dx form and the dropout-masked operand copy dx2 (regenerated mask)."""
+    from arcweld import kernels as K
+    R = 1000
+    g = torch.Generator(device="cuda").manual_seed(D)
+    x = torch.randn(R, D, device="cuda", generator=g) * 3 + 1
+    w = torch.randn(D, device="cuda", generator=g)
+    b = torch.randn(D, device="cuda", generator=g)
+    dy = torch.randn(R, D, device="cuda", generator=g)
+    y = torch.empty(R, D, device="cuda", dtype=out_dtype)
+    mu, rs = torch.empty(R, device="cuda"), torch.empty(R, device="cuda")
+    K.layernorm_fwd(x, w, b, 1e-5, y, mu, rs)
+    xr = x.clone().requires_grad_()
+    wr, br = w.clone().requires_grad_(), b.clone().requires_grad_()
+    ry = torch.nn.functional.layer_norm(xr, (D,), wr, br, 1e-5)
+    tol = 1e-5 if out_dtype == torch.float32 else 1e-2
+    torch.testing.assert_close(y.float(), ry.detach(), rtol=tol, atol=tol)
+    ry.backward(dy)
+    prior = torch.randn(R, D, device="cuda", generator=g)
+    dx = prior.clone()
+    dw, db = torch.zeros(D, device="cuda"), torch.zeros(D, device="cuda")
+    dx2 = torch.empty(R, D, device="cuda", dtype=out_dtype)
+    K.layernorm_bwd(x, dy, w, mu, rs, dx, True, dw, db, dx2=dx2, drop=(0.25, 1234))
+    torch.testing.assert_close(dx, prior + xr.grad, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(dw, wr.grad, rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(db, br.grad, rtol=1e-4, atol=1e-3)
+    kept = dx2.float() != 0
+    frac = kept.float().mean().item()
+    assert 0.72 < frac < 0.78
+    torch.testing.assert_close(dx2.float()[kept], (dx / 0.75)[kept], rtol=tol, atol=tol)

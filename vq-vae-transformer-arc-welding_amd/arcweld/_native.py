@@ -44,6 +44,7 @@ class GemmArgs(ctypes.Structure):
         ("a_rowsum", c_p),
         ("bias_mod", c_int),
         ("accumulate", c_int), ("col_mod", c_int), ("col_mul", c_int), ("col_off", c_int),
+        ("seed_ptr", c_p),
     ]
 
 
@@ -70,12 +71,14 @@ SIGNATURES = {
     "aw_mse_bwd": [c_p, c_p, c_i64, c_p, c_p, c_p],
     "aw_scalar_add": [c_p, c_p, c_p, c_p],
     "aw_mse_finalize": [c_p, c_i64, c_p, c_p],
-    "aw_radam_step": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_int, c_i64, c_i64, c_f, c_f, c_f, c_f, c_p, c_p],
+    "aw_radam_step": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_int, c_i64, c_i64, c_f, c_f, c_f, c_f, c_p, c_p,
+                      c_p],
+    "aw_counter_add": [c_p, c_i64, c_p],
     "aw_grad_norm_clip": [c_p, c_p, c_p, c_p, c_int, c_f, c_p, c_p, c_p, c_p],
     "aw_scale": [c_p, c_i64, c_p, c_p],
     "aw_layernorm_fwd": [c_p, c_i64, c_int, c_p, c_p, c_f, c_p, c_int, c_p, c_p, c_p],
     "aw_layernorm_bwd": [c_p, c_p, c_i64, c_int, c_p, c_p, c_p, c_p, c_int, c_p, c_p, c_p, c_int, c_f,
-                         ctypes.c_uint64, c_p],
+                         ctypes.c_uint64, c_p, c_p],
     "aw_class_head_fwd": [c_p, c_i64, c_int, c_int, c_p, c_p, c_p, c_p, c_p, c_p, c_p],
     "aw_class_head_bwd": [c_p, c_p, c_p, c_i64, c_int, c_int, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p],
     "aw_embed_fwd": [c_p, c_i64, c_int, c_int, c_p, c_p, c_p, c_p],

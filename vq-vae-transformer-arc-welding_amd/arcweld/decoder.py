@@ -21,7 +21,7 @@ from __future__ import annotations
 import torch
 
 from . import kernels as K
-from .vqvae import _mix, operand_dtype
+from .vqvae import _mix, operand_dtype, rng_snapshot
 
 F32 = torch.float32
 
@@ -66,6 +66,7 @@ def forward(m, ids, generate: bool, training: bool, need_backward: bool, seed: i
     nb = len(m.transformer.h)
     sv.seed_attn = [_mix(seed, 300 + i) for i in range(nb)]
     sv.seed_mlp = [_mix(seed, 400 + i) for i in range(nb)]
+    sv.ctr = rng_snapshot(m, dev, p_drop)
     ids = ids.contiguous()
 
     x = e(R, d)
@@ -84,13 +85,15 @@ def forward(m, ids, generate: bool, training: bool, need_backward: bool, seed: i
         y, lse = e(R, d, dt=T_), e(B * nh * T)
         K.attn_fwd(qkv, B, T, nh, d, y, lse)
         x1 = e(R, d)
-        K.gemm(y, Wo, R, d, d, bias=at.c_proj.bias, drop=(p_drop, sv.seed_attn[i]), resid=x, C=x1)
+        K.gemm(y, Wo, R, d, d, bias=at.c_proj.bias, drop=(p_drop, sv.seed_attn[i]), resid=x, C=x1,
+               seed_ptr=sv.ctr)
         a2, mu2, rs2 = e(R, d, dt=T_), e(R), e(R)
         K.layernorm_fwd(x1, blk.ln_2.weight, blk.ln_2.bias, blk.ln_2.eps, a2, mu2, rs2)
         h, g = e(R, 4 * d), e(R, 4 * d, dt=T_)
         K.gemm(a2, Wfc, R, 4 * d, d, bias=mlp.c_fc.bias, act=K.AW_ACT_GELU_TANH, C=h, C2=g, c2_mode=1)
         x2 = e(R, d)
-        K.gemm(g, Wp, R, d, 4 * d, bias=mlp.c_proj.bias, drop=(p_drop, sv.seed_mlp[i]), resid=x1, C=x2)
+        K.gemm(g, Wp, R, d, 4 * d, bias=mlp.c_proj.bias, drop=(p_drop, sv.seed_mlp[i]), resid=x1, C=x2,
+               seed_ptr=sv.ctr)
         blocks.append(dict(x=x, a=a, mu1=mu1, rs1=rs1, qkv=qkv, y=y, lse=lse, x1=x1, a2=a2, mu2=mu2, rs2=rs2, h=h, g=g,
                            Wqkv=Wqkv, Wo=Wo, Wfc=Wfc, Wp=Wp))
         x = x2
@@ -145,7 +148,7 @@ def backward(m, sv, g_out, slot):
     go = e(R, d, dt=T_)
     last = nb - 1
     K.layernorm_bwd(sv.x_last, gxf, lnf.weight, sv.muf, sv.rsf, gx, False, slot(lnf.weight), slot(lnf.bias),
-                    dx2=go, drop=(sv.p_drop, sv.seed_mlp[last] if nb else 0))
+                    dx2=go, drop=(sv.p_drop, sv.seed_mlp[last] if nb else 0), seed_ptr=sv.ctr)
     for i in reversed(range(nb)):
         blk = m.transformer.h[i]
         at, mlp = blk.attn, blk.mlp
@@ -161,7 +164,8 @@ def backward(m, sv, g_out, slot):
                a_rowsum=slot(mlp.c_fc.bias))
         go2 = e(R, d, dt=T_)
         K.layernorm_bwd(c["x1"], ga2, blk.ln_2.weight, c["mu2"], c["rs2"], gx, True, slot(blk.ln_2.weight),
-                        slot(blk.ln_2.bias), dx2=go2, drop=(sv.p_drop, sv.seed_attn[i]))
+                        slot(blk.ln_2.bias), dx2=go2, drop=(sv.p_drop, sv.seed_attn[i]),
+                        seed_ptr=sv.ctr)
         # ---- attention
         gy = e(R, d, dt=T_)
         K.gemm(go2, c["Wo"], R, d, d, b_trans=True, C=gy)
@@ -176,7 +180,8 @@ def backward(m, sv, g_out, slot):
         K.gemm(dqkv, c["Wqkv"], R, d, 3 * d, b_trans=True, C=ga)
         go = e(R, d, dt=T_) if i > 0 else None
         K.layernorm_bwd(c["x"], ga, blk.ln_1.weight, c["mu1"], c["rs1"], gx, True, slot(blk.ln_1.weight),
-                        slot(blk.ln_1.bias), dx2=go, drop=(sv.p_drop, sv.seed_mlp[i - 1] if i > 0 else 0))
+                        slot(blk.ln_1.bias), dx2=go, drop=(sv.p_drop, sv.seed_mlp[i - 1] if i > 0 else 0),
+                        seed_ptr=sv.ctr)
     K.embed_bwd(sv_ids(sv), gx, slot(m.embedding.latent_embedding.weight))
 
 

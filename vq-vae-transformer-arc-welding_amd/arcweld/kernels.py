@@ -44,7 +44,7 @@ def _algorithmic_flops(M, N, Kd, conv, flops):
 def gemm(A, B, M, N, K, *, a_trans=False, b_trans=False, conv=None, alpha=1.0, beta=0.0, bias=None,
          act=AW_ACT_GELU_ERF, pre=None, resid=None, drop=(0.0, 0), C=None, C2=None, c2_mode=0, drop2=(0.0, 0),
          colstats=None, stats_mod=0, a_rowsum=None, bias_mod=0, accumulate=False, col_map=(0, 1, 0), stream=None,
-         flops=None):
+         flops=None, seed_ptr=None):
     """C = epilogue(alpha * op(A) @ op(B)); see aw_gemm in include/arcweld_amd.h for the exact semantics.
 
     conv = (cin, seg, dir, operand) selects the implicit k=3 convolution form."""
@@ -77,6 +77,7 @@ def gemm(A, B, M, N, K, *, a_trans=False, b_trans=False, conv=None, alpha=1.0, b
     a.bias_mod = int(bias_mod)
     a.accumulate = int(bool(accumulate))
     a.col_mod, a.col_mul, a.col_off = (int(v) for v in col_map)
+    a.seed_ptr = ptr(seed_ptr)
     lib = nat.load()
     wsn = lib.aw_gemm_workspace(ctypes.byref(a))
     ws = torch.empty(wsn, device=A.device, dtype=torch.float32) if wsn > 0 else None
@@ -176,10 +177,15 @@ def mse_finalize(sqerr, numel, out, stream=None):
 
 # ------------------------------------------------------------------------------------------ optimizer
 def radam_step(param, grad, m, v, seg_off, seg_len, seg_wd, seg_active, nseg, total, step, lr, beta1, beta2, eps,
-               gscale=None, stream=None):
+               gscale=None, stream=None, step_ptr=None):
     call("aw_radam_step", ptr(param), ptr(grad), ptr(m), ptr(v), ptr(seg_off), ptr(seg_len), ptr(seg_wd),
          ptr(seg_active), int(nseg), int(total), int(step), float(lr), float(beta1), float(beta2), float(eps),
-         ptr(gscale), stream_ptr(stream))
+         ptr(gscale), ptr(step_ptr), stream_ptr(stream))
+
+
+def counter_add(counter, v=1, stream=None):
+    """counter (int64 device tensor) += v on the stream (per-step RNG / optimizer-step counters)."""
+    call("aw_counter_add", ptr(counter), int(v), stream_ptr(stream))
 
 
 def grad_norm_clip(grad, seg_off, seg_len, seg_active, nseg, max_norm, ws, out_norm, out_coef, stream=None):
@@ -198,11 +204,12 @@ def layernorm_fwd(x, w, b, eps, y, mean, rstd, stream=None):
          ptr(rstd), stream_ptr(stream))
 
 
-def layernorm_bwd(x, dy, w, mean, rstd, dx, accumulate, dw, db, dx2=None, drop=(0.0, 0), stream=None):
+def layernorm_bwd(x, dy, w, mean, rstd, dx, accumulate, dw, db, dx2=None, drop=(0.0, 0), stream=None,
+                  seed_ptr=None):
     R, D = x.shape
     call("aw_layernorm_bwd", ptr(x), ptr(dy), R, D, ptr(w), ptr(mean), ptr(rstd), ptr(dx), int(accumulate), ptr(dw),
          ptr(db), ptr(dx2), dtype_code(dx2.dtype) if dx2 is not None else AW_F32, float(drop[0]),
-         int(drop[1]) & 0xFFFFFFFFFFFFFFFF, stream_ptr(stream))
+         int(drop[1]) & 0xFFFFFFFFFFFFFFFF, ptr(seed_ptr), stream_ptr(stream))
 
 
 def class_head_fwd(xf, B, T, w1, b1, W2, b2, s, out, stream=None):

@@ -60,7 +60,8 @@ class RAdam(torch.optim.Optimizer):
                           len_d=torch.tensor(lens, device=dev, dtype=torch.int64),
                           wd_d=torch.tensor(wds, device=dev, dtype=torch.float32),
                           ws=torch.zeros(1, device=dev, dtype=torch.float64),
-                          norm=torch.zeros((), device=dev), coef=torch.ones((), device=dev))
+                          norm=torch.zeros((), device=dev), coef=torch.ones((), device=dev),
+                          step=torch.full((1,), self._step_count, device=dev, dtype=torch.int64))
         self.set_active(self._pending_active)
 
     def flatten(self):
@@ -115,17 +116,21 @@ class RAdam(torch.optim.Optimizer):
         self.flatten()
         F = self._flat
         self._step_count += 1
-        # one launch per group (groups may differ in lr/betas/eps); segments of other groups are masked off
+        # the step number also lives on the device, so a captured step graph replays with the right bias
+        # corrections; one launch per group (groups may differ in lr/betas/eps), other groups' segments masked
+        K.counter_add(F["step"], 1)
         for gi, g in enumerate(self.param_groups):
             act = F["act_group"][gi]
             b1, b2 = g["betas"]
             K.radam_step(F["p"], F["g"], F["m"], F["v"], F["off_d"], F["len_d"], F["wd_d"], act, len(F["params"]),
-                         F["total"], self._step_count, g["lr"], b1, b2, g["eps"], gscale=self._coef)
+                         F["total"], self._step_count, g["lr"], b1, b2, g["eps"], gscale=self._coef,
+                         step_ptr=F["step"])
         self._coef = None
         return loss
 
     def state_dict(self):
         sd = super().state_dict()
         if self._flat is not None:
-            sd["arcweld_flat"] = {"m": self._flat["m"].cpu(), "v": self._flat["v"].cpu(), "step": self._step_count}
+            sd["arcweld_flat"] = {"m": self._flat["m"].cpu(), "v": self._flat["v"].cpu(),
+                                  "step": int(self._flat["step"].item())}
         return sd

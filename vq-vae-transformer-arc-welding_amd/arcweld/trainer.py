@@ -49,7 +49,7 @@ def broadcast_params(model: torch.nn.Module):
 class Trainer:
     def __init__(self, devices=1, num_nodes=1, max_epochs=1, max_steps=-1, logger=None, callbacks=None,
                  gradient_clip_val=None, strategy="auto", accumulate_grad_batches=1, log_every_n_steps=50,
-                 fused_grad_sink=True, **_ignored):
+                 fused_grad_sink=True, hip_graphs=False, **_ignored):
         self.max_epochs = max_epochs
         self.max_steps = max_steps
         self.logger = logger
@@ -57,6 +57,7 @@ class Trainer:
         self.accumulate = max(1, int(accumulate_grad_batches))
         self.log_every = log_every_n_steps
         self.fused_grad_sink = fused_grad_sink
+        self.hip_graphs = hip_graphs   # capture the step (needs accumulate_grad_batches == 1, fixed batch shape)
         self.global_step = 0
         self.history = []
         self.optimizer = None
@@ -79,6 +80,8 @@ class Trainer:
             model._grad_sink = {p: p.grad for p in model.parameters()}
         broadcast_params(model)
         self.optimizer = opt
+        self._graphs = None          # a captured step belongs to one optimizer
+        self._graph_shape = None
         return opt
 
     def micro_step(self, model, batch, batch_idx, scale):
@@ -87,14 +90,25 @@ class Trainer:
         (loss * scale).backward()
         return loss
 
-    def optimizer_step(self, model):
+    def _update(self, model):
         opt = self.optimizer
-        allreduce_flat(opt.flat_grad)
         if self.gradient_clip_val:
             opt.clip_grad_norm_(float(self.gradient_clip_val))
         opt.step()
         opt.zero_grad()
+
+    def optimizer_step(self, model):
+        allreduce_flat(self.optimizer.flat_grad)
+        self._update(model)
         self.global_step += 1
+
+    def graphed_step(self, model, batch, scale):
+        """One full optimizer step (accumulate_grad_batches == 1) replayed from captured HIP graphs; the first
+        call warms up eagerly and captures.  Returns the (static) loss tensor."""
+        from .graphs import StepGraphs
+        if getattr(self, "_graphs", None) is None or self._graphs.model is not model:
+            self._graphs = StepGraphs(self, model, scale, lambda: allreduce_flat(self.optimizer.flat_grad))
+        return self._graphs.run(batch)
 
     def fit(self, model, datamodule=None, train_dataloaders=None, val_dataloaders=None):
         if datamodule is not None:
@@ -117,6 +131,11 @@ class Trainer:
             n = len(loader) if hasattr(loader, "__len__") else None
             for i, batch in enumerate(loader):
                 batch = _to_device(batch, dev)
+                if self.hip_graphs and self.accumulate == 1 and _fixed_shape(self, batch):
+                    loss = self.graphed_step(model, batch, scale)
+                    if 0 < self.max_steps <= self.global_step:
+                        break
+                    continue
                 loss = self.micro_step(model, batch, i, scale)
                 # Lightning steps on every accumulate-th batch and on the last batch of the epoch
                 if (i + 1) % self.accumulate == 0 or (n is not None and i + 1 == n):
@@ -226,6 +245,20 @@ class ModelCheckpoint:
                 model.save_checkpoint(self.best_model_path)
         if self.save_last:
             model.save_checkpoint(os.path.join(self.dirpath, "last.ckpt"))
+
+
+def _shapes(batch):
+    if isinstance(batch, torch.Tensor):
+        return (tuple(batch.shape), batch.dtype)
+    return tuple(_shapes(b) for b in batch)
+
+
+def _fixed_shape(trainer, batch):
+    """Graph replay needs the captured shapes; a ragged last batch runs eagerly."""
+    sh = _shapes(batch)
+    if getattr(trainer, "_graph_shape", None) is None:
+        trainer._graph_shape = sh
+    return sh == trainer._graph_shape
 
 
 def _to_device(batch, dev):

@@ -41,6 +41,20 @@ def _mix(seed: int, salt: int) -> int:
     return z ^ (z >> 32)
 
 
+def rng_snapshot(m, dev, p_drop):
+    """Advance the module's device-side dropout counter and return a device copy of it for this forward (None
+    when no dropout is active).  The kernels mix it into the host seeds (aw_gemm_args.seed_ptr), so a captured
+    HIP graph draws fresh masks on every replay and the backward regenerates exactly the forward's masks."""
+    if p_drop <= 0.0:
+        return None
+    ctr = getattr(m, "_rng_counter", None)
+    if ctr is None or ctr.device != dev:
+        ctr = torch.zeros(1, dtype=torch.int64, device=dev)
+        m._rng_counter = ctr
+    K.counter_add(ctr, 1)
+    return ctr.clone()
+
+
 class VQVAEShapes:
     def __init__(self, m, B):
         self.B = B
@@ -85,6 +99,7 @@ def forward(m, x, training: bool, need_backward: bool, dtype=None, seed: int = 0
     sv.sh, sv.T, sv.p_drop, sv.training = sh, T, p_drop, training
     sv.enc_seed = [_mix(seed, 100 + r) for r in range(R)]
     sv.dec_seed = [_mix(seed, 200 + r) for r in range(R)]
+    sv.ctr = rng_snapshot(m, dev, p_drop)
 
     # ---- operand copies of the weights (relayout + cast)
     Wp = e(H, sh.ldp, dt=T)
@@ -121,11 +136,13 @@ def forward(m, x, training: bool, need_backward: bool, dtype=None, seed: int = 0
         K.gemm(a0s[r], enc_w[r][0], N, H, H, bias=c1.bias, C=h, C2=a1, c2_mode=1)
         if r < R - 1:
             xn, an = e(N, H), e(N, H, dt=T)
-            K.gemm(a1, enc_w[r][1], N, H, H, bias=c2.bias, drop=(p_drop, sv.enc_seed[r]), resid=xs[r], C=xn, C2=an,
+            K.gemm(a1, enc_w[r][1], N, H, H, bias=c2.bias, drop=(p_drop, sv.enc_seed[r]), seed_ptr=sv.ctr,
+                   resid=xs[r], C=xn, C2=an,
                    c2_mode=1)
         else:  # last block: only the operand copy of x_R is consumed (sep conv)
             xn, an = None, e(N, H, dt=T)
-            K.gemm(a1, enc_w[r][1], N, H, H, bias=c2.bias, drop=(p_drop, sv.enc_seed[r]), resid=xs[r], C=an)
+            K.gemm(a1, enc_w[r][1], N, H, H, bias=c2.bias, drop=(p_drop, sv.enc_seed[r]), seed_ptr=sv.ctr,
+                   resid=xs[r], C=an)
         xs.append(xn)
         a0s.append(an)
         hs.append(h)
@@ -157,11 +174,13 @@ def forward(m, x, training: bool, need_backward: bool, dtype=None, seed: int = 0
         K.gemm(ya0s[r], dec_w[r][0], N, H, 3 * H, conv=conv, bias=c1.bias, C=h, C2=a1, c2_mode=1)
         if r < R - 1:
             yn, an = e(N, H), e(N, H, dt=T)
-            K.gemm(a1, dec_w[r][1], N, H, 3 * H, conv=conv, bias=c2.bias, drop=(p_drop, sv.dec_seed[r]), resid=ys[r],
+            K.gemm(a1, dec_w[r][1], N, H, 3 * H, conv=conv, bias=c2.bias, drop=(p_drop, sv.dec_seed[r]),
+                   seed_ptr=sv.ctr, resid=ys[r],
                    C=yn, C2=an, c2_mode=1)
         else:
             yn, an = None, e(N, H, dt=T)
-            K.gemm(a1, dec_w[r][1], N, H, 3 * H, conv=conv, bias=c2.bias, drop=(p_drop, sv.dec_seed[r]), resid=ys[r],
+            K.gemm(a1, dec_w[r][1], N, H, 3 * H, conv=conv, bias=c2.bias, drop=(p_drop, sv.dec_seed[r]),
+                   seed_ptr=sv.ctr, resid=ys[r],
                    C=an)
         ys.append(yn)
         ya0s.append(an)
@@ -269,7 +288,7 @@ def backward(m, sv, g_emb, g_xhat, slot):
     gy, go = e(N, H), e(N, H, dt=T)
     last = R - 1
     K.gemm(gY2, sv.Wt1, N, H, k1 * H, b_trans=True, C=gy, C2=go, c2_mode=3 if R > 0 else 2,
-           drop2=(p_drop, sv.dec_seed[last] if R > 0 else 0))
+           drop2=(p_drop, sv.dec_seed[last] if R > 0 else 0), seed_ptr=sv.ctr)
 
     # ---- decoder ResBlocks (reverse)
     dconv_in = (H, S, -1, 0)
@@ -285,7 +304,8 @@ def backward(m, sv, g_emb, g_xhat, slot):
                C=slot(c2.weight).view(H, 3 * H), accumulate=True, col_map=(H, 3, 0), a_rowsum=slot(c2.bias))
         gyn, gon = e(N, H), e(N, H, dt=T)
         K.gemm(gh, W1d, N, H, 3 * H, b_trans=True, conv=dconv_in, pre=sv.ys[r], resid=gy, C=gyn, C2=gon,
-               c2_mode=3 if r > 0 else 2, drop2=(p_drop, sv.dec_seed[r - 1] if r > 0 else 0))
+               c2_mode=3 if r > 0 else 2, drop2=(p_drop, sv.dec_seed[r - 1] if r > 0 else 0),
+               seed_ptr=sv.ctr)
         K.gemm(gh, sv.ya0s[r], H, 3 * H, N, a_trans=True, b_trans=True, conv=wconv,
                C=slot(c1.weight).view(H, 3 * H), accumulate=True, col_map=(H, 3, 0), a_rowsum=slot(c1.bias))
         gy, go = gyn, gon
@@ -306,7 +326,7 @@ def backward(m, sv, g_emb, g_xhat, slot):
            a_rowsum=slot(pr["sep"].bias))
     gx, gxo = e(N, H), e(N, H, dt=T)
     K.gemm(dz_T, sv.Ws, N, H, D, b_trans=True, C=gx, C2=gxo, c2_mode=3 if R > 0 else 2,
-           drop2=(p_drop, sv.enc_seed[R - 1] if R > 0 else 0))
+           drop2=(p_drop, sv.enc_seed[R - 1] if R > 0 else 0), seed_ptr=sv.ctr)
 
     # ---- encoder ResBlocks (reverse)
     for r in reversed(range(R)):
@@ -318,7 +338,7 @@ def backward(m, sv, g_emb, g_xhat, slot):
                accumulate=True, col_map=(0, 3, 1), a_rowsum=slot(c2.bias))
         gxn, gxon = e(N, H), e(N, H, dt=T)
         K.gemm(gh, w1, N, H, H, b_trans=True, pre=sv.xs[r], resid=gx, C=gxn, C2=gxon, c2_mode=3 if r > 0 else 2,
-               drop2=(p_drop, sv.enc_seed[r - 1] if r > 0 else 0))
+               drop2=(p_drop, sv.enc_seed[r - 1] if r > 0 else 0), seed_ptr=sv.ctr)
         K.gemm(gh, sv.a0s[r], H, H, N, a_trans=True, b_trans=True, C=slot(c1.weight).view(H, 3 * H),
                accumulate=True, col_map=(0, 3, 1), a_rowsum=slot(c1.bias))
         gx, gxo = gxn, gxon

@@ -59,6 +59,13 @@ __device__ __forceinline__ float aw_uniform(uint64_t seed, uint64_t e) {
   z ^= z >> 31;
   return (float)(z >> 40) * (1.0f / 16777216.0f);
 }
+// Effective seed when a device-side per-step counter is supplied (seed_ptr in the ABI).
+__device__ __forceinline__ uint64_t aw_seed_mix(uint64_t salt, const uint64_t* ctr) {
+  if (!ctr) return salt;
+  uint64_t z = salt ^ (*ctr * 0xD1B54A32D192ED03ull + 0x8CB92BA72F3D8DD7ull);
+  z = (z ^ (z >> 32)) * 0xD6E8FEB86659FD93ull;
+  return z ^ (z >> 32);
+}
 __device__ __forceinline__ float aw_dropout_scale(uint64_t seed, uint64_t e, float p) {
   if (p <= 0.f) return 1.f;
   return aw_uniform(seed, e) < p ? 0.f : 1.f / (1.f - p);

@@ -384,6 +384,8 @@ __global__ __launch_bounds__(NTHREADS, RAGGED ? 1 : 2) void gemm_kernel(GemmP P)
       atomicAdd(C + (int64_t)(m0 + lr) * p.ldc + oc, p.alpha * Cs[lr * CPITCH + lc]);
     return;
   }
+  const uint64_t dseed = p.drop_p > 0.f ? aw_seed_mix(p.drop_seed, p.seed_ptr) : 0ull;
+  const uint64_t dseed2 = p.c2_mode == 3 ? aw_seed_mix(p.drop2_seed, p.seed_ptr) : 0ull;
   // thread -> 4 consecutive columns (c4) x rows r0, r0+8, ...; 4 rows of loads in flight per thread
   const int c4 = (tid & 31) * 4, r0 = tid >> 5;
   const int col = n0 + c4;
@@ -435,13 +437,13 @@ __global__ __launch_bounds__(NTHREADS, RAGGED ? 1 : 2) void gemm_kernel(GemmP P)
         for (int e = 0; e < 4; ++e) {
           float x = p.alpha * av[e] + bias[e];
           if (p.pre) x *= act_bwd(p.act, pv[e]);
-          if (p.drop_p > 0.f) x *= aw_dropout_scale(p.drop_seed, (uint64_t)row * N + col + e, p.drop_p);
+          if (p.drop_p > 0.f) x *= aw_dropout_scale(dseed, (uint64_t)row * N + col + e, p.drop_p);
           if (p.resid) x += rv[e];
           if (p.beta != 0.f) x += p.beta * ov[e];
           v[e] = x;
           float y = x;
           if (p.c2_mode == 1) y = act_fwd(p.act, x);
-          else if (p.c2_mode == 3) y = x * aw_dropout_scale(p.drop2_seed, (uint64_t)row * N + col + e, p.drop2_p);
+          else if (p.c2_mode == 3) y = x * aw_dropout_scale(dseed2, (uint64_t)row * N + col + e, p.drop2_p);
           w[e] = y;
           if (col + e < N) {
             csum[e] += x;

@@ -16,6 +16,26 @@ struct RAdamScalars {
   int rectified;
 };
 
+// Bias corrections and rectification for step t, in double (torch computes them as python floats).
+__host__ __device__ inline RAdamScalars radam_scalars(int64_t step, float lr, float beta1, float beta2, float eps) {
+  const double b1 = beta1, b2 = beta2, t = (double)step;
+  const double bc1 = 1.0 - pow(b1, t), bc2 = 1.0 - pow(b2, t);
+  const double rho_inf = 2.0 / (1.0 - b2) - 1.0;
+  const double rho_t = rho_inf - 2.0 * t * pow(b2, t) / bc2;
+  RAdamScalars S;
+  S.lr = lr;
+  S.beta1 = beta1;
+  S.beta2 = beta2;
+  S.eps = eps;
+  S.bc1 = (float)bc1;
+  S.sqrt_bc2 = (float)sqrt(bc2);
+  S.rectified = rho_t > 5.0;
+  S.rect = S.rectified ? (float)sqrt((rho_t - 4) * (rho_t - 2) * rho_inf / ((rho_inf - 4) * (rho_inf - 2) * rho_t)) : 1.f;
+  return S;
+}
+
+__global__ void counter_add_kernel(int64_t* c, int64_t v) { c[0] += v; }
+
 __device__ __forceinline__ int find_seg(const int64_t* off, int nseg, int64_t e) {
   int lo = 0, hi = nseg - 1;
   while (lo < hi) {  // last segment with off <= e
@@ -32,10 +52,14 @@ __global__ __launch_bounds__(256) void radam_kernel(float* __restrict__ p, const
                                                     const int64_t* __restrict__ seg_len,
                                                     const float* __restrict__ seg_wd, const int* __restrict__ seg_active,
                                                     int nseg, int64_t total, RAdamScalars S,
-                                                    const float* __restrict__ gscale) {
+                                                    const float* __restrict__ gscale,
+                                                    const int64_t* __restrict__ step_ptr) {
   __shared__ int64_t s_off[MAXSEG_LDS];
+  __shared__ RAdamScalars s_S;
   for (int i = threadIdx.x; i < nseg; i += blockDim.x) s_off[i] = seg_off[i];
+  if (step_ptr && threadIdx.x == 0) s_S = radam_scalars(*step_ptr, S.lr, S.beta1, S.beta2, S.eps);
   __syncthreads();
+  if (step_ptr) S = s_S;
   const float gs = gscale ? gscale[0] : 1.0f;
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
     const int s = find_seg(s_off, nseg, e);
@@ -98,31 +122,26 @@ __global__ void scale_kernel(float* x, int64_t n, const float* s) {
 extern "C" int aw_radam_step(float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
                              const int64_t* seg_off, const int64_t* seg_len, const float* seg_wd, const int* seg_active,
                              int nseg, int64_t total, int64_t step, float lr, float beta1, float beta2, float eps,
-                             const float* gscale, void* stream) {
+                             const float* gscale, const int64_t* step_ptr, void* stream) {
   AW_REQUIRE(param && grad && exp_avg && exp_avg_sq && seg_off && seg_len && seg_wd && seg_active,
              "aw_radam_step: null pointer");
   AW_REQUIRE(nseg > 0 && nseg <= MAXSEG_LDS, "aw_radam_step: nseg must be in [1, %d]", MAXSEG_LDS);
-  AW_REQUIRE(step >= 1 && total >= 0, "aw_radam_step: step counts from 1");
-  // host-side scalars in double, as torch's _single_tensor_radam computes them (python floats)
-  const double b1 = beta1, b2 = beta2, t = (double)step;
-  const double bc1 = 1.0 - pow(b1, t), bc2 = 1.0 - pow(b2, t);
-  const double rho_inf = 2.0 / (1.0 - b2) - 1.0;
-  const double rho_t = rho_inf - 2.0 * t * pow(b2, t) / bc2;
-  RAdamScalars S;
-  S.lr = lr;
-  S.beta1 = beta1;
-  S.beta2 = beta2;
-  S.eps = eps;
-  S.bc1 = (float)bc1;
-  S.sqrt_bc2 = (float)sqrt(bc2);
-  S.rectified = rho_t > 5.0;
-  S.rect = S.rectified ? (float)sqrt((rho_t - 4) * (rho_t - 2) * rho_inf / ((rho_inf - 4) * (rho_inf - 2) * rho_t)) : 1.f;
+  AW_REQUIRE((step_ptr || step >= 1) && total >= 0, "aw_radam_step: step counts from 1");
+  // scalars in double, as torch's _single_tensor_radam computes them (python floats); on the device when the
+  // step number lives there
+  const RAdamScalars S = radam_scalars(step_ptr ? 1 : step, lr, beta1, beta2, eps);
   if (total == 0) return AW_OK;
   int64_t g = (total + 255) / 256;
   if (g > 4096) g = 4096;
   hipLaunchKernelGGL(radam_kernel, dim3((int)g), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), param, grad,
-                     exp_avg, exp_avg_sq, seg_off, seg_len, seg_wd, seg_active, nseg, total, S, gscale);
+                     exp_avg, exp_avg_sq, seg_off, seg_len, seg_wd, seg_active, nseg, total, S, gscale, step_ptr);
   return aw::check_launch("aw_radam_step");
+}
+
+extern "C" int aw_counter_add(int64_t* counter, int64_t v, void* stream) {
+  AW_REQUIRE(counter, "aw_counter_add: null counter");
+  hipLaunchKernelGGL(counter_add_kernel, dim3(1), dim3(1), 0, reinterpret_cast<hipStream_t>(stream), counter, v);
+  return aw::check_launch("aw_counter_add");
 }
 
 extern "C" int aw_grad_norm_clip(const float* grad, const int64_t* seg_off, const int64_t* seg_len,

@@ -45,7 +45,8 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ x
                                                      const float* __restrict__ mean, const float* __restrict__ rstd,
                                                      float* __restrict__ dx, int accumulate, float* __restrict__ dw,
                                                      float* __restrict__ db, T2* __restrict__ dx2, float drop_p,
-                                                     uint64_t drop_seed) {
+                                                     uint64_t drop_seed, const uint64_t* __restrict__ seed_ptr) {
+  drop_seed = aw_seed_mix(drop_seed, seed_ptr);
   extern __shared__ float red[];  // 2*D
   for (int i = threadIdx.x; i < 2 * D; i += blockDim.x) red[i] = 0.f;
   __syncthreads();
@@ -80,6 +81,128 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ x
   for (int i = threadIdx.x; i < D; i += blockDim.x) {
     atomicAdd(dw + i, red[i]);
     atomicAdd(db + i, red[D + i]);
+  }
+}
+
+// Vectorised forms for D % 256 == 0 (d_model 512): lane owns float4 columns 4*lane + 256*j, j < NV; the row
+// statistics come from one pass over registers.  Backward keeps the dw/db partial sums of its columns in
+// registers across all rows the wave visits, then reduces the block's waves through LDS: one atomic per
+// column per block instead of two LDS atomics per element.
+template <typename T, int NV>
+__global__ __launch_bounds__(256) void ln_fwd_vec_kernel(const float* __restrict__ x, int64_t R, int D,
+                                                         const float* __restrict__ w, const float* __restrict__ b,
+                                                         float eps, T* __restrict__ y, float* __restrict__ mean,
+                                                         float* __restrict__ rstd) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  if (r >= R) return;
+  float4 v[NV];
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    v[j] = *reinterpret_cast<const float4*>(x + r * D + 4 * lane + 256 * j);
+    s += (v[j].x + v[j].y) + (v[j].z + v[j].w);
+  }
+  const float mu = wave_sum(s) / (float)D;
+  float q = 0.f;
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const float a = v[j].x - mu, bb = v[j].y - mu, c = v[j].z - mu, e = v[j].w - mu;
+    q += (a * a + bb * bb) + (c * c + e * e);
+  }
+  const float rs = rsqrtf(wave_sum(q) / (float)D + eps);
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const int c = 4 * lane + 256 * j;
+    const float4 w4 = *reinterpret_cast<const float4*>(w + c), b4 = *reinterpret_cast<const float4*>(b + c);
+    const float o[4] = {(v[j].x - mu) * rs * w4.x + b4.x, (v[j].y - mu) * rs * w4.y + b4.y,
+                        (v[j].z - mu) * rs * w4.z + b4.z, (v[j].w - mu) * rs * w4.w + b4.w};
+    if constexpr (sizeof(T) == 2) {
+      bf16 h[4] = {(bf16)o[0], (bf16)o[1], (bf16)o[2], (bf16)o[3]};
+      uint2 u;
+      memcpy(&u, h, 8);
+      *reinterpret_cast<uint2*>(y + r * D + c) = u;
+    } else {
+      *reinterpret_cast<float4*>(y + r * D + c) = make_float4(o[0], o[1], o[2], o[3]);
+    }
+  }
+  if (lane == 0) {
+    mean[r] = mu;
+    rstd[r] = rs;
+  }
+}
+
+template <typename T2, int NV>
+__global__ __launch_bounds__(256) void ln_bwd_vec_kernel(const float* __restrict__ x, const float* __restrict__ dy,
+                                                         int64_t R, int D, const float* __restrict__ w,
+                                                         const float* __restrict__ mean,
+                                                         const float* __restrict__ rstd, float* __restrict__ dx,
+                                                         int accumulate, float* __restrict__ dw,
+                                                         float* __restrict__ db, T2* __restrict__ dx2, float drop_p,
+                                                         uint64_t drop_seed, const uint64_t* __restrict__ seed_ptr) {
+  __shared__ float red[4][2][256 * NV];
+  drop_seed = aw_seed_mix(drop_seed, seed_ptr);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  float4 w4[NV], pdw[NV], pdb[NV];
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    w4[j] = *reinterpret_cast<const float4*>(w + 4 * lane + 256 * j);
+    pdw[j] = pdb[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  for (int64_t r = wave; r < R; r += nw) {
+    const float mu = mean[r], rs = rstd[r];
+    float4 xh[NV], g[NV];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      const int c = 4 * lane + 256 * j;
+      const float4 xv = *reinterpret_cast<const float4*>(x + r * D + c);
+      const float4 dv = *reinterpret_cast<const float4*>(dy + r * D + c);
+      xh[j] = make_float4((xv.x - mu) * rs, (xv.y - mu) * rs, (xv.z - mu) * rs, (xv.w - mu) * rs);
+      g[j] = make_float4(dv.x * w4[j].x, dv.y * w4[j].y, dv.z * w4[j].z, dv.w * w4[j].w);
+      pdw[j].x += dv.x * xh[j].x; pdw[j].y += dv.y * xh[j].y; pdw[j].z += dv.z * xh[j].z; pdw[j].w += dv.w * xh[j].w;
+      pdb[j].x += dv.x; pdb[j].y += dv.y; pdb[j].z += dv.z; pdb[j].w += dv.w;
+      s1 += (g[j].x + g[j].y) + (g[j].z + g[j].w);
+      s2 += (g[j].x * xh[j].x + g[j].y * xh[j].y) + (g[j].z * xh[j].z + g[j].w * xh[j].w);
+    }
+    s1 = wave_sum(s1) / (float)D;
+    s2 = wave_sum(s2) / (float)D;
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      const int c = 4 * lane + 256 * j;
+      float v[4] = {rs * (g[j].x - s1 - xh[j].x * s2), rs * (g[j].y - s1 - xh[j].y * s2),
+                    rs * (g[j].z - s1 - xh[j].z * s2), rs * (g[j].w - s1 - xh[j].w * s2)};
+      if (accumulate) {
+        const float4 o = *reinterpret_cast<const float4*>(dx + r * D + c);
+        v[0] += o.x; v[1] += o.y; v[2] += o.z; v[3] += o.w;
+      }
+      *reinterpret_cast<float4*>(dx + r * D + c) = make_float4(v[0], v[1], v[2], v[3]);
+      if (dx2) {
+        float m[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) m[e] = v[e] * aw_dropout_scale(drop_seed, (uint64_t)r * D + c + e, drop_p);
+        if constexpr (sizeof(T2) == 2) {
+          bf16 h[4] = {(bf16)m[0], (bf16)m[1], (bf16)m[2], (bf16)m[3]};
+          uint2 u;
+          memcpy(&u, h, 8);
+          *reinterpret_cast<uint2*>(dx2 + r * D + c) = u;
+        } else {
+          *reinterpret_cast<float4*>(dx2 + r * D + c) = make_float4(m[0], m[1], m[2], m[3]);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    *reinterpret_cast<float4*>(&red[wv][0][4 * lane + 256 * j]) = pdw[j];
+    *reinterpret_cast<float4*>(&red[wv][1][4 * lane + 256 * j]) = pdb[j];
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 256 * NV; i += 256) {
+    atomicAdd(dw + i, (red[0][0][i] + red[1][0][i]) + (red[2][0][i] + red[3][0][i]));
+    atomicAdd(db + i, (red[0][1][i] + red[1][1][i]) + (red[2][1][i] + red[3][1][i]));
   }
 }
 
@@ -483,6 +606,20 @@ extern "C" int aw_layernorm_fwd(const float* x, int64_t R, int D, const float* w
   if (R == 0) return AW_OK;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   dim3 grid(aw_cdiv(R, 4));
+#define AW_LNF(NV)                                                                                              \
+  if (y_dtype == AW_BF16)                                                                                       \
+    hipLaunchKernelGGL((ln_fwd_vec_kernel<bf16, NV>), grid, dim3(256), 0, s, x, R, D, w, b, eps, (bf16*)y, mean, \
+                       rstd);                                                                                   \
+  else                                                                                                          \
+    hipLaunchKernelGGL((ln_fwd_vec_kernel<float, NV>), grid, dim3(256), 0, s, x, R, D, w, b, eps, (float*)y,     \
+                       mean, rstd);                                                                             \
+  return aw::check_launch("aw_layernorm_fwd");
+  const bool al = (((uintptr_t)x | (uintptr_t)w | (uintptr_t)b | (uintptr_t)y) & 15) == 0;
+  if (al && D == 256) { AW_LNF(1) }
+  if (al && D == 512) { AW_LNF(2) }
+  if (al && D == 768) { AW_LNF(3) }
+  if (al && D == 1024) { AW_LNF(4) }
+#undef AW_LNF
   if (y_dtype == AW_BF16)
     hipLaunchKernelGGL(ln_fwd_kernel<bf16>, grid, dim3(256), 0, s, x, R, D, w, b, eps, (bf16*)y, mean, rstd);
   else
@@ -492,18 +629,33 @@ extern "C" int aw_layernorm_fwd(const float* x, int64_t R, int D, const float* w
 
 extern "C" int aw_layernorm_bwd(const float* x, const float* dy, int64_t R, int D, const float* w, const float* mean,
                                 const float* rstd, float* dx, int accumulate, float* dw, float* db, void* dx2,
-                                int dx2_dtype, float drop_p, uint64_t drop_seed, void* stream) {
+                                int dx2_dtype, float drop_p, uint64_t drop_seed, const uint64_t* seed_ptr,
+                                void* stream) {
   AW_REQUIRE(x && dy && w && mean && rstd && dx && dw && db && R >= 0 && D > 0 && D <= 8192,
              "aw_layernorm_bwd: bad args");
   if (R == 0) return AW_OK;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   dim3 grid(gridcap(R * 64, 256, 512));
+#define AW_LNB(NV)                                                                                               \
+  if (dx2_dtype == AW_BF16)                                                                                      \
+    hipLaunchKernelGGL((ln_bwd_vec_kernel<bf16, NV>), grid, dim3(256), 0, s, x, dy, R, D, w, mean, rstd, dx,      \
+                       accumulate, dw, db, (bf16*)dx2, drop_p, drop_seed, seed_ptr);                                       \
+  else                                                                                                           \
+    hipLaunchKernelGGL((ln_bwd_vec_kernel<float, NV>), grid, dim3(256), 0, s, x, dy, R, D, w, mean, rstd, dx,     \
+                       accumulate, dw, db, (float*)dx2, drop_p, drop_seed, seed_ptr);                                      \
+  return aw::check_launch("aw_layernorm_bwd");
+  const bool al = (((uintptr_t)x | (uintptr_t)dy | (uintptr_t)w | (uintptr_t)dx | (uintptr_t)dx2) & 15) == 0;
+  if (al && D == 256) { AW_LNB(1) }
+  if (al && D == 512) { AW_LNB(2) }
+  if (al && D == 768) { AW_LNB(3) }
+  if (al && D == 1024) { AW_LNB(4) }
+#undef AW_LNB
   if (dx2_dtype == AW_BF16)
     hipLaunchKernelGGL(ln_bwd_kernel<bf16>, grid, dim3(256), 2 * D * sizeof(float), s, x, dy, R, D, w, mean, rstd, dx,
-                       accumulate, dw, db, (bf16*)dx2, drop_p, drop_seed);
+                       accumulate, dw, db, (bf16*)dx2, drop_p, drop_seed, seed_ptr);
   else
     hipLaunchKernelGGL(ln_bwd_kernel<float>, grid, dim3(256), 2 * D * sizeof(float), s, x, dy, R, D, w, mean, rstd, dx,
-                       accumulate, dw, db, (float*)dx2, drop_p, drop_seed);
+                       accumulate, dw, db, (float*)dx2, drop_p, drop_seed, seed_ptr);
   return aw::check_launch("aw_layernorm_bwd");
 }
 

@@ -62,7 +62,6 @@ class MyTransformerDecoder(LightningModule):
                 torch.nn.init.normal_(p, mean=0.0, std=0.02 / math.sqrt(2 * n_blocks))
         n_params = sum(p.numel() for p in self.transformer.parameters())
         print("number of parameters: %.4fM" % (n_params / 1e6,))
-        self._step_seed = 0
         self.save_hyperparameters()
 
     def _init_weights(self, module):
@@ -115,8 +114,11 @@ class MyTransformerDecoder(LightningModule):
         return self._task_params(self.task == "generate")
 
     def _next_seed(self):
-        self._step_seed += 1
-        return (torch.initial_seed() * 1000003 + 7919 * self._step_seed) & 0x7FFFFFFFFFFFFFFF
+        """Host part of the dropout seed: fixed per (torch seed, rank).  The per-call variation comes from the
+        module's device-side counter (arcweld.vqvae.rng_snapshot), so eager calls and replays of a captured step
+        graph draw the same sequence of masks."""
+        rank = torch.distributed.get_rank() if torch.distributed.is_initialized() else 0
+        return (torch.initial_seed() * 1000003 + 7919 + (rank << 40)) & 0x7FFFFFFFFFFFFFFF
 
     def forward(self, x, generate: bool = True):
         """ids (B, T) -> logits (B, T, n_classes) [generate] or (B, 2) [classification] (reference :116-131)."""

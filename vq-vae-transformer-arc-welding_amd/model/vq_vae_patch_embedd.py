@@ -225,12 +225,14 @@ class VQVAEPatch(Autoencoder):
         self.patch_size = patch_size
         self.batch_norm = batch_norm
         self.apply(self.weights_init)
-        self._step_seed = 0
         self._last_indices = None
 
     def _next_seed(self):
-        self._step_seed += 1
-        return (torch.initial_seed() * 1000003 + self._step_seed) & 0x7FFFFFFFFFFFFFFF
+        """Host part of the dropout seed: fixed per (torch seed, rank).  The per-call variation comes from the
+        module's device-side counter (arcweld.vqvae.rng_snapshot), so eager calls and replays of a captured step
+        graph draw the same sequence of masks."""
+        rank = torch.distributed.get_rank() if torch.distributed.is_initialized() else 0
+        return (torch.initial_seed() * 1000003 + 1 + (rank << 40)) & 0x7FFFFFFFFFFFFFFF
 
     def forward(self, x):
         """(B, seq_len, input_dim) -> (embedding_loss, x_hat (B, seq_len, input_dim), perplexity)."""
