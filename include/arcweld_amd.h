@@ -171,7 +171,8 @@ int aw_counter_add(int64_t* counter, int64_t v, void* stream);
 /* Global L2 norm of the active segments of `grad` -> out_norm (f32 device scalar) and the clip coefficient
  * min(max_norm/(norm+1e-6), 1) -> out_coef (Lightning gradient_clip_val -> clip_grad_norm_).  ws: f64[1]. */
 int aw_grad_norm_clip(const float* grad, const int64_t* seg_off, const int64_t* seg_len, const int* seg_active,
-                      int nseg, float max_norm, double* ws, float* out_norm, float* out_coef, void* stream);
+                      int nseg, int64_t total, float max_norm, double* ws, float* out_norm, float* out_coef,
+                      void* stream);
 /* x[i] *= s (device scalar), over n elements. */
 int aw_scale(float* x, int64_t n, const float* s, void* stream);
 

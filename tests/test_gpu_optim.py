@@ -1,0 +1,52 @@
+"""Flat-buffer RAdam + clip-norm kernels against the reference's torch.optim.RAdam / clip_grad_norm_ golden
+trajectories (tests/golden/radam.npz: both parameter-group setups the reference builds), plus the
+find_unused_parameters semantics (inactive segments are neither clipped nor updated)."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden
+from oracle import gen
+
+pytestmark = pytest.mark.gpu
+SHAPES = [(33, 7), (7,), (5, 3, 2)]
+
+
+@pytest.mark.parametrize("tag,betas,groups", [
+    ("vqvae", (0.9, 0.999), [(0.0, [0, 1, 2])]),
+    ("decoder", (0.9, 0.95), [(0.1, [0, 2]), (0.0, [1])]),
+])
+def test_radam_clip_trajectory_matches_reference(tag, betas, groups):
+    from arcweld.optim import RAdam
+    g = golden("radam.npz")
+    params = [torch.nn.Parameter(torch.tensor(gen.normal(500 + i, s, 0.3), device="cuda"))
+              for i, s in enumerate(SHAPES)]
+    opt = RAdam([{"params": [params[i] for i in idx], "weight_decay": wd} for wd, idx in groups], lr=1e-3,
+                betas=betas)
+    opt.flatten()
+    for step in range(8):
+        for i, p in enumerate(params):
+            p.grad.copy_(torch.tensor(gen.normal(600 + 17 * step + i, p.shape, 1.0)))
+        norm = opt.clip_grad_norm_(0.7)
+        np.testing.assert_allclose(norm.item(), g[f"{tag}/prenorm_{step}"], rtol=2e-6)
+        opt.step()
+        opt.zero_grad()
+        for i, p in enumerate(params):
+            np.testing.assert_allclose(p.detach().cpu().numpy(), g[f"{tag}/p{i}_step{step}"], rtol=2e-6, atol=2e-7,
+                                       err_msg=f"step {step} param {i}")
+
+
+def test_inactive_segments_untouched():
+    from arcweld.optim import RAdam
+    params = [torch.nn.Parameter(torch.randn(s, device="cuda")) for s in [(300,), (17, 5), (64,)]]
+    before = [p.detach().clone() for p in params]
+    opt = RAdam(params, lr=1e-2, weight_decay=0.1)
+    opt.flatten()
+    opt.set_active([params[0], params[2]])
+    for p in params:
+        p.grad.fill_(1.0)
+    norm = opt.clip_grad_norm_(1e9)
+    assert abs(norm.item() - (300 + 64) ** 0.5) < 1e-3          # the inactive segment is not in the norm
+    opt.step()
+    assert torch.equal(params[1].detach(), before[1])
+    assert not torch.equal(params[0].detach(), before[0]) and not torch.equal(params[2].detach(), before[2])

@@ -74,7 +74,7 @@ SIGNATURES = {
     "aw_radam_step": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_int, c_i64, c_i64, c_f, c_f, c_f, c_f, c_p, c_p,
                       c_p],
     "aw_counter_add": [c_p, c_i64, c_p],
-    "aw_grad_norm_clip": [c_p, c_p, c_p, c_p, c_int, c_f, c_p, c_p, c_p, c_p],
+    "aw_grad_norm_clip": [c_p, c_p, c_p, c_p, c_int, c_i64, c_f, c_p, c_p, c_p, c_p],
     "aw_scale": [c_p, c_i64, c_p, c_p],
     "aw_layernorm_fwd": [c_p, c_i64, c_int, c_p, c_p, c_f, c_p, c_int, c_p, c_p, c_p],
     "aw_layernorm_bwd": [c_p, c_p, c_i64, c_int, c_p, c_p, c_p, c_p, c_int, c_p, c_p, c_p, c_int, c_f,

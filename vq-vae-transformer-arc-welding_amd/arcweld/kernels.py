@@ -189,8 +189,8 @@ def counter_add(counter, v=1, stream=None):
 
 
 def grad_norm_clip(grad, seg_off, seg_len, seg_active, nseg, max_norm, ws, out_norm, out_coef, stream=None):
-    call("aw_grad_norm_clip", ptr(grad), ptr(seg_off), ptr(seg_len), ptr(seg_active), int(nseg), float(max_norm),
-         ptr(ws), ptr(out_norm), ptr(out_coef), stream_ptr(stream))
+    call("aw_grad_norm_clip", ptr(grad), ptr(seg_off), ptr(seg_len), ptr(seg_active), int(nseg), grad.numel(),
+         float(max_norm), ptr(ws), ptr(out_norm), ptr(out_coef), stream_ptr(stream))
 
 
 def scale_(x, s, stream=None):

@@ -119,14 +119,19 @@ class RAdam(torch.optim.Optimizer):
         # the step number also lives on the device, so a captured step graph replays with the right bias
         # corrections; one launch per group (groups may differ in lr/betas/eps), other groups' segments masked
         K.counter_add(F["step"], 1)
-        for gi, g in enumerate(self.param_groups):
-            act = F["act_group"][gi]
-            b1, b2 = g["betas"]
+        # groups that differ only in weight decay (per segment already) share one launch
+        for (lr, (b1, b2), eps), act in self._launch_groups():
             K.radam_step(F["p"], F["g"], F["m"], F["v"], F["off_d"], F["len_d"], F["wd_d"], act, len(F["params"]),
-                         F["total"], self._step_count, g["lr"], b1, b2, g["eps"], gscale=self._coef,
-                         step_ptr=F["step"])
+                         F["total"], self._step_count, lr, b1, b2, eps, gscale=self._coef, step_ptr=F["step"])
         self._coef = None
         return loss
+
+    def _launch_groups(self):
+        F = self._flat
+        keys = [(float(g["lr"]), tuple(g["betas"]), float(g["eps"])) for g in self.param_groups]
+        if len(set(keys)) == 1:
+            return [(keys[0], F["act_d"])]
+        return [(k, F["act_group"][gi]) for gi, k in enumerate(keys)]
 
     def state_dict(self):
         sd = super().state_dict()

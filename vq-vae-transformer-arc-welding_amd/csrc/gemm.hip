@@ -544,9 +544,11 @@ static int choose_splits(const aw_gemm_args& a, int nblocks, int BK, int* ksplit
   const bool plain = !a.bias && !a.pre && !a.resid && a.drop_p <= 0.f && !a.C2 && !a.colstats && a.C &&
                      a.c_dtype == AW_F32 && (a.beta == 0.f || a.beta == 1.f || a.accumulate);
   int splits = 1;
-  if (plain && nblocks < 192 && a.K >= 64 * BK) {
-    splits = aw_cdiv(256, nblocks);
-    const int max_splits = a.K / (16 * BK);  // at least 16 K-steps per split
+  if (plain && nblocks < 192 && a.K >= 32 * BK) {
+    // two co-resident blocks per CU (256 CUs): one block per CU leaves a single wave per SIMD, which cannot
+    // hide the staging latency; keep >= 12 K-steps per split so the slab write + reduce stays small
+    splits = 512 / nblocks;
+    const int max_splits = a.K / (12 * BK);
     if (splits > max_splits) splits = max_splits;
     if (splits < 1) splits = 1;
   }

@@ -84,22 +84,27 @@ __global__ __launch_bounds__(256) void radam_kernel(float* __restrict__ p, const
   }
 }
 
+// Sum of squares of the active segments over the flat buffer: float4 grid-stride (segments are 256-B aligned,
+// so a float4 never straddles two), segment found by binary search over the offsets staged in LDS.
 __global__ __launch_bounds__(256) void sumsq_kernel(const float* __restrict__ g, const int64_t* __restrict__ seg_off,
                                                     const int64_t* __restrict__ seg_len,
-                                                    const int* __restrict__ seg_active, int nseg, double* ws) {
-  double acc = 0.0;
-  for (int s = 0; s < nseg; ++s) {
-    if (!seg_active[s]) continue;
-    const float* gp = g + seg_off[s];
-    const int64_t n = seg_len[s];
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-      const float x = gp[i];
-      acc += (double)(x * x);
-    }
-  }
+                                                    const int* __restrict__ seg_active, int nseg, int64_t total,
+                                                    double* ws) {
+  __shared__ int64_t s_off[MAXSEG_LDS];
+  for (int i = threadIdx.x; i < nseg; i += blockDim.x) s_off[i] = seg_off[i];
+  __syncthreads();
+  float acc = 0.f;
+  const int64_t n4 = total >> 2;
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n4; q += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t e = q << 2;
+    const int s = find_seg(s_off, nseg, e);
+    if (!seg_active[s] || e >= s_off[s] + seg_len[s]) continue;
+    const float4 v = reinterpret_cast<const float4*>(g)[q];
+    acc += (v.x * v.x + v.y * v.y) + (v.z * v.z + v.w * v.w);   // past seg_len inside the float4: alignment
+  }                                                                 // padding, always zero
   __shared__ double red[4];
-  acc = wave_sum_d(acc);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  double d = wave_sum_d((double)acc);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = d;
   __syncthreads();
   if (threadIdx.x == 0) atomicAdd(ws, red[0] + red[1] + red[2] + red[3]);
 }
@@ -145,13 +150,18 @@ extern "C" int aw_counter_add(int64_t* counter, int64_t v, void* stream) {
 }
 
 extern "C" int aw_grad_norm_clip(const float* grad, const int64_t* seg_off, const int64_t* seg_len,
-                                 const int* seg_active, int nseg, float max_norm, double* ws, float* out_norm,
-                                 float* out_coef, void* stream) {
-  AW_REQUIRE(grad && seg_off && seg_len && seg_active && ws && out_norm && out_coef && nseg > 0,
-             "aw_grad_norm_clip: bad args");
+                                 const int* seg_active, int nseg, int64_t total, float max_norm, double* ws,
+                                 float* out_norm, float* out_coef, void* stream) {
+  AW_REQUIRE(grad && seg_off && seg_len && seg_active && ws && out_norm && out_coef && nseg > 0 &&
+                 nseg <= MAXSEG_LDS && total >= 0 && total % 4 == 0 && ((uintptr_t)grad & 15) == 0,
+             "aw_grad_norm_clip: bad args (segments <= %d, 16-B aligned, total %% 4 == 0)", MAXSEG_LDS);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (hipMemsetAsync(ws, 0, sizeof(double), s) != hipSuccess) return aw::check_launch("aw_grad_norm_clip memset");
-  hipLaunchKernelGGL(sumsq_kernel, dim3(1024), dim3(256), 0, s, grad, seg_off, seg_len, seg_active, nseg, ws);
+  int64_t g = (total / 4 + 255) / 256;
+  if (g > 1024) g = 1024;
+  if (g < 1) g = 1;
+  hipLaunchKernelGGL(sumsq_kernel, dim3((int)g), dim3(256), 0, s, grad, seg_off, seg_len, seg_active, nseg, total,
+                     ws);
   hipLaunchKernelGGL(clip_coef_kernel, dim3(1), dim3(1), 0, s, ws, max_norm, out_norm, out_coef);
   return aw::check_launch("aw_grad_norm_clip");
 }

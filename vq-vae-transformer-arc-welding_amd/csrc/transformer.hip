@@ -462,24 +462,38 @@ __global__ __launch_bounds__(128) void attn_bwd_dkv_kernel(const T* __restrict__
 __global__ __launch_bounds__(256) void ce_fwd_kernel(const float* __restrict__ logits, int64_t R, int V, int64_t ldl,
                                                      const int64_t* __restrict__ y, int ignore, double* loss_sum,
                                                      double* count, float* __restrict__ lse) {
-  const int lane = threadIdx.x & 63;
-  const int64_t r = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  if (r >= R) return;
-  const float* lr = logits + r * ldl;
-  float mx = -__builtin_huge_valf();
-  for (int i = lane; i < V; i += 64) mx = fmaxf(mx, lr[i]);
-  mx = wave_max(mx);
-  float s = 0.f;
-  for (int i = lane; i < V; i += 64) s += __expf(lr[i] - mx);
-  s = wave_sum(s);
-  const float L = mx + logf(s);
-  if (lane == 0) {
-    lse[r] = L;
-    const int64_t t = y[r];
-    if (t != ignore) {
-      atomicAdd(loss_sum, (double)(L - lr[t]));
-      atomicAdd(count, 1.0);
+  // one wave per row, grid-strided; per-block partial sums -> one pair of f64 atomics per block (thousands of
+  // same-address atomics, one per row, serialise)
+  __shared__ double part[4][2];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  double ls = 0.0, cnt = 0.0;
+  for (int64_t r = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; r < R; r += nw) {
+    const float* lr = logits + r * ldl;
+    float mx = -__builtin_huge_valf();
+    for (int i = lane; i < V; i += 64) mx = fmaxf(mx, lr[i]);
+    mx = wave_max(mx);
+    float s = 0.f;
+    for (int i = lane; i < V; i += 64) s += __expf(lr[i] - mx);
+    s = wave_sum(s);
+    const float L = mx + logf(s);
+    if (lane == 0) {
+      lse[r] = L;
+      const int64_t t = y[r];
+      if (t != ignore) {
+        ls += (double)(L - lr[t]);
+        cnt += 1.0;
+      }
     }
+  }
+  if (lane == 0) {
+    part[wv][0] = ls;
+    part[wv][1] = cnt;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    atomicAdd(loss_sum, (part[0][0] + part[1][0]) + (part[2][0] + part[3][0]));
+    atomicAdd(count, (part[0][1] + part[1][1]) + (part[2][1] + part[3][1]));
   }
 }
 
@@ -759,7 +773,7 @@ extern "C" int aw_ce_fwd(const float* logits, int64_t R, int V, int64_t ldl, con
                          double* loss_sum, double* count, float* lse, void* stream) {
   AW_REQUIRE(logits && y && loss_sum && count && lse && R >= 0 && V > 0 && ldl >= V, "aw_ce_fwd: bad args");
   if (R == 0) return AW_OK;
-  hipLaunchKernelGGL(ce_fwd_kernel, dim3(aw_cdiv(R, 4)), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), logits, R,
+  hipLaunchKernelGGL(ce_fwd_kernel, dim3(gridcap(R * 64, 256, 1024)), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), logits, R,
                      V, ldl, y, ignore_index, loss_sum, count, lse);
   return aw::check_launch("aw_ce_fwd");
 }
