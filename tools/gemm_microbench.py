@@ -73,5 +73,23 @@ def run():
         print(f"{r[0]:28s} {r[1]:9.1f} {r[2]:9.1f} {r[3]:9.1f}")
 
 
-if __name__ == "__main__":
+if __name__ == "__main__" and len(sys.argv) == 1:
     run()
+
+
+def sweep():
+    """K sweep at M=16384, N=512 (C f32 only / no output at all via C bf16 tiny?): run under rocprofv3 to get pure
+    kernel durations; python tools/gemm_microbench.py sweep"""
+    M, N = 16384, 512
+    for Kd in (64, 128, 256, 512, 1024, 2048):
+        A = torch.randn(M, Kd, device=dev).to(bf)
+        W = torch.randn(N, Kd, device=dev).to(bf)
+        C = torch.empty(M, N, device=dev)
+        Cb = torch.empty(M, N, device=dev, dtype=bf)
+        t1 = timeit(lambda: K.gemm(A, W, M, N, Kd, C=C))
+        t2 = timeit(lambda: K.gemm(A, W, M, N, Kd, C=Cb))
+        print(f"K={Kd:5d}  C f32 {t1:7.1f} us   C bf16 {t2:7.1f} us", flush=True)
+
+
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "sweep":
+    sweep()
