@@ -50,15 +50,16 @@ __device__ __forceinline__ float gelu_tanh_grad(float x) {
 }
 
 // ---------------------------------------------------------------- counter-based RNG (dropout masks)
-// keep(e) for element e of a launch with seed s: splitmix64 finaliser of s + (e+1)*golden, top 24 bits
-// as a uniform in [0,1).  Forward and backward regenerate the identical mask from (seed, element).
-__device__ __forceinline__ float aw_uniform(uint64_t seed, uint64_t e) {
-  uint64_t z = seed + (e + 1ull) * 0x9E3779B97F4A7C15ull;
+// One splitmix64 draw per aligned group of 4 elements (g = e >> 2) of a launch with seed s; element e takes the
+// 16-bit uniform in bits [16*(e & 3), 16*(e & 3) + 16) and is dropped iff u < round(p * 65536).  Forward and
+// backward regenerate the identical mask from (seed, element); a row of 4 aligned columns costs one hash.
+__device__ __forceinline__ uint64_t aw_hash_group(uint64_t seed, uint64_t g) {
+  uint64_t z = seed + (g + 1ull) * 0x9E3779B97F4A7C15ull;
   z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
   z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-  z ^= z >> 31;
-  return (float)(z >> 40) * (1.0f / 16777216.0f);
+  return z ^ (z >> 31);
 }
+__device__ __forceinline__ uint32_t aw_drop_threshold(float p) { return (uint32_t)(p * 65536.f + 0.5f); }
 // Effective seed when a device-side per-step counter is supplied (seed_ptr in the ABI).
 __device__ __forceinline__ uint64_t aw_seed_mix(uint64_t salt, const uint64_t* ctr) {
   if (!ctr) return salt;
@@ -68,7 +69,21 @@ __device__ __forceinline__ uint64_t aw_seed_mix(uint64_t salt, const uint64_t* c
 }
 __device__ __forceinline__ float aw_dropout_scale(uint64_t seed, uint64_t e, float p) {
   if (p <= 0.f) return 1.f;
-  return aw_uniform(seed, e) < p ? 0.f : 1.f / (1.f - p);
+  const uint32_t u = (uint32_t)(aw_hash_group(seed, e >> 2) >> (16 * (e & 3))) & 0xFFFFu;
+  return u < aw_drop_threshold(p) ? 0.f : 1.f / (1.f - p);
+}
+// scales of elements e0 .. e0+3 (one hash when e0 is group-aligned)
+__device__ __forceinline__ void aw_dropout_scale4(uint64_t seed, uint64_t e0, float p, float (&s)[4]) {
+  if ((e0 & 3) == 0) {
+    const uint64_t h = aw_hash_group(seed, e0 >> 2);
+    const uint32_t t = aw_drop_threshold(p);
+    const float k = 1.f / (1.f - p);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) s[i] = ((uint32_t)(h >> (16 * i)) & 0xFFFFu) < t ? 0.f : k;
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) s[i] = aw_dropout_scale(seed, e0 + i, p);
+  }
 }
 
 // ---------------------------------------------------------------- typed load/store helpers

@@ -1,491 +1,74 @@
-// MFMA GEMM family for gfx950 (CDNA4): one kernel body for every dense contraction of the hot path.
-//
-// Tile 128x128 per 256-thread workgroup (4 waves as 2x2, each wave 64x64 = 4x4 fragments of 16x16),
-// K staged through LDS 64 bytes per row per step (32 bf16 / 16 f32), register-staged double buffer, one barrier
-// per K step.  Operand layouts are compile-time template parameters:
-//   K-contiguous operand ([rows][K], e.g. activations in forward, weights [out][in]) -> LDS image [row][k],
-//       fragments by one ds_read_b128;
-//   row-contiguous operand ([K][rows], e.g. activations as the weight-gradient reduction operand) -> LDS image
-//       [k][row] written with one ds_write_b128 per staged chunk; bf16 fragments come from two
-//       ds_read_b64_tr_b16 hardware-transposed reads (gfx950), f32 fragments from four ds_read_b32.
-// Implicit k=3/pad=1 convolution (decoder ResBlocks) = row-shifted loads with a per-window zero mask.
-//   bf16: v_mfma_f32_16x16x32_bf16 (fp32 accumulate)      f32: v_mfma_f32_16x16x4_f32 (exact f32)
-// Split-K (grid.y) with fp32 atomics serves the weight-gradient shapes (M x N = 512 x 512 .. 2560 x 512,
-// K = tokens), whose tile count alone would leave most of the 256 CUs idle.
-// Fused epilogue (non-split): bias, act' (GELU backward), dropout (counter-based mask), residual add,
-// beta*C, second output (act / copy / dropout-masked copy), BatchNorm column statistics; and a fused A-row-sum
-// (bias gradients) from the staged A tiles in every mode.
-#include "common.h"
+// MFMA GEMM family: host entry points (aw_gemm, aw_gemm_ws, aw_gemm_workspace) and the EP_GENERIC / EP_ACCUM
+// kernel instantiations.  The kernel itself is in gemm_core.h; specialised epilogues in gemm_fast_*.hip.
+#include "gemm_core.h"
+
+using namespace awg;
 
 namespace {
 
-constexpr int BM = 128, BN = 128, NTHREADS = 256;
-constexpr int ROWB = 128;                // bytes of K per operand row per step (K-contiguous image pitch)
-constexpr int STAGE_OP = 16384;          // bytes per operand per stage (both images are exactly 16 KiB)
-constexpr int CPITCH = BN + 4;           // f32 pitch of the epilogue tile
-constexpr int SMEM = (BM * CPITCH * 4 > 4 * STAGE_OP) ? BM * CPITCH * 4 : 4 * STAGE_OP;
-constexpr int NCH = STAGE_OP / 16 / NTHREADS;   // 16-B chunks per thread per operand per step (4)
+template <typename T, Layout LY>
+void launch_generic(const GemmP& P, hipStream_t s, bool ragged) {
+  if (ragged) launch_kernel<T, LY, true, EP_GENERIC>(P, s);
+  else launch_kernel<T, LY, false, EP_GENERIC>(P, s);
+}
 
-template <typename T> struct TT;
-template <> struct TT<bf16> {
-  static constexpr int EPC = 8, BK = 64;
-  static constexpr int MPB = 256;          // k-row of the row-contiguous image: 128 rows x 2 B
-  // rotation of k-row k (bytes): conflict-free ds_read_b64_tr_b16 for the 32-lane halves
-  __device__ static constexpr int rot(int k) { return 32 * ((k & 3) + 4 * ((k >> 3) & 1)); }
-};
-template <> struct TT<float> {
-  static constexpr int EPC = 4, BK = 32;
-  static constexpr int MPB = 512;          // 128 rows x 4 B
-  __device__ static constexpr int rot(int k) { return 64 * ((k >> 2) & 1); }
-};
+Layout layout_of(const aw_gemm_args& a) {
+  const bool conv = a.conv_cin > 0;
+  const bool aconv = conv && a.conv_operand == 0, bconv = conv && a.conv_operand == 1;
+  if (!a.a_trans && !a.b_trans) return aconv ? L_NN_CONV : L_NN;
+  if (!a.a_trans && a.b_trans) return aconv ? L_NT_CONV : L_NT;
+  if (a.a_trans && !a.b_trans) return L_TN;
+  return bconv ? L_TT_KCONV : L_TT;
+}
 
-// K-contiguous image [row][128 B]: logical 16-B chunk c of row r lives at physical chunk c ^ ((r >> 1) & 7)
-// (conflict-free ds_read_b128 for the 16-row fragments; verified against the gfx950 lane groups).
-__device__ __forceinline__ int nt_off(int row, int chunk) { return row * ROWB + ((chunk ^ ((row >> 1) & 7)) << 4); }
+// compile-time epilogue code of a launch (EP_GENERIC when no specialisation can apply)
+uint32_t epi_code(const aw_gemm_args& a, const GemmP& P, bool ragged) {
+  if (P.splits > 1 || a.accumulate) return ragged ? EP_GENERIC : EP_ACCUM;
+  if (ragged || !P.vec || a.N % 4 != 0 || a.alpha != 1.f) return EP_GENERIC;
+  uint32_t c = 0;
+  if (a.bias) c |= EP_BIAS;
+  if (a.bias && a.bias_mod > 0) c |= EP_BIASMOD;
+  if (a.pre) c |= EP_PRE;
+  if ((a.pre || a.c2_mode == 1) && a.act == AW_ACT_GELU_TANH) c |= EP_TANH;
+  if (a.drop_p > 0.f) c |= EP_DROP;
+  if (a.resid) c |= EP_RESID;
+  if (a.beta != 0.f) c |= EP_BETA;
+  if (a.C) c |= EP_C | (a.c_dtype == AW_BF16 ? EP_CBF : 0u);
+  if (a.c2_mode == 1) c |= EP_C2ACT;
+  else if (a.c2_mode == 2 || (a.c2_mode == 3 && a.drop2_p <= 0.f)) c |= EP_C2COPY;
+  else if (a.c2_mode == 3) c |= EP_C2DROP;
+  if (a.c2_mode && a.c2_dtype == AW_BF16) c |= EP_C2BF;
+  if (a.colstats) c |= EP_STATS;
+  return c;
+}
+
 template <typename T>
-__device__ __forceinline__ int tr_off(int krow, int byte_in_row) {
-  return krow * TT<T>::MPB + ((byte_in_row + TT<T>::rot(krow)) & (TT<T>::MPB - 1));
-}
-
-struct GemmP {
-  aw_gemm_args a;
-  int tiles_n, nblocks, splits, ksplit;
-  int vec;   // every epilogue operand row is 16-B aligned: vectorised epilogue
-  int a_bytes, b_bytes;  // extents of A and B (buffer-descriptor ranges; < 2^31)
-  float* ws; // split-K partial slabs [splits][M][N] (NULL: fp32 atomics)
-};
-
-enum { CONV_NONE = 0, CONV_ROWSHIFT = 1, CONV_KSHIFT = 2 };
-
-// ---------------------------------------------------------------- operand staging (global -> regs -> LDS)
-// Loads are raw buffer loads: an out-of-range byte offset returns zeros, which implements every mask
-// (M/N/K tails, implicit-conv window edges) without branches, so the compiler can keep two K steps of
-// loads in flight and wait with a counted vmcnt.
-constexpr int OOB = 0x7FFFFFF0;
-
-template <typename T, bool TR, int CONV, bool RAGGED>
-struct Stager {
-  static constexpr int EPC = TT<T>::EPC, BK = TT<T>::BK;
-  static constexpr int CPR = 128 / EPC;   // chunks per k-row of a row-contiguous tile
-  static constexpr int CPK = BK / EPC;    // chunks per row of a K-contiguous tile (8)
-  const T* base;
-  int64_t ld;
-  int rows_total, row0, kend, cin, seg, dir;
-  __amdgpu_buffer_rsrc_t rsrc;
-  // per-thread invariants of the implicit convolution (window position / tap of each chunk)
-  int wpos[NCH];    // ROWSHIFT: row % seg (fixed rows);  KSHIFT: (k0 + krow) % seg, advanced per K step
-  int tapoff[NCH];  // KSHIFT: row shift j-1 of the chunk's column tap
-  int colin[NCH];   // KSHIFT: column within the tap (m - j*cin)
-
-  __device__ __forceinline__ void init(int kbeg, int tid, int nbytes) {
-    rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, nbytes, 0x00020000);
-#pragma unroll
-    for (int i = 0; i < NCH; ++i) {
-      const int c = tid + i * NTHREADS;
-      if constexpr (CONV == CONV_ROWSHIFT) {
-        wpos[i] = (row0 + c / CPK) % seg;
-      } else if constexpr (CONV == CONV_KSHIFT) {
-        const int m = row0 + (c % CPR) * EPC;
-        const int j = m / cin;
-        tapoff[i] = j - 1;
-        colin[i] = m - j * cin;
-        wpos[i] = (kbeg + c / CPR) % seg;
-      }
+void dispatch(const GemmP& P, hipStream_t s, bool ragged) {
+  const Layout ly = layout_of(P.a);
+  const uint32_t code = epi_code(P.a, P, ragged);
+  constexpr bool BF = sizeof(T) == 2;
+  if (code == EP_ACCUM) {
+    switch (ly) {
+      case L_TN: launch_kernel<T, L_TN, false, EP_ACCUM>(P, s); return;
+      case L_TT: launch_kernel<T, L_TT, false, EP_ACCUM>(P, s); return;
+      case L_TT_KCONV: launch_kernel<T, L_TT_KCONV, false, EP_ACCUM>(P, s); return;
+      default: break;
     }
+  } else if (code != EP_GENERIC) {
+    if ((ly == L_NN || ly == L_NN_CONV) && launch_fast_fwd(P, s, BF, ly, code)) return;
+    if ((ly == L_NT || ly == L_NT_CONV) && launch_fast_bwd(P, s, BF, ly, code)) return;
   }
-
-  __device__ __forceinline__ uint4 bload(int off) const {
-    auto r = __builtin_amdgcn_raw_buffer_load_b128(rsrc, off, 0, 0);
-    uint4 u;
-    memcpy(&u, &r, 16);
-    return u;
-  }
-
-  __device__ __forceinline__ void load(int k0, int tid, uint4 (&v)[NCH]) {
-    // ROWSHIFT: cin % BK == 0, so the tap is uniform over the whole K step
-    const int jrow = (CONV == CONV_ROWSHIFT) ? k0 / cin : 0;
-#pragma unroll
-    for (int i = 0; i < NCH; ++i) {
-      const int c = tid + i * NTHREADS;
-      if constexpr (!TR) {
-        const int row = row0 + c / CPK;
-        const int k = k0 + (c % CPK) * EPC;
-        bool ok = row < rows_total && k < kend;
-        int src = row, kk = k;
-        if constexpr (CONV == CONV_ROWSHIFT) {
-          kk = k - jrow * cin;
-          const int sft = dir * (jrow - 1);
-          ok = ok && (wpos[i] + sft >= 0) && (wpos[i] + sft < seg);
-          src = row + sft;
-        }
-        if constexpr (RAGGED) {
-          if (ok && k + EPC > kend) {
-            const T* p = base + (int64_t)src * ld + kk;
-            T tmp[EPC];
-#pragma unroll
-            for (int e = 0; e < EPC; ++e) tmp[e] = (k + e < kend) ? p[e] : from_f32<T>(0.f);
-            memcpy(&v[i], tmp, 16);
-            continue;
-          }
-        }
-        v[i] = bload(ok ? (int)(((int64_t)src * ld + kk) * (int)sizeof(T)) : OOB);
-      } else {
-        const int k = k0 + c / CPR;
-        const int m = row0 + (c % CPR) * EPC;
-        bool ok = k < kend && m < rows_total;
-        int srck = k, mm = m;
-        if constexpr (CONV == CONV_KSHIFT) {
-          mm = colin[i];
-          const int sft = tapoff[i];
-          ok = ok && (wpos[i] + sft >= 0) && (wpos[i] + sft < seg);
-          srck = k + sft;
-          wpos[i] += BK % seg;                 // advance the window position to the next K step
-          if (wpos[i] >= seg) wpos[i] -= seg;
-        }
-        if constexpr (RAGGED) {
-          if (ok && m + EPC > rows_total) {
-            const T* p = base + (int64_t)srck * ld + mm;
-            T tmp[EPC];
-#pragma unroll
-            for (int e = 0; e < EPC; ++e) tmp[e] = (m + e < rows_total) ? p[e] : from_f32<T>(0.f);
-            memcpy(&v[i], tmp, 16);
-            continue;
-          }
-        }
-        v[i] = bload(ok ? (int)(((int64_t)srck * ld + mm) * (int)sizeof(T)) : OOB);
-      }
-    }
-  }
-
-  __device__ __forceinline__ void store(char* lds, int tid, const uint4 (&v)[NCH]) const {
-#pragma unroll
-    for (int i = 0; i < NCH; ++i) {
-      const int c = tid + i * NTHREADS;
-      if constexpr (!TR)
-        *reinterpret_cast<uint4*>(lds + nt_off(c / CPK, c % CPK)) = v[i];
-      else
-        *reinterpret_cast<uint4*>(lds + tr_off<T>(c / CPR, (c % CPR) * 16)) = v[i];
-    }
-  }
-};
-
-// ---------------------------------------------------------------- fragments
-typedef short v4i16 __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
-
-// Fragment of the 16 rows [rbase, rbase+16) x this lane's K slice of MFMA sub-step u, as 16 bytes.
-// K order inside a sub-step is the same for A and B: lane group g holds k = 8g..8g+7 (bf16) /
-// k = 4g..4g+3 with one element per f32 MFMA (f32).
-template <typename T, bool TR>
-__device__ __forceinline__ uint4 frag(const char* lds, int rbase, int lane, int u) {
-  const int g = lane >> 4, i = lane & 15;
-  if constexpr (!TR) {
-    return *reinterpret_cast<const uint4*>(lds + nt_off(rbase + i, 4 * u + g));
-  } else if constexpr (sizeof(T) == 2) {
-    // two 4(k) x 16(row) transposed reads: lane 4q+p addresses k-row q, rows 4p..4p+3 of the block;
-    // lane i receives row i, k-rows 0..3
-    const int q = i >> 2, p = i & 3;
-    const int k0 = 32 * u + 8 * g + q;
-    const v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-        (lds_v4i16*)(uintptr_t)(lds + tr_off<T>(k0, 2 * (rbase + 4 * p))));
-    const v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-        (lds_v4i16*)(uintptr_t)(lds + tr_off<T>(k0 + 4, 2 * (rbase + 4 * p))));
-    uint4 out;
-    memcpy(&out, &lo, 8);
-    memcpy(reinterpret_cast<char*>(&out) + 8, &hi, 8);
-    return out;
-  } else {
-    float f[4];
-#pragma unroll
-    for (int s = 0; s < 4; ++s) f[s] = *reinterpret_cast<const float*>(lds + tr_off<T>(16 * u + 4 * g + s, 4 * (rbase + i)));
-    uint4 out;
-    memcpy(&out, f, 16);
-    return out;
+  switch (ly) {
+    case L_NN: launch_generic<T, L_NN>(P, s, ragged); break;
+    case L_NN_CONV: launch_generic<T, L_NN_CONV>(P, s, ragged); break;
+    case L_NT: launch_generic<T, L_NT>(P, s, ragged); break;
+    case L_NT_CONV: launch_generic<T, L_NT_CONV>(P, s, ragged); break;
+    case L_TN: launch_generic<T, L_TN>(P, s, ragged); break;
+    case L_TT: launch_generic<T, L_TT>(P, s, ragged); break;
+    case L_TT_KCONV: launch_generic<T, L_TT_KCONV>(P, s, ragged); break;
   }
 }
 
-template <typename T> struct Mfma;
-template <> struct Mfma<bf16> {
-  __device__ __forceinline__ static void run(f32x4& acc, const uint4& a, const uint4& b) {
-    bf16x8 av, bv;
-    memcpy(&av, &a, 16);
-    memcpy(&bv, &b, 16);
-    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv, acc, 0, 0, 0);
-  }
-};
-template <> struct Mfma<float> {
-  __device__ __forceinline__ static void run(f32x4& acc, const uint4& a, const uint4& b) {
-    f32x4 av, bv;
-    memcpy(&av, &a, 16);
-    memcpy(&bv, &b, 16);
-#pragma unroll
-    for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[s], bv[s], acc, 0, 0, 0);
-  }
-};
-
-__device__ __forceinline__ float act_fwd(int act, float x) { return act == AW_ACT_GELU_TANH ? gelu_tanh(x) : gelu_erf(x); }
-__device__ __forceinline__ float act_bwd(int act, float x) {
-  return act == AW_ACT_GELU_TANH ? gelu_tanh_grad(x) : gelu_erf_grad(x);
-}
-
-// 4 consecutive elements (16-B aligned for f32, 8-B for bf16)
-__device__ __forceinline__ void store4(void* base, int dtype, int64_t e, const float (&v)[4]) {
-  if (dtype == AW_BF16) {
-    bf16 h[4] = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
-    uint2 u;
-    memcpy(&u, h, 8);
-    *reinterpret_cast<uint2*>(reinterpret_cast<bf16*>(base) + e) = u;
-  } else {
-    *reinterpret_cast<float4*>(reinterpret_cast<float*>(base) + e) = make_float4(v[0], v[1], v[2], v[3]);
-  }
-}
-
-// Bijective XCD-aware remap: consecutive logical tiles land on the same XCD (blocks b and b+8 share one).
-__device__ __forceinline__ int xcd_remap(int bid, int nblocks) {
-  const int q = nblocks / 8, r = nblocks % 8;
-  const int xcd = bid % 8, slot = bid / 8;
-  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + slot;
-}
-
-// sum over this thread's half of the staged A K-slice (fused bias gradient of weight-gradient GEMMs)
-template <typename T, bool TR>
-__device__ __forceinline__ float a_row_partial(const char* lds, int tid) {
-  constexpr int BK = TT<T>::BK, EPC = TT<T>::EPC;
-  const int r = tid >> 1, h = tid & 1;
-  float s = 0.f;
-  if constexpr (!TR) {
-#pragma unroll
-    for (int cc = 0; cc < BK / EPC / 2; ++cc) {
-      const T* cp = reinterpret_cast<const T*>(lds + nt_off(r, h * (BK / EPC / 2) + cc));
-#pragma unroll
-      for (int e = 0; e < EPC; ++e) s += to_f32<T>(cp[e]);
-    }
-  } else {
-#pragma unroll
-    for (int e = 0; e < BK / 2; ++e)
-      s += to_f32<T>(*reinterpret_cast<const T*>(lds + tr_off<T>(h * (BK / 2) + e, r * (int)sizeof(T))));
-  }
-  return s;
-}
-
-template <typename T, bool ATR, bool BTR, int ACONV, int BCONV, bool RAGGED>
-__global__ __launch_bounds__(NTHREADS, RAGGED ? 1 : 2) void gemm_kernel(GemmP P) {
-  constexpr int BK = TT<T>::BK;
-  const aw_gemm_args& p = P.a;
-  __shared__ __attribute__((aligned(16))) char smem[SMEM];
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63, wid = tid >> 6;
-  const int wm = wid >> 1, wn = wid & 1;
-  const int tile = xcd_remap(blockIdx.x, P.nblocks);
-  const int tm = tile / P.tiles_n, tn = tile % P.tiles_n;
-  const int m0 = tm * BM, n0 = tn * BN;
-  const int M = p.M, N = p.N;
-  const int kbeg = blockIdx.y * P.ksplit;
-  const int kend = min(p.K, kbeg + P.ksplit);
-
-  Stager<T, ATR, ACONV, RAGGED> sa{reinterpret_cast<const T*>(p.A), p.lda, M, m0, kend, p.conv_cin, p.conv_seg,
-                                   p.conv_dir};
-  Stager<T, BTR, BCONV, RAGGED> sb{reinterpret_cast<const T*>(p.B), p.ldb, N, n0, kend, p.conv_cin, p.conv_seg, 1};
-  sa.init(kbeg, tid, P.a_bytes);
-  sb.init(kbeg, tid, P.b_bytes);
-  const bool do_rowsum = p.a_rowsum != nullptr && tn == 0;
-
-  f32x4 acc[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float rowsum = 0.f;
-
-  auto compute = [&](const char* a_l) {
-    const char* b_l = a_l + STAGE_OP;
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      uint4 af[4], bfr[4];
-#pragma unroll
-      for (int f = 0; f < 4; ++f) {
-        af[f] = frag<T, ATR>(a_l, wm * 64 + f * 16, lane, u);
-        bfr[f] = frag<T, BTR>(b_l, wn * 64 + f * 16, lane, u);
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) Mfma<T>::run(acc[i][j], af[i], bfr[j]);
-    }
-    if (do_rowsum) rowsum += a_row_partial<T, ATR>(a_l, tid);
-  };
-
-  // Pipeline: LDS stage s holds K step t (t % 2 == s) while the registers of the other set carry the loads
-  // of step t+1 and the loads of step t+2 are issued at the top of step t: two steps of latency cover.
-  char* L0 = smem;
-  char* L1 = smem + 2 * STAGE_OP;
-  const int nk = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
-  uint4 ra0[NCH], rb0[NCH], ra1[NCH], rb1[NCH];
-  sa.load(kbeg, tid, ra0);
-  sb.load(kbeg, tid, rb0);
-  sa.load(kbeg + BK, tid, ra1);
-  sb.load(kbeg + BK, tid, rb1);
-  sa.store(L0, tid, ra0);
-  sb.store(L0 + STAGE_OP, tid, rb0);
-  __syncthreads();
-  for (int kt = 0; kt < nk; kt += 2) {
-    sa.load(kbeg + (kt + 2) * BK, tid, ra0);   // beyond kend: out-of-range -> zeros, never read
-    sb.load(kbeg + (kt + 2) * BK, tid, rb0);
-    compute(L0);
-    sa.store(L1, tid, ra1);
-    sb.store(L1 + STAGE_OP, tid, rb1);
-    __syncthreads();
-    if (kt + 1 >= nk) break;
-    sa.load(kbeg + (kt + 3) * BK, tid, ra1);
-    sb.load(kbeg + (kt + 3) * BK, tid, rb1);
-    compute(L1);
-    sa.store(L0, tid, ra0);
-    sb.store(L0 + STAGE_OP, tid, rb0);
-    __syncthreads();
-  }
-
-  if (do_rowsum) {
-    rowsum += __shfl_xor(rowsum, 1, 64);
-    const int r = m0 + (tid >> 1);
-    if ((tid & 1) == 0 && r < M) atomicAdd(p.a_rowsum + r, rowsum);
-  }
-
-  // ---------------------------------------------------------------- epilogue
-  // 1) accumulators -> LDS tile (static register indexing), 2) one element per thread per step with
-  //    consecutive threads on consecutive columns: every wave instruction touches 256 contiguous bytes.
-  float* Cs = reinterpret_cast<float*>(smem);
-  {
-    const int cq = lane & 15, rq = (lane >> 4) * 4;
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          Cs[(wm * 64 + i * 16 + rq + r) * CPITCH + wn * 64 + j * 16 + cq] = acc[i][j][r];
-  }
-  __syncthreads();
-  const int rows_here = min(BM, M - m0);
-  if (P.splits > 1 && P.ws) {  // partial slab of this split: plain coalesced stores, reduced by gemm_reduce
-    const int lc = tid & 127, col = n0 + lc;
-    if (col >= N) return;
-    float* slab = P.ws + (int64_t)blockIdx.y * M * N;
-    for (int lr = tid >> 7; lr < rows_here; lr += 2) slab[(int64_t)(m0 + lr) * N + col] = Cs[lr * CPITCH + lc];
-    return;
-  }
-  if (P.splits > 1 || p.accumulate) {  // accumulate into f32 C with atomics (consecutive lanes -> columns)
-    const int lc = tid & 127, col = n0 + lc;
-    if (col >= N) return;
-    const int64_t oc = p.col_mod > 0 ? (int64_t)(col % p.col_mod) * p.col_mul + col / p.col_mod + p.col_off
-                                     : (int64_t)col * (p.col_mul > 0 ? p.col_mul : 1) + p.col_off;
-    float* C = reinterpret_cast<float*>(p.C);
-    for (int lr = tid >> 7; lr < rows_here; lr += 2)
-      atomicAdd(C + (int64_t)(m0 + lr) * p.ldc + oc, p.alpha * Cs[lr * CPITCH + lc]);
-    return;
-  }
-  const uint64_t dseed = p.drop_p > 0.f ? aw_seed_mix(p.drop_seed, p.seed_ptr) : 0ull;
-  const uint64_t dseed2 = p.c2_mode == 3 ? aw_seed_mix(p.drop2_seed, p.seed_ptr) : 0ull;
-  // thread -> 4 consecutive columns (c4) x rows r0, r0+8, ...; 4 rows of loads in flight per thread
-  const int c4 = (tid & 31) * 4, r0 = tid >> 5;
-  const int col = n0 + c4;
-  const bool vec = P.vec && col + 4 <= N;
-  float bias[4], csum[4] = {0.f, 0.f, 0.f, 0.f}, csq[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    const int c = col + e;
-    bias[e] = (p.bias && c < N) ? p.bias[p.bias_mod > 0 ? c % p.bias_mod : c] : 0.f;
-  }
-  if (col < N) {
-    for (int lr0 = r0; lr0 < rows_here; lr0 += 32) {
-      float4 pre4[4], res4[4], old4[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {  // issue the operand loads of 4 rows first
-        const int lr = lr0 + 8 * u;
-        if (lr >= rows_here) break;
-        const int64_t row = m0 + lr;
-        if (vec) {
-          if (p.pre) pre4[u] = *reinterpret_cast<const float4*>(p.pre + row * p.ld_pre + col);
-          if (p.resid) res4[u] = *reinterpret_cast<const float4*>(p.resid + row * p.ld_resid + col);
-          if (p.beta != 0.f) old4[u] = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(p.C) + row * p.ldc + col);
-        } else {
-          float a[4] = {0.f, 0.f, 0.f, 0.f}, b[4] = {0.f, 0.f, 0.f, 0.f}, c[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            if (col + e >= N) break;
-            if (p.pre) a[e] = p.pre[row * p.ld_pre + col + e];
-            if (p.resid) b[e] = p.resid[row * p.ld_resid + col + e];
-            if (p.beta != 0.f) c[e] = reinterpret_cast<const float*>(p.C)[row * p.ldc + col + e];
-          }
-          pre4[u] = make_float4(a[0], a[1], a[2], a[3]);
-          res4[u] = make_float4(b[0], b[1], b[2], b[3]);
-          old4[u] = make_float4(c[0], c[1], c[2], c[3]);
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int lr = lr0 + 8 * u;
-        if (lr >= rows_here) break;
-        const int64_t row = m0 + lr;
-        const float4 a4 = *reinterpret_cast<const float4*>(Cs + lr * CPITCH + c4);
-        const float av[4] = {a4.x, a4.y, a4.z, a4.w};
-        const float pv[4] = {pre4[u].x, pre4[u].y, pre4[u].z, pre4[u].w};
-        const float rv[4] = {res4[u].x, res4[u].y, res4[u].z, res4[u].w};
-        const float ov[4] = {old4[u].x, old4[u].y, old4[u].z, old4[u].w};
-        float v[4], w[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          float x = p.alpha * av[e] + bias[e];
-          if (p.pre) x *= act_bwd(p.act, pv[e]);
-          if (p.drop_p > 0.f) x *= aw_dropout_scale(dseed, (uint64_t)row * N + col + e, p.drop_p);
-          if (p.resid) x += rv[e];
-          if (p.beta != 0.f) x += p.beta * ov[e];
-          v[e] = x;
-          float y = x;
-          if (p.c2_mode == 1) y = act_fwd(p.act, x);
-          else if (p.c2_mode == 3) y = x * aw_dropout_scale(dseed2, (uint64_t)row * N + col + e, p.drop2_p);
-          w[e] = y;
-          if (col + e < N) {
-            csum[e] += x;
-            csq[e] += x * x;
-          }
-        }
-        if (vec) {
-          if (p.C) store4(p.C, p.c_dtype, row * p.ldc + col, v);
-          if (p.c2_mode) store4(p.C2, p.c2_dtype, row * p.ldc2 + col, w);
-        } else {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            if (col + e >= N) break;
-            if (p.C) store_from_f32(p.C, p.c_dtype, row * p.ldc + col + e, v[e]);
-            if (p.c2_mode) store_from_f32(p.C2, p.c2_dtype, row * p.ldc2 + col + e, w[e]);
-          }
-        }
-      }
-    }
-  }
-  if (p.colstats) {  // BatchNorm batch statistics: reduce the 8 row-groups of a column, one f64 atomic each
-    __syncthreads();
-    float* red = Cs;   // [8][2][128]
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      red[(r0 * 2 + 0) * 128 + c4 + e] = csum[e];
-      red[(r0 * 2 + 1) * 128 + c4 + e] = csq[e];
-    }
-    __syncthreads();
-    if (tid < 128 && n0 + tid < N) {
-      float a = 0.f, b = 0.f;
-#pragma unroll
-      for (int g = 0; g < 8; ++g) {
-        a += red[(g * 2 + 0) * 128 + tid];
-        b += red[(g * 2 + 1) * 128 + tid];
-      }
-      const int sl = (n0 + tid) % p.stats_mod;
-      atomicAdd(p.colstats + sl, (double)a);
-      atomicAdd(p.colstats + p.stats_mod + sl, (double)b);
-    }
-  }
-}
 
 // sum of the split-K slabs -> C (accumulate mode: += through the column map; else alpha*sum + beta*C)
 __global__ __launch_bounds__(256) void gemm_reduce_kernel(const float* __restrict__ ws, int splits, int M, int N,
@@ -506,34 +89,6 @@ __global__ __launch_bounds__(256) void gemm_reduce_kernel(const float* __restric
       if (p.beta != 0.f) v += p.beta * C[r * p.ldc + c];
       C[r * p.ldc + c] = v;
     }
-  }
-}
-
-template <typename T, bool ATR, bool BTR, int ACONV, int BCONV>
-void launch(const GemmP& P, hipStream_t s, bool ragged) {
-  dim3 grid(P.nblocks, P.splits);
-  if (ragged)
-    hipLaunchKernelGGL((gemm_kernel<T, ATR, BTR, ACONV, BCONV, true>), grid, dim3(NTHREADS), 0, s, P);
-  else
-    hipLaunchKernelGGL((gemm_kernel<T, ATR, BTR, ACONV, BCONV, false>), grid, dim3(NTHREADS), 0, s, P);
-}
-
-template <typename T>
-void dispatch(const GemmP& P, hipStream_t s, bool ragged) {
-  const aw_gemm_args& a = P.a;
-  const bool conv = a.conv_cin > 0;
-  const bool aconv = conv && a.conv_operand == 0, bconv = conv && a.conv_operand == 1;
-  if (!a.a_trans && !a.b_trans) {
-    if (aconv) launch<T, false, false, CONV_ROWSHIFT, CONV_NONE>(P, s, ragged);
-    else launch<T, false, false, CONV_NONE, CONV_NONE>(P, s, ragged);
-  } else if (!a.a_trans && a.b_trans) {
-    if (aconv) launch<T, false, true, CONV_ROWSHIFT, CONV_NONE>(P, s, ragged);
-    else launch<T, false, true, CONV_NONE, CONV_NONE>(P, s, ragged);
-  } else if (a.a_trans && !a.b_trans) {
-    launch<T, true, false, CONV_NONE, CONV_NONE>(P, s, ragged);
-  } else {
-    if (bconv) launch<T, true, true, CONV_NONE, CONV_KSHIFT>(P, s, ragged);
-    else launch<T, true, true, CONV_NONE, CONV_NONE>(P, s, ragged);
   }
 }
 

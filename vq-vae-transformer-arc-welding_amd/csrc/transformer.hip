@@ -180,9 +180,13 @@ __global__ __launch_bounds__(256) void ln_bwd_vec_kernel(const float* __restrict
       }
       *reinterpret_cast<float4*>(dx + r * D + c) = make_float4(v[0], v[1], v[2], v[3]);
       if (dx2) {
-        float m[4];
+        float m[4] = {v[0], v[1], v[2], v[3]};
+        if (drop_p > 0.f) {
+          float ds[4];
+          aw_dropout_scale4(drop_seed, (uint64_t)r * D + c, drop_p, ds);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) m[e] = v[e] * aw_dropout_scale(drop_seed, (uint64_t)r * D + c + e, drop_p);
+          for (int e = 0; e < 4; ++e) m[e] *= ds[e];
+        }
         if constexpr (sizeof(T2) == 2) {
           bf16 h[4] = {(bf16)m[0], (bf16)m[1], (bf16)m[2], (bf16)m[3]};
           uint2 u;
