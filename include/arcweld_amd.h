@@ -79,6 +79,12 @@ int aw_gemm(const aw_gemm_args* args, void* stream);
  * aw_gemm_workspace returns the number of f32 elements needed (0: no split). */
 int64_t aw_gemm_workspace(const aw_gemm_args* args);
 int aw_gemm_ws(const aw_gemm_args* args, float* ws, int64_t ws_elems, void* stream);
+/* Grouped launch of n <= AW_GEMM_MAX_GROUPS accumulate-mode problems (weight gradients) that share every field
+ * except A, B, C and a_rowsum: one kernel over all groups' tiles.  The backward defers the weight gradients of
+ * the ResBlock stack and issues them as one launch per layer kind (model/vq_vae_patch_embedd.py:60-74 grads;
+ * model/transformer_block.py:30,32,78-79 grads), so each tile runs the full token reduction without split-K. */
+#define AW_GEMM_MAX_GROUPS 16
+int aw_gemm_grouped(const aw_gemm_args* args, int n, void* stream);
 
 /* -------------------------------------------------------------------------------- vector quantizer
  * VectorQuantizer.forward (model/vector_quantizer.py:76-119), fp32, codebook staged in LDS, no MFMA:

@@ -221,3 +221,35 @@ def test_gemm_split_k_accumulate_colmap(K, dtype, use_ws):
     ref = G0.cpu() + prod
     rtol, atol = _tol(dtype, Kd)
     torch.testing.assert_close(G.cpu(), ref, rtol=rtol, atol=atol * np.sqrt(Kd) * 4)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("conv", [False, True])
+def test_gemm_grouped_weight_grads_match_single_launches(K, dtype, conv):
+    """aw_gemm_grouped (deferred ResBlock weight gradients, one launch for the stack) == one aw_gemm per problem:
+    accumulate mode with the conv-tap column map, fused bias-gradient row sums, per-group pointers."""
+    S, Cin, Cout, Ntok = 16, 64, 128, 16 * 40
+    probs_g, probs_s, outs_g, outs_s = [], [], [], []
+    for g in range(3):
+        go = _rand((Ntok, Cout), 30 + g, dtype)
+        x = _rand((Ntok, Cin), 40 + g, dtype)
+        for outs, probs in ((outs_g, probs_g), (outs_s, probs_s)):
+            Wg = torch.zeros(Cout, Cin, 3, device=DEV)
+            bg = torch.zeros(Cout, device=DEV)
+            outs.append((Wg, bg))
+            if conv:
+                kw = dict(a_trans=True, b_trans=True, conv=(Cin, S, 1, 1), C=Wg.view(Cout, 3 * Cin), accumulate=True,
+                          col_map=(Cin, 3, 0), a_rowsum=bg)
+                probs.append((go, x, Cout, 3 * Cin, Ntok, kw))
+            else:
+                kw = dict(a_trans=True, b_trans=True, C=Wg.view(Cout, 3 * Cin), accumulate=True, col_map=(0, 3, 1),
+                          a_rowsum=bg)
+                probs.append((go, x, Cout, Cin, Ntok, kw))
+    K.gemm_grouped(probs_g)
+    for (A, B, M, N, Kd, kw) in probs_s:
+        K.gemm(A, B, M, N, Kd, **kw)
+    rtol, atol = _tol(dtype, Ntok)
+    for (Wg, bg), (Ws, bs) in zip(outs_g, outs_s):
+        assert Wg.abs().sum() > 0
+        torch.testing.assert_close(Wg.cpu(), Ws.cpu(), rtol=rtol, atol=atol * 10)
+        torch.testing.assert_close(bg.cpu(), bs.cpu(), rtol=1e-5, atol=1e-4)

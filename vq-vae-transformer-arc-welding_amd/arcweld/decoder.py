@@ -149,6 +149,8 @@ def backward(m, sv, g_out, slot):
     last = nb - 1
     K.layernorm_bwd(sv.x_last, gxf, lnf.weight, sv.muf, sv.rsf, gx, False, slot(lnf.weight), slot(lnf.bias),
                     dx2=go, drop=(sv.p_drop, sv.seed_mlp[last] if nb else 0), seed_ptr=sv.ctr)
+    # per-layer-kind weight gradients are deferred and issued as one grouped launch per kind over all blocks
+    wg = {"fc2": [], "fc1": [], "proj": [], "qkv": []}
     for i in reversed(range(nb)):
         blk = m.transformer.h[i]
         at, mlp = blk.attn, blk.mlp
@@ -156,12 +158,12 @@ def backward(m, sv, g_out, slot):
         # ---- MLP
         gh = e(R, 4 * d, dt=T_)
         K.gemm(go, c["Wp"], R, 4 * d, d, b_trans=True, act=K.AW_ACT_GELU_TANH, pre=c["h"], C=gh)
-        K.gemm(go, c["g"], d, 4 * d, R, a_trans=True, b_trans=True, C=slot(mlp.c_proj.weight), accumulate=True,
-               a_rowsum=slot(mlp.c_proj.bias))
+        wg["fc2"].append((go, c["g"], d, 4 * d, R, dict(a_trans=True, b_trans=True, C=slot(mlp.c_proj.weight),
+                                                         accumulate=True, a_rowsum=slot(mlp.c_proj.bias))))
         ga2 = e(R, d)
         K.gemm(gh, c["Wfc"], R, d, 4 * d, b_trans=True, C=ga2)
-        K.gemm(gh, c["a2"], 4 * d, d, R, a_trans=True, b_trans=True, C=slot(mlp.c_fc.weight), accumulate=True,
-               a_rowsum=slot(mlp.c_fc.bias))
+        wg["fc1"].append((gh, c["a2"], 4 * d, d, R, dict(a_trans=True, b_trans=True, C=slot(mlp.c_fc.weight),
+                                                          accumulate=True, a_rowsum=slot(mlp.c_fc.bias))))
         go2 = e(R, d, dt=T_)
         K.layernorm_bwd(c["x1"], ga2, blk.ln_2.weight, c["mu2"], c["rs2"], gx, True, slot(blk.ln_2.weight),
                         slot(blk.ln_2.bias), dx2=go2, drop=(sv.p_drop, sv.seed_attn[i]),
@@ -169,19 +171,21 @@ def backward(m, sv, g_out, slot):
         # ---- attention
         gy = e(R, d, dt=T_)
         K.gemm(go2, c["Wo"], R, d, d, b_trans=True, C=gy)
-        K.gemm(go2, c["y"], d, d, R, a_trans=True, b_trans=True, C=slot(at.c_proj.weight), accumulate=True,
-               a_rowsum=slot(at.c_proj.bias))
+        wg["proj"].append((go2, c["y"], d, d, R, dict(a_trans=True, b_trans=True, C=slot(at.c_proj.weight),
+                                                       accumulate=True, a_rowsum=slot(at.c_proj.bias))))
         dqkv = e(R, 3 * d, dt=T_)
         ws = e(B * nh * T)
         K.attn_bwd(c["qkv"], c["y"], gy, c["lse"], B, T, nh, d, dqkv, ws)
-        K.gemm(dqkv, c["a"], 3 * d, d, R, a_trans=True, b_trans=True, C=slot(at.c_attn.weight), accumulate=True,
-               a_rowsum=slot(at.c_attn.bias))
+        wg["qkv"].append((dqkv, c["a"], 3 * d, d, R, dict(a_trans=True, b_trans=True, C=slot(at.c_attn.weight),
+                                                           accumulate=True, a_rowsum=slot(at.c_attn.bias))))
         ga = e(R, d)
         K.gemm(dqkv, c["Wqkv"], R, d, 3 * d, b_trans=True, C=ga)
         go = e(R, d, dt=T_) if i > 0 else None
         K.layernorm_bwd(c["x"], ga, blk.ln_1.weight, c["mu1"], c["rs1"], gx, True, slot(blk.ln_1.weight),
                         slot(blk.ln_1.bias), dx2=go, drop=(sv.p_drop, sv.seed_mlp[i - 1] if i > 0 else 0),
                         seed_ptr=sv.ctr)
+    for probs in wg.values():
+        K.gemm_grouped(probs)
     K.embed_bwd(sv_ids(sv), gx, slot(m.embedding.latent_embedding.weight))
 
 

@@ -41,13 +41,10 @@ def _algorithmic_flops(M, N, Kd, conv, flops):
     return 2.0 * M * N * Kd
 
 
-def gemm(A, B, M, N, K, *, a_trans=False, b_trans=False, conv=None, alpha=1.0, beta=0.0, bias=None,
-         act=AW_ACT_GELU_ERF, pre=None, resid=None, drop=(0.0, 0), C=None, C2=None, c2_mode=0, drop2=(0.0, 0),
-         colstats=None, stats_mod=0, a_rowsum=None, bias_mod=0, accumulate=False, col_map=(0, 1, 0), stream=None,
-         flops=None, seed_ptr=None):
-    """C = epilogue(alpha * op(A) @ op(B)); see aw_gemm in include/arcweld_amd.h for the exact semantics.
-
-    conv = (cin, seg, dir, operand) selects the implicit k=3 convolution form."""
+def _gemm_args(A, B, M, N, K, *, a_trans=False, b_trans=False, conv=None, alpha=1.0, beta=0.0, bias=None,
+               act=AW_ACT_GELU_ERF, pre=None, resid=None, drop=(0.0, 0), C=None, C2=None, c2_mode=0, drop2=(0.0, 0),
+               colstats=None, stats_mod=0, a_rowsum=None, bias_mod=0, accumulate=False, col_map=(0, 1, 0),
+               seed_ptr=None):
     if A.dtype != B.dtype:
         raise nat.NativeError(f"gemm operands must share a dtype ({A.dtype} vs {B.dtype})")
     a = GemmArgs()
@@ -78,19 +75,49 @@ def gemm(A, B, M, N, K, *, a_trans=False, b_trans=False, conv=None, alpha=1.0, b
     a.accumulate = int(bool(accumulate))
     a.col_mod, a.col_mul, a.col_off = (int(v) for v in col_map)
     a.seed_ptr = ptr(seed_ptr)
+    return a
+
+
+def _timed(s, fn, flops):
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(s)
+    fn(s.cuda_stream)
+    e1.record(s)
+    PROFILE.append((e0, e1, flops))
+
+
+def gemm(A, B, M, N, K, *, stream=None, flops=None, **kw):
+    """C = epilogue(alpha * op(A) @ op(B)); see aw_gemm in include/arcweld_amd.h for the exact semantics.
+
+    conv = (cin, seg, dir, operand) selects the implicit k=3 convolution form."""
+    a = _gemm_args(A, B, M, N, K, **kw)
     lib = nat.load()
     wsn = lib.aw_gemm_workspace(ctypes.byref(a))
     ws = torch.empty(wsn, device=A.device, dtype=torch.float32) if wsn > 0 else None
     if PROFILE is None:
         call("aw_gemm_ws", ctypes.byref(a), ptr(ws), wsn, stream_ptr(stream))
-        return C
+        return kw.get("C")
     s = stream if stream is not None else torch.cuda.current_stream()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record(s)
-    call("aw_gemm_ws", ctypes.byref(a), ptr(ws), wsn, s.cuda_stream)
-    e1.record(s)
-    PROFILE.append((e0, e1, _algorithmic_flops(M, N, K, conv, flops)))
-    return C
+    _timed(s, lambda sp: call("aw_gemm_ws", ctypes.byref(a), ptr(ws), wsn, sp),
+           _algorithmic_flops(M, N, K, kw.get("conv"), flops))
+    return kw.get("C")
+
+
+MAX_GROUPS = 16
+
+
+def gemm_grouped(problems, stream=None):
+    """One aw_gemm_grouped launch per chunk of <= 16 accumulate-mode problems that share everything except
+    (A, B, C, a_rowsum).  ``problems`` is a list of (A, B, M, N, K, kwargs) tuples as for ``gemm``."""
+    for c0 in range(0, len(problems), MAX_GROUPS):
+        chunk = problems[c0:c0 + MAX_GROUPS]
+        arr = (GemmArgs * len(chunk))(*[_gemm_args(A, B, M, N, K, **kw) for (A, B, M, N, K, kw) in chunk])
+        if PROFILE is None:
+            call("aw_gemm_grouped", arr, len(chunk), stream_ptr(stream))
+            continue
+        s = stream if stream is not None else torch.cuda.current_stream()
+        fl = sum(_algorithmic_flops(M, N, K, kw.get("conv"), None) for (_, _, M, N, K, kw) in chunk)
+        _timed(s, lambda sp: call("aw_gemm_grouped", arr, len(chunk), sp), fl)
 
 
 # ------------------------------------------------------------------------------------------------ VQ

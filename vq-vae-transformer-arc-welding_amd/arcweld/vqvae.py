@@ -293,6 +293,9 @@ def backward(m, sv, g_emb, g_xhat, slot):
     # ---- decoder ResBlocks (reverse)
     dconv_in = (H, S, -1, 0)
     wconv = (H, S, 1, 1)
+    # weight gradients of the whole ResBlock stack are deferred and issued as ONE grouped launch (every tile runs
+    # the full token reduction: no split-K, no slab reduce); their operands stay alive until then
+    wgrads = []
     for r in reversed(range(R)):
         c1, c2 = pr["dec"][r]
         W1d, W2d = e(3 * H, H, dt=T), e(3 * H, H, dt=T)
@@ -300,15 +303,16 @@ def backward(m, sv, g_emb, g_xhat, slot):
         K.weight_relayout(c2.weight, H, H, 3, 0, 2, W2d)
         gh = e(N, H, dt=T)
         K.gemm(go, W2d, N, H, 3 * H, b_trans=True, conv=dconv_in, pre=sv.dhs[r], C=gh)
-        K.gemm(go, sv.da1s[r], H, 3 * H, N, a_trans=True, b_trans=True, conv=wconv,
-               C=slot(c2.weight).view(H, 3 * H), accumulate=True, col_map=(H, 3, 0), a_rowsum=slot(c2.bias))
+        wgrads.append((go, sv.da1s[r], H, 3 * H, N, dict(a_trans=True, b_trans=True, conv=wconv,
+                       C=slot(c2.weight).view(H, 3 * H), accumulate=True, col_map=(H, 3, 0), a_rowsum=slot(c2.bias))))
         gyn, gon = e(N, H), e(N, H, dt=T)
         K.gemm(gh, W1d, N, H, 3 * H, b_trans=True, conv=dconv_in, pre=sv.ys[r], resid=gy, C=gyn, C2=gon,
                c2_mode=3 if r > 0 else 2, drop2=(p_drop, sv.dec_seed[r - 1] if r > 0 else 0),
                seed_ptr=sv.ctr)
-        K.gemm(gh, sv.ya0s[r], H, 3 * H, N, a_trans=True, b_trans=True, conv=wconv,
-               C=slot(c1.weight).view(H, 3 * H), accumulate=True, col_map=(H, 3, 0), a_rowsum=slot(c1.bias))
+        wgrads.append((gh, sv.ya0s[r], H, 3 * H, N, dict(a_trans=True, b_trans=True, conv=wconv,
+                       C=slot(c1.weight).view(H, 3 * H), accumulate=True, col_map=(H, 3, 0), a_rowsum=slot(c1.bias))))
         gy, go = gyn, gon
+    K.gemm_grouped(wgrads)
 
     # ---- decoder 1x1 conv (weight (H, D, 1) is a contiguous [H][D] matrix)
     K.gemm(go, sv.zq_T, H, D, N, a_trans=True, b_trans=True, C=slot(pr["dec0"].weight).view(H, D), accumulate=True,
@@ -328,20 +332,22 @@ def backward(m, sv, g_emb, g_xhat, slot):
     K.gemm(dz_T, sv.Ws, N, H, D, b_trans=True, C=gx, C2=gxo, c2_mode=3 if R > 0 else 2,
            drop2=(p_drop, sv.enc_seed[R - 1] if R > 0 else 0), seed_ptr=sv.ctr)
 
-    # ---- encoder ResBlocks (reverse)
+    # ---- encoder ResBlocks (reverse); weight gradients deferred into one grouped launch as in the decoder
+    wgrads = []
     for r in reversed(range(R)):
         c1, c2 = pr["enc"][r]
         w1, w2 = sv.enc_w[r]
         gh = e(N, H, dt=T)
         K.gemm(gxo, w2, N, H, H, b_trans=True, pre=sv.hs[r], C=gh)
-        K.gemm(gxo, sv.a1s[r], H, H, N, a_trans=True, b_trans=True, C=slot(c2.weight).view(H, 3 * H),
-               accumulate=True, col_map=(0, 3, 1), a_rowsum=slot(c2.bias))
+        wgrads.append((gxo, sv.a1s[r], H, H, N, dict(a_trans=True, b_trans=True, C=slot(c2.weight).view(H, 3 * H),
+                       accumulate=True, col_map=(0, 3, 1), a_rowsum=slot(c2.bias))))
         gxn, gxon = e(N, H), e(N, H, dt=T)
         K.gemm(gh, w1, N, H, H, b_trans=True, pre=sv.xs[r], resid=gx, C=gxn, C2=gxon, c2_mode=3 if r > 0 else 2,
                drop2=(p_drop, sv.enc_seed[r - 1] if r > 0 else 0), seed_ptr=sv.ctr)
-        K.gemm(gh, sv.a0s[r], H, H, N, a_trans=True, b_trans=True, C=slot(c1.weight).view(H, 3 * H),
-               accumulate=True, col_map=(0, 3, 1), a_rowsum=slot(c1.bias))
+        wgrads.append((gh, sv.a0s[r], H, H, N, dict(a_trans=True, b_trans=True, C=slot(c1.weight).view(H, 3 * H),
+                       accumulate=True, col_map=(0, 3, 1), a_rowsum=slot(c1.bias))))
         gx, gxo = gxn, gxon
+    K.gemm_grouped(wgrads)
 
     # ---- patch embed weight/bias
     K.gemm(gxo, sv.patches, H, P, N, a_trans=True, b_trans=True, C=slot(pr["pe"].weight).view(H, P),

@@ -124,12 +124,8 @@ extern "C" int aw_gemm_ws(const aw_gemm_args* args, float* ws, int64_t ws_elems,
 
 extern "C" int aw_gemm(const aw_gemm_args* args, void* stream) { return aw_gemm_ws(args, nullptr, 0, stream); }
 
-extern "C" int aw_gemm_ws(const aw_gemm_args* args, float* ws, int64_t ws_elems, void* stream) {
-  if (!args) {
-    aw::set_error("aw_gemm: null args");
-    return AW_ERR_ARG;
-  }
-  const aw_gemm_args& a = *args;
+// argument checks shared by aw_gemm_ws and aw_gemm_grouped
+static int validate(const aw_gemm_args& a) {
   AW_REQUIRE(a.M >= 0 && a.N >= 0 && a.K >= 0, "aw_gemm: negative size");
   AW_REQUIRE(a.a_dtype == AW_F32 || a.a_dtype == AW_BF16, "aw_gemm: bad a_dtype %d", a.a_dtype);
   AW_REQUIRE(a.A && a.B, "aw_gemm: null operand");
@@ -144,48 +140,69 @@ extern "C" int aw_gemm_ws(const aw_gemm_args* args, float* ws, int64_t ws_elems,
     else
       AW_REQUIRE(a.a_trans == 1 && a.b_trans == 1 && a.N == 3 * a.conv_cin,
                  "aw_gemm: B-conv needs a_trans=1, b_trans=1 and N=3*cin");
+    AW_REQUIRE(a.conv_cin % BK == 0, "aw_gemm: conv_cin must be a multiple of %d", BK);
   }
   AW_REQUIRE(!(a.beta != 0.f && a.c_dtype != AW_F32), "aw_gemm: beta != 0 needs an f32 C");
   AW_REQUIRE(!(a.c2_mode && !a.C2), "aw_gemm: c2_mode without C2");
   AW_REQUIRE(!(a.colstats && a.stats_mod <= 0), "aw_gemm: colstats needs stats_mod > 0");
-  if (a.M == 0 || a.N == 0) return AW_OK;
-  GemmP P;
-  P.a = a;
-  const int tiles_m = aw_cdiv(a.M, BM);
-  P.tiles_n = aw_cdiv(a.N, BN);
-  P.nblocks = tiles_m * P.tiles_n;
-  // split-K for plain-accumulate shapes that cannot fill the chip with tiles alone
   const bool plain = !a.bias && !a.pre && !a.resid && a.drop_p <= 0.f && !a.C2 && !a.colstats && a.C &&
                      a.c_dtype == AW_F32 && (a.beta == 0.f || a.beta == 1.f || a.accumulate);
   AW_REQUIRE(!a.accumulate || plain, "aw_gemm: accumulate mode allows no other epilogue field (f32 C only)");
   AW_REQUIRE(!(a.accumulate && a.beta != 0.f), "aw_gemm: accumulate mode already adds into C (beta must be 0)");
-  if (a.conv_cin > 0) AW_REQUIRE(a.conv_cin % BK == 0, "aw_gemm: conv_cin must be a multiple of %d", BK);
-  P.splits = choose_splits(a, P.nblocks, BK, &P.ksplit);
-  P.ws = nullptr;
-  if (P.splits > 1 && ws && ws_elems >= (int64_t)P.splits * a.M * a.N) P.ws = ws;
-  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  if (P.splits > 1 && !P.ws && a.beta == 0.f && !a.accumulate) {
-    if (hipMemset2DAsync(a.C, a.ldc * sizeof(float), 0, a.N * sizeof(float), a.M, s) != hipSuccess)
-      return aw::check_launch("aw_gemm split-K zero");
-  }
-  {
-    auto al = [](const void* ptr, int64_t ld, int dt) {
-      return ptr == nullptr || (((uintptr_t)ptr % 16) == 0 && (ld * (dt == AW_BF16 ? 2 : 4)) % 16 == 0);
-    };
-    P.vec = al(a.C, a.ldc, a.c_dtype) && al(a.C2, a.ldc2, a.c2_dtype) && al(a.pre, a.ld_pre, AW_F32) &&
-            al(a.resid, a.ld_resid, AW_F32);
-  }
   {
     const int64_t es = a.a_dtype == AW_BF16 ? 2 : 4;
     const int64_t ka = a.K > 0 ? a.K : 1;
     const int64_t ea = (!a.a_trans ? ((int64_t)(a.M - 1) * a.lda + ka) : ((ka - 1) * a.lda + a.M)) * es;
     const int64_t eb = (!a.b_trans ? ((int64_t)(a.N - 1) * a.ldb + ka) : ((ka - 1) * a.ldb + a.N)) * es;
     AW_REQUIRE(ea < OOB && eb < OOB, "aw_gemm: operand extent >= 2 GiB is not supported");
-    P.a_bytes = (int)ea;
-    P.b_bytes = (int)eb;
   }
-  // ragged: a contiguous extent that is not a whole number of 16-byte chunks
-  const bool ragged = (!a.a_trans ? (a.K % epc) : (a.M % epc)) != 0 || (!a.b_trans ? (a.K % epc) : (a.N % epc)) != 0;
+  return AW_OK;
+}
+
+// launch geometry, alignment flags and buffer extents of one problem (no split decision)
+static void prepare(const aw_gemm_args& a, GemmP& P) {
+  P.a = a;
+  P.tiles_n = aw_cdiv(a.N, BN);
+  P.nblocks = aw_cdiv(a.M, BM) * P.tiles_n;
+  P.ngroups = 1;
+  P.tiles_per_group = P.nblocks;
+  P.ws = nullptr;
+  auto al = [](const void* ptr, int64_t ld, int dt) {
+    return ptr == nullptr || (((uintptr_t)ptr % 16) == 0 && (ld * (dt == AW_BF16 ? 2 : 4)) % 16 == 0);
+  };
+  P.vec = al(a.C, a.ldc, a.c_dtype) && al(a.C2, a.ldc2, a.c2_dtype) && al(a.pre, a.ld_pre, AW_F32) &&
+          al(a.resid, a.ld_resid, AW_F32);
+  const int64_t es = a.a_dtype == AW_BF16 ? 2 : 4;
+  const int64_t ka = a.K > 0 ? a.K : 1;
+  P.a_bytes = (int)((!a.a_trans ? ((int64_t)(a.M - 1) * a.lda + ka) : ((ka - 1) * a.lda + a.M)) * es);
+  P.b_bytes = (int)((!a.b_trans ? ((int64_t)(a.N - 1) * a.ldb + ka) : ((ka - 1) * a.ldb + a.N)) * es);
+}
+
+static bool is_ragged(const aw_gemm_args& a) {   // a contiguous extent that is not a whole number of 16-B chunks
+  const int epc = a.a_dtype == AW_BF16 ? 8 : 4;
+  return (!a.a_trans ? (a.K % epc) : (a.M % epc)) != 0 || (!a.b_trans ? (a.K % epc) : (a.N % epc)) != 0;
+}
+
+extern "C" int aw_gemm_ws(const aw_gemm_args* args, float* ws, int64_t ws_elems, void* stream) {
+  if (!args) {
+    aw::set_error("aw_gemm: null args");
+    return AW_ERR_ARG;
+  }
+  const aw_gemm_args& a = *args;
+  if (int st = validate(a)) return st;
+  if (a.M == 0 || a.N == 0) return AW_OK;
+  const int BK = a.a_dtype == AW_BF16 ? 64 : 32;
+  GemmP P;
+  prepare(a, P);
+  // split-K for plain-accumulate shapes that cannot fill the chip with tiles alone
+  P.splits = choose_splits(a, P.nblocks, BK, &P.ksplit);
+  if (P.splits > 1 && ws && ws_elems >= (int64_t)P.splits * a.M * a.N) P.ws = ws;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (P.splits > 1 && !P.ws && a.beta == 0.f && !a.accumulate) {
+    if (hipMemset2DAsync(a.C, a.ldc * sizeof(float), 0, a.N * sizeof(float), a.M, s) != hipSuccess)
+      return aw::check_launch("aw_gemm split-K zero");
+  }
+  const bool ragged = is_ragged(a);
   if (a.a_dtype == AW_BF16)
     dispatch<bf16>(P, s, ragged);
   else
@@ -197,4 +214,49 @@ extern "C" int aw_gemm_ws(const aw_gemm_args* args, float* ws, int64_t ws_elems,
     hipLaunchKernelGGL(gemm_reduce_kernel, dim3((int)g), dim3(256), 0, s, P.ws, P.splits, a.M, a.N, a);
   }
   return aw::check_launch("aw_gemm");
+}
+
+extern "C" int aw_gemm_grouped(const aw_gemm_args* args, int n, void* stream) {
+  AW_REQUIRE(args && n >= 1 && n <= AW_GEMM_MAX_GROUPS, "aw_gemm_grouped: need 1..%d problems", AW_GEMM_MAX_GROUPS);
+  const aw_gemm_args& a = args[0];
+  for (int g = 0; g < n; ++g) {
+    if (int st = validate(args[g])) return st;
+    const aw_gemm_args& b = args[g];
+    // every field but the four per-group pointers must match problem 0
+    const bool same = b.M == a.M && b.N == a.N && b.K == a.K && b.a_dtype == a.a_dtype && b.lda == a.lda &&
+                      b.a_trans == a.a_trans && b.ldb == a.ldb && b.b_trans == a.b_trans &&
+                      b.conv_cin == a.conv_cin && b.conv_seg == a.conv_seg && b.conv_dir == a.conv_dir &&
+                      b.conv_operand == a.conv_operand && b.alpha == a.alpha && b.beta == a.beta &&
+                      b.ldc == a.ldc && b.c_dtype == a.c_dtype && b.accumulate == a.accumulate &&
+                      b.col_mod == a.col_mod && b.col_mul == a.col_mul && b.col_off == a.col_off &&
+                      (b.a_rowsum == nullptr) == (a.a_rowsum == nullptr) && b.C != nullptr;
+    AW_REQUIRE(same, "aw_gemm_grouped: problem %d differs from problem 0 in more than A, B, C, a_rowsum", g);
+  }
+  AW_REQUIRE(a.accumulate && !a.C2 && !a.bias && !a.colstats, "aw_gemm_grouped: accumulate-mode problems only");
+  if (a.M == 0 || a.N == 0) return AW_OK;
+  const int BK = a.a_dtype == AW_BF16 ? 64 : 32;
+  GemmP P;
+  prepare(a, P);
+  P.ngroups = n;
+  P.tiles_per_group = P.nblocks;
+  P.nblocks *= n;
+  for (int g = 0; g < n; ++g) {
+    P.gA[g] = args[g].A;
+    P.gB[g] = args[g].B;
+    P.gC[g] = args[g].C;
+    P.gRow[g] = args[g].a_rowsum;
+  }
+  // split-K over f32 atomics only (no slab workspace) while the groups' tiles cannot fill two blocks per CU
+  P.splits = choose_splits(a, P.nblocks, BK, &P.ksplit);
+  if (P.splits > 2) {   // at most two atomic adders per element
+    P.ksplit = aw_cdiv(aw_cdiv(a.K, 2), BK) * BK;
+    P.splits = aw_cdiv(a.K, P.ksplit);
+  }
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const bool ragged = is_ragged(a);
+  if (a.a_dtype == AW_BF16)
+    dispatch<bf16>(P, s, ragged);
+  else
+    dispatch<float>(P, s, ragged);
+  return aw::check_launch("aw_gemm_grouped");
 }

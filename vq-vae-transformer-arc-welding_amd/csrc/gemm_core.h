@@ -54,6 +54,13 @@ struct GemmP {
   int vec;   // every epilogue operand row is 16-B aligned: vectorised epilogue
   int a_bytes, b_bytes;  // extents of A and B (buffer-descriptor ranges; < 2^31)
   float* ws; // split-K partial slabs [splits][M][N] (NULL: fp32 atomics)
+  // grouped launch (aw_gemm_grouped): ngroups problems of one shape, tiles_per_group consecutive logical tiles
+  // each; the operand / output / row-sum pointers of group g replace a.A, a.B, a.C, a.a_rowsum
+  int ngroups, tiles_per_group;
+  const void* gA[AW_GEMM_MAX_GROUPS];
+  const void* gB[AW_GEMM_MAX_GROUPS];
+  void* gC[AW_GEMM_MAX_GROUPS];
+  float* gRow[AW_GEMM_MAX_GROUPS];
 };
 
 enum { CONV_NONE = 0, CONV_ROWSHIFT = 1, CONV_KSHIFT = 2 };
@@ -293,19 +300,31 @@ __global__ __launch_bounds__(NTHREADS, RAGGED ? 1 : 2) void gemm_kernel(GemmP P)
   const int tid = threadIdx.x;
   const int lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
-  const int tile = xcd_remap(blockIdx.x, P.nblocks);
+  int tile = xcd_remap(blockIdx.x, P.nblocks);
+  const void* Aptr = p.A;
+  const void* Bptr = p.B;
+  void* Cptr = p.C;
+  float* rowptr = p.a_rowsum;
+  if (P.ngroups > 1) {   // consecutive logical tiles (one XCD) belong to one group: its operands share that L2
+    const int g = tile / P.tiles_per_group;
+    tile -= g * P.tiles_per_group;
+    Aptr = P.gA[g];
+    Bptr = P.gB[g];
+    Cptr = P.gC[g];
+    rowptr = P.gRow[g];
+  }
   const int tm = tile / P.tiles_n, tn = tile % P.tiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
   const int M = p.M, N = p.N;
   const int kbeg = blockIdx.y * P.ksplit;
   const int kend = min(p.K, kbeg + P.ksplit);
 
-  Stager<T, ATR, ACONV, RAGGED> sa{reinterpret_cast<const T*>(p.A), p.lda, M, m0, kend, p.conv_cin, p.conv_seg,
+  Stager<T, ATR, ACONV, RAGGED> sa{reinterpret_cast<const T*>(Aptr), p.lda, M, m0, kend, p.conv_cin, p.conv_seg,
                                    p.conv_dir};
-  Stager<T, BTR, BCONV, RAGGED> sb{reinterpret_cast<const T*>(p.B), p.ldb, N, n0, kend, p.conv_cin, p.conv_seg, 1};
+  Stager<T, BTR, BCONV, RAGGED> sb{reinterpret_cast<const T*>(Bptr), p.ldb, N, n0, kend, p.conv_cin, p.conv_seg, 1};
   sa.init(kbeg, tid, P.a_bytes);
   sb.init(kbeg, tid, P.b_bytes);
-  const bool do_rowsum = p.a_rowsum != nullptr && tn == 0;
+  const bool do_rowsum = rowptr != nullptr && tn == 0;
 
   f32x4 acc[4][4];
 #pragma unroll
@@ -366,7 +385,7 @@ __global__ __launch_bounds__(NTHREADS, RAGGED ? 1 : 2) void gemm_kernel(GemmP P)
   if (do_rowsum) {
     rowsum += __shfl_xor(rowsum, 1, 64);
     const int r = m0 + (tid >> 1);
-    if ((tid & 1) == 0 && r < M) atomicAdd(p.a_rowsum + r, rowsum);
+    if ((tid & 1) == 0 && r < M) atomicAdd(rowptr + r, rowsum);
   }
 
   // ---------------------------------------------------------------- epilogue
@@ -403,7 +422,7 @@ __global__ __launch_bounds__(NTHREADS, RAGGED ? 1 : 2) void gemm_kernel(GemmP P)
     if (col >= N) return;
     const int64_t oc = p.col_mod > 0 ? (int64_t)(col % p.col_mod) * p.col_mul + col / p.col_mod + p.col_off
                                      : (int64_t)col * (p.col_mul > 0 ? p.col_mul : 1) + p.col_off;
-    float* C = reinterpret_cast<float*>(p.C);
+    float* C = reinterpret_cast<float*>(Cptr);
     for (int lr = tid >> 7; lr < rows_here; lr += 2)
       atomicAdd(C + (int64_t)(m0 + lr) * p.ldc + oc, p.alpha * Cs[lr * CPITCH + lc]);
     return;
@@ -417,7 +436,7 @@ __global__ __launch_bounds__(NTHREADS, RAGGED ? 1 : 2) void gemm_kernel(GemmP P)
   const bool f_drop = EPF(EP_DROP, p.drop_p > 0.f);
   const bool f_resid = EPF(EP_RESID, p.resid != nullptr);
   const bool f_beta = EPF(EP_BETA, p.beta != 0.f);
-  const bool f_c = EPF(EP_C, p.C != nullptr);
+  const bool f_c = EPF(EP_C, Cptr != nullptr);
   const bool f_cbf = EPF(EP_CBF, p.c_dtype == AW_BF16);
   const int c2m = GEN ? p.c2_mode : ((EPI & EP_C2ACT) ? 1 : (EPI & EP_C2COPY) ? 2 : (EPI & EP_C2DROP) ? 3 : 0);
   const bool f_c2bf = EPF(EP_C2BF, p.c2_dtype == AW_BF16);
@@ -447,7 +466,7 @@ __global__ __launch_bounds__(NTHREADS, RAGGED ? 1 : 2) void gemm_kernel(GemmP P)
         if (vec) {
           if (f_pre) pre4[u] = *reinterpret_cast<const float4*>(p.pre + row * p.ld_pre + col);
           if (f_resid) res4[u] = *reinterpret_cast<const float4*>(p.resid + row * p.ld_resid + col);
-          if (f_beta) old4[u] = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(p.C) + row * p.ldc + col);
+          if (f_beta) old4[u] = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(Cptr) + row * p.ldc + col);
         } else if constexpr (GEN) {
           float a[4] = {0.f, 0.f, 0.f, 0.f}, b[4] = {0.f, 0.f, 0.f, 0.f}, c[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -455,7 +474,7 @@ __global__ __launch_bounds__(NTHREADS, RAGGED ? 1 : 2) void gemm_kernel(GemmP P)
             if (col + e >= N) break;
             if (f_pre) a[e] = p.pre[row * p.ld_pre + col + e];
             if (f_resid) b[e] = p.resid[row * p.ld_resid + col + e];
-            if (f_beta) c[e] = reinterpret_cast<const float*>(p.C)[row * p.ldc + col + e];
+            if (f_beta) c[e] = reinterpret_cast<const float*>(Cptr)[row * p.ldc + col + e];
           }
           pre4[u] = make_float4(a[0], a[1], a[2], a[3]);
           res4[u] = make_float4(b[0], b[1], b[2], b[3]);
@@ -495,13 +514,13 @@ __global__ __launch_bounds__(NTHREADS, RAGGED ? 1 : 2) void gemm_kernel(GemmP P)
           }
         }
         if (vec) {
-          if (f_c) store4(p.C, f_cbf, row * p.ldc + col, v);
+          if (f_c) store4(Cptr, f_cbf, row * p.ldc + col, v);
           if (c2m) store4(p.C2, f_c2bf, row * p.ldc2 + col, w);
         } else if constexpr (GEN) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             if (col + e >= N) break;
-            if (f_c) store_from_f32(p.C, p.c_dtype, row * p.ldc + col + e, v[e]);
+            if (f_c) store_from_f32(Cptr, p.c_dtype, row * p.ldc + col + e, v[e]);
             if (c2m) store_from_f32(p.C2, p.c2_dtype, row * p.ldc2 + col + e, w[e]);
           }
         }
