@@ -34,6 +34,9 @@ int aw_version(void);
  * Operand storage (dtype = a_dtype for A and B; AW_F32 or AW_BF16):
  *   a_trans = 0: A[m*lda + k]        a_trans = 1: A[k*lda + m]
  *   b_trans = 0: B[n*ldb + k]        b_trans = 1: B[k*ldb + n]      (weights [out][in] are b_trans = 0)
+ *   A transposed operand whose width (M or N) is not a multiple of 16 bytes but whose leading dimension is at
+ *   least that width rounded up is read in whole 16-B chunks: every row, the last included, must be readable up
+ *   to the rounded width (the padding values are never used).
  * Implicit k=3/pad=1 convolution along windows of `conv_seg` rows (conv_cin > 0):
  *   conv_operand = 0 (A, a_trans = 0): K = 3*conv_cin, A[m][j*cin+i] = src[(m + conv_dir*(j-1))*lda + i],
  *                  zero where the shifted row leaves its window;
@@ -121,6 +124,16 @@ int aw_patchify(const float* x, int64_t B, int L, int C, int P, void* patches, i
  * `ldo` is the output row length (ignored except for mode 4). */
 int aw_weight_relayout(const float* W, int O, int I, int k, int tap, int mode, void* out, int64_t ldo,
                        int dtype, void* stream);
+/* Batched form: up to AW_RELAYOUT_MAX_JOBS relayouts (modes 0-4 above, mode 5 = plain cast of O*I elements,
+ * e.g. the Linear weights of model/transformer_block.py) into one output dtype, one launch per call. */
+#define AW_RELAYOUT_MAX_JOBS 40
+typedef struct {
+  const float* W;
+  void* out;
+  int O, I, k, tap, mode;
+  int64_t ldo;
+} aw_relayout_job;
+int aw_weight_relayout_batch(const aw_relayout_job* jobs, int n, int dtype, void* stream);
 /* Inverse relayout of weight GRADIENTS, accumulated (+=) into the reference-layout gradient:
  * mode 0: g[O][I] -> G[o][i][tap];  mode 1: g[O][3I] -> G[o][i][j];  mode 3: g[kO][I] -> G[i][o][j];
  * mode 4: g[O][ldo] -> G[o][0][j]. */

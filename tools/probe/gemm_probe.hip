@@ -28,6 +28,14 @@ __global__ __launch_bounds__(256, 2) void probe_store(float* C, int N, int tiles
   }
 }
 
+__global__ void probe_fill(bf16* x, size_t n, uint32_t seed) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    uint32_t h = (uint32_t)i * 2654435761u ^ seed;
+    h ^= h >> 13; h *= 0x5bd1e995u; h ^= h >> 15;
+    x[i] = (bf16)(((float)(h & 0xFFFF) / 65536.f - 0.5f) * 2.f);
+  }
+}
+
 template <typename F> float timeit(F f, int reps = 50) {
   for (int i = 0; i < 5; ++i) f();
   hipEvent_t a, b;
@@ -45,7 +53,7 @@ int main() {
   bf16 *A, *B; float* C; bf16* Cb;
   CK(hipMalloc(&A, (size_t)M * Kmax * 2)); CK(hipMalloc(&B, (size_t)N * Kmax * 2));
   CK(hipMalloc(&C, (size_t)M * N * 4)); CK(hipMalloc(&Cb, (size_t)M * N * 2));
-  CK(hipMemset(A, 0x3c, (size_t)M * Kmax * 2)); CK(hipMemset(B, 0x3c, (size_t)N * Kmax * 2));
+  probe_fill<<<1024, 256>>>(A, (size_t)M * Kmax, 1); probe_fill<<<1024, 256>>>(B, (size_t)N * Kmax, 2);
   const int tiles = (M / 128) * (N / 128);
   printf("empty kernel (512 blocks, 66 KiB LDS)     %8.2f us\n", timeit([&] { probe_empty<<<tiles, 256>>>(C); }));
   printf("store-only 128x128 f32 tiles (32 MiB)      %8.2f us\n", timeit([&] { probe_store<<<tiles, 256>>>(C, N, N / 128); }));
@@ -83,6 +91,31 @@ int main() {
       if (v == 3) { a.b_trans = 1; a.bias = nullptr; a.drop_p = 0.f; a.pre = pre; a.ld_pre = N; a.c2_mode = 3;
                     a.drop2_p = 0.1f; a.drop2_seed = 3; nm = "bwd: pre'+resid+C+C2 dropcopy"; }
       printf("aw_gemm M16384 N512 K512 %-30s %8.2f us\n", nm, timeit([&] { aw_gemm(&a, 0); }));
+    }
+  }
+  // weight-gradient form: 16 grouped problems of 512x512, K = 16384 tokens
+  {
+    const int Mw = 512, Nw = 512, Kw = 16384, G = 16;
+    bf16 *X; float* Wg;
+    CK(hipMalloc(&X, (size_t)Kw * Mw * 2 * 2)); CK(hipMalloc(&Wg, (size_t)G * Mw * Nw * 4 * 3));
+    probe_fill<<<1024, 256>>>(X, (size_t)Kw * Mw * 2, 7);
+    float* rows; CK(hipMalloc(&rows, G * Mw * 4));
+    for (int form = 0; form < 2; ++form) {
+      std::vector<aw_gemm_args> v(G);
+      for (int g = 0; g < G; ++g) {
+        aw_gemm_args& a = v[g]; memset(&a, 0, sizeof(a));
+        a.M = Mw; a.N = Nw; a.K = Kw; a.a_dtype = AW_BF16; a.alpha = 1.f; a.c_dtype = AW_F32; a.accumulate = 1;
+        a.C = Wg + (size_t)g * Mw * Nw * 3; a.ldc = 3 * Nw; a.col_mul = 3; a.col_off = 1;
+        if (form == 0) a.a_rowsum = rows + g * Mw;
+        if (form == 0) { a.A = X; a.lda = Mw; a.a_trans = 1; a.B = X + (size_t)Kw * Mw; a.ldb = Nw; a.b_trans = 1; }
+        else { a.A = X; a.lda = Kw; a.B = X + (size_t)Kw * Mw; a.ldb = Kw; }
+      }
+      float us = timeit([&] { aw_gemm_grouped(v.data(), G, 0); }, 10);
+      printf("grouped x16 512x512xK16384 %s  %8.2f us  (%.0f TF)\n", form == 0 ? "TT (tokens-major, tr reads)" :
+             "NN (K-contiguous)          ", us, 2.0 * G * Mw * Nw * Kw / us / 1e6);
+      float us1 = timeit([&] { aw_gemm_grouped(v.data(), 8, 0); }, 10);
+      printf("grouped x8  512x512xK16384 %s  %8.2f us  (%.0f TF)\n", form == 0 ? "TT" : "NN", us1,
+             2.0 * 8 * Mw * Nw * Kw / us1 / 1e6);
     }
   }
   // phase stamps (s_memrealtime, 10 ns ticks) of one launch

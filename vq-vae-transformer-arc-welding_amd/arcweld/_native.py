@@ -48,6 +48,12 @@ class GemmArgs(ctypes.Structure):
     ]
 
 
+class RelayoutJob(ctypes.Structure):
+    """aw_relayout_job (include/arcweld_amd.h)."""
+    _fields_ = [("W", c_p), ("out", c_p), ("O", c_int), ("I", c_int), ("k", c_int), ("tap", c_int),
+                ("mode", c_int), ("ldo", c_i64)]
+
+
 # name -> argtypes (every entry returns int status except aw_last_error)
 SIGNATURES = {
     "aw_version": [],
@@ -55,6 +61,7 @@ SIGNATURES = {
     "aw_gemm_ws": [ctypes.POINTER(GemmArgs), c_p, c_i64, c_p],
     "aw_gemm_workspace": [ctypes.POINTER(GemmArgs)],
     "aw_gemm_grouped": [ctypes.POINTER(GemmArgs), c_int, c_p],
+    "aw_weight_relayout_batch": [ctypes.POINTER(RelayoutJob), c_int, c_int, c_p],
     "aw_vq_forward": [c_p, c_p, c_i64, c_int, c_int, c_p, c_p, c_p, c_p, c_p],
     "aw_vq_finalize": [c_p, c_p, c_i64, c_int, c_int, c_f, c_p, c_p, c_p],
     "aw_vq_backward": [c_p, c_p, c_p, c_p, c_p, c_i64, c_int, c_int, c_f, c_p, c_p, c_p],

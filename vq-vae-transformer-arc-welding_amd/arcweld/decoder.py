@@ -71,13 +71,25 @@ def forward(m, ids, generate: bool, training: bool, need_backward: bool, seed: i
 
     x = e(R, d)
     K.embed_fwd(ids, m.embedding.latent_embedding.weight, pe[0], x)
+    # operand copies of every block's Linear weights: one batched cast launch (f32 operands are used as they are)
+    wops = []
+    casts = []
+    for blk in m.transformer.h:
+        ws = []
+        for lin in (blk.attn.c_attn, blk.attn.c_proj, blk.mlp.c_fc, blk.mlp.c_proj):
+            w = lin.weight
+            if T_ == w.dtype:
+                ws.append(w)
+            else:
+                o = torch.empty(w.shape, device=dev, dtype=T_)
+                casts.append((w, w.shape[0], w.shape[1], 1, 0, 5, o))
+                ws.append(o)
+        wops.append(ws)
+    K.weight_relayout_batch(casts)
     blocks = []
     for i, blk in enumerate(m.transformer.h):
         at, mlp = blk.attn, blk.mlp
-        Wqkv = _cast(at.c_attn.weight, T_)
-        Wo = _cast(at.c_proj.weight, T_)
-        Wfc = _cast(mlp.c_fc.weight, T_)
-        Wp = _cast(mlp.c_proj.weight, T_)
+        Wqkv, Wo, Wfc, Wp = wops[i]
         a, mu1, rs1 = e(R, d, dt=T_), e(R), e(R)
         K.layernorm_fwd(x, blk.ln_1.weight, blk.ln_1.bias, blk.ln_1.eps, a, mu1, rs1)
         qkv = e(R, 3 * d, dt=T_)

@@ -156,6 +156,27 @@ def weight_relayout(W, O, I, k, tap, mode, out, ldo=0, stream=None):
     call("aw_weight_relayout", ptr(W), O, I, k, tap, mode, ptr(out), ldo, dtype_code(out.dtype), stream_ptr(stream))
 
 
+RELAYOUT_MAX_JOBS = 40
+
+
+def weight_relayout_batch(jobs, stream=None):
+    """Many weight_relayout calls in one launch per output dtype.  jobs: (W, O, I, k, tap, mode, out[, ldo]);
+    mode 5 is a plain cast of O*I elements."""
+    by_dtype = {}
+    for jb in jobs:
+        by_dtype.setdefault(jb[6].dtype, []).append(jb)
+    for dt, js in by_dtype.items():
+        for c0 in range(0, len(js), RELAYOUT_MAX_JOBS):
+            chunk = js[c0:c0 + RELAYOUT_MAX_JOBS]
+            arr = (nat.RelayoutJob * len(chunk))()
+            for r, jb in zip(arr, chunk):
+                W, O, I, k, tap, mode, out = jb[:7]
+                r.W, r.out = ptr(W), ptr(out)
+                r.O, r.I, r.k, r.tap, r.mode = int(O), int(I), int(k), int(tap), int(mode)
+                r.ldo = int(jb[7]) if len(jb) > 7 else 0
+            call("aw_weight_relayout_batch", arr, len(chunk), dtype_code(dt), stream_ptr(stream))
+
+
 def weight_grad_scatter(g, O, I, k, tap, mode, G, stream=None):
     call("aw_weight_grad_scatter", ptr(g), O, I, k, tap, mode, g.stride(0), ptr(G), stream_ptr(stream))
 

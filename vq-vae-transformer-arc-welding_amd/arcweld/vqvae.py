@@ -101,27 +101,27 @@ def forward(m, x, training: bool, need_backward: bool, dtype=None, seed: int = 0
     sv.dec_seed = [_mix(seed, 200 + r) for r in range(R)]
     sv.ctr = rng_snapshot(m, dev, p_drop)
 
-    # ---- operand copies of the weights (relayout + cast)
+    # ---- operand copies of the weights (relayout + cast), one batched launch
+    jobs = []
     Wp = e(H, sh.ldp, dt=T)
-    K.weight_relayout(pr["pe"].weight, H, 1, P, 0, 4, Wp, ldo=sh.ldp)
+    jobs.append((pr["pe"].weight, H, 1, P, 0, 4, Wp, sh.ldp))
     enc_w = []
     for c1, c2 in pr["enc"]:
         w1, w2 = e(H, H, dt=T), e(H, H, dt=T)
-        K.weight_relayout(c1.weight, H, H, 3, 1, 0, w1)
-        K.weight_relayout(c2.weight, H, H, 3, 1, 0, w2)
+        jobs += [(c1.weight, H, H, 3, 1, 0, w1), (c2.weight, H, H, 3, 1, 0, w2)]
         enc_w.append((w1, w2))
     Ws = e(D, H, dt=T)
-    K.weight_relayout(pr["sep"].weight, D, H, 1, 0, 0, Ws)
+    jobs.append((pr["sep"].weight, D, H, 1, 0, 0, Ws))
     Wd0 = e(H, D, dt=T)
-    K.weight_relayout(pr["dec0"].weight, H, D, 1, 0, 0, Wd0)
+    jobs.append((pr["dec0"].weight, H, D, 1, 0, 0, Wd0))
     dec_w = []
     for c1, c2 in pr["dec"]:
         w1, w2 = e(H, 3 * H, dt=T), e(H, 3 * H, dt=T)
-        K.weight_relayout(c1.weight, H, H, 3, 0, 1, w1)
-        K.weight_relayout(c2.weight, H, H, 3, 0, 1, w2)
+        jobs += [(c1.weight, H, H, 3, 0, 1, w1), (c2.weight, H, H, 3, 0, 1, w2)]
         dec_w.append((w1, w2))
     Wt1 = e(k1 * H, H, dt=T)
-    K.weight_relayout(pr["t1"].weight, H, H, k1, 0, 3, Wt1)
+    jobs.append((pr["t1"].weight, H, H, k1, 0, 3, Wt1))
+    K.weight_relayout_batch(jobs)
 
     # ---- patch embed
     patches = e(N, sh.ldp, dt=T)
@@ -235,19 +235,20 @@ def encode(m, x, dtype=F32):
     K.patchify(x, P, patches)
     xr, a = e(N, H), e(N, H, dt=T)
     K.gemm(patches, Wp, N, H, sh.ldp, bias=pr["pe"].bias, C=xr, C2=a, c2_mode=1, flops=2 * N * H * P)
-    w1, w2 = e(H, H, dt=T), e(H, H, dt=T)
+    ew = [(e(H, H, dt=T), e(H, H, dt=T)) for _ in range(R)]
+    Ws = e(D, H, dt=T)
+    K.weight_relayout_batch([jb for r, (c1, c2) in enumerate(pr["enc"])
+                             for jb in ((c1.weight, H, H, 3, 1, 0, ew[r][0]), (c2.weight, H, H, 3, 1, 0, ew[r][1]))]
+                            + [(pr["sep"].weight, D, H, 1, 0, 0, Ws)])
     h, a1 = e(N, H), e(N, H, dt=T)
     for r, (c1, c2) in enumerate(pr["enc"]):
-        K.weight_relayout(c1.weight, H, H, 3, 1, 0, w1)
-        K.weight_relayout(c2.weight, H, H, 3, 1, 0, w2)
+        w1, w2 = ew[r]
         K.gemm(a, w1, N, H, H, bias=c1.bias, C=h, C2=a1, c2_mode=1)
         if r < R - 1:   # x <- x + conv2(gelu(h)) in place (row-local epilogue), a <- gelu(x)
             K.gemm(a1, w2, N, H, H, bias=c2.bias, resid=xr, C=xr, C2=a, c2_mode=1)
         else:           # the sep conv consumes x_R itself (no GELU): write it in the operand dtype
             K.gemm(a1, w2, N, H, H, bias=c2.bias, resid=xr, C=a)
     xR_T = a if R > 0 else (xr if T == F32 else _cast(xr, T))
-    Ws = e(D, H, dt=T)
-    K.weight_relayout(pr["sep"].weight, D, H, 1, 0, 0, Ws)
     z = e(N, D)
     K.gemm(xR_T, Ws, N, D, H, bias=pr["sep"].bias, C=z)
     zq, idx = e(N, D), e(N, dt=torch.int64)
@@ -296,11 +297,12 @@ def backward(m, sv, g_emb, g_xhat, slot):
     # weight gradients of the whole ResBlock stack are deferred and issued as ONE grouped launch (every tile runs
     # the full token reduction: no split-K, no slab reduce); their operands stay alive until then
     wgrads = []
+    dgw = [(e(3 * H, H, dt=T), e(3 * H, H, dt=T)) for _ in range(R)]
+    K.weight_relayout_batch([jb for r in range(R) for jb in ((pr["dec"][r][0].weight, H, H, 3, 0, 2, dgw[r][0]),
+                                                             (pr["dec"][r][1].weight, H, H, 3, 0, 2, dgw[r][1]))])
     for r in reversed(range(R)):
         c1, c2 = pr["dec"][r]
-        W1d, W2d = e(3 * H, H, dt=T), e(3 * H, H, dt=T)
-        K.weight_relayout(c1.weight, H, H, 3, 0, 2, W1d)
-        K.weight_relayout(c2.weight, H, H, 3, 0, 2, W2d)
+        W1d, W2d = dgw[r]
         gh = e(N, H, dt=T)
         K.gemm(go, W2d, N, H, 3 * H, b_trans=True, conv=dconv_in, pre=sv.dhs[r], C=gh)
         wgrads.append((go, sv.da1s[r], H, 3 * H, N, dict(a_trans=True, b_trans=True, conv=wconv,

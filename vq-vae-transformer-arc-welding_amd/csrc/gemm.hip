@@ -174,13 +174,22 @@ static void prepare(const aw_gemm_args& a, GemmP& P) {
           al(a.resid, a.ld_resid, AW_F32);
   const int64_t es = a.a_dtype == AW_BF16 ? 2 : 4;
   const int64_t ka = a.K > 0 ? a.K : 1;
-  P.a_bytes = (int)((!a.a_trans ? ((int64_t)(a.M - 1) * a.lda + ka) : ((ka - 1) * a.lda + a.M)) * es);
-  P.b_bytes = (int)((!a.b_trans ? ((int64_t)(a.N - 1) * a.ldb + ka) : ((ka - 1) * a.ldb + a.N)) * es);
+  // a padded transposed operand is read in whole chunks up to its padded width (see is_ragged)
+  const int epc = a.a_dtype == AW_BF16 ? 8 : 4;
+  auto wide = [epc](int n, int64_t ld) { const int64_t r = (int64_t)(n + epc - 1) / epc * epc; return ld >= r ? r : n; };
+  P.a_bytes = (int)((!a.a_trans ? ((int64_t)(a.M - 1) * a.lda + ka) : ((ka - 1) * a.lda + wide(a.M, a.lda))) * es);
+  P.b_bytes = (int)((!a.b_trans ? ((int64_t)(a.N - 1) * a.ldb + ka) : ((ka - 1) * a.ldb + wide(a.N, a.ldb))) * es);
 }
 
-static bool is_ragged(const aw_gemm_args& a) {   // a contiguous extent that is not a whole number of 16-B chunks
+// ragged: a contiguous extent that is not a whole number of 16-B chunks.  A row-contiguous (transposed) operand
+// whose leading dimension is padded to whole chunks is not ragged: the over-read lanes only feed output rows /
+// columns >= M / N, which are never stored (e.g. the patch-embed weight gradient, N = P = 25, ldb = 32).
+static bool is_ragged(const aw_gemm_args& a) {
   const int epc = a.a_dtype == AW_BF16 ? 8 : 4;
-  return (!a.a_trans ? (a.K % epc) : (a.M % epc)) != 0 || (!a.b_trans ? (a.K % epc) : (a.N % epc)) != 0;
+  auto padded = [epc](int n, int64_t ld) { return ld >= (int64_t)(n + epc - 1) / epc * epc; };
+  const bool ra = !a.a_trans ? (a.K % epc) != 0 : (a.M % epc != 0 && !padded(a.M, a.lda));
+  const bool rb = !a.b_trans ? (a.K % epc) != 0 : (a.N % epc != 0 && !padded(a.N, a.ldb));
+  return ra || rb;
 }
 
 extern "C" int aw_gemm_ws(const aw_gemm_args* args, float* ws, int64_t ws_elems, void* stream) {

@@ -269,25 +269,21 @@ __device__ __forceinline__ int xcd_remap(int bid, int nblocks) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + slot;
 }
 
-// sum over this thread's half of the staged A K-slice (fused bias gradient of weight-gradient GEMMs)
-template <typename T, bool TR>
-__device__ __forceinline__ float a_row_partial(const char* lds, int tid) {
-  constexpr int BK = TT<T>::BK, EPC = TT<T>::EPC;
-  const int r = tid >> 1, h = tid & 1;
-  float s = 0.f;
-  if constexpr (!TR) {
+// sum of the K values one lane holds in an A fragment (8 bf16 or 4 f32)
+template <typename T>
+__device__ __forceinline__ float frag_sum(const uint4& v) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+  if constexpr (sizeof(T) == 2) {
+    float s0 = 0.f, s1 = 0.f;
 #pragma unroll
-    for (int cc = 0; cc < BK / EPC / 2; ++cc) {
-      const T* cp = reinterpret_cast<const T*>(lds + nt_off(r, h * (BK / EPC / 2) + cc));
-#pragma unroll
-      for (int e = 0; e < EPC; ++e) s += to_f32<T>(cp[e]);
+    for (int i = 0; i < 4; ++i) {
+      s0 += __uint_as_float(w[i] << 16);
+      s1 += __uint_as_float(w[i] & 0xFFFF0000u);
     }
+    return s0 + s1;
   } else {
-#pragma unroll
-    for (int e = 0; e < BK / 2; ++e)
-      s += to_f32<T>(*reinterpret_cast<const T*>(lds + tr_off<T>(h * (BK / 2) + e, r * (int)sizeof(T))));
+    return (__uint_as_float(w[0]) + __uint_as_float(w[1])) + (__uint_as_float(w[2]) + __uint_as_float(w[3]));
   }
-  return s;
 }
 
 template <typename T, bool ATR, bool BTR, int ACONV, int BCONV, bool RAGGED, uint32_t EPI>
@@ -331,7 +327,10 @@ __global__ __launch_bounds__(NTHREADS, RAGGED ? 1 : 2) void gemm_kernel(GemmP P)
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float rowsum = 0.f;
+  // fused A-row sums (bias gradients) from the A fragments already in registers: waves wn == 0 of the tn == 0
+  // tiles add their 8 (bf16) / 4 (f32) k-values per fragment; the lane groups are reduced once at the end
+  const bool wave_rowsum = do_rowsum && wn == 0;
+  float rowacc[4] = {0.f, 0.f, 0.f, 0.f};
 
   auto compute = [&](const char* a_l) {
     const char* b_l = a_l + STAGE_OP;
@@ -347,8 +346,11 @@ __global__ __launch_bounds__(NTHREADS, RAGGED ? 1 : 2) void gemm_kernel(GemmP P)
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) Mfma<T>::run(acc[i][j], af[i], bfr[j]);
+      if (wave_rowsum) {
+#pragma unroll
+        for (int f = 0; f < 4; ++f) rowacc[f] += frag_sum<T>(af[f]);
+      }
     }
-    if (do_rowsum) rowsum += a_row_partial<T, ATR>(a_l, tid);
   };
 
   // Pipeline: LDS stage s holds K step t (t % 2 == s) while the registers of the other set carry the loads
@@ -382,10 +384,15 @@ __global__ __launch_bounds__(NTHREADS, RAGGED ? 1 : 2) void gemm_kernel(GemmP P)
   }
 
   AW_STAMP(2);
-  if (do_rowsum) {
-    rowsum += __shfl_xor(rowsum, 1, 64);
-    const int r = m0 + (tid >> 1);
-    if ((tid & 1) == 0 && r < M) atomicAdd(rowptr + r, rowsum);
+  if (wave_rowsum) {
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+      float v = rowacc[f];
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      const int r = m0 + wm * 64 + f * 16 + lane;
+      if (lane < 16 && r < M) atomicAdd(rowptr + r, v);
+    }
   }
 
   // ---------------------------------------------------------------- epilogue

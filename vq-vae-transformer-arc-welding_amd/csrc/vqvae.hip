@@ -62,6 +62,56 @@ __global__ void relayout_kernel(const float* __restrict__ W, int O, int I, int k
   }
 }
 
+// many relayouts in one launch: blockIdx.y = job; jobs travel in the kernel arguments
+struct RelayoutJobs {
+  aw_relayout_job j[AW_RELAYOUT_MAX_JOBS];
+};
+
+__device__ __forceinline__ int64_t relayout_count(const aw_relayout_job& jb) {
+  switch (jb.mode) {
+    case 0: return (int64_t)jb.O * jb.I;
+    case 1: return (int64_t)jb.O * 3 * jb.I;
+    case 2: return (int64_t)3 * jb.O * jb.I;
+    case 3: return (int64_t)jb.k * jb.O * jb.I;
+    case 4: return (int64_t)jb.O * jb.ldo;
+    default: return (int64_t)jb.O * jb.I;
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void relayout_batch_kernel(RelayoutJobs J) {
+  const aw_relayout_job& jb = J.j[blockIdx.y];
+  const float* __restrict__ W = jb.W;
+  T* __restrict__ out = reinterpret_cast<T*>(jb.out);
+  const int O = jb.O, I = jb.I, k = jb.k, tap = jb.tap, mode = jb.mode;
+  const int64_t ldo = jb.ldo, n = relayout_count(jb);
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
+    float v;
+    if (mode == 0) {
+      const int64_t o = e / I, i = e - o * I;
+      v = W[(o * I + i) * k + tap];
+    } else if (mode == 1) {
+      const int64_t o = e / (3 * I), r = e - o * 3 * I;
+      const int64_t j = r / I, i = r - j * I;
+      v = W[(o * I + i) * 3 + j];
+    } else if (mode == 2) {
+      const int64_t jo = e / I, i = e - jo * I;
+      const int64_t j = jo / O, o = jo - j * O;
+      v = W[(o * I + i) * 3 + j];
+    } else if (mode == 3) {
+      const int64_t jo = e / I, i = e - jo * I;
+      const int64_t j = jo / O, o = jo - j * O;
+      v = W[(i * O + o) * k + j];
+    } else if (mode == 4) {
+      const int64_t o = e / ldo, j = e - o * ldo;
+      v = j < k ? W[o * k + j] : 0.f;
+    } else {
+      v = W[e];
+    }
+    out[e] = from_f32<T>(v);
+  }
+}
+
 __global__ void grad_scatter_kernel(const float* __restrict__ g, int O, int I, int k, int tap, int mode, int64_t ldg,
                                     float* __restrict__ G) {
   int64_t n;
@@ -403,6 +453,34 @@ extern "C" int aw_weight_relayout(const float* W, int O, int I, int k, int tap, 
   else
     hipLaunchKernelGGL(relayout_kernel<float>, dim3(grid_for(n)), dim3(256), 0, s, W, O, I, k, tap, mode, (float*)out, ldo);
   return aw::check_launch("aw_weight_relayout");
+}
+
+extern "C" int aw_weight_relayout_batch(const aw_relayout_job* jobs, int n, int dtype, void* stream) {
+  AW_REQUIRE(jobs && n >= 0 && n <= AW_RELAYOUT_MAX_JOBS, "aw_weight_relayout_batch: need 0..%d jobs",
+             AW_RELAYOUT_MAX_JOBS);
+  AW_REQUIRE(dtype == AW_BF16 || dtype == AW_F32, "aw_weight_relayout_batch: bad dtype");
+  if (n == 0) return AW_OK;
+  RelayoutJobs J;
+  memset(&J, 0, sizeof(J));
+  int64_t most = 0;
+  for (int i = 0; i < n; ++i) {
+    const aw_relayout_job& jb = jobs[i];
+    AW_REQUIRE(jb.W && jb.out && jb.O > 0 && jb.I > 0 && jb.k > 0 && jb.mode >= 0 && jb.mode <= 5,
+               "aw_weight_relayout_batch: bad job %d", i);
+    AW_REQUIRE(!(jb.mode == 4 && jb.ldo < jb.k), "aw_weight_relayout_batch: job %d ldo < k", i);
+    J.j[i] = jb;
+    const int64_t c = jb.mode == 4 ? (int64_t)jb.O * jb.ldo
+                                    : (int64_t)jb.O * jb.I * (jb.mode == 0 || jb.mode == 5 ? 1 : (jb.mode == 3 ? jb.k : 3));
+    most = c > most ? c : most;
+  }
+  int gx = (int)((most + 255) / 256);
+  gx = gx < 1 ? 1 : (gx > 256 ? 256 : gx);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (dtype == AW_BF16)
+    hipLaunchKernelGGL(relayout_batch_kernel<bf16>, dim3(gx, n), dim3(256), 0, s, J);
+  else
+    hipLaunchKernelGGL(relayout_batch_kernel<float>, dim3(gx, n), dim3(256), 0, s, J);
+  return aw::check_launch("aw_weight_relayout_batch");
 }
 
 extern "C" int aw_weight_grad_scatter(const float* g, int O, int I, int k, int tap, int mode, int64_t ldg, float* G,
