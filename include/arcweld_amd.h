@@ -88,6 +88,9 @@ int aw_gemm_ws(const aw_gemm_args* args, float* ws, int64_t ws_elems, void* stre
  * model/transformer_block.py:30,32,78-79 grads), so each tile runs the full token reduction without split-K. */
 #define AW_GEMM_MAX_GROUPS 16
 int aw_gemm_grouped(const aw_gemm_args* args, int n, void* stream);
+/* Tile policy knob: 0 = automatic (256x128 tiles for bf16 launches that fill the chip, else 128x128), 128 or 256 =
+ * force that tile for every eligible launch (bf16, non-ragged) -- used by the tests to cover both pipelines. */
+int aw_gemm_set_tile(int bm);
 
 /* -------------------------------------------------------------------------------- vector quantizer
  * VectorQuantizer.forward (model/vector_quantizer.py:76-119), fp32, codebook staged in LDS, no MFMA:

@@ -20,6 +20,16 @@ def K():
     return kernels
 
 
+@pytest.fixture(params=[0, 256], ids=["tile_auto", "tile256"])
+def tile(request, K):
+    """Runs a test under the automatic tile policy and with every eligible (bf16, non-ragged) launch forced onto
+    the 256x128 three-stage pipeline (aw_gemm_set_tile), so both kernels are covered at small shapes."""
+    from arcweld import _native
+    _native.call("aw_gemm_set_tile", request.param)
+    yield request.param
+    _native.call("aw_gemm_set_tile", 0)
+
+
 def _rand(shape, seed, dtype=torch.float32, scale=1.0):
     return torch.tensor(gen.normal(seed, shape, scale)).to(DEV, dtype)
 
@@ -37,7 +47,7 @@ def _padded(rows, cols, seed, dtype):
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("a_trans,b_trans", [(0, 0), (0, 1), (1, 0), (1, 1)])
 @pytest.mark.parametrize("M,N,Kd", [(256, 128, 64), (300, 200, 72), (17, 514, 512), (1000, 64, 48), (64, 96, 514)])
-def test_gemm_layouts(K, dtype, a_trans, b_trans, M, N, Kd):
+def test_gemm_layouts(K, tile, dtype, a_trans, b_trans, M, N, Kd):
     A = _padded(Kd, M, 1, dtype) if a_trans else _padded(M, Kd, 1, dtype)
     B = _padded(Kd, N, 2, dtype) if b_trans else _padded(N, Kd, 2, dtype)
     C = torch.empty(M, N, device=DEV)
@@ -50,7 +60,7 @@ def test_gemm_layouts(K, dtype, a_trans, b_trans, M, N, Kd):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-def test_gemm_epilogue_chain(K, dtype):
+def test_gemm_epilogue_chain(K, tile, dtype):
     M, N, Kd = 384, 256, 128
     A = _rand((M, Kd), 3, dtype)
     W = _rand((N, Kd), 4, dtype, 0.1)
@@ -79,7 +89,7 @@ def test_gemm_epilogue_chain(K, dtype):
     torch.testing.assert_close(rows.cpu(), A.float().cpu().sum(1), rtol=1e-5, atol=1e-4)
 
 
-def test_gemm_beta_and_dropout(K):
+def test_gemm_beta_and_dropout(K, tile):
     M, N, Kd = 256, 128, 64
     A = _rand((M, Kd), 8)
     W = _rand((N, Kd), 9)
@@ -100,7 +110,7 @@ def test_gemm_beta_and_dropout(K):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-def test_gemm_implicit_conv3(K, dtype):
+def test_gemm_implicit_conv3(K, tile, dtype):
     """Decoder conv (k=3, pad=1 per window of S tokens): forward, input-gradient and weight-gradient forms."""
     Bw, S, Cin, Cout = 6, 16, 64, 128
     M = Bw * S
@@ -195,7 +205,7 @@ def test_vq_small_forward_backward_vs_reference(K):
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("use_ws", [True, False])
-def test_gemm_split_k_accumulate_colmap(K, dtype, use_ws):
+def test_gemm_split_k_accumulate_colmap(K, tile, dtype, use_ws):
     """Weight-gradient form (A^T B, long K): split-K through slabs (workspace) or atomics, accumulated into a
     strided reference layout via the column map (conv weight (O, I, 3): colmap(c) = (c % I)*3 + c // I)."""
     import ctypes
@@ -225,7 +235,7 @@ def test_gemm_split_k_accumulate_colmap(K, dtype, use_ws):
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("conv", [False, True])
-def test_gemm_grouped_weight_grads_match_single_launches(K, dtype, conv):
+def test_gemm_grouped_weight_grads_match_single_launches(K, tile, dtype, conv):
     """aw_gemm_grouped (deferred ResBlock weight gradients, one launch for the stack) == one aw_gemm per problem:
     accumulate mode with the conv-tap column map, fused bias-gradient row sums, per-group pointers."""
     S, Cin, Cout, Ntok = 16, 64, 128, 16 * 40

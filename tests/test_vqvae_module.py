@@ -167,3 +167,32 @@ def test_graphed_steps_match_eager_steps(fp32_parity):
     np.testing.assert_allclose(l1, l0, rtol=1e-4)
     for k in s0:
         torch.testing.assert_close(s1[k].float(), s0[k].float(), rtol=1e-4, atol=1e-5, msg=k)
+
+
+@pytest.mark.gpu
+def test_full_size_bf16_grads_agree_across_gemm_tiles():
+    """Full-size model, bf16 operands: the automatic tile policy (256x128 three-stage pipeline for the grouped
+    weight gradients) and every launch forced onto 128x128 tiles give the same step up to summation order."""
+    from arcweld import _native
+    kw = dict(hidden_dim=512, num_embeddings=512, embedding_dim=64, n_resblocks=8, patch_size=25)
+    m = make_model(kw, 311, "cuda").train()
+    x = torch.tensor(gen.windows(312, 64), device="cuda")
+    old = torch.get_float32_matmul_precision()
+    grads = {}
+    try:
+        torch.set_float32_matmul_precision("medium")
+        for bm in (0, 128):
+            _native.call("aw_gemm_set_tile", bm)
+            m.zero_grad()
+            emb, x_hat, _ = m(x)
+            (torch.nn.functional.mse_loss(x_hat, x) + emb).backward()
+            grads[bm] = {n: p.grad.detach().clone() for n, p in m.named_parameters()}
+    finally:
+        _native.call("aw_gemm_set_tile", 0)
+        torch.set_float32_matmul_precision(old)
+    for n in grads[0]:
+        if n == "reverse_patch_embed.proj.0.bias":
+            continue   # feeds a train-mode BatchNorm: its gradient is zero up to rounding noise
+        a, b = grads[0][n], grads[128][n]
+        rel = ((a - b).norm() / (b.norm() + 1e-20)).item()
+        assert rel < 2e-3, (n, rel)

@@ -110,6 +110,12 @@ int main() {
         if (form == 0) { a.A = X; a.lda = Mw; a.a_trans = 1; a.B = X + (size_t)Kw * Mw; a.ldb = Nw; a.b_trans = 1; }
         else { a.A = X; a.lda = Kw; a.B = X + (size_t)Kw * Mw; a.ldb = Kw; }
       }
+      aw_gemm_set_tile(128);
+      float u128 = timeit([&] { aw_gemm_grouped(v.data(), G, 0); }, 10);
+      aw_gemm_set_tile(256);
+      float u256 = timeit([&] { aw_gemm_grouped(v.data(), G, 0); }, 10);
+      aw_gemm_set_tile(0);
+      printf("  (forced tile 128: %.2f us, forced 256: %.2f us)\n", u128, u256);
       float us = timeit([&] { aw_gemm_grouped(v.data(), G, 0); }, 10);
       printf("grouped x16 512x512xK16384 %s  %8.2f us  (%.0f TF)\n", form == 0 ? "TT (tokens-major, tr reads)" :
              "NN (K-contiguous)          ", us, 2.0 * G * Mw * Nw * Kw / us / 1e6);
@@ -118,6 +124,18 @@ int main() {
              2.0 * 8 * Mw * Nw * Kw / us1 / 1e6);
     }
   }
+  // tile A/B (aw_gemm_set_tile): 128x128 two-stage vs 256x128 three-stage
+  for (int bmv : {128, 256}) {
+    aw_gemm_set_tile(bmv);
+    for (int K : {512, 1536, 2048}) {
+      aw_gemm_args a; memset(&a, 0, sizeof(a));
+      a.M = M; a.N = N; a.K = K; a.a_dtype = AW_BF16; a.A = A; a.lda = K; a.B = B; a.ldb = K;
+      a.alpha = 1.f; a.C = Cb; a.ldc = N; a.c_dtype = AW_BF16; a.col_mul = 1;
+      float us = timeit([&] { aw_gemm(&a, 0); });
+      printf("tile %d: M16384 N512 K%-5d C bf16  %8.2f us  (%.0f TF)\n", bmv, K, us, 2.0 * M * N * K / us / 1e6);
+    }
+  }
+  aw_gemm_set_tile(0);
   // phase stamps (s_memrealtime, 10 ns ticks) of one launch
   for (int Kx : {64, 512, 1536}) {
     aw_gemm_args a; memset(&a, 0, sizeof(a));

@@ -61,6 +61,7 @@ SIGNATURES = {
     "aw_gemm_ws": [ctypes.POINTER(GemmArgs), c_p, c_i64, c_p],
     "aw_gemm_workspace": [ctypes.POINTER(GemmArgs)],
     "aw_gemm_grouped": [ctypes.POINTER(GemmArgs), c_int, c_p],
+    "aw_gemm_set_tile": [c_int],
     "aw_weight_relayout_batch": [ctypes.POINTER(RelayoutJob), c_int, c_int, c_p],
     "aw_vq_forward": [c_p, c_p, c_i64, c_int, c_int, c_p, c_p, c_p, c_p, c_p],
     "aw_vq_finalize": [c_p, c_p, c_i64, c_int, c_int, c_f, c_p, c_p, c_p],

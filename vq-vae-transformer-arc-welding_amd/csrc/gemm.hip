@@ -1,5 +1,7 @@
 // MFMA GEMM family: host entry points (aw_gemm, aw_gemm_ws, aw_gemm_workspace) and the EP_GENERIC / EP_ACCUM
 // kernel instantiations.  The kernel itself is in gemm_core.h; specialised epilogues in gemm_fast_*.hip.
+#include <stdlib.h>
+
 #include "gemm_core.h"
 
 using namespace awg;
@@ -8,8 +10,8 @@ namespace {
 
 template <typename T, Layout LY>
 void launch_generic(const GemmP& P, hipStream_t s, bool ragged) {
-  if (ragged) launch_kernel<T, LY, true, EP_GENERIC>(P, s);
-  else launch_kernel<T, LY, false, EP_GENERIC>(P, s);
+  if (ragged) launch_kernel<T, LY, true, EP_GENERIC, 128>(P, s);
+  else launch_tiled<T, LY, EP_GENERIC>(P, s);
 }
 
 Layout layout_of(const aw_gemm_args& a) {
@@ -49,9 +51,9 @@ void dispatch(const GemmP& P, hipStream_t s, bool ragged) {
   constexpr bool BF = sizeof(T) == 2;
   if (code == EP_ACCUM) {
     switch (ly) {
-      case L_TN: launch_kernel<T, L_TN, false, EP_ACCUM>(P, s); return;
-      case L_TT: launch_kernel<T, L_TT, false, EP_ACCUM>(P, s); return;
-      case L_TT_KCONV: launch_kernel<T, L_TT_KCONV, false, EP_ACCUM>(P, s); return;
+      case L_TN: launch_tiled<T, L_TN, EP_ACCUM>(P, s); return;
+      case L_TT: launch_tiled<T, L_TT, EP_ACCUM>(P, s); return;
+      case L_TT_KCONV: launch_tiled<T, L_TT_KCONV, EP_ACCUM>(P, s); return;
       default: break;
     }
   } else if (code != EP_GENERIC) {
@@ -94,32 +96,6 @@ __global__ __launch_bounds__(256) void gemm_reduce_kernel(const float* __restric
 
 }  // namespace
 
-// split-K choice shared by aw_gemm and aw_gemm_workspace
-static int choose_splits(const aw_gemm_args& a, int nblocks, int BK, int* ksplit) {
-  const bool plain = !a.bias && !a.pre && !a.resid && a.drop_p <= 0.f && !a.C2 && !a.colstats && a.C &&
-                     a.c_dtype == AW_F32 && (a.beta == 0.f || a.beta == 1.f || a.accumulate);
-  int splits = 1;
-  if (plain && nblocks < 192 && a.K >= 32 * BK) {
-    // two co-resident blocks per CU (256 CUs): one block per CU leaves a single wave per SIMD, which cannot
-    // hide the staging latency; keep >= 12 K-steps per split so the slab write + reduce stays small
-    splits = 512 / nblocks;
-    const int max_splits = a.K / (12 * BK);
-    if (splits > max_splits) splits = max_splits;
-    if (splits < 1) splits = 1;
-  }
-  *ksplit = splits > 1 ? aw_cdiv(aw_cdiv(a.K, splits), BK) * BK : (a.K > 0 ? a.K : 1);
-  return splits > 1 ? aw_cdiv(a.K, *ksplit) : 1;
-}
-
-extern "C" int64_t aw_gemm_workspace(const aw_gemm_args* a) {
-  if (!a || a->M <= 0 || a->N <= 0) return 0;
-  const int BK = a->a_dtype == AW_BF16 ? 64 : 32;
-  int ks;
-  const int nb = aw_cdiv(a->M, BM) * aw_cdiv(a->N, BN);
-  const int sp = choose_splits(*a, nb, BK, &ks);
-  return sp > 1 ? (int64_t)sp * a->M * a->N : 0;
-}
-
 extern "C" int aw_gemm_ws(const aw_gemm_args* args, float* ws, int64_t ws_elems, void* stream);
 
 extern "C" int aw_gemm(const aw_gemm_args* args, void* stream) { return aw_gemm_ws(args, nullptr, 0, stream); }
@@ -159,13 +135,39 @@ static int validate(const aw_gemm_args& a) {
   return AW_OK;
 }
 
-// launch geometry, alignment flags and buffer extents of one problem (no split decision)
-static void prepare(const aw_gemm_args& a, GemmP& P) {
+// ragged: a contiguous extent that is not a whole number of 16-B chunks.  A row-contiguous (transposed) operand
+// whose leading dimension is padded to whole chunks is not ragged: the over-read lanes only feed output rows /
+// columns >= M / N, which are never stored (e.g. the patch-embed weight gradient, N = P = 25, ldb = 32).
+static bool is_ragged(const aw_gemm_args& a) {
+  const int epc = a.a_dtype == AW_BF16 ? 8 : 4;
+  auto padded = [epc](int n, int64_t ld) { return ld >= (int64_t)(n + epc - 1) / epc * epc; };
+  const bool ra = !a.a_trans ? (a.K % epc) != 0 : (a.M % epc != 0 && !padded(a.M, a.lda));
+  const bool rb = !a.b_trans ? (a.K % epc) != 0 : (a.N % epc != 0 && !padded(a.N, a.ldb));
+  return ra || rb;
+}
+
+static int g_tile_override = 0;   // aw_gemm_set_tile: 0 = automatic, 128 / 256 = force (tests, tuning)
+
+extern "C" int aw_gemm_set_tile(int bm) {
+  AW_REQUIRE(bm == 0 || bm == 128 || bm == 256, "aw_gemm_set_tile: bm must be 0, 128 or 256");
+  g_tile_override = bm;
+  return AW_OK;
+}
+
+static bool plain_output(const aw_gemm_args& a) {
+  return !a.bias && !a.pre && !a.resid && a.drop_p <= 0.f && !a.C2 && !a.colstats && a.C && a.c_dtype == AW_F32 &&
+         (a.beta == 0.f || a.beta == 1.f || a.accumulate);
+}
+
+// Launch plan of ngroups problems of one shape: tile (128 or 256 rows), grid and split-K.
+//  * bf16 accumulate-mode (weight-gradient) launches with >= 120 tiles of 256x128 take the 256-row tile with its
+//    three-stage pipeline, one workgroup per CU, split over K in two (f32 atomics) below 240 tiles;
+//  * everything else runs 128x128 tiles, two workgroups per CU (measured equal or faster for the M = 16384,
+//    K = 512 .. 2048 forward / input-gradient shapes); plain f32 outputs that cannot fill the chip twice are
+//    split over K (slab workspace when the caller provides one, f32 atomics in grouped launches, <= 2 adders).
+static void plan(const aw_gemm_args& a, int ngroups, bool grouped, GemmP& P) {
   P.a = a;
-  P.tiles_n = aw_cdiv(a.N, BN);
-  P.nblocks = aw_cdiv(a.M, BM) * P.tiles_n;
-  P.ngroups = 1;
-  P.tiles_per_group = P.nblocks;
+  P.ngroups = ngroups;
   P.ws = nullptr;
   auto al = [](const void* ptr, int64_t ld, int dt) {
     return ptr == nullptr || (((uintptr_t)ptr % 16) == 0 && (ld * (dt == AW_BF16 ? 2 : 4)) % 16 == 0);
@@ -179,17 +181,46 @@ static void prepare(const aw_gemm_args& a, GemmP& P) {
   auto wide = [epc](int n, int64_t ld) { const int64_t r = (int64_t)(n + epc - 1) / epc * epc; return ld >= r ? r : n; };
   P.a_bytes = (int)((!a.a_trans ? ((int64_t)(a.M - 1) * a.lda + ka) : ((ka - 1) * a.lda + wide(a.M, a.lda))) * es);
   P.b_bytes = (int)((!a.b_trans ? ((int64_t)(a.N - 1) * a.ldb + ka) : ((ka - 1) * a.ldb + wide(a.N, a.ldb))) * es);
+
+  const int BK = a.a_dtype == AW_BF16 ? 64 : 32;
+  const bool plain = plain_output(a);
+  P.tiles_n = aw_cdiv(a.N, BN);
+  const int t256 = aw_cdiv(a.M, 256) * P.tiles_n * ngroups;
+  int bm = 128, splits = 1;
+  if (a.a_dtype == AW_BF16 && !is_ragged(a) && g_tile_override != 128) {
+    if (g_tile_override == 256) {
+      bm = 256;
+    } else if (a.accumulate && t256 >= 120 && a.K >= 24 * BK) {
+      bm = 256;                               // long-K weight gradients: the three-stage pipeline
+      if (t256 < 240) splits = 2;
+    }
+  }
+  if (bm == 128) {
+    const int nb = aw_cdiv(a.M, 128) * P.tiles_n * ngroups;
+    if (plain && nb < 384 && a.K >= 24 * BK) {
+      // two co-resident blocks per CU (256 CUs); keep >= 12 K-steps per split so the slab write + reduce is small
+      splits = 512 / nb;
+      const int max_splits = a.K / (12 * BK);
+      if (splits > max_splits) splits = max_splits;
+      if (grouped && splits > 2) splits = 2;
+      if (splits < 1) splits = 1;
+    }
+  }
+  P.bm = bm;
+  P.tiles_per_group = aw_cdiv(a.M, bm) * P.tiles_n;
+  P.nblocks = P.tiles_per_group * ngroups;
+  P.ksplit = splits > 1 ? aw_cdiv(aw_cdiv(a.K, splits), BK) * BK : (a.K > 0 ? a.K : 1);
+  P.splits = splits > 1 ? aw_cdiv(a.K, P.ksplit) : 1;
 }
 
-// ragged: a contiguous extent that is not a whole number of 16-B chunks.  A row-contiguous (transposed) operand
-// whose leading dimension is padded to whole chunks is not ragged: the over-read lanes only feed output rows /
-// columns >= M / N, which are never stored (e.g. the patch-embed weight gradient, N = P = 25, ldb = 32).
-static bool is_ragged(const aw_gemm_args& a) {
-  const int epc = a.a_dtype == AW_BF16 ? 8 : 4;
-  auto padded = [epc](int n, int64_t ld) { return ld >= (int64_t)(n + epc - 1) / epc * epc; };
-  const bool ra = !a.a_trans ? (a.K % epc) != 0 : (a.M % epc != 0 && !padded(a.M, a.lda));
-  const bool rb = !a.b_trans ? (a.K % epc) != 0 : (a.N % epc != 0 && !padded(a.N, a.ldb));
-  return ra || rb;
+// the slab workspace is used by single 128-tile launches split over K (grouped and 256-tile splits use atomics)
+static bool wants_slabs(const aw_gemm_args& a, const GemmP& P) { return P.splits > 1 && P.bm == 128 && (a.beta == 0.f || a.beta == 1.f || a.accumulate); }
+
+extern "C" int64_t aw_gemm_workspace(const aw_gemm_args* a) {
+  if (!a || a->M <= 0 || a->N <= 0) return 0;
+  GemmP P;
+  plan(*a, 1, false, P);
+  return wants_slabs(*a, P) ? (int64_t)P.splits * a->M * a->N : 0;
 }
 
 extern "C" int aw_gemm_ws(const aw_gemm_args* args, float* ws, int64_t ws_elems, void* stream) {
@@ -200,14 +231,11 @@ extern "C" int aw_gemm_ws(const aw_gemm_args* args, float* ws, int64_t ws_elems,
   const aw_gemm_args& a = *args;
   if (int st = validate(a)) return st;
   if (a.M == 0 || a.N == 0) return AW_OK;
-  const int BK = a.a_dtype == AW_BF16 ? 64 : 32;
   GemmP P;
-  prepare(a, P);
-  // split-K for plain-accumulate shapes that cannot fill the chip with tiles alone
-  P.splits = choose_splits(a, P.nblocks, BK, &P.ksplit);
-  if (P.splits > 1 && ws && ws_elems >= (int64_t)P.splits * a.M * a.N) P.ws = ws;
+  plan(a, 1, false, P);
+  if (wants_slabs(a, P) && ws && ws_elems >= (int64_t)P.splits * a.M * a.N) P.ws = ws;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  if (P.splits > 1 && !P.ws && a.beta == 0.f && !a.accumulate) {
+  if (P.splits > 1 && !P.ws && a.beta == 0.f && !a.accumulate) {   // atomics into a zeroed C
     if (hipMemset2DAsync(a.C, a.ldc * sizeof(float), 0, a.N * sizeof(float), a.M, s) != hipSuccess)
       return aw::check_launch("aw_gemm split-K zero");
   }
@@ -243,23 +271,13 @@ extern "C" int aw_gemm_grouped(const aw_gemm_args* args, int n, void* stream) {
   }
   AW_REQUIRE(a.accumulate && !a.C2 && !a.bias && !a.colstats, "aw_gemm_grouped: accumulate-mode problems only");
   if (a.M == 0 || a.N == 0) return AW_OK;
-  const int BK = a.a_dtype == AW_BF16 ? 64 : 32;
   GemmP P;
-  prepare(a, P);
-  P.ngroups = n;
-  P.tiles_per_group = P.nblocks;
-  P.nblocks *= n;
+  plan(a, n, true, P);
   for (int g = 0; g < n; ++g) {
     P.gA[g] = args[g].A;
     P.gB[g] = args[g].B;
     P.gC[g] = args[g].C;
     P.gRow[g] = args[g].a_rowsum;
-  }
-  // split-K over f32 atomics only (no slab workspace) while the groups' tiles cannot fill two blocks per CU
-  P.splits = choose_splits(a, P.nblocks, BK, &P.ksplit);
-  if (P.splits > 2) {   // at most two atomic adders per element
-    P.ksplit = aw_cdiv(aw_cdiv(a.K, 2), BK) * BK;
-    P.splits = aw_cdiv(a.K, P.ksplit);
   }
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const bool ragged = is_ragged(a);

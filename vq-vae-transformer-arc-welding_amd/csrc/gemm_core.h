@@ -1,51 +1,61 @@
 // MFMA GEMM family for gfx950 (CDNA4): one kernel body for every dense contraction of the hot path.
 //
-// Tile 128x128 per 256-thread workgroup (4 waves as 2x2, each wave 64x64 = 4x4 fragments of 16x16),
-// K staged through LDS 64 bytes per row per step (32 bf16 / 16 f32), register-staged double buffer, one barrier
-// per K step.  Operand layouts are compile-time template parameters:
+// Two tile configurations (template BMT):
+//   BMT = 128: 128x128 tile, 256 threads (4 waves as 2x2), two LDS stages, two workgroups per CU;
+//   BMT = 256: 256x128 tile, 512 threads (8 waves as 4x2), three LDS stages (two K steps of loads in flight),
+//              one workgroup per CU -- launches whose tiles alone fill the chip (the host picks per launch).
+// Every wave owns a 64x64 output block = 4x4 fragments of 16x16.  K is staged 128 bytes per operand row per step
+// (64 bf16 / 32 f32).  Operands reach LDS by LDS-DMA (gfx950 `buffer_load ... lds`): the image swizzle is applied
+// to the source address, out-of-range offsets implement every mask (M/N/K tails, implicit-conv window edges).
+// Ragged shapes (a contiguous extent that is not whole 16-B chunks) use register staging instead.
+// Operand layouts are compile-time template parameters:
 //   K-contiguous operand ([rows][K], e.g. activations in forward, weights [out][in]) -> LDS image [row][k],
-//       fragments by one ds_read_b128;
+//       16-B chunks XOR-swizzled per row pair, fragments by one ds_read_b128;
 //   row-contiguous operand ([K][rows], e.g. activations as the weight-gradient reduction operand) -> LDS image
-//       [k][row] written with one ds_write_b128 per staged chunk; bf16 fragments come from two
-//       ds_read_b64_tr_b16 hardware-transposed reads (gfx950), f32 fragments from four ds_read_b32.
+//       [k][row] with a per-k-row rotation; bf16 fragments come from two ds_read_b64_tr_b16 hardware-transposed
+//       reads (gfx950), f32 fragments from four ds_read_b32.
 // Implicit k=3/pad=1 convolution (decoder ResBlocks) = row-shifted loads with a per-window zero mask.
 //   bf16: v_mfma_f32_16x16x32_bf16 (fp32 accumulate)      f32: v_mfma_f32_16x16x4_f32 (exact f32)
-// Split-K (grid.y) with fp32 atomics serves the weight-gradient shapes (M x N = 512 x 512 .. 2560 x 512,
-// K = tokens), whose tile count alone would leave most of the 256 CUs idle.
-// Fused epilogue (non-split): bias, act' (GELU backward), dropout (counter-based mask), residual add,
-// beta*C, second output (act / copy / dropout-masked copy), BatchNorm column statistics; and a fused A-row-sum
-// (bias gradients) from the staged A tiles in every mode.
+// Split-K (grid.y) serves weight-gradient shapes whose tile count alone would leave CUs idle.
+// Fused epilogue: bias, act' (GELU backward), dropout (counter-based mask), residual add, beta*C, second output
+// (act / copy / dropout-masked copy), BatchNorm column statistics; fused A-row sums (bias gradients) from the
+// A fragments in registers.
 #pragma once
 #include "common.h"
 
 namespace awg {
 
-constexpr int BM = 128, BN = 128, NTHREADS = 256;
+constexpr int BN = 128;
 constexpr int ROWB = 128;                // bytes of K per operand row per step (K-contiguous image pitch)
-constexpr int STAGE_OP = 16384;          // bytes per operand per stage (both images are exactly 16 KiB)
 constexpr int CPITCH = BN + 4;           // f32 pitch of the epilogue tile
-constexpr int SMEM = (BM * CPITCH * 4 > 4 * STAGE_OP) ? BM * CPITCH * 4 : 4 * STAGE_OP;
-constexpr int NCH = STAGE_OP / 16 / NTHREADS;   // 16-B chunks per thread per operand per step (4)
+
+template <int BMT> struct Cfg;
+template <> struct Cfg<128> { static constexpr int NTH = 256, NSTAGE = 2, MINB = 2; };
+template <> struct Cfg<256> { static constexpr int NTH = 512, NSTAGE = 3, MINB = 1; };
+template <int BMT> constexpr int stage_bytes() { return (BMT + BN) * ROWB; }
+template <int BMT> constexpr int smem_bytes() {
+  return Cfg<BMT>::NSTAGE * stage_bytes<BMT>() > BMT * CPITCH * 4 ? Cfg<BMT>::NSTAGE * stage_bytes<BMT>()
+                                                                   : BMT * CPITCH * 4;
+}
 
 template <typename T> struct TT;
 template <> struct TT<bf16> {
   static constexpr int EPC = 8, BK = 64;
-  static constexpr int MPB = 256;          // k-row of the row-contiguous image: 128 rows x 2 B
   // rotation of k-row k (bytes): conflict-free ds_read_b64_tr_b16 for the 32-lane halves
   __device__ static constexpr int rot(int k) { return 32 * ((k & 3) + 4 * ((k >> 3) & 1)); }
 };
 template <> struct TT<float> {
   static constexpr int EPC = 4, BK = 32;
-  static constexpr int MPB = 512;          // 128 rows x 4 B
   __device__ static constexpr int rot(int k) { return 64 * ((k >> 2) & 1); }
 };
 
 // K-contiguous image [row][128 B]: logical 16-B chunk c of row r lives at physical chunk c ^ ((r >> 1) & 7)
 // (conflict-free ds_read_b128 for the 16-row fragments; verified against the gfx950 lane groups).
 __device__ __forceinline__ int nt_off(int row, int chunk) { return row * ROWB + ((chunk ^ ((row >> 1) & 7)) << 4); }
-template <typename T>
+// row-contiguous image [k][MPB bytes] (MPB = rows * sizeof(T)): byte b of k-row k lives at (b + rot(k)) mod MPB
+template <typename T, int MPB>
 __device__ __forceinline__ int tr_off(int krow, int byte_in_row) {
-  return krow * TT<T>::MPB + ((byte_in_row + TT<T>::rot(krow)) & (TT<T>::MPB - 1));
+  return krow * MPB + ((byte_in_row + TT<T>::rot(krow)) & (MPB - 1));
 }
 
 struct GemmP {
@@ -57,6 +67,7 @@ struct GemmP {
   // grouped launch (aw_gemm_grouped): ngroups problems of one shape, tiles_per_group consecutive logical tiles
   // each; the operand / output / row-sum pointers of group g replace a.A, a.B, a.C, a.a_rowsum
   int ngroups, tiles_per_group;
+  int bm;    // tile rows of this launch (128 or 256)
   const void* gA[AW_GEMM_MAX_GROUPS];
   const void* gB[AW_GEMM_MAX_GROUPS];
   void* gC[AW_GEMM_MAX_GROUPS];
@@ -83,35 +94,50 @@ __device__ uint64_t g_gemm_stamps[8192 * 8];
 #define AW_STAMP(i) do { } while (0)
 #endif
 
-// ---------------------------------------------------------------- operand staging (global -> regs -> LDS)
+// ---------------------------------------------------------------- operand staging
 // Loads are raw buffer loads: an out-of-range byte offset returns zeros, which implements every mask
-// (M/N/K tails, implicit-conv window edges) without branches, so the compiler can keep two K steps of
-// loads in flight and wait with a counted vmcnt.
+// (M/N/K tails, implicit-conv window edges) without branches.
 constexpr int OOB = 0x7FFFFFF0;
+typedef int v4i32 __attribute__((ext_vector_type(4)));
 
-template <typename T, bool TR, int CONV, bool RAGGED>
+template <typename T, bool TR, int CONV, bool RAGGED, int ROWS, int NTH>
 struct Stager {
   static constexpr int EPC = TT<T>::EPC, BK = TT<T>::BK;
-  static constexpr int CPR = 128 / EPC;   // chunks per k-row of a row-contiguous tile
-  static constexpr int CPK = BK / EPC;    // chunks per row of a K-contiguous tile (8)
+  static constexpr int CPR = ROWS / EPC;            // 16-B chunks per k-row of a row-contiguous tile
+  static constexpr int CPK = BK / EPC;              // chunks per row of a K-contiguous tile (8)
+  static constexpr int MPB = ROWS * (int)sizeof(T); // bytes per k-row of the row-contiguous image
+  static constexpr int NCH = ROWS * 8 / NTH;        // 16-B chunks per thread per step
   const T* base;
   int64_t ld;
   int rows_total, row0, kend, cin, seg, dir;
   __amdgpu_buffer_rsrc_t rsrc;
+  v4i32 desc;       // the same buffer descriptor as four SGPR words (inline-asm LDS-DMA)
   // per-thread invariants of the implicit convolution (window position / tap of each chunk)
   int wpos[NCH];    // ROWSHIFT: row % seg (fixed rows);  KSHIFT: (k0 + krow) % seg, advanced per K step
   int tapoff[NCH];  // KSHIFT: row shift j-1 of the chunk's column tap
   int colin[NCH];   // KSHIFT: column within the tap (m - j*cin)
 
-  __device__ __forceinline__ void init(int kbeg, int tid, int nbytes) {
+  // logical row offset (in elements) of chunk c of a row-contiguous image: register staging writes chunk c at
+  // its logical place; LDS-DMA staging lands chunk c at physical byte 16*c, so it loads the logical chunk there
+  __device__ __forceinline__ static int tr_logical_m(int c, bool dma) {
+    if (!dma) return (c % CPR) * EPC;
+    const int pb = (c % CPR) * 16;
+    return ((pb - TT<T>::rot(c / CPR)) & (MPB - 1)) / (int)sizeof(T);
+  }
+
+  __device__ __forceinline__ void init(int kbeg, int tid, int nbytes, bool dma) {
     rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, nbytes, 0x00020000);
+    const uint64_t b = (uint64_t)(uintptr_t)base;
+    desc = v4i32{(int)__builtin_amdgcn_readfirstlane((uint32_t)b),
+                 (int)__builtin_amdgcn_readfirstlane((uint32_t)(b >> 32) & 0xFFFFu),
+                 (int)__builtin_amdgcn_readfirstlane((uint32_t)nbytes), 0x00020000};
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
-      const int c = tid + i * NTHREADS;
+      const int c = tid + i * NTH;
       if constexpr (CONV == CONV_ROWSHIFT) {
         wpos[i] = (row0 + c / CPK) % seg;
       } else if constexpr (CONV == CONV_KSHIFT) {
-        const int m = row0 + (c % CPR) * EPC;
+        const int m = row0 + tr_logical_m(c, dma);
         const int j = m / cin;
         tapoff[i] = j - 1;
         colin[i] = m - j * cin;
@@ -127,58 +153,67 @@ struct Stager {
     return u;
   }
 
+  // source element index of the chunk at logical (row, k) of a K-contiguous tile; ok = not masked
+  __device__ __forceinline__ int64_t src_nt(int i, int jrow, int row, int k, bool& ok) const {
+    ok = row < rows_total && k < kend;
+    int src = row, kk = k;
+    if constexpr (CONV == CONV_ROWSHIFT) {
+      kk = k - jrow * cin;
+      const int sft = dir * (jrow - 1);
+      ok = ok && (wpos[i] + sft >= 0) && (wpos[i] + sft < seg);
+      src = row + sft;
+    }
+    return (int64_t)src * ld + kk;
+  }
+  // source element index of the chunk at logical (k, m) of a row-contiguous tile (KSHIFT advances its window)
+  __device__ __forceinline__ int64_t src_tr(int i, int k, int m, bool& ok) {
+    ok = k < kend && m < rows_total;
+    int srck = k, mm = m;
+    if constexpr (CONV == CONV_KSHIFT) {
+      mm = colin[i];
+      const int sft = tapoff[i];
+      ok = ok && (wpos[i] + sft >= 0) && (wpos[i] + sft < seg);
+      srck = k + sft;
+      wpos[i] += BK % seg;                 // advance the window position to the next K step
+      if (wpos[i] >= seg) wpos[i] -= seg;
+    }
+    return (int64_t)srck * ld + mm;
+  }
+
+  // register staging (ragged shapes): global -> VGPRs
   __device__ __forceinline__ void load(int k0, int tid, uint4 (&v)[NCH]) {
     // ROWSHIFT: cin % BK == 0, so the tap is uniform over the whole K step
     const int jrow = (CONV == CONV_ROWSHIFT) ? k0 / cin : 0;
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
-      const int c = tid + i * NTHREADS;
+      const int c = tid + i * NTH;
+      bool ok;
       if constexpr (!TR) {
-        const int row = row0 + c / CPK;
         const int k = k0 + (c % CPK) * EPC;
-        bool ok = row < rows_total && k < kend;
-        int src = row, kk = k;
-        if constexpr (CONV == CONV_ROWSHIFT) {
-          kk = k - jrow * cin;
-          const int sft = dir * (jrow - 1);
-          ok = ok && (wpos[i] + sft >= 0) && (wpos[i] + sft < seg);
-          src = row + sft;
-        }
+        const int64_t e = src_nt(i, jrow, row0 + c / CPK, k, ok);
         if constexpr (RAGGED) {
           if (ok && k + EPC > kend) {
-            const T* p = base + (int64_t)src * ld + kk;
             T tmp[EPC];
 #pragma unroll
-            for (int e = 0; e < EPC; ++e) tmp[e] = (k + e < kend) ? p[e] : from_f32<T>(0.f);
+            for (int q = 0; q < EPC; ++q) tmp[q] = (k + q < kend) ? base[e + q] : from_f32<T>(0.f);
             memcpy(&v[i], tmp, 16);
             continue;
           }
         }
-        v[i] = bload(ok ? (int)(((int64_t)src * ld + kk) * (int)sizeof(T)) : OOB);
+        v[i] = bload(ok ? (int)(e * (int)sizeof(T)) : OOB);
       } else {
-        const int k = k0 + c / CPR;
         const int m = row0 + (c % CPR) * EPC;
-        bool ok = k < kend && m < rows_total;
-        int srck = k, mm = m;
-        if constexpr (CONV == CONV_KSHIFT) {
-          mm = colin[i];
-          const int sft = tapoff[i];
-          ok = ok && (wpos[i] + sft >= 0) && (wpos[i] + sft < seg);
-          srck = k + sft;
-          wpos[i] += BK % seg;                 // advance the window position to the next K step
-          if (wpos[i] >= seg) wpos[i] -= seg;
-        }
+        const int64_t e = src_tr(i, k0 + c / CPR, m, ok);
         if constexpr (RAGGED) {
           if (ok && m + EPC > rows_total) {
-            const T* p = base + (int64_t)srck * ld + mm;
             T tmp[EPC];
 #pragma unroll
-            for (int e = 0; e < EPC; ++e) tmp[e] = (m + e < rows_total) ? p[e] : from_f32<T>(0.f);
+            for (int q = 0; q < EPC; ++q) tmp[q] = (m + q < rows_total) ? base[e + q] : from_f32<T>(0.f);
             memcpy(&v[i], tmp, 16);
             continue;
           }
         }
-        v[i] = bload(ok ? (int)(((int64_t)srck * ld + mm) * (int)sizeof(T)) : OOB);
+        v[i] = bload(ok ? (int)(e * (int)sizeof(T)) : OOB);
       }
     }
   }
@@ -186,11 +221,39 @@ struct Stager {
   __device__ __forceinline__ void store(char* lds, int tid, const uint4 (&v)[NCH]) const {
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
-      const int c = tid + i * NTHREADS;
+      const int c = tid + i * NTH;
       if constexpr (!TR)
         *reinterpret_cast<uint4*>(lds + nt_off(c / CPK, c % CPK)) = v[i];
       else
-        *reinterpret_cast<uint4*>(lds + tr_off<T>(c / CPR, (c % CPR) * 16)) = v[i];
+        *reinterpret_cast<uint4*>(lds + tr_off<T, MPB>(c / CPR, (c % CPR) * 16)) = v[i];
+    }
+  }
+
+  // LDS-DMA staging (gfx950 buffer_load ... lds): chunk c = tid + i*NTH lands at byte 16*c of the operand's stage
+  // image (lane-linear per wave instruction, base in M0); the swizzle is applied to the SOURCE address.
+  // Issued from inline asm so that the compiler does not see an LDS write it cannot disambiguate from the ds_reads
+  // of the other stages (it would drain vmcnt to 0 before every compute step and serialise the pipeline); the
+  // kernel orders the DMA itself with counted vmcnt waits and barriers.
+  __device__ __forceinline__ void dma(int k0, int tid, char* img) {
+    const int jrow = (CONV == CONV_ROWSHIFT) ? k0 / cin : 0;
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      const int c = tid + i * NTH;
+      bool ok;
+      int64_t e;
+      if constexpr (!TR) {
+        const int r = c / CPK;
+        const int lc = (c % CPK) ^ ((r >> 1) & 7);
+        e = src_nt(i, jrow, row0 + r, k0 + lc * EPC, ok);
+      } else {
+        e = src_tr(i, k0 + c / CPR, row0 + tr_logical_m(c, true), ok);
+      }
+      const int off = ok ? (int)(e * (int)sizeof(T)) : OOB;
+      char* dst = img + ((tid & ~63) + i * NTH) * 16;    // wave-uniform base of this wave instruction
+      const uint32_t m0 = __builtin_amdgcn_readfirstlane(
+          (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)dst);
+      asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" ::"s"(m0), "v"(off), "s"(desc)
+                   : "memory", "m0");
     }
   }
 };
@@ -202,7 +265,7 @@ typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
 // Fragment of the 16 rows [rbase, rbase+16) x this lane's K slice of MFMA sub-step u, as 16 bytes.
 // K order inside a sub-step is the same for A and B: lane group g holds k = 8g..8g+7 (bf16) /
 // k = 4g..4g+3 with one element per f32 MFMA (f32).
-template <typename T, bool TR>
+template <typename T, bool TR, int MPB>
 __device__ __forceinline__ uint4 frag(const char* lds, int rbase, int lane, int u) {
   const int g = lane >> 4, i = lane & 15;
   if constexpr (!TR) {
@@ -213,9 +276,9 @@ __device__ __forceinline__ uint4 frag(const char* lds, int rbase, int lane, int 
     const int q = i >> 2, p = i & 3;
     const int k0 = 32 * u + 8 * g + q;
     const v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-        (lds_v4i16*)(uintptr_t)(lds + tr_off<T>(k0, 2 * (rbase + 4 * p))));
+        (lds_v4i16*)(uintptr_t)(lds + tr_off<T, MPB>(k0, 2 * (rbase + 4 * p))));
     const v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-        (lds_v4i16*)(uintptr_t)(lds + tr_off<T>(k0 + 4, 2 * (rbase + 4 * p))));
+        (lds_v4i16*)(uintptr_t)(lds + tr_off<T, MPB>(k0 + 4, 2 * (rbase + 4 * p))));
     uint4 out;
     memcpy(&out, &lo, 8);
     memcpy(reinterpret_cast<char*>(&out) + 8, &hi, 8);
@@ -223,7 +286,8 @@ __device__ __forceinline__ uint4 frag(const char* lds, int rbase, int lane, int 
   } else {
     float f[4];
 #pragma unroll
-    for (int s = 0; s < 4; ++s) f[s] = *reinterpret_cast<const float*>(lds + tr_off<T>(16 * u + 4 * g + s, 4 * (rbase + i)));
+    for (int s = 0; s < 4; ++s)
+      f[s] = *reinterpret_cast<const float*>(lds + tr_off<T, MPB>(16 * u + 4 * g + s, 4 * (rbase + i)));
     uint4 out;
     memcpy(&out, f, 16);
     return out;
@@ -248,7 +312,6 @@ template <> struct Mfma<float> {
     for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[s], bv[s], acc, 0, 0, 0);
   }
 };
-
 
 // 4 consecutive elements (16-B aligned for f32, 8-B for bf16)
 __device__ __forceinline__ void store4(void* base, bool is_bf16, int64_t e, const float (&v)[4]) {
@@ -286,11 +349,19 @@ __device__ __forceinline__ float frag_sum(const uint4& v) {
   }
 }
 
-template <typename T, bool ATR, bool BTR, int ACONV, int BCONV, bool RAGGED, uint32_t EPI>
-__global__ __launch_bounds__(NTHREADS, RAGGED ? 1 : 2) void gemm_kernel(GemmP P) {
+template <int N> __device__ __forceinline__ void wait_vmcnt() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+
+template <typename T, bool ATR, bool BTR, int ACONV, int BCONV, bool RAGGED, uint32_t EPI, int BMT>
+__global__ __launch_bounds__(Cfg<BMT>::NTH, RAGGED ? 1 : Cfg<BMT>::MINB) void gemm_kernel(GemmP P) {
+  constexpr int NTH = Cfg<BMT>::NTH;
   constexpr int BK = TT<T>::BK;
+  constexpr int A_IMG = BMT * ROWB;                // A stage image bytes; the B image follows it
+  constexpr int STAGE = stage_bytes<BMT>();
+  static_assert(!(RAGGED && BMT != 128), "ragged shapes use the 128-row register-staged tile");
+  using SA = Stager<T, ATR, ACONV, RAGGED, BMT, NTH>;
+  using SB = Stager<T, BTR, BCONV, RAGGED, BN, NTH>;
   const aw_gemm_args& p = P.a;
-  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+  __shared__ __attribute__((aligned(16))) char smem[smem_bytes<BMT>()];
 
   AW_STAMP(0);
   const int tid = threadIdx.x;
@@ -310,16 +381,16 @@ __global__ __launch_bounds__(NTHREADS, RAGGED ? 1 : 2) void gemm_kernel(GemmP P)
     rowptr = P.gRow[g];
   }
   const int tm = tile / P.tiles_n, tn = tile % P.tiles_n;
-  const int m0 = tm * BM, n0 = tn * BN;
+  const int m0 = tm * BMT, n0 = tn * BN;
   const int M = p.M, N = p.N;
   const int kbeg = blockIdx.y * P.ksplit;
   const int kend = min(p.K, kbeg + P.ksplit);
 
-  Stager<T, ATR, ACONV, RAGGED> sa{reinterpret_cast<const T*>(Aptr), p.lda, M, m0, kend, p.conv_cin, p.conv_seg,
-                                   p.conv_dir};
-  Stager<T, BTR, BCONV, RAGGED> sb{reinterpret_cast<const T*>(Bptr), p.ldb, N, n0, kend, p.conv_cin, p.conv_seg, 1};
-  sa.init(kbeg, tid, P.a_bytes);
-  sb.init(kbeg, tid, P.b_bytes);
+  SA sa{reinterpret_cast<const T*>(Aptr), p.lda, M, m0, kend, p.conv_cin, p.conv_seg, p.conv_dir};
+  SB sb{reinterpret_cast<const T*>(Bptr), p.ldb, N, n0, kend, p.conv_cin, p.conv_seg, 1};
+  constexpr bool use_dma = !RAGGED;
+  sa.init(kbeg, tid, P.a_bytes, use_dma);
+  sb.init(kbeg, tid, P.b_bytes, use_dma);
   const bool do_rowsum = rowptr != nullptr && tn == 0;
 
   f32x4 acc[4][4];
@@ -333,14 +404,14 @@ __global__ __launch_bounds__(NTHREADS, RAGGED ? 1 : 2) void gemm_kernel(GemmP P)
   float rowacc[4] = {0.f, 0.f, 0.f, 0.f};
 
   auto compute = [&](const char* a_l) {
-    const char* b_l = a_l + STAGE_OP;
+    const char* b_l = a_l + A_IMG;
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       uint4 af[4], bfr[4];
 #pragma unroll
       for (int f = 0; f < 4; ++f) {
-        af[f] = frag<T, ATR>(a_l, wm * 64 + f * 16, lane, u);
-        bfr[f] = frag<T, BTR>(b_l, wn * 64 + f * 16, lane, u);
+        af[f] = frag<T, ATR, BMT * (int)sizeof(T)>(a_l, wm * 64 + f * 16, lane, u);
+        bfr[f] = frag<T, BTR, BN * (int)sizeof(T)>(b_l, wn * 64 + f * 16, lane, u);
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i)
@@ -353,34 +424,93 @@ __global__ __launch_bounds__(NTHREADS, RAGGED ? 1 : 2) void gemm_kernel(GemmP P)
     }
   };
 
-  // Pipeline: LDS stage s holds K step t (t % 2 == s) while the registers of the other set carry the loads
-  // of step t+1 and the loads of step t+2 are issued at the top of step t: two steps of latency cover.
-  char* L0 = smem;
-  char* L1 = smem + 2 * STAGE_OP;
   const int nk = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
-  uint4 ra0[NCH], rb0[NCH], ra1[NCH], rb1[NCH];
-  sa.load(kbeg, tid, ra0);
-  sb.load(kbeg, tid, rb0);
-  sa.load(kbeg + BK, tid, ra1);
-  sb.load(kbeg + BK, tid, rb1);
-  sa.store(L0, tid, ra0);
-  sb.store(L0 + STAGE_OP, tid, rb0);
-  __syncthreads();
-  AW_STAMP(1);
-  for (int kt = 0; kt < nk; kt += 2) {
-    sa.load(kbeg + (kt + 2) * BK, tid, ra0);   // beyond kend: out-of-range -> zeros, never read
-    sb.load(kbeg + (kt + 2) * BK, tid, rb0);
-    compute(L0);
-    sa.store(L1, tid, ra1);
-    sb.store(L1 + STAGE_OP, tid, rb1);
+  if constexpr (use_dma && Cfg<BMT>::NSTAGE == 2) {
+    // two stages: the loads of step t+1 fly into the other stage while step t computes
+    char* L0 = smem;
+    char* L1 = smem + STAGE;
+    sa.dma(kbeg, tid, L0);
+    sb.dma(kbeg, tid, L0 + A_IMG);
+    wait_vmcnt<0>();
     __syncthreads();
-    if (kt + 1 >= nk) break;
-    sa.load(kbeg + (kt + 3) * BK, tid, ra1);
-    sb.load(kbeg + (kt + 3) * BK, tid, rb1);
-    compute(L1);
+    AW_STAMP(1);
+    for (int kt = 0; kt < nk; ++kt) {
+      char* cur = (kt & 1) ? L1 : L0;
+      char* nxt = (kt & 1) ? L0 : L1;
+      if (kt + 1 < nk) {
+        sa.dma(kbeg + (kt + 1) * BK, tid, nxt);
+        sb.dma(kbeg + (kt + 1) * BK, tid, nxt + A_IMG);
+      }
+      compute(cur);
+      wait_vmcnt<0>();
+      __syncthreads();
+    }
+  } else if constexpr (use_dma) {
+    // three-stage ring: steps t+1 and t+2 are in flight while step t computes.  Each wave retires its own DMA of
+    // step t+1 with a counted vmcnt (leaving step t+2 in flight) and the raw barrier publishes it to every wave;
+    // the barrier also orders every wave's reads of stage t before the DMA of step t+3 overwrites it.
+    constexpr int PER_STEP = SA::NCH + SB::NCH;
+    char* S0 = smem;
+    char* S1 = smem + STAGE;
+    char* S2 = smem + 2 * STAGE;
+    sa.dma(kbeg, tid, S0);
+    sb.dma(kbeg, tid, S0 + A_IMG);
+    if (nk > 1) {
+      sa.dma(kbeg + BK, tid, S1);
+      sb.dma(kbeg + BK, tid, S1 + A_IMG);
+      wait_vmcnt<PER_STEP>();
+    } else {
+      wait_vmcnt<0>();
+    }
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    AW_STAMP(1);
+    for (int kt = 0; kt < nk; ++kt) {
+      // stages rotate S0 -> S1 -> S2: step kt computes from S0 and step kt+2 loads into S2
+      if (kt + 2 < nk) {
+        sa.dma(kbeg + (kt + 2) * BK, tid, S2);
+        sb.dma(kbeg + (kt + 2) * BK, tid, S2 + A_IMG);
+      }
+      compute(S0);
+      if (kt + 2 < nk) wait_vmcnt<PER_STEP>();
+      else wait_vmcnt<0>();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      char* t0 = S0;
+      S0 = S1;
+      S1 = S2;
+      S2 = t0;
+    }
+  } else {
+    // register staging (ragged shapes): LDS stage s holds K step t (t % 2 == s) while the registers of the other
+    // set carry the loads of step t+1; the loads of step t+2 are issued at the top of step t
+    char* L0 = smem;
+    char* L1 = smem + STAGE;
+    uint4 ra0[SA::NCH], rb0[SB::NCH], ra1[SA::NCH], rb1[SB::NCH];
+    sa.load(kbeg, tid, ra0);
+    sb.load(kbeg, tid, rb0);
+    sa.load(kbeg + BK, tid, ra1);
+    sb.load(kbeg + BK, tid, rb1);
     sa.store(L0, tid, ra0);
-    sb.store(L0 + STAGE_OP, tid, rb0);
+    sb.store(L0 + A_IMG, tid, rb0);
     __syncthreads();
+    AW_STAMP(1);
+    for (int kt = 0; kt < nk; kt += 2) {
+      sa.load(kbeg + (kt + 2) * BK, tid, ra0);   // beyond kend: out-of-range -> zeros, never read
+      sb.load(kbeg + (kt + 2) * BK, tid, rb0);
+      compute(L0);
+      sa.store(L1, tid, ra1);
+      sb.store(L1 + A_IMG, tid, rb1);
+      __syncthreads();
+      if (kt + 1 >= nk) break;
+      sa.load(kbeg + (kt + 3) * BK, tid, ra1);
+      sb.load(kbeg + (kt + 3) * BK, tid, rb1);
+      compute(L1);
+      sa.store(L0, tid, ra0);
+      sb.store(L0 + A_IMG, tid, rb0);
+      __syncthreads();
+    }
   }
 
   AW_STAMP(2);
@@ -400,6 +530,7 @@ __global__ __launch_bounds__(NTHREADS, RAGGED ? 1 : 2) void gemm_kernel(GemmP P)
   // test of the argument block for EP_GENERIC, so each hot epilogue compiles to straight-line code.
 #define EPF(bit, rt) ((EPI & EP_GENERIC) ? (rt) : ((EPI & (bit)) != 0))
   constexpr bool GEN = (EPI & EP_GENERIC) != 0;
+  constexpr int NR = NTH / 32;                     // rows per pass of the row-major epilogue walk
   // 1) accumulators -> LDS tile (static register indexing), 2) one element per thread per step with
   //    consecutive threads on consecutive columns: every wave instruction touches 256 contiguous bytes.
   float* Cs = reinterpret_cast<float*>(smem);
@@ -415,13 +546,14 @@ __global__ __launch_bounds__(NTHREADS, RAGGED ? 1 : 2) void gemm_kernel(GemmP P)
   }
   __syncthreads();
   AW_STAMP(3);
-  const int rows_here = min(BM, M - m0);
+  const int rows_here = min(BMT, M - m0);
   if (EPF(EP_ACCUM, P.splits > 1 || p.accumulate)) {
     if (P.splits > 1 && P.ws) {  // partial slab of this split: plain coalesced stores, reduced by gemm_reduce
       const int lc = tid & 127, col = n0 + lc;
       if (col >= N) return;
       float* slab = P.ws + (int64_t)blockIdx.y * M * N;
-      for (int lr = tid >> 7; lr < rows_here; lr += 2) slab[(int64_t)(m0 + lr) * N + col] = Cs[lr * CPITCH + lc];
+      for (int lr = tid >> 7; lr < rows_here; lr += NTH / 128)
+        slab[(int64_t)(m0 + lr) * N + col] = Cs[lr * CPITCH + lc];
       return;
     }
     // accumulate into f32 C with atomics (consecutive lanes -> columns)
@@ -430,7 +562,7 @@ __global__ __launch_bounds__(NTHREADS, RAGGED ? 1 : 2) void gemm_kernel(GemmP P)
     const int64_t oc = p.col_mod > 0 ? (int64_t)(col % p.col_mod) * p.col_mul + col / p.col_mod + p.col_off
                                      : (int64_t)col * (p.col_mul > 0 ? p.col_mul : 1) + p.col_off;
     float* C = reinterpret_cast<float*>(Cptr);
-    for (int lr = tid >> 7; lr < rows_here; lr += 2)
+    for (int lr = tid >> 7; lr < rows_here; lr += NTH / 128)
       atomicAdd(C + (int64_t)(m0 + lr) * p.ldc + oc, p.alpha * Cs[lr * CPITCH + lc]);
     return;
   }
@@ -451,7 +583,7 @@ __global__ __launch_bounds__(NTHREADS, RAGGED ? 1 : 2) void gemm_kernel(GemmP P)
   const float alpha = GEN ? p.alpha : 1.f;       // specialised codes are issued for alpha == 1 only
   const uint64_t dseed = f_drop ? aw_seed_mix(p.drop_seed, p.seed_ptr) : 0ull;
   const uint64_t dseed2 = c2m == 3 ? aw_seed_mix(p.drop2_seed, p.seed_ptr) : 0ull;
-  // thread -> 4 consecutive columns (c4) x rows r0, r0+8, ...; 4 rows of loads in flight per thread
+  // thread -> 4 consecutive columns (c4) x rows r0, r0+NR, ...; 4 rows of loads in flight per thread
   const int c4 = (tid & 31) * 4, r0 = tid >> 5;
   const int col = n0 + c4;
   // specialised codes are issued only when every operand row is 16-B aligned and N % 4 == 0
@@ -463,11 +595,11 @@ __global__ __launch_bounds__(NTHREADS, RAGGED ? 1 : 2) void gemm_kernel(GemmP P)
     bias[e] = (f_bias && c < N) ? p.bias[f_bmod ? c % p.bias_mod : c] : 0.f;
   }
   if (col < N) {
-    for (int lr0 = r0; lr0 < rows_here; lr0 += 32) {
+    for (int lr0 = r0; lr0 < rows_here; lr0 += 4 * NR) {
       float4 pre4[4], res4[4], old4[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {  // issue the operand loads of 4 rows first
-        const int lr = lr0 + 8 * u;
+        const int lr = lr0 + NR * u;
         if (lr >= rows_here) break;
         const int64_t row = m0 + lr;
         if (vec) {
@@ -490,7 +622,7 @@ __global__ __launch_bounds__(NTHREADS, RAGGED ? 1 : 2) void gemm_kernel(GemmP P)
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        const int lr = lr0 + 8 * u;
+        const int lr = lr0 + NR * u;
         if (lr >= rows_here) break;
         const int64_t row = m0 + lr;
         const float4 a4 = *reinterpret_cast<const float4*>(Cs + lr * CPITCH + c4);
@@ -535,9 +667,9 @@ __global__ __launch_bounds__(NTHREADS, RAGGED ? 1 : 2) void gemm_kernel(GemmP P)
     }
   }
   AW_STAMP(4);
-  if (f_stats) {  // BatchNorm batch statistics: reduce the 8 row-groups of a column, one f64 atomic each
+  if (f_stats) {  // BatchNorm batch statistics: reduce the NR row-groups of a column, one f64 atomic each
     __syncthreads();
-    float* red = Cs;   // [8][2][128]
+    float* red = Cs;   // [NR][2][128]
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       red[(r0 * 2 + 0) * 128 + c4 + e] = csum[e];
@@ -547,7 +679,7 @@ __global__ __launch_bounds__(NTHREADS, RAGGED ? 1 : 2) void gemm_kernel(GemmP P)
     if (tid < 128 && n0 + tid < N) {
       float a = 0.f, b = 0.f;
 #pragma unroll
-      for (int g = 0; g < 8; ++g) {
+      for (int g = 0; g < NR; ++g) {
         a += red[(g * 2 + 0) * 128 + tid];
         b += red[(g * 2 + 1) * 128 + tid];
       }
@@ -572,11 +704,23 @@ template <> struct LayoutArgs<L_TN> { static constexpr bool ATR = true, BTR = fa
 template <> struct LayoutArgs<L_TT> { static constexpr bool ATR = true, BTR = true; static constexpr int AC = CONV_NONE, BC = CONV_NONE; };
 template <> struct LayoutArgs<L_TT_KCONV> { static constexpr bool ATR = true, BTR = true; static constexpr int AC = CONV_NONE, BC = CONV_KSHIFT; };
 
-template <typename T, Layout LY, bool RAGGED, uint32_t EPI>
+template <typename T, Layout LY, bool RAGGED, uint32_t EPI, int BMT>
 inline void launch_kernel(const GemmP& P, hipStream_t s) {
   using LA = LayoutArgs<LY>;
-  hipLaunchKernelGGL((gemm_kernel<T, LA::ATR, LA::BTR, LA::AC, LA::BC, RAGGED, EPI>), dim3(P.nblocks, P.splits),
-                     dim3(NTHREADS), 0, s, P);
+  hipLaunchKernelGGL((gemm_kernel<T, LA::ATR, LA::BTR, LA::AC, LA::BC, RAGGED, EPI, BMT>), dim3(P.nblocks, P.splits),
+                     dim3(Cfg<BMT>::NTH), 0, s, P);
+}
+
+// non-ragged launch with the tile the host chose (P.bm: 256-row tiles for bf16 launches that fill the chip)
+template <typename T, Layout LY, uint32_t EPI>
+inline void launch_tiled(const GemmP& P, hipStream_t s) {
+  if constexpr (sizeof(T) == 2) {
+    if (P.bm == 256) {
+      launch_kernel<T, LY, false, EPI, 256>(P, s);
+      return;
+    }
+  }
+  launch_kernel<T, LY, false, EPI, 128>(P, s);
 }
 
 // Specialised-epilogue launchers (gemm_fast_fwd.hip, gemm_fast_bwd.hip): return false when (dtype, layout,
@@ -585,6 +729,6 @@ bool launch_fast_fwd(const GemmP& P, hipStream_t s, bool is_bf16, Layout ly, uin
 bool launch_fast_bwd(const GemmP& P, hipStream_t s, bool is_bf16, Layout ly, uint32_t code);
 
 #define AW_FAST_CASE(T, LY, CODE) \
-  case (CODE): launch_kernel<T, LY, false, (CODE)>(P, s); return true;
+  case (CODE): launch_tiled<T, LY, (CODE)>(P, s); return true;
 
 }  // namespace awg
