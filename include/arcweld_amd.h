@@ -42,7 +42,7 @@ int aw_version(void);
  *                  zero where the shifted row leaves its window;
  *   conv_operand = 1 (B, b_trans = 1): N = 3*conv_cin, B[k][j*cin+i] = src[(k + (j-1))*ldb + i], same mask.
  * Epilogue, per element (row r, col c), in this order:
- *   v = alpha*acc;  v += bias[c] (bias[c % bias_mod] if bias_mod > 0);  v *= act'(pre[r*ld_pre + c]);  v *= dropout(drop_seed, r*N+c, drop_p);
+ *   v = alpha*acc;  v += bias[c] (bias[c % bias_mod] if bias_mod > 0);  v *= act'(pre[r*ld_pre + c]) (pre f32/bf16);  v *= dropout(drop_seed, r*N+c, drop_p);
  *   v += resid[r*ld_resid + c];  v += beta * C_old (C must be f32 when beta != 0);  C[r*ldc + c] = v (c_dtype)
  *   C2 (c2_mode): 1 = act(v), 2 = v, 3 = v * dropout(drop2_seed, r*N+c, drop2_p); stored as c2_dtype
  *   colstats (f64, 2*stats_mod): += v and v*v into slot (c % stats_mod)      (BatchNorm batch statistics)
@@ -74,6 +74,8 @@ typedef struct {
   /* seed_ptr != NULL: the dropout seeds become mix(drop_seed, *seed_ptr) and mix(drop2_seed, *seed_ptr), with
    * *seed_ptr read on the device (a per-step counter, so one captured HIP graph replays with fresh masks). */
   const uint64_t* seed_ptr;
+  /* dtype of `pre` (AW_F32 or AW_BF16): bf16-mode forwards keep the GELU pre-activations in the operand dtype */
+  int pre_dtype;
 } aw_gemm_args;
 
 int aw_gemm(const aw_gemm_args* args, void* stream);

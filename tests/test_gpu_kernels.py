@@ -263,3 +263,21 @@ def test_gemm_grouped_weight_grads_match_single_launches(K, tile, dtype, conv):
         assert Wg.abs().sum() > 0
         torch.testing.assert_close(Wg.cpu(), Ws.cpu(), rtol=rtol, atol=atol * 10)
         torch.testing.assert_close(bg.cpu(), bs.cpu(), rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.parametrize("act", [0, 1])
+def test_gemm_bf16_pre_activation_operand(K, tile, act):
+    """pre (the saved GELU pre-activation) may be bf16: identical to passing the same values as f32."""
+    M, N, Kd = 256, 256, 128
+    A = _rand((M, Kd), 50, torch.bfloat16)
+    W = _rand((N, Kd), 51, torch.bfloat16, 0.1)
+    pre = _rand((M, N), 52).to(torch.bfloat16)
+    resid = _rand((M, N), 53)
+    act_code = K.AW_ACT_GELU_TANH if act else K.AW_ACT_GELU_ERF
+    outs = []
+    for p in (pre, pre.float()):
+        C = torch.empty(M, N, device=DEV)
+        C2 = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+        K.gemm(A, W, M, N, Kd, b_trans=False, act=act_code, pre=p, resid=resid, C=C, C2=C2, c2_mode=2)
+        outs.append((C.cpu(), C2.cpu()))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])

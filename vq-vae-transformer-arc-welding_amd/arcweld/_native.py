@@ -45,6 +45,7 @@ class GemmArgs(ctypes.Structure):
         ("bias_mod", c_int),
         ("accumulate", c_int), ("col_mod", c_int), ("col_mul", c_int), ("col_off", c_int),
         ("seed_ptr", c_p),
+        ("pre_dtype", c_int),
     ]
 
 

@@ -101,7 +101,7 @@ def forward(m, ids, generate: bool, training: bool, need_backward: bool, seed: i
                seed_ptr=sv.ctr)
         a2, mu2, rs2 = e(R, d, dt=T_), e(R), e(R)
         K.layernorm_fwd(x1, blk.ln_2.weight, blk.ln_2.bias, blk.ln_2.eps, a2, mu2, rs2)
-        h, g = e(R, 4 * d), e(R, 4 * d, dt=T_)
+        h, g = e(R, 4 * d, dt=T_), e(R, 4 * d, dt=T_)   # pre-activation in the operand dtype
         K.gemm(a2, Wfc, R, 4 * d, d, bias=mlp.c_fc.bias, act=K.AW_ACT_GELU_TANH, C=h, C2=g, c2_mode=1)
         x2 = e(R, d)
         K.gemm(g, Wp, R, d, 4 * d, bias=mlp.c_proj.bias, drop=(p_drop, sv.seed_mlp[i]), resid=x1, C=x2,

@@ -58,6 +58,10 @@ def _gemm_args(A, B, M, N, K, *, a_trans=False, b_trans=False, conv=None, alpha=
     a.bias = ptr(bias)
     a.act = int(act)
     a.pre, a.ld_pre = ptr(pre), _ld(pre)
+    if pre is not None:
+        if pre.dtype not in (torch.float32, torch.bfloat16):
+            raise nat.NativeError("pre must be float32 or bfloat16")
+        a.pre_dtype = dtype_code(pre.dtype)
     a.resid, a.ld_resid = ptr(resid), _ld(resid)
     a.drop_p, a.drop_seed = float(drop[0]), int(drop[1]) & 0xFFFFFFFFFFFFFFFF
     if C is not None:

@@ -132,7 +132,7 @@ def forward(m, x, training: bool, need_backward: bool, dtype=None, seed: int = 0
     # ---- encoder ResBlocks (per-token: centre taps)
     xs, a0s, hs, a1s = [x0], [a0], [], []
     for r, (c1, c2) in enumerate(pr["enc"]):
-        h, a1 = e(N, H), e(N, H, dt=T)
+        h, a1 = e(N, H, dt=T), e(N, H, dt=T)   # pre-activation kept in the operand dtype
         K.gemm(a0s[r], enc_w[r][0], N, H, H, bias=c1.bias, C=h, C2=a1, c2_mode=1)
         if r < R - 1:
             xn, an = e(N, H), e(N, H, dt=T)
@@ -170,7 +170,7 @@ def forward(m, x, training: bool, need_backward: bool, dtype=None, seed: int = 0
     conv = (H, S, 1, 0)
     ys, ya0s, dhs, da1s = [y0], [ya0], [], []
     for r, (c1, c2) in enumerate(pr["dec"]):
-        h, a1 = e(N, H), e(N, H, dt=T)
+        h, a1 = e(N, H, dt=T), e(N, H, dt=T)   # pre-activation kept in the operand dtype
         K.gemm(ya0s[r], dec_w[r][0], N, H, 3 * H, conv=conv, bias=c1.bias, C=h, C2=a1, c2_mode=1)
         if r < R - 1:
             yn, an = e(N, H), e(N, H, dt=T)
@@ -240,7 +240,7 @@ def encode(m, x, dtype=F32):
     K.weight_relayout_batch([jb for r, (c1, c2) in enumerate(pr["enc"])
                              for jb in ((c1.weight, H, H, 3, 1, 0, ew[r][0]), (c2.weight, H, H, 3, 1, 0, ew[r][1]))]
                             + [(pr["sep"].weight, D, H, 1, 0, 0, Ws)])
-    h, a1 = e(N, H), e(N, H, dt=T)
+    h, a1 = e(N, H, dt=T), e(N, H, dt=T)   # pre-activation kept in the operand dtype
     for r, (c1, c2) in enumerate(pr["enc"]):
         w1, w2 = ew[r]
         K.gemm(a, w1, N, H, H, bias=c1.bias, C=h, C2=a1, c2_mode=1)

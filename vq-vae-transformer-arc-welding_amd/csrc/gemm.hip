@@ -30,7 +30,7 @@ uint32_t epi_code(const aw_gemm_args& a, const GemmP& P, bool ragged) {
   uint32_t c = 0;
   if (a.bias) c |= EP_BIAS;
   if (a.bias && a.bias_mod > 0) c |= EP_BIASMOD;
-  if (a.pre) c |= EP_PRE;
+  if (a.pre) c |= EP_PRE | (a.pre_dtype == AW_BF16 ? EP_PREBF : 0u);
   if ((a.pre || a.c2_mode == 1) && a.act == AW_ACT_GELU_TANH) c |= EP_TANH;
   if (a.drop_p > 0.f) c |= EP_DROP;
   if (a.resid) c |= EP_RESID;
@@ -121,6 +121,7 @@ static int validate(const aw_gemm_args& a) {
   AW_REQUIRE(!(a.beta != 0.f && a.c_dtype != AW_F32), "aw_gemm: beta != 0 needs an f32 C");
   AW_REQUIRE(!(a.c2_mode && !a.C2), "aw_gemm: c2_mode without C2");
   AW_REQUIRE(!(a.colstats && a.stats_mod <= 0), "aw_gemm: colstats needs stats_mod > 0");
+  AW_REQUIRE(a.pre_dtype == AW_F32 || a.pre_dtype == AW_BF16, "aw_gemm: bad pre_dtype %d", a.pre_dtype);
   const bool plain = !a.bias && !a.pre && !a.resid && a.drop_p <= 0.f && !a.C2 && !a.colstats && a.C &&
                      a.c_dtype == AW_F32 && (a.beta == 0.f || a.beta == 1.f || a.accumulate);
   AW_REQUIRE(!a.accumulate || plain, "aw_gemm: accumulate mode allows no other epilogue field (f32 C only)");
@@ -172,7 +173,7 @@ static void plan(const aw_gemm_args& a, int ngroups, bool grouped, GemmP& P) {
   auto al = [](const void* ptr, int64_t ld, int dt) {
     return ptr == nullptr || (((uintptr_t)ptr % 16) == 0 && (ld * (dt == AW_BF16 ? 2 : 4)) % 16 == 0);
   };
-  P.vec = al(a.C, a.ldc, a.c_dtype) && al(a.C2, a.ldc2, a.c2_dtype) && al(a.pre, a.ld_pre, AW_F32) &&
+  P.vec = al(a.C, a.ldc, a.c_dtype) && al(a.C2, a.ldc2, a.c2_dtype) && al(a.pre, a.ld_pre, a.pre_dtype) &&
           al(a.resid, a.ld_resid, AW_F32);
   const int64_t es = a.a_dtype == AW_BF16 ? 2 : 4;
   const int64_t ka = a.K > 0 ? a.K : 1;

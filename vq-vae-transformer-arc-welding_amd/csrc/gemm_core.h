@@ -82,7 +82,7 @@ enum EpiBits : uint32_t {
   EP_BIAS = 1u << 0, EP_BIASMOD = 1u << 1, EP_PRE = 1u << 2, EP_TANH = 1u << 3, EP_DROP = 1u << 4,
   EP_RESID = 1u << 5, EP_BETA = 1u << 6, EP_C = 1u << 7, EP_CBF = 1u << 8, EP_C2ACT = 1u << 9,
   EP_C2COPY = 1u << 10, EP_C2DROP = 1u << 11, EP_C2BF = 1u << 12, EP_STATS = 1u << 13, EP_ACCUM = 1u << 14,
-  EP_GENERIC = 1u << 31
+  EP_PREBF = 1u << 15, EP_GENERIC = 1u << 31
 };
 
 // Diagnostic phase stamps (tools/probe only: defined there before this file is included; never in the library).
@@ -571,6 +571,7 @@ __global__ __launch_bounds__(Cfg<BMT>::NTH, RAGGED ? 1 : Cfg<BMT>::MINB) void ge
   const bool f_bias = EPF(EP_BIAS, p.bias != nullptr);
   const bool f_bmod = EPF(EP_BIASMOD, p.bias_mod > 0);
   const bool f_pre = EPF(EP_PRE, p.pre != nullptr);
+  const bool f_prebf = EPF(EP_PREBF, p.pre_dtype == AW_BF16);
   const bool f_tanh = EPF(EP_TANH, p.act == AW_ACT_GELU_TANH);
   const bool f_drop = EPF(EP_DROP, p.drop_p > 0.f);
   const bool f_resid = EPF(EP_RESID, p.resid != nullptr);
@@ -603,7 +604,15 @@ __global__ __launch_bounds__(Cfg<BMT>::NTH, RAGGED ? 1 : Cfg<BMT>::MINB) void ge
         if (lr >= rows_here) break;
         const int64_t row = m0 + lr;
         if (vec) {
-          if (f_pre) pre4[u] = *reinterpret_cast<const float4*>(p.pre + row * p.ld_pre + col);
+          if (f_pre) {
+            if (f_prebf) {
+              const uint2 h = *reinterpret_cast<const uint2*>(reinterpret_cast<const bf16*>(p.pre) + row * p.ld_pre + col);
+              pre4[u] = make_float4(__uint_as_float(h.x << 16), __uint_as_float(h.x & 0xFFFF0000u),
+                                    __uint_as_float(h.y << 16), __uint_as_float(h.y & 0xFFFF0000u));
+            } else {
+              pre4[u] = *reinterpret_cast<const float4*>(p.pre + row * p.ld_pre + col);
+            }
+          }
           if (f_resid) res4[u] = *reinterpret_cast<const float4*>(p.resid + row * p.ld_resid + col);
           if (f_beta) old4[u] = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(Cptr) + row * p.ldc + col);
         } else if constexpr (GEN) {
@@ -611,7 +620,7 @@ __global__ __launch_bounds__(Cfg<BMT>::NTH, RAGGED ? 1 : Cfg<BMT>::MINB) void ge
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             if (col + e >= N) break;
-            if (f_pre) a[e] = p.pre[row * p.ld_pre + col + e];
+            if (f_pre) a[e] = load_as_f32(p.pre, p.pre_dtype, row * p.ld_pre + col + e);
             if (f_resid) b[e] = p.resid[row * p.ld_resid + col + e];
             if (f_beta) c[e] = reinterpret_cast<const float*>(Cptr)[row * p.ldc + col + e];
           }

@@ -8,6 +8,7 @@ namespace awg {
 
 #define AW_BWD_CONV_CODES(X, T, LY)                                         \
   X(T, LY, EP_PRE | EP_C | EP_CBF)                                          \
+  X(T, LY, EP_PRE | EP_PREBF | EP_C | EP_CBF)                               \
   X(T, LY, EP_PRE | EP_RESID | EP_C | EP_C2DROP | EP_C2BF)                  \
   X(T, LY, EP_PRE | EP_RESID | EP_C | EP_C2COPY | EP_C2BF)
 
@@ -16,7 +17,8 @@ namespace awg {
   X(T, LY, EP_C | EP_C2COPY | EP_C2BF)                                      \
   X(T, LY, EP_C)                                                            \
   X(T, LY, EP_C | EP_CBF)                                                   \
-  X(T, LY, EP_PRE | EP_TANH | EP_C | EP_CBF)
+  X(T, LY, EP_PRE | EP_TANH | EP_C | EP_CBF)                               \
+  X(T, LY, EP_PRE | EP_PREBF | EP_TANH | EP_C | EP_CBF)
 
 bool launch_fast_bwd(const GemmP& P, hipStream_t s, bool is_bf16, Layout ly, uint32_t code) {
   if (is_bf16 && ly == L_NT) {

@@ -10,6 +10,7 @@ namespace awg {
 
 #define AW_FWD_CODES(X, T, LY)                                              \
   X(T, LY, EP_BIAS | EP_C | EP_C2ACT | EP_C2BF)                             \
+  X(T, LY, EP_BIAS | EP_C | EP_CBF | EP_C2ACT | EP_C2BF)                    \
   X(T, LY, EP_BIAS | EP_DROP | EP_RESID | EP_C | EP_C2ACT | EP_C2BF)        \
   X(T, LY, EP_BIAS | EP_RESID | EP_C | EP_C2ACT | EP_C2BF)                  \
   X(T, LY, EP_BIAS | EP_DROP | EP_RESID | EP_C | EP_CBF)                    \
@@ -23,6 +24,7 @@ namespace awg {
   X(T, LY, EP_BIAS | EP_DROP | EP_RESID | EP_C)                             \
   X(T, LY, EP_BIAS | EP_RESID | EP_C)                                       \
   X(T, LY, EP_BIAS | EP_TANH | EP_C | EP_C2ACT | EP_C2BF)                   \
+  X(T, LY, EP_BIAS | EP_TANH | EP_C | EP_CBF | EP_C2ACT | EP_C2BF)          \
   X(T, LY, EP_C)                                                            \
   X(T, LY, EP_C | EP_CBF)
 
