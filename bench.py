@@ -45,6 +45,8 @@ def parse():
                     help="skip the secondary configs[2] line item (tokenize + 8-block Transformer train step)")
     ap.add_argument("--seqs", type=int, default=51, help="Transformer sequences per GPU per step (configs[2])")
     ap.add_argument("--n-cycles", type=int, default=20)
+    ap.add_argument("--gemm-tile", type=int, default=0, choices=[0, 128, 256],
+                    help="GEMM tile policy (aw_gemm_set_tile): 0 = automatic")
     return ap.parse_args()
 
 
@@ -174,8 +176,9 @@ def main():
     dev = torch.device("cuda", local)
     torch.set_float32_matmul_precision("medium")    # as train_reconstruction_embedding.py:253 -> bf16 MFMA
 
-    from arcweld import kernels
+    from arcweld import _native, kernels
     from arcweld.trainer import Trainer
+    _native.call("aw_gemm_set_tile", args.gemm_tile)
 
     model = build_model(dev)
     trainer = Trainer(gradient_clip_val=0.7)

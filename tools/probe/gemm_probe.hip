@@ -124,6 +124,28 @@ int main() {
              2.0 * 8 * Mw * Nw * Kw / us1 / 1e6);
     }
   }
+  // power-of-two row strides: transformer-like grouped wgrad M=2048 (A = [K][2048] bf16), N=512, K=16371, 8 groups
+  {
+    const int Mw = 2048, Nw = 512, Kw = 16371, G = 8;
+    for (int pad : {0, 64}) {
+      const int lda = Mw + pad, ldb = Nw + pad;
+      bf16 *Xa, *Xb; float* Wg; float* rows;
+      CK(hipMalloc(&Xa, (size_t)Kw * lda * 2 * G)); CK(hipMalloc(&Xb, (size_t)Kw * ldb * 2 * G));
+      CK(hipMalloc(&Wg, (size_t)G * Mw * Nw * 4)); CK(hipMalloc(&rows, (size_t)G * Mw * 4));
+      probe_fill<<<1024, 256>>>(Xa, (size_t)Kw * lda * G, 11); probe_fill<<<1024, 256>>>(Xb, (size_t)Kw * ldb * G, 12);
+      std::vector<aw_gemm_args> v(G);
+      for (int g = 0; g < G; ++g) {
+        aw_gemm_args& a = v[g]; memset(&a, 0, sizeof(a));
+        a.M = Mw; a.N = Nw; a.K = Kw; a.a_dtype = AW_BF16; a.alpha = 1.f; a.c_dtype = AW_F32; a.accumulate = 1;
+        a.A = Xa + (size_t)g * Kw * lda; a.lda = lda; a.a_trans = 1; a.B = Xb + (size_t)g * Kw * ldb; a.ldb = ldb; a.b_trans = 1;
+        a.C = Wg + (size_t)g * Mw * Nw; a.ldc = Nw; a.col_mul = 1; a.a_rowsum = rows + g * Mw;
+      }
+      float us = timeit([&] { aw_gemm_grouped(v.data(), G, 0); }, 10);
+      printf("transformer-like grouped wgrad x8 2048x512xK16371 lda pad %2d: %8.2f us (%.0f TF)\n", pad, us,
+             2.0 * G * Mw * Nw * Kw / us / 1e6);
+      CK(hipFree(Xa)); CK(hipFree(Xb)); CK(hipFree(Wg)); CK(hipFree(rows));
+    }
+  }
   // tile A/B (aw_gemm_set_tile): 128x128 two-stage vs 256x128 three-stage
   for (int bmv : {128, 256}) {
     aw_gemm_set_tile(bmv);

@@ -47,7 +47,8 @@ uint32_t epi_code(const aw_gemm_args& a, const GemmP& P, bool ragged) {
 template <typename T>
 void dispatch(const GemmP& P, hipStream_t s, bool ragged) {
   const Layout ly = layout_of(P.a);
-  const uint32_t code = epi_code(P.a, P, ragged);
+  uint32_t code = epi_code(P.a, P, ragged);
+  if (P.bm == 256 && code != EP_ACCUM) code = EP_GENERIC;   // specialised epilogues are compiled for 128-row tiles
   constexpr bool BF = sizeof(T) == 2;
   if (code == EP_ACCUM) {
     switch (ly) {
@@ -161,11 +162,11 @@ static bool plain_output(const aw_gemm_args& a) {
 }
 
 // Launch plan of ngroups problems of one shape: tile (128 or 256 rows), grid and split-K.
-//  * bf16 accumulate-mode (weight-gradient) launches with >= 120 tiles of 256x128 take the 256-row tile with its
-//    three-stage pipeline, one workgroup per CU, split over K in two (f32 atomics) below 240 tiles;
-//  * everything else runs 128x128 tiles, two workgroups per CU (measured equal or faster for the M = 16384,
-//    K = 512 .. 2048 forward / input-gradient shapes); plain f32 outputs that cannot fill the chip twice are
-//    split over K (slab workspace when the caller provides one, f32 atomics in grouped launches, <= 2 adders).
+//  * 128x128 tiles, two workgroups per CU (measured equal or faster than the 256x128 three-stage tile on every
+//    shape of the path: forward / input-gradient M = 16384, K = 512 .. 2048 and the grouped weight gradients);
+//    plain f32 outputs that cannot fill the chip twice are split over K (slab workspace when the caller provides
+//    one, f32 atomics in grouped launches, <= 2 adders);
+//  * aw_gemm_set_tile(256) forces the 256x128 tile (generic / accumulate epilogues) for eligible bf16 launches.
 static void plan(const aw_gemm_args& a, int ngroups, bool grouped, GemmP& P) {
   P.a = a;
   P.ngroups = ngroups;
@@ -188,13 +189,9 @@ static void plan(const aw_gemm_args& a, int ngroups, bool grouped, GemmP& P) {
   P.tiles_n = aw_cdiv(a.N, BN);
   const int t256 = aw_cdiv(a.M, 256) * P.tiles_n * ngroups;
   int bm = 128, splits = 1;
-  if (a.a_dtype == AW_BF16 && !is_ragged(a) && g_tile_override != 128) {
-    if (g_tile_override == 256) {
-      bm = 256;
-    } else if (a.accumulate && t256 >= 120 && a.K >= 24 * BK) {
-      bm = 256;                               // long-K weight gradients: the three-stage pipeline
-      if (t256 < 240) splits = 2;
-    }
+  if (a.a_dtype == AW_BF16 && !is_ragged(a) && g_tile_override == 256) {
+    bm = 256;
+    if (a.accumulate && t256 < 240 && a.K >= 24 * BK) splits = 2;
   }
   if (bm == 128) {
     const int nb = aw_cdiv(a.M, 128) * P.tiles_n * ngroups;

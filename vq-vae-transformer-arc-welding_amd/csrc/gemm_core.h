@@ -3,7 +3,8 @@
 // Two tile configurations (template BMT):
 //   BMT = 128: 128x128 tile, 256 threads (4 waves as 2x2), two LDS stages, two workgroups per CU;
 //   BMT = 256: 256x128 tile, 512 threads (8 waves as 4x2), three LDS stages (two K steps of loads in flight),
-//              one workgroup per CU -- launches whose tiles alone fill the chip (the host picks per launch).
+//              one workgroup per CU (aw_gemm_set_tile; measured slower than two 128-row workgroups per CU on every
+//              shape of this path, so the automatic policy does not pick it).
 // Every wave owns a 64x64 output block = 4x4 fragments of 16x16.  K is staged 128 bytes per operand row per step
 // (64 bf16 / 32 f32).  Operands reach LDS by LDS-DMA (gfx950 `buffer_load ... lds`): the image swizzle is applied
 // to the source address, out-of-range offsets implement every mask (M/N/K tails, implicit-conv window edges).
@@ -22,6 +23,10 @@
 // A fragments in registers.
 #pragma once
 #include "common.h"
+
+// The LDS-DMA inline asm writes M0 (declared as clobbered).  No compiler-generated code in these kernels uses M0
+// (checked in the ISA: every M0 write is this asm's), so the "reserved register" warning is silenced here.
+#pragma clang diagnostic ignored "-Winline-asm"
 
 namespace awg {
 
@@ -720,10 +725,11 @@ inline void launch_kernel(const GemmP& P, hipStream_t s) {
                      dim3(Cfg<BMT>::NTH), 0, s, P);
 }
 
-// non-ragged launch with the tile the host chose (P.bm: 256-row tiles for bf16 launches that fill the chip)
+// non-ragged launch with the tile the host chose (P.bm; the 256-row tile exists for the generic and accumulate
+// epilogues only -- the host issues specialised codes with 128-row tiles)
 template <typename T, Layout LY, uint32_t EPI>
 inline void launch_tiled(const GemmP& P, hipStream_t s) {
-  if constexpr (sizeof(T) == 2) {
+  if constexpr (sizeof(T) == 2 && (EPI == EP_GENERIC || EPI == EP_ACCUM)) {
     if (P.bm == 256) {
       launch_kernel<T, LY, false, EPI, 256>(P, s);
       return;
