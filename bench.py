@@ -128,6 +128,20 @@ def transformer_workload(dev, rank, world, args):
             "transformer_tflops": round(flops_seq * args.seqs * world * args.steps / el / 1e12, 2)}
 
 
+def gemm_traffic():
+    """HBM bytes per launch of the GEMM family from the committed rocprofv3 PMC passes (FETCH_SIZE and WRITE_SIZE in
+    separate runs, FETCH_SIZE doubled on gfx950; tools/pmc_traffic.py) of this same workload: counters cannot be
+    read from inside the timed run."""
+    import glob
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*", "*", "pmc_gemm_traffic.json")) +
+                   glob.glob(os.path.join(REPO, "profiles", "*", "pmc_gemm_traffic.json")))
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        d = json.load(f)
+    return round(d["avg_bytes_per_launch"]), os.path.relpath(files[-1], REPO)
+
+
 def cpu_baseline(seconds):
     """Oracle port (oracle/vqvae.py, torch CPU fp32, all host threads) on a bounded sample of the same workload:
     full-size model, B=32 windows per step, fwd+bwd+RAdam; windows/s."""
@@ -235,13 +249,15 @@ def main():
     value = world * args.batch * args.steps / elapsed
 
     roofline = None
+    traffic, traffic_src = gemm_traffic()
     if prof:
         ms = sum(e0.elapsed_time(e1) for e0, e1, _ in prof)
         flops = sum(f for _, _, f in prof)
         n = len(prof)
         achieved = flops / (ms * 1e-3) / 1e12
         roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
-                    "frac": round(achieved / BF16_PEAK_TFLOPS, 4), "traffic": None,
+                    "frac": round(achieved / BF16_PEAK_TFLOPS, 4), "traffic": traffic, "traffic_unit": "bytes/launch",
+                    "traffic_source": traffic_src,
                     "kernel": "gemm_kernel<bf16> (aw_gemm)", "launches_per_step": n // prof_steps,
                     "avg_launch_us": round(ms * 1e3 / n, 2), "avg_algorithmic_gflop_per_launch": round(flops / n / 1e9, 4),
                     "gemm_ms_per_step": round(ms / prof_steps, 3),
