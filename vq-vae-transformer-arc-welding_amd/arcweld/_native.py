@@ -12,7 +12,8 @@ import os
 import torch  # noqa: F401  (must precede the library load, see module docstring)
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_DIR, "lib", "libarcweld_amd.so")
+# ARCWELD_LIB overrides the library path (A/B timing of two builds in one process tree: tools/ab_bench.sh)
+LIB_PATH = os.environ.get("ARCWELD_LIB") or os.path.join(PKG_DIR, "lib", "libarcweld_amd.so")
 HEADER = os.path.join(os.path.dirname(PKG_DIR), "include", "arcweld_amd.h")
 
 AW_F32, AW_BF16 = 0, 1

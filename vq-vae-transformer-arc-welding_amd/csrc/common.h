@@ -36,16 +36,43 @@ __device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + e
 __device__ __forceinline__ float gelu_erf_grad(float x) {
   return 0.5f * (1.0f + erff(x * AW_INV_SQRT2)) + x * AW_INV_SQRT2PI * __expf(-0.5f * x * x);
 }
+// Branch-free GELU(erf) for the bf16-operand paths and the un-patch head: erfc by the Chebyshev fit of Numerical
+// Recipes 6.2 (fractional error < 1.2e-7 everywhere), Phi(x) = erfc(-x/sqrt 2)/2 evaluated without cancellation
+// for x < 0; ~16 VALU ops against ~50 (with divergence) for erff.  The exact-f32 (parity / tokenization) GEMMs keep
+// erff so that the codebook indices stay bit-exact.
+__device__ __forceinline__ float aw_erfc_nr(float z) {   // z >= 0
+  const float t = __builtin_amdgcn_rcpf(1.0f + 0.5f * z);      // v_rcp_f32 (1 ulp), not the IEEE division
+  float p = 0.17087277f;
+  p = fmaf(p, t, -0.82215223f);
+  p = fmaf(p, t, 1.48851587f);
+  p = fmaf(p, t, -1.13520398f);
+  p = fmaf(p, t, 0.27886807f);
+  p = fmaf(p, t, -0.18628806f);
+  p = fmaf(p, t, 0.09678418f);
+  p = fmaf(p, t, 0.37409196f);
+  p = fmaf(p, t, 1.00002368f);
+  p = fmaf(p, t, -1.26551223f);
+  return t * __expf(fmaf(-z, z, p));
+}
+__device__ __forceinline__ float aw_phi_cdf(float x) {    // P(N(0,1) <= x) = 0.5 * (1 + erf(x / sqrt 2))
+  const float r = 0.5f * aw_erfc_nr(fabsf(x) * AW_INV_SQRT2);
+  return x >= 0.f ? 1.0f - r : r;
+}
+__device__ __forceinline__ float gelu_erf_fast(float x) { return x * aw_phi_cdf(x); }
+__device__ __forceinline__ float gelu_erf_grad_fast(float x) {
+  return aw_phi_cdf(x) + x * AW_INV_SQRT2PI * __expf(-0.5f * x * x);
+}
+
 // GELU tanh form (model/transformer_block.py:8-15): 0.5*x*(1 + tanh(u)) == x * sigmoid(2u), u = sqrt(2/pi)(x +
 // 0.044715 x^3) -- one exp and one division instead of tanhf (same value to fp32 rounding).
 #define AW_SQRT_2_OVER_PI 0.79788456080286535588f
 __device__ __forceinline__ float gelu_tanh(float x) {
   const float u = AW_SQRT_2_OVER_PI * (x + 0.044715f * x * x * x);
-  return x / (1.0f + __expf(-2.0f * u));
+  return x * __builtin_amdgcn_rcpf(1.0f + __expf(-2.0f * u));
 }
 __device__ __forceinline__ float gelu_tanh_grad(float x) {
   const float u = AW_SQRT_2_OVER_PI * (x + 0.044715f * x * x * x);
-  const float s = 1.0f / (1.0f + __expf(-2.0f * u));          // = 0.5 * (1 + tanh(u))
+  const float s = __builtin_amdgcn_rcpf(1.0f + __expf(-2.0f * u));   // = 0.5 * (1 + tanh(u))
   const float du = AW_SQRT_2_OVER_PI * (1.0f + 3.0f * 0.044715f * x * x);
   return s + 2.0f * x * s * (1.0f - s) * du;
 }

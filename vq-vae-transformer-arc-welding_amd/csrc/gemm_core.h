@@ -587,6 +587,7 @@ __global__ __launch_bounds__(Cfg<BMT>::NTH, RAGGED ? 1 : Cfg<BMT>::MINB) void ge
   const bool f_c2bf = EPF(EP_C2BF, p.c2_dtype == AW_BF16);
   const bool f_stats = EPF(EP_STATS, p.colstats != nullptr);
   const float alpha = GEN ? p.alpha : 1.f;       // specialised codes are issued for alpha == 1 only
+  constexpr bool FASTGELU = sizeof(T) == 2;      // bf16 operands: branch-free erf (exact-f32 mode keeps erff)
   const uint64_t dseed = f_drop ? aw_seed_mix(p.drop_seed, p.seed_ptr) : 0ull;
   const uint64_t dseed2 = c2m == 3 ? aw_seed_mix(p.drop2_seed, p.seed_ptr) : 0ull;
   // thread -> 4 consecutive columns (c4) x rows r0, r0+NR, ...; 4 rows of loads in flight per thread
@@ -652,13 +653,13 @@ __global__ __launch_bounds__(Cfg<BMT>::NTH, RAGGED ? 1 : Cfg<BMT>::MINB) void ge
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           float x = alpha * av[e] + bias[e];
-          if (f_pre) x *= f_tanh ? gelu_tanh_grad(pv[e]) : gelu_erf_grad(pv[e]);
+          if (f_pre) x *= f_tanh ? gelu_tanh_grad(pv[e]) : (FASTGELU ? gelu_erf_grad_fast(pv[e]) : gelu_erf_grad(pv[e]));
           if (f_drop) x *= ds[e];
           if (f_resid) x += rv[e];
           if (f_beta) x += p.beta * ov[e];
           v[e] = x;
           float y = x;
-          if (c2m == 1) y = f_tanh ? gelu_tanh(x) : gelu_erf(x);
+          if (c2m == 1) y = f_tanh ? gelu_tanh(x) : (FASTGELU ? gelu_erf_fast(x) : gelu_erf(x));
           else if (c2m == 3) y = x * ds2[e];
           w[e] = y;
           if (f_stats && col + e < N) {

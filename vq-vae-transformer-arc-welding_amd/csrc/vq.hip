@@ -68,7 +68,35 @@ __global__ __launch_bounds__(VQ_THREADS) void vq_fwd_kernel(const float* __restr
     __syncthreads();
     const int per = (kt + 3) / 4;
     const int kb = wid * per, ke = min(kt, kb + per);
-    for (int k = kb; k < ke; ++k) {
+    // four codes per iteration: four independent in-order fmaf chains (each chain is the reference's dot
+    // product bit for bit; the chains only interleave to hide the fma latency), compared in code order
+    int k = kb;
+    constexpr int NC = D <= 64 ? 4 : 1;   // wide embeddings: the row itself fills the register file
+    for (; NC == 4 && k + 4 <= ke; k += 4) {
+      const float4* e0 = reinterpret_cast<const float4*>(Es + k * D);
+      float dt[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int q = 0; q < D / 4; ++q) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const float4 e = e0[c * (D / 4) + q];
+          dt[c] = fmaf(zr[4 * q + 0], e.x, dt[c]);
+          dt[c] = fmaf(zr[4 * q + 1], e.y, dt[c]);
+          dt[c] = fmaf(zr[4 * q + 2], e.z, dt[c]);
+          dt[c] = fmaf(zr[4 * q + 3], e.w, dt[c]);
+        }
+      }
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const float dist = __fsub_rn(__fadd_rn(zz, ee[k + c]), __fmul_rn(2.f, dt[c]));
+        const int gk = t0 + k + c;
+        if (dist < best || (dist == best && gk < bestk)) {
+          best = dist;
+          bestk = gk;
+        }
+      }
+    }
+    for (; k < ke; ++k) {
       const float4* e4 = reinterpret_cast<const float4*>(Es + k * D);
       float dot = 0.f;
 #pragma unroll

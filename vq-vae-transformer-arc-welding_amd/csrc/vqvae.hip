@@ -230,7 +230,7 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(const float* __restrict__
       const float vv[4] = {v[s].x, v[s].y, v[s].z, v[s].w};
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const float a = gelu_erf((vv[e] - hp.mean[s][e]) * hp.inv[s][e] * hp.gam[s][e] + hp.bet[s][e]);
+        const float a = gelu_erf_fast((vv[e] - hp.mean[s][e]) * hp.inv[s][e] * hp.gam[s][e] + hp.bet[s][e]);
 #pragma unroll
         for (int j = 0; j < 5; ++j) part[j] = fmaf(a, hp.w[s][e][j], part[j]);
       }
@@ -287,14 +287,14 @@ __global__ __launch_bounds__(256) void head_bwd1_kernel(const float* __restrict_
       for (int e = 0; e < 4; ++e) {
         const float xn = (vv[e] - hp.mean[s][e]) * hp.inv[s][e];
         const float bn = xn * hp.gam[s][e] + hp.bet[s][e];
-        const float a = gelu_erf(bn);
+        const float a = gelu_erf_fast(bn);
         float ga = 0.f;
 #pragma unroll
         for (int j = 0; j < 5; ++j) {
           ga = fmaf(go[j], hp.w[s][e][j], ga);
           accw[s][e][j] = fmaf(a, go[j], accw[s][e][j]);
         }
-        const float gbn = ga * gelu_erf_grad(bn);
+        const float gbn = ga * gelu_erf_grad_fast(bn);
         accg[s][e] += gbn;
         accgx[s][e] = fmaf(gbn, xn, accgx[s][e]);
       }
@@ -370,7 +370,7 @@ __global__ __launch_bounds__(256) void head_bwd2_kernel(const float* __restrict_
         float ga = 0.f;
 #pragma unroll
         for (int j = 0; j < 5; ++j) ga = fmaf(go[j], hp.w[s][e][j], ga);
-        const float gbn = ga * gelu_erf_grad(bn);
+        const float gbn = ga * gelu_erf_grad_fast(bn);
         const float g = hp.gam[s][e] * hp.inv[s][e] * (gbn - sg[s][e] - xn * sgx[s][e]);
         accd[s][e] += g;
         g4[e] = g;
