@@ -7,6 +7,7 @@
 #include "../../vq-vae-transformer-arc-welding_amd/csrc/gemm_fast_fwd.hip"
 #include "../../vq-vae-transformer-arc-welding_amd/csrc/gemm_fast_bwd.hip"
 #include <vector>
+#include <string.h>
 #include <algorithm>
 
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP %s @%d\n", hipGetErrorString(e_), __LINE__); exit(1);} } while (0)
@@ -48,13 +49,27 @@ template <typename F> float timeit(F f, int reps = 50) {
   return ms * 1000.f / reps;
 }
 
-int main() {
+int main(int argc, char** argv) {
   const int M = 16384, N = 512, Kmax = 2048;
+  const bool only_conv = argc > 1 && strcmp(argv[1], "conv") == 0;
   bf16 *A, *B; float* C; bf16* Cb;
   CK(hipMalloc(&A, (size_t)M * Kmax * 2)); CK(hipMalloc(&B, (size_t)N * Kmax * 2));
   CK(hipMalloc(&C, (size_t)M * N * 4)); CK(hipMalloc(&Cb, (size_t)M * N * 2));
   probe_fill<<<1024, 256>>>(A, (size_t)M * Kmax, 1); probe_fill<<<1024, 256>>>(B, (size_t)N * Kmax, 2);
   const int tiles = (M / 128) * (N / 128);
+  if (only_conv) {   // PMC target: the decoder forward conv GEMM (K = 3 x 512, bias + GELU operand epilogue)
+    bf16* C2; float* bias;
+    CK(hipMalloc(&C2, (size_t)M * N * 2)); CK(hipMalloc(&bias, N * 4)); CK(hipMemset(bias, 0, N * 4));
+    aw_gemm_args a; memset(&a, 0, sizeof(a));
+    a.M = M; a.N = N; a.K = 3 * 512; a.a_dtype = AW_BF16; a.A = A; a.lda = 512; a.B = B; a.ldb = 3 * 512;
+    a.conv_cin = 512; a.conv_seg = 16; a.conv_dir = 1; a.conv_operand = 0;
+    a.alpha = 1.f; a.C = Cb; a.ldc = N; a.c_dtype = AW_BF16; a.col_mul = 1; a.bias = bias;
+    a.C2 = C2; a.ldc2 = N; a.c2_dtype = AW_BF16; a.c2_mode = 1;
+    printf("conv fwd K1536 bias + C bf16 + C2 gelu bf16: %.2f us\n", timeit([&] { aw_gemm(&a, 0); }, 50));
+    a.C2 = nullptr; a.c2_mode = 0; a.bias = nullptr;
+    printf("conv fwd K1536 C bf16 only: %.2f us\n", timeit([&] { aw_gemm(&a, 0); }, 50));
+    return 0;
+  }
   printf("empty kernel (512 blocks, 66 KiB LDS)     %8.2f us\n", timeit([&] { probe_empty<<<tiles, 256>>>(C); }));
   printf("store-only 128x128 f32 tiles (32 MiB)      %8.2f us\n", timeit([&] { probe_store<<<tiles, 256>>>(C, N, N / 128); }));
   for (int K : {64, 512, 2048}) {

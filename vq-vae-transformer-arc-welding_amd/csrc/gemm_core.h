@@ -239,24 +239,59 @@ struct Stager {
   // Issued from inline asm so that the compiler does not see an LDS write it cannot disambiguate from the ds_reads
   // of the other stages (it would drain vmcnt to 0 before every compute step and serialise the pipeline); the
   // kernel orders the DMA itself with counted vmcnt waits and barriers.
-  __device__ __forceinline__ void dma(int k0, int tid, char* img) {
-    const int jrow = (CONV == CONV_ROWSHIFT) ? k0 / cin : 0;
+  // Everything that does not depend on the K step is computed once (dma_init): per step a chunk costs one add,
+  // a few compares and a select; the step-dependent parts (tap shift, k0 * ld) are wave-uniform scalars.
+  int doff[NCH];    // source byte offset of the chunk at K step 0 (tap-independent part)
+  int dpos[NCH];    // logical k (K-contiguous image) or k-row (row-contiguous image) of the chunk within a step
+  bool rok[NCH];    // the chunk's row (K-contiguous) / column block (row-contiguous) lies inside the operand
+  uint32_t lds0;    // LDS byte address of this wave's first chunk in stage 0
+
+  __device__ __forceinline__ void dma_init(int tid, uint32_t img_lds) {
+    lds0 = img_lds + __builtin_amdgcn_readfirstlane((uint32_t)(tid & ~63)) * 16u;
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
       const int c = tid + i * NTH;
-      bool ok;
-      int64_t e;
       if constexpr (!TR) {
         const int r = c / CPK;
         const int lc = (c % CPK) ^ ((r >> 1) & 7);
-        e = src_nt(i, jrow, row0 + r, k0 + lc * EPC, ok);
+        const int row = row0 + r;
+        rok[i] = row < rows_total;
+        dpos[i] = lc * EPC;
+        doff[i] = rok[i] ? (int)(((int64_t)row * ld + lc * EPC) * (int)sizeof(T)) : 0;
       } else {
-        e = src_tr(i, k0 + c / CPR, row0 + tr_logical_m(c, true), ok);
+        const int kr = c / CPR;
+        const int m = row0 + tr_logical_m(c, true);
+        rok[i] = m < rows_total;
+        dpos[i] = kr;
+        if constexpr (CONV == CONV_KSHIFT)
+          doff[i] = (int)(((int64_t)(kr + tapoff[i]) * ld + colin[i]) * (int)sizeof(T));
+        else
+          doff[i] = rok[i] ? (int)(((int64_t)kr * ld + m) * (int)sizeof(T)) : 0;
       }
-      const int off = ok ? (int)(e * (int)sizeof(T)) : OOB;
-      char* dst = img + ((tid & ~63) + i * NTH) * 16;    // wave-uniform base of this wave instruction
-      const uint32_t m0 = __builtin_amdgcn_readfirstlane(
-          (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)dst);
+    }
+  }
+
+  __device__ __forceinline__ void dma(int k0, uint32_t stage_off) {
+    int delta;
+    int sft = 0;
+    if constexpr (!TR) {
+      const int jrow = (CONV == CONV_ROWSHIFT) ? k0 / cin : 0;   // tap of this step (cin % BK == 0)
+      sft = (CONV == CONV_ROWSHIFT) ? dir * (jrow - 1) : 0;
+      delta = (int)(((int64_t)sft * ld + (k0 - jrow * cin)) * (int)sizeof(T));
+    } else {
+      delta = (int)((int64_t)k0 * ld * (int)sizeof(T));
+    }
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      bool ok = rok[i] & (k0 + dpos[i] < kend);
+      if constexpr (CONV == CONV_ROWSHIFT) ok = ok & ((unsigned)(wpos[i] + sft) < (unsigned)seg);
+      if constexpr (CONV == CONV_KSHIFT) {
+        ok = ok & ((unsigned)(wpos[i] + tapoff[i]) < (unsigned)seg);
+        wpos[i] += BK % seg;                 // advance the window position to the next K step
+        if (wpos[i] >= seg) wpos[i] -= seg;
+      }
+      const int off = ok ? doff[i] + delta : OOB;
+      const uint32_t m0 = lds0 + stage_off + (uint32_t)(i * NTH * 16);
       asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" ::"s"(m0), "v"(off), "s"(desc)
                    : "memory", "m0");
     }
@@ -396,6 +431,11 @@ __global__ __launch_bounds__(Cfg<BMT>::NTH, RAGGED ? 1 : Cfg<BMT>::MINB) void ge
   constexpr bool use_dma = !RAGGED;
   sa.init(kbeg, tid, P.a_bytes, use_dma);
   sb.init(kbeg, tid, P.b_bytes, use_dma);
+  if constexpr (use_dma) {
+    const uint32_t smem_lds = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
+    sa.dma_init(tid, smem_lds);
+    sb.dma_init(tid, smem_lds + A_IMG);
+  }
   const bool do_rowsum = rowptr != nullptr && tn == 0;
 
   f32x4 acc[4][4];
@@ -434,17 +474,17 @@ __global__ __launch_bounds__(Cfg<BMT>::NTH, RAGGED ? 1 : Cfg<BMT>::MINB) void ge
     // two stages: the loads of step t+1 fly into the other stage while step t computes
     char* L0 = smem;
     char* L1 = smem + STAGE;
-    sa.dma(kbeg, tid, L0);
-    sb.dma(kbeg, tid, L0 + A_IMG);
+    sa.dma(kbeg, 0u);
+    sb.dma(kbeg, 0u);
     wait_vmcnt<0>();
     __syncthreads();
     AW_STAMP(1);
     for (int kt = 0; kt < nk; ++kt) {
       char* cur = (kt & 1) ? L1 : L0;
-      char* nxt = (kt & 1) ? L0 : L1;
+      const uint32_t nxt = (kt & 1) ? 0u : (uint32_t)STAGE;
       if (kt + 1 < nk) {
-        sa.dma(kbeg + (kt + 1) * BK, tid, nxt);
-        sb.dma(kbeg + (kt + 1) * BK, tid, nxt + A_IMG);
+        sa.dma(kbeg + (kt + 1) * BK, nxt);
+        sb.dma(kbeg + (kt + 1) * BK, nxt);
       }
       compute(cur);
       wait_vmcnt<0>();
@@ -455,14 +495,12 @@ __global__ __launch_bounds__(Cfg<BMT>::NTH, RAGGED ? 1 : Cfg<BMT>::MINB) void ge
     // step t+1 with a counted vmcnt (leaving step t+2 in flight) and the raw barrier publishes it to every wave;
     // the barrier also orders every wave's reads of stage t before the DMA of step t+3 overwrites it.
     constexpr int PER_STEP = SA::NCH + SB::NCH;
-    char* S0 = smem;
-    char* S1 = smem + STAGE;
-    char* S2 = smem + 2 * STAGE;
-    sa.dma(kbeg, tid, S0);
-    sb.dma(kbeg, tid, S0 + A_IMG);
+    uint32_t S0 = 0u, S1 = (uint32_t)STAGE, S2 = 2u * (uint32_t)STAGE;
+    sa.dma(kbeg, S0);
+    sb.dma(kbeg, S0);
     if (nk > 1) {
-      sa.dma(kbeg + BK, tid, S1);
-      sb.dma(kbeg + BK, tid, S1 + A_IMG);
+      sa.dma(kbeg + BK, S1);
+      sb.dma(kbeg + BK, S1);
       wait_vmcnt<PER_STEP>();
     } else {
       wait_vmcnt<0>();
@@ -473,16 +511,16 @@ __global__ __launch_bounds__(Cfg<BMT>::NTH, RAGGED ? 1 : Cfg<BMT>::MINB) void ge
     for (int kt = 0; kt < nk; ++kt) {
       // stages rotate S0 -> S1 -> S2: step kt computes from S0 and step kt+2 loads into S2
       if (kt + 2 < nk) {
-        sa.dma(kbeg + (kt + 2) * BK, tid, S2);
-        sb.dma(kbeg + (kt + 2) * BK, tid, S2 + A_IMG);
+        sa.dma(kbeg + (kt + 2) * BK, S2);
+        sb.dma(kbeg + (kt + 2) * BK, S2);
       }
-      compute(S0);
+      compute(smem + S0);
       if (kt + 2 < nk) wait_vmcnt<PER_STEP>();
       else wait_vmcnt<0>();
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
-      char* t0 = S0;
+      const uint32_t t0 = S0;
       S0 = S1;
       S1 = S2;
       S2 = t0;
