@@ -337,10 +337,8 @@ __device__ __forceinline__ uint4 frag(const char* lds, int rbase, int lane, int 
 template <typename T> struct Mfma;
 template <> struct Mfma<bf16> {
   __device__ __forceinline__ static void run(f32x4& acc, const uint4& a, const uint4& b) {
-    bf16x8 av, bv;
-    memcpy(&av, &a, 16);
-    memcpy(&bv, &b, 16);
-    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), acc,
+                                                  0, 0, 0);
   }
 };
 template <> struct Mfma<float> {
@@ -377,11 +375,12 @@ template <typename T>
 __device__ __forceinline__ float frag_sum(const uint4& v) {
   const uint32_t w[4] = {v.x, v.y, v.z, v.w};
   if constexpr (sizeof(T) == 2) {
+    const bf16x8 h = __builtin_bit_cast(bf16x8, v);
     float s0 = 0.f, s1 = 0.f;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      s0 += __uint_as_float(w[i] << 16);
-      s1 += __uint_as_float(w[i] & 0xFFFF0000u);
+      s0 += (float)h[2 * i];
+      s1 += (float)h[2 * i + 1];
     }
     return s0 + s1;
   } else {
@@ -445,7 +444,8 @@ __global__ __launch_bounds__(Cfg<BMT>::NTH, RAGGED ? 1 : Cfg<BMT>::MINB) void ge
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   // fused A-row sums (bias gradients) from the A fragments already in registers: waves wn == 0 of the tn == 0
   // tiles add their 8 (bf16) / 4 (f32) k-values per fragment; the lane groups are reduced once at the end
-  const bool wave_rowsum = do_rowsum && wn == 0;
+  constexpr bool ROWSUM_OK = (EPI & EP_GENERIC) || (EPI & EP_ACCUM);   // bias gradients: weight-gradient launches
+  const bool wave_rowsum = ROWSUM_OK && do_rowsum && wn == 0;
   float rowacc[4] = {0.f, 0.f, 0.f, 0.f};
 
   auto compute = [&](const char* a_l) {
