@@ -181,9 +181,11 @@ def main():
     args = parse()
     distributed = int(os.environ.get("WORLD_SIZE", "1")) > 1
     if distributed:
-        dist.init_process_group("nccl")
+        # ARCWELD_DIST_BACKEND=gloo rehearses N ranks on one GPU (RCCL refuses two ranks per device); the
+        # measured multi-GPU path is "nccl" (= RCCL over xGMI)
+        dist.init_process_group(os.environ.get("ARCWELD_DIST_BACKEND", "nccl"))
         rank, world = dist.get_rank(), dist.get_world_size()
-        local = int(os.environ.get("LOCAL_RANK", "0"))
+        local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
     else:
         rank, world, local = 0, 1, 0
     torch.cuda.set_device(local)

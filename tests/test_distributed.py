@@ -88,6 +88,14 @@ def _worker(rank, world, port, out, accumulate):
         flat = torch.arange(10, dtype=torch.float32) * (rank + 1)
         T.allreduce_flat(flat, bucket=3)
         assert torch.equal(flat, torch.arange(10, dtype=torch.float32) * 3)
+        # region all-reduce as the split step graph issues it: [cut, n) first (async), then [0, cut)
+        flat = torch.arange(10, dtype=torch.float32) * (rank + 1)
+        works = T.allreduce_flat(flat, bucket=3, lo=6, wait=False)
+        assert len(works) == 2
+        works += T.allreduce_flat(flat, bucket=4, hi=6, wait=False)
+        for w in works:
+            w.wait()
+        assert torch.equal(flat, torch.arange(10, dtype=torch.float32) * 3)
         # broadcast: rank 1 starts from different weights and receives rank 0's
         m = TinyModel()
         if rank == 1:

@@ -170,6 +170,34 @@ def test_graphed_steps_match_eager_steps(fp32_parity):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("fname", ["vqvae_small.npz", "vqvae_small_p10.npz"])
+def test_fused_train_step_matches_golden_and_split_point_is_final(fname, fp32_parity):
+    """fused_train_step (no autograd; what the captured step runs) gives the golden loss and gradients, and at its
+    mid_hook every gradient from backward_split_parameter() on is already final while the ones before it are
+    untouched -- the invariant the overlapped decoder-side all-reduce relies on."""
+    kw, B, wseed, xseed = CASES[fname]
+    g = golden(fname)
+    m = make_model(kw, wseed, "cuda").train()
+    for p in m.parameters():
+        p.grad = torch.zeros_like(p)
+    x = torch.tensor(gen.windows(xseed, B), device="cuda")
+    names = [n for n, _ in m.named_parameters()]
+    params = list(m.parameters())
+    cut = next(i for i, p in enumerate(params) if p is m.backward_split_parameter())
+    snap = []
+    loss = m.fused_train_step(x, 1.0, mid_hook=lambda: snap.append([p.grad.clone() for p in params]))
+    assert len(snap) == 1
+    np.testing.assert_allclose(loss.item(), g["loss"], rtol=1e-4)
+    assert np.array_equal(m._last_indices.cpu().numpy(), g["idx"])
+    _check_grads(m, g)
+    for i, (n, p) in enumerate(zip(names, params)):
+        if i >= cut:
+            assert torch.equal(snap[0][i], p.grad), n
+        else:
+            assert not snap[0][i].any(), n
+
+
+@pytest.mark.gpu
 def test_full_size_bf16_grads_agree_across_gemm_tiles():
     """Full-size model, bf16 operands: the automatic tile policy (256x128 three-stage pipeline for the grouped
     weight gradients) and every launch forced onto 128x128 tiles give the same step up to summation order."""

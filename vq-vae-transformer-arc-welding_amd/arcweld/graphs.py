@@ -1,11 +1,14 @@
 """HIP-graph capture of the training step (the launch-bound loop: ~200 kernel launches per step from Python).
 
-A step is captured as two graphs on the current stream:
+A step is captured as graphs on the current stream:
   g_fwd_bwd : forward + backward of one micro-batch (gradients accumulate into the flat buffer)
   g_update  : clip-norm + RAdam + zero_grad
-With data parallelism the RCCL all-reduce of the flat gradient buffer runs eagerly between the two.  Replay
-needs no host values: dropout masks come from a device counter (aw_gemm_args.seed_ptr), the RAdam step number
-and clip coefficient live on the device.  Inputs are copied into static buffers before each replay.
+With data parallelism the RCCL all-reduce of the flat gradient buffer runs eagerly between the two.  A model
+with ``fused_train_step`` (VQVAEPatch) is captured as TWO forward/backward graphs split where its decoder-side
+gradients are final: the decoder-side all-reduce is launched (async, RCCL stream) between them and overlaps the
+encoder-side backward; the encoder-side all-reduce follows.  Replay needs no host values: dropout masks come from
+a device counter (aw_gemm_args.seed_ptr), the RAdam step number and clip coefficient live on the device.  Inputs
+are copied into static buffers before each replay.
 
 The first `warmup` calls run eagerly on their own batches (lazy device state -- RNG counters, optimizer
 buffers -- is created there); the next call captures and replays, so every call is exactly one step on the
@@ -31,19 +34,39 @@ def _copy_into(dst, src):
 
 
 class StepGraphs:
+    """allreduce(region) launches the SUM all-reduce of a flat-gradient region ("all", "late" = the part final at
+    the mid-backward split, "early" = the rest) and returns the async work handles."""
+
     def __init__(self, trainer, model, scale, allreduce, warmup=2):
         self.trainer, self.model, self.scale, self.allreduce = trainer, model, scale, allreduce
         self.warmup = warmup
         self.calls = 0
         self.static = None
+        self.split = hasattr(model, "fused_train_step") and hasattr(model, "backward_split_parameter")
 
     def _capture(self, batch):
         self.static = _clone_static(batch)
         torch.cuda.synchronize()
-        self.g1, self.g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
         pool = torch.cuda.graph_pool_handle()
-        with torch.cuda.graph(self.g1, pool=pool):
-            self.loss = self.trainer.micro_step(self.model, self.static, 0, self.scale)
+        self.g2 = torch.cuda.CUDAGraph()
+        if self.split:
+            self.g1a, self.g1b = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+            state = {"ctx": torch.cuda.graph(self.g1a, pool=pool)}
+            state["ctx"].__enter__()
+
+            def mid():   # end the first capture where the decoder-side gradients are final, start the second
+                state["ctx"].__exit__(None, None, None)
+                state["ctx"] = torch.cuda.graph(self.g1b, pool=pool)
+                state["ctx"].__enter__()
+
+            try:
+                self.loss = self.model.fused_train_step(self.static, self.scale, mid_hook=mid)
+            finally:
+                state["ctx"].__exit__(None, None, None)
+        else:
+            self.g1 = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.g1, pool=pool):
+                self.loss = self.trainer.micro_step(self.model, self.static, 0, self.scale)
         with torch.cuda.graph(self.g2, pool=pool):
             self.trainer._update(self.model)
 
@@ -51,7 +74,8 @@ class StepGraphs:
         self.calls += 1
         if self.calls <= self.warmup:
             loss = self.trainer.micro_step(self.model, batch, 0, self.scale)
-            self.allreduce()
+            for w in self.allreduce("all"):
+                w.wait()
             self.trainer._update(self.model)
             self.trainer.global_step += 1
             return loss
@@ -59,8 +83,16 @@ class StepGraphs:
             self._capture(batch)
         else:
             _copy_into(self.static, batch)
-        self.g1.replay()
-        self.allreduce()
+        if self.split:
+            self.g1a.replay()
+            works = self.allreduce("late")       # decoder side: overlaps the encoder-side backward below
+            self.g1b.replay()
+            works += self.allreduce("early")
+        else:
+            self.g1.replay()
+            works = self.allreduce("all")
+        for w in works:
+            w.wait()
         self.g2.replay()
         self.trainer.global_step += 1
         return self.loss

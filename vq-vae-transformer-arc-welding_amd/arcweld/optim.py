@@ -84,6 +84,15 @@ class RAdam(torch.optim.Optimizer):
         F["act_group"] = [torch.tensor([a if o == gi else 0 for a, o in zip(act, F["owner"])], device=dev,
                                        dtype=torch.int32) for gi in range(len(self.param_groups))]
 
+    def flat_offset(self, param):
+        """Element offset of ``param``'s segment in the flat buffers."""
+        self.flatten()
+        F = self._flat
+        for p, o in zip(F["params"], F["offs"]):
+            if p is param:
+                return o
+        raise KeyError("parameter is not managed by this optimizer")
+
     @property
     def flat_grad(self):
         return self.flatten()[1]

@@ -29,14 +29,19 @@ def world():
     return dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
 
 
-def allreduce_flat(flat: torch.Tensor, bucket: int = BUCKET_ELEMS):
-    """SUM all-reduce of a flat buffer in large buckets (RCCL rings are link-bound; few large messages)."""
+def allreduce_flat(flat: torch.Tensor, bucket: int = BUCKET_ELEMS, lo: int = 0, hi: int = None, wait: bool = True):
+    """SUM all-reduce of flat[lo:hi] in large buckets (RCCL rings are link-bound; few large messages).  With
+    wait=False the async work handles are returned (the collectives are ordered after the work already queued on
+    the current stream and run on RCCL's stream)."""
     if world() == 1:
-        return
-    n = flat.numel()
-    works = [dist.all_reduce(flat[o:min(o + bucket, n)], async_op=True) for o in range(0, n, bucket)]
-    for w in works:
-        w.wait()
+        return []
+    hi = flat.numel() if hi is None else hi
+    works = [dist.all_reduce(flat[o:min(o + bucket, hi)], async_op=True) for o in range(lo, hi, bucket)]
+    if wait:
+        for w in works:
+            w.wait()
+        return []
+    return works
 
 
 def broadcast_params(model: torch.nn.Module):
@@ -107,8 +112,19 @@ class Trainer:
         call warms up eagerly and captures.  Returns the (static) loss tensor."""
         from .graphs import StepGraphs
         if getattr(self, "_graphs", None) is None or self._graphs.model is not model:
-            self._graphs = StepGraphs(self, model, scale, lambda: allreduce_flat(self.optimizer.flat_grad))
+            self._graphs = StepGraphs(self, model, scale, lambda region: self._allreduce_region(model, region))
         return self._graphs.run(batch)
+
+    def _allreduce_region(self, model, region):
+        """Async all-reduce of the flat gradients: "all", or split at the model's backward_split_parameter into
+        "late" (that parameter onwards: final mid-backward) and "early" (the parameters before it)."""
+        flat = self.optimizer.flat_grad
+        if region == "all" or not hasattr(model, "backward_split_parameter"):
+            return allreduce_flat(flat, wait=False) if region in ("all", "late") else []
+        cut = self.optimizer.flat_offset(model.backward_split_parameter())
+        if region == "late":
+            return allreduce_flat(flat, lo=cut, wait=False)
+        return allreduce_flat(flat, hi=cut, wait=False)
 
     def fit(self, model, datamodule=None, train_dataloaders=None, val_dataloaders=None):
         if datamodule is not None:

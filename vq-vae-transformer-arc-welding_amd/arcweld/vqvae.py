@@ -264,8 +264,11 @@ def _cast(t, T):
     return out
 
 
-def backward(m, sv, g_emb, g_xhat, slot):
-    """Accumulate parameter gradients into ``slot(param)`` (f32 tensors shaped like the parameter)."""
+def backward(m, sv, g_emb, g_xhat, slot, mid_hook=None):
+    """Accumulate parameter gradients into ``slot(param)`` (f32 tensors shaped like the parameter).
+
+    ``mid_hook()`` runs once the decoder side is done (head, ConvT, decoder ResBlocks, decoder 1x1, codebook): those
+    gradients are final there, which lets a data-parallel step reduce them while the encoder backward runs."""
     sh, T, p_drop = sv.sh, sv.T, sv.p_drop
     H, D, N, S, R, P, k1 = sh.H, sh.D, sh.N, sh.S, sh.R, sh.P, sh.k1
     pr = _params(m)
@@ -325,6 +328,8 @@ def backward(m, sv, g_emb, g_xhat, slot):
     # ---- vector quantizer (straight-through + codebook/commitment loss)
     dz = e(N, D)
     K.vq_backward(sv.z, pr["E"], sv.idx, gzq, g_emb, m.vector_quantization.beta, dz, slot(pr["E"]))
+    if mid_hook is not None:
+        mid_hook()
     dz_T = dz if T == F32 else _cast(dz, T)
 
     # ---- SepCNNBlock

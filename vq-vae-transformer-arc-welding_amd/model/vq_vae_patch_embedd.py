@@ -248,6 +248,46 @@ class VQVAEPatch(Autoencoder):
         return emb, x_hat, perp
 
     @torch.no_grad()
+    def fused_train_step(self, x, scale, mid_hook=None):
+        """One training micro-step on the kernels without autograd: the same work as ``training_step`` followed by
+        ``(loss * scale).backward()`` (loss = mse(x_hat, x) + embedding loss, autencoder_lightning_base.py:80-97).
+        Gradients accumulate into each parameter's ``.grad`` (the flat optimizer views when a Trainer installed
+        ``_grad_sink``).  ``mid_hook`` is called between the decoder-side and the encoder-side backward (see
+        arcweld.vqvae.backward): the data-parallel step starts the decoder-side all-reduce there.  Returns the loss."""
+        if self.batch_norm:
+            raise NotImplementedError("ResBlock BatchNorm (--batchnorm 1) is not on the HIP path yet")
+        x = x.contiguous()
+        emb, x_hat, perp, idx, sv = engine.forward(self, x, self.training, need_backward=True, seed=self._next_seed())
+        self._last_indices = idx
+        sq = torch.zeros(1, device=x.device, dtype=torch.float64)
+        K.mse_fwd(x_hat, x, sq)
+        recon = torch.empty((), device=x.device)
+        K.mse_finalize(sq, x.numel(), recon)
+        loss = torch.empty((), device=x.device)
+        K.scalar_add(recon.reshape(1), emb.reshape(1), loss)
+        g = torch.full((1,), float(scale), device=x.device)
+        g_xhat = torch.empty_like(x_hat)
+        K.mse_bwd(x_hat, x, g, g_xhat)
+        sink = getattr(self, "_grad_sink", None)
+
+        def slot(p):
+            if sink is not None and p in sink:
+                return sink[p]
+            if p.grad is None:
+                p.grad = torch.zeros_like(p)
+            return p.grad
+
+        engine.backward(self, sv, g, g_xhat, slot, mid_hook=mid_hook)
+        self.log('train/loss', loss, prog_bar=True)
+        self.log('train/recon_error', recon)
+        self.last_recon = (x[:1], x_hat[:1])
+        return loss
+
+    def backward_split_parameter(self):
+        """First parameter (in registration order) whose gradient is final at fused_train_step's mid_hook."""
+        return self.vector_quantization.embedding.weight
+
+    @torch.no_grad()
     def encode_ids(self, x):
         """Frozen-encoder tokenization (latentspace_dataloader.py:154-161): windows (B, L, C) -> ids (B, S) int64,
         fused patch_embed -> encoder -> VQ on the HIP path (eval-mode semantics of the current module state)."""
