@@ -50,3 +50,48 @@ def test_inactive_segments_untouched():
     opt.step()
     assert torch.equal(params[1].detach(), before[1])
     assert not torch.equal(params[0].detach(), before[0]) and not torch.equal(params[2].detach(), before[2])
+
+
+def test_centre_tap_layout_matches_dense_layout():
+    """declare_centre_tap: (O, I, 3) weights become tap-major strided views, their dead side taps leave the
+    norm / update / all-reduce spans, and the trajectory equals the dense layout's when those taps get zero
+    gradient (the per-token encoder convs)."""
+    from arcweld.optim import RAdam
+    shapes = [(6, 5, 3), (6,), (6, 5, 3), (4, 7), (6, 5, 3)]
+    centre = [0, 2, 4]
+    runs = []
+    for declare in (False, True):
+        params = [torch.nn.Parameter(torch.tensor(gen.normal(800 + i, s, 0.3), device="cuda"))
+                  for i, s in enumerate(shapes)]
+        init = [p.detach().clone() for p in params]
+        opt = RAdam(params, lr=1e-2)
+        if declare:
+            opt.declare_centre_tap([params[i] for i in centre])
+        opt.flatten()
+        for i, p in enumerate(params):
+            assert p.shape == init[i].shape and torch.equal(p.detach(), init[i])
+            assert p.is_contiguous() == (not declare or i not in centre)
+        norms = []
+        for step in range(5):
+            for i, p in enumerate(params):
+                g = torch.tensor(gen.normal(900 + 7 * step + i, p.shape, 1.0), device="cuda")
+                if i in centre:
+                    g[:, :, 0] = 0
+                    g[:, :, 2] = 0
+                p.grad.copy_(g)
+            norms.append(opt.clip_grad_norm_(0.5).item())
+            opt.step()
+            opt.zero_grad()
+        if declare:
+            spans = opt.live_spans()
+            covered = sum(b - a for a, b in spans)
+            assert covered < opt.flatten()[0].numel() - 2 * 3 * 30     # both dead tap blocks are outside
+            for i in centre:
+                assert torch.equal(params[i].detach()[:, :, 0], init[i][:, :, 0])
+                assert torch.equal(params[i].detach()[:, :, 2], init[i][:, :, 2])
+                assert params[i].grad[:, :, 1].is_contiguous()
+        runs.append(([p.detach().clone() for p in params], norms))
+    (p0, n0), (p1, n1) = runs
+    np.testing.assert_allclose(n1, n0, rtol=1e-6)
+    for a, b in zip(p0, p1):
+        torch.testing.assert_close(b, a, rtol=1e-6, atol=1e-7)

@@ -224,3 +224,32 @@ def test_full_size_bf16_grads_agree_across_gemm_tiles():
         a, b = grads[0][n], grads[128][n]
         rel = ((a - b).norm() / (b.norm() + 1e-20)).item()
         assert rel < 2e-3, (n, rel)
+
+
+@pytest.mark.gpu
+def test_trainer_centre_tap_layout_matches_dense_layout(fp32_parity, monkeypatch):
+    """The Trainer stores the encoder conv weights tap-major (side taps out of the optimizer); three steps give the
+    same parameters as the dense layout, and the side taps stay at their initial values."""
+    from arcweld.optim import RAdam
+    from arcweld.trainer import Trainer
+    kw = dict(hidden_dim=64, num_embeddings=64, embedding_dim=16, n_resblocks=2, patch_size=25)
+    xs = [torch.tensor(gen.windows(720 + i, 16), device="cuda") for i in range(3)]
+    out = []
+    for declare in (True, False):
+        if not declare:
+            monkeypatch.setattr(RAdam, "declare_centre_tap", lambda self, ps: None)
+        m = make_model(kw, 301, "cuda").train()
+        init = {k: v.detach().clone() for k, v in m.state_dict().items()}
+        tr = Trainer(gradient_clip_val=0.7)
+        tr.setup_optimizer(m)
+        assert (not m.encoder[0].shared_conv[0].block[1].weight.is_contiguous()) == declare
+        for x in xs:
+            tr.micro_step(m, x, 0, 1.0)
+            tr.optimizer_step(m)
+        sd = {k: v.detach().clone() for k, v in m.state_dict().items()}
+        for k, v in sd.items():
+            if k.startswith("encoder.0.") and k.endswith("weight"):
+                assert torch.equal(v[:, :, 0], init[k][:, :, 0]) and torch.equal(v[:, :, 2], init[k][:, :, 2]), k
+        out.append(sd)
+    for k in out[0]:
+        torch.testing.assert_close(out[0][k].float(), out[1][k].float(), rtol=1e-5, atol=1e-6, msg=k)

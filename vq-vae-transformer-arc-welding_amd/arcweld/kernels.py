@@ -157,10 +157,16 @@ def patchify(x, P, out, stream=None):
 
 
 def weight_relayout(W, O, I, k, tap, mode, out, ldo=0, stream=None):
+    _dense(W, "weight_relayout")
     call("aw_weight_relayout", ptr(W), O, I, k, tap, mode, ptr(out), ldo, dtype_code(out.dtype), stream_ptr(stream))
 
 
 RELAYOUT_MAX_JOBS = 40
+
+
+def _dense(W, who):
+    if not W.is_contiguous():
+        raise nat.NativeError(f"{who}: the source weight must be contiguous (got strides {tuple(W.stride())})")
 
 
 def weight_relayout_batch(jobs, stream=None):
@@ -175,6 +181,7 @@ def weight_relayout_batch(jobs, stream=None):
             arr = (nat.RelayoutJob * len(chunk))()
             for r, jb in zip(arr, chunk):
                 W, O, I, k, tap, mode, out = jb[:7]
+                _dense(W, "weight_relayout_batch")
                 r.W, r.out = ptr(W), ptr(out)
                 r.O, r.I, r.k, r.tap, r.mode = int(O), int(I), int(k), int(tap), int(mode)
                 r.ldo = int(jb[7]) if len(jb) > 7 else 0

@@ -8,6 +8,8 @@ is re-bound to a view of it, so that
 * the optimizer update is one kernel over the flat buffer (segments carry per-group weight decay and an
   "active" flag -- a parameter that produced no gradient this stage is skipped, like torch skips grad None),
 * the gradient all-reduce of data parallelism is a few large RCCL calls over the flat gradient buffer,
+* conv weights declared centre-tap (declare_centre_tap) keep their provably-dead side taps out of the
+  all-reduce, the norm and the update,
 * the clip coefficient (Lightning ``gradient_clip_val``) is computed on device and fed to the update kernel:
   no host synchronisation anywhere in the step.
 
@@ -29,6 +31,16 @@ class RAdam(torch.optim.Optimizer):
         self._pending_active = None
 
     # ------------------------------------------------------------------ flat layout
+    def declare_centre_tap(self, params):
+        """Conv weights (O, I, 3) whose side taps provably receive an exactly-zero gradient (a k = 3, pad = 1
+        conv applied to length-1 inputs: the per-token encoder ResBlocks, model/vq_vae_patch_embedd.py:60-74,108-110).
+        With weight decay 0 their side taps never change under RAdam (zero m, zero v -> zero update), so they are
+        stored tap-major in one block [3][n][O][I] and only the centre-tap block is reduced, clipped and updated.
+        The parameters become strided views (shape and values unchanged).  Call before the first flatten()."""
+        if self._flat is not None:
+            raise RuntimeError("declare_centre_tap must precede flatten()")
+        self._centre = [p for p in params]
+
     def _build(self):
         params = [p for g in self.param_groups for p in g["params"]]
         dev = params[0].device
@@ -36,29 +48,60 @@ class RAdam(torch.optim.Optimizer):
             raise RuntimeError("arcweld RAdam needs all parameters as float32 on one device")
         if dev.type != "cuda":
             raise RuntimeError("arcweld RAdam runs on the GPU only (no CPU fallback)")
-        offs, lens, wds, owner = [], [], [], []
-        total = 0
+        owner_of = {id(p): gi for gi, g in enumerate(self.param_groups) for p in g["params"]}
+        centre = [p for p in getattr(self, "_centre", []) if id(p) in owner_of]
+        if centre and not (all(p.dim() == 3 and p.shape == centre[0].shape and p.shape[2] == 3 for p in centre)
+                           and len(set(owner_of[id(p)] for p in centre)) == 1
+                           and float(self.param_groups[owner_of[id(centre[0])]]["weight_decay"]) == 0.0):
+            centre = []          # the exactness argument needs one group, wd 0 and one (O, I, 3) shape
+        cidx = {id(p): j for j, p in enumerate(centre)}
+        al = lambda n: (n + 63) // 64 * 64      # 256-B aligned segments  # noqa: E731
+        # segments: (param, offset, length, weight decay, group); a centre-tap param has ONE segment (its centre)
+        segs, place, total, blk = [], {}, 0, None
         for gi, g in enumerate(self.param_groups):
             for p in g["params"]:
-                offs.append(total)
-                lens.append(p.numel())
-                wds.append(float(g["weight_decay"]))
-                owner.append(gi)
-                total += (p.numel() + 63) // 64 * 64        # 256-B aligned segments
+                if id(p) in cidx:
+                    if blk is None:
+                        blk = total
+                        total += al(3 * len(centre) * centre[0][:, :, 0].numel())
+                    oi = centre[0][:, :, 0].numel()
+                    segs.append((p, blk + (len(centre) + cidx[id(p)]) * oi, oi, float(g["weight_decay"]), gi))
+                    continue
+                place[id(p)] = total
+                segs.append((p, total, p.numel(), float(g["weight_decay"]), gi))
+                total += al(p.numel())
+        segs.sort(key=lambda s: s[1])          # the kernels find a segment by binary search over offsets
         flat_p = torch.zeros(total, device=dev)
         flat_g = torch.zeros(total, device=dev)
-        for p, o in zip(params, offs):
-            n = p.numel()
-            flat_p[o:o + n].copy_(p.detach().reshape(-1))
+
+        def view(buf, p):
+            if id(p) in cidx:
+                O, I, _ = p.shape
+                return buf[blk:blk + 3 * len(centre) * O * I].view(3, len(centre), O, I)[:, cidx[id(p)]].permute(1, 2, 0)
+            o = place[id(p)]
+            return buf[o:o + p.numel()].view_as(p)
+
+        for p in params:
+            view(flat_p, p).copy_(p.detach())
             if p.grad is not None:
-                flat_g[o:o + n].copy_(p.grad.reshape(-1))
-            p.data = flat_p[o:o + n].view_as(p)
-            p.grad = flat_g[o:o + n].view_as(p)
-        self._flat = dict(params=params, p=flat_p, g=flat_g, m=torch.zeros(total, device=dev),
-                          v=torch.zeros(total, device=dev), total=total, owner=owner, offs=offs, lens=lens,
+                view(flat_g, p).copy_(p.grad)
+            p.data = view(flat_p, p)
+            p.grad = view(flat_g, p)
+        # contiguous ranges holding every segment (alignment padding included, dead side-tap blocks excluded)
+        spans = []
+        for _, o, n, _, _ in segs:
+            if spans and o <= al(spans[-1][1]):
+                spans[-1][1] = max(spans[-1][1], o + n)
+            else:
+                spans.append([o, o + n])
+        offs = [s[1] for s in segs]
+        lens = [s[2] for s in segs]
+        self._flat = dict(params=params, segs=segs, spans=[tuple(s) for s in spans], p=flat_p, g=flat_g,
+                          m=torch.zeros(total, device=dev), v=torch.zeros(total, device=dev), total=total,
+                          owner=[s[4] for s in segs], offs=offs, lens=lens,
                           off_d=torch.tensor(offs, device=dev, dtype=torch.int64),
                           len_d=torch.tensor(lens, device=dev, dtype=torch.int64),
-                          wd_d=torch.tensor(wds, device=dev, dtype=torch.float32),
+                          wd_d=torch.tensor([s[3] for s in segs], device=dev, dtype=torch.float32),
                           ws=torch.zeros(1, device=dev, dtype=torch.float64),
                           norm=torch.zeros((), device=dev), coef=torch.ones((), device=dev),
                           step=torch.full((1,), self._step_count, device=dev, dtype=torch.int64))
@@ -78,20 +121,26 @@ class RAdam(torch.optim.Optimizer):
             return
         F = self._flat
         keep = None if params is None else set(id(p) for p in params)
-        act = [1 if keep is None or id(p) in keep else 0 for p in F["params"]]
+        act = [1 if keep is None or id(s[0]) in keep else 0 for s in F["segs"]]
         dev = F["p"].device
         F["act_d"] = torch.tensor(act, device=dev, dtype=torch.int32)
         F["act_group"] = [torch.tensor([a if o == gi else 0 for a, o in zip(act, F["owner"])], device=dev,
                                        dtype=torch.int32) for gi in range(len(self.param_groups))]
 
     def flat_offset(self, param):
-        """Element offset of ``param``'s segment in the flat buffers."""
+        """Element offset of ``param``'s (first) segment in the flat buffers."""
         self.flatten()
-        F = self._flat
-        for p, o in zip(F["params"], F["offs"]):
-            if p is param:
-                return o
+        for s in self._flat["segs"]:
+            if s[0] is param:
+                return s[1]
         raise KeyError("parameter is not managed by this optimizer")
+
+    def live_spans(self, lo=0, hi=None):
+        """Contiguous [a, b) ranges of the flat buffers that hold gradients, clipped to [lo, hi): what a gradient
+        all-reduce must move (the dead side-tap blocks of declare_centre_tap are left out)."""
+        self.flatten()
+        hi = self._flat["total"] if hi is None else hi
+        return [(max(a, lo), min(b, hi)) for a, b in self._flat["spans"] if min(b, hi) > max(a, lo)]
 
     @property
     def flat_grad(self):
@@ -104,14 +153,16 @@ class RAdam(torch.optim.Optimizer):
                 for p in g["params"]:
                     p.grad = None
             return
-        self._flat["g"].zero_()
+        g = self._flat["g"]
+        for a, b in self._flat["spans"]:
+            g[a:b].zero_()
 
     def clip_grad_norm_(self, max_norm):
         """L2 norm over the active gradients; the clip coefficient is applied inside the next step().
         Returns the (pre-clip) total norm as a device scalar."""
         self.flatten()
         F = self._flat
-        K.grad_norm_clip(F["g"], F["off_d"], F["len_d"], F["act_d"], len(F["params"]), max_norm, F["ws"], F["norm"],
+        K.grad_norm_clip(F["g"], F["off_d"], F["len_d"], F["act_d"], len(F["segs"]), max_norm, F["ws"], F["norm"],
                          F["coef"])
         self._coef = F["coef"]
         return F["norm"]
@@ -130,7 +181,7 @@ class RAdam(torch.optim.Optimizer):
         K.counter_add(F["step"], 1)
         # groups that differ only in weight decay (per segment already) share one launch
         for (lr, (b1, b2), eps), act in self._launch_groups():
-            K.radam_step(F["p"], F["g"], F["m"], F["v"], F["off_d"], F["len_d"], F["wd_d"], act, len(F["params"]),
+            K.radam_step(F["p"], F["g"], F["m"], F["v"], F["off_d"], F["len_d"], F["wd_d"], act, len(F["segs"]),
                          F["total"], self._step_count, lr, b1, b2, eps, gscale=self._coef, step_ptr=F["step"])
         self._coef = None
         return loss

@@ -44,11 +44,32 @@ def allreduce_flat(flat: torch.Tensor, bucket: int = BUCKET_ELEMS, lo: int = 0, 
     return works
 
 
-def broadcast_params(model: torch.nn.Module):
+def allreduce_spans(flat: torch.Tensor, spans, bucket: int = BUCKET_ELEMS):
+    """Async SUM all-reduce of the [a, b) ranges of a flat buffer, each cut into buckets; returns the work handles."""
+    if world() == 1:
+        return []
+    return [dist.all_reduce(flat[o:min(o + bucket, b)], async_op=True) for a, b in spans for o in range(a, b, bucket)]
+
+
+def _spans(opt, lo=0, hi=None):
+    if hasattr(opt, "live_spans"):
+        return opt.live_spans(lo, hi)
+    return [(lo, opt.flat_grad.numel() if hi is None else hi)]
+
+
+def broadcast_params(model: torch.nn.Module, opt=None):
+    """Rank 0's parameters and buffers to every rank (DDP's initial broadcast).  Parameters packed into the
+    optimizer's flat buffer go as that one buffer (some are strided views, which collectives do not take)."""
     if world() == 1:
         return
+    packed = set()
+    if opt is not None and hasattr(opt, "live_spans"):
+        flat_p = opt.flatten()[0]
+        dist.broadcast(flat_p, src=0)
+        packed = set(id(p) for p in opt._flat["params"])
     for t in list(model.parameters()) + list(model.buffers()):
-        dist.broadcast(t.data, src=0)
+        if id(t) not in packed:
+            dist.broadcast(t.data, src=0)
 
 
 class Trainer:
@@ -77,13 +98,15 @@ class Trainer:
         opt = model.configure_optimizers()
         if isinstance(opt, (list, tuple)):
             opt = opt[0]
+        if hasattr(model, "centre_tap_parameters") and hasattr(opt, "declare_centre_tap"):
+            opt.declare_centre_tap(model.centre_tap_parameters())
         opt.flatten()
         active = model.active_parameters() if hasattr(model, "active_parameters") else None
         opt.set_active(active)
         if self.fused_grad_sink:
             # fused autograd nodes accumulate straight into the flat gradient views (no extra add)
             model._grad_sink = {p: p.grad for p in model.parameters()}
-        broadcast_params(model)
+        broadcast_params(model, opt)
         self.optimizer = opt
         self._graphs = None          # a captured step belongs to one optimizer
         self._graph_shape = None
@@ -103,7 +126,8 @@ class Trainer:
         opt.zero_grad()
 
     def optimizer_step(self, model):
-        allreduce_flat(self.optimizer.flat_grad)
+        for w in allreduce_spans(self.optimizer.flat_grad, _spans(self.optimizer)):
+            w.wait()
         self._update(model)
         self.global_step += 1
 
@@ -118,13 +142,14 @@ class Trainer:
     def _allreduce_region(self, model, region):
         """Async all-reduce of the flat gradients: "all", or split at the model's backward_split_parameter into
         "late" (that parameter onwards: final mid-backward) and "early" (the parameters before it)."""
-        flat = self.optimizer.flat_grad
+        opt = self.optimizer
+        flat = opt.flat_grad
         if region == "all" or not hasattr(model, "backward_split_parameter"):
-            return allreduce_flat(flat, wait=False) if region in ("all", "late") else []
-        cut = self.optimizer.flat_offset(model.backward_split_parameter())
+            return allreduce_spans(flat, _spans(opt)) if region in ("all", "late") else []
+        cut = opt.flat_offset(model.backward_split_parameter())
         if region == "late":
-            return allreduce_flat(flat, lo=cut, wait=False)
-        return allreduce_flat(flat, hi=cut, wait=False)
+            return allreduce_spans(flat, _spans(opt, lo=cut))
+        return allreduce_spans(flat, _spans(opt, hi=cut))
 
     def fit(self, model, datamodule=None, train_dataloaders=None, val_dataloaders=None):
         if datamodule is not None:

@@ -81,6 +81,30 @@ class Saved:
     pass
 
 
+def _centre_job(w, out):
+    """Relayout job: the centre tap of a per-token encoder conv weight (O, I, 3) -> [O][I].  The weight is either
+    the reference's contiguous layout or the optimizer's tap-major view (arcweld.optim.RAdam.declare_centre_tap),
+    whose centre tap is already a contiguous [O][I] matrix."""
+    O, I = w.shape[0], w.shape[1]
+    c = w[:, :, 1]
+    if w.is_contiguous():
+        return (w, O, I, 3, 1, 0, out)
+    if not c.is_contiguous():
+        raise ValueError("encoder conv weight: unsupported layout")
+    return (c, O, I, 1, 0, 0, out)
+
+
+def _centre_grad(g):
+    """Where the encoder conv weight-gradient GEMM writes: (C [O][ldc], col_map) for either weight layout."""
+    O, I = g.shape[0], g.shape[1]
+    if g.is_contiguous():
+        return g.view(O, 3 * I), (0, 3, 1)
+    c = g[:, :, 1]
+    if not c.is_contiguous():
+        raise ValueError("encoder conv gradient: unsupported layout")
+    return c, (0, 1, 0)
+
+
 def forward(m, x, training: bool, need_backward: bool, dtype=None, seed: int = 0):
     """Returns (emb_loss (), x_hat (B, L, C), perplexity (), indices (N,), saved-or-None)."""
     T = operand_dtype(dtype)
@@ -108,7 +132,7 @@ def forward(m, x, training: bool, need_backward: bool, dtype=None, seed: int = 0
     enc_w = []
     for c1, c2 in pr["enc"]:
         w1, w2 = e(H, H, dt=T), e(H, H, dt=T)
-        jobs += [(c1.weight, H, H, 3, 1, 0, w1), (c2.weight, H, H, 3, 1, 0, w2)]
+        jobs += [_centre_job(c1.weight, w1), _centre_job(c2.weight, w2)]
         enc_w.append((w1, w2))
     Ws = e(D, H, dt=T)
     jobs.append((pr["sep"].weight, D, H, 1, 0, 0, Ws))
@@ -238,7 +262,7 @@ def encode(m, x, dtype=F32):
     ew = [(e(H, H, dt=T), e(H, H, dt=T)) for _ in range(R)]
     Ws = e(D, H, dt=T)
     K.weight_relayout_batch([jb for r, (c1, c2) in enumerate(pr["enc"])
-                             for jb in ((c1.weight, H, H, 3, 1, 0, ew[r][0]), (c2.weight, H, H, 3, 1, 0, ew[r][1]))]
+                             for jb in (_centre_job(c1.weight, ew[r][0]), _centre_job(c2.weight, ew[r][1]))]
                             + [(pr["sep"].weight, D, H, 1, 0, 0, Ws)])
     h, a1 = e(N, H, dt=T), e(N, H, dt=T)   # pre-activation kept in the operand dtype
     for r, (c1, c2) in enumerate(pr["enc"]):
@@ -346,13 +370,15 @@ def backward(m, sv, g_emb, g_xhat, slot, mid_hook=None):
         w1, w2 = sv.enc_w[r]
         gh = e(N, H, dt=T)
         K.gemm(gxo, w2, N, H, H, b_trans=True, pre=sv.hs[r], C=gh)
-        wgrads.append((gxo, sv.a1s[r], H, H, N, dict(a_trans=True, b_trans=True, C=slot(c2.weight).view(H, 3 * H),
-                       accumulate=True, col_map=(0, 3, 1), a_rowsum=slot(c2.bias))))
+        C2w, cm2 = _centre_grad(slot(c2.weight))
+        wgrads.append((gxo, sv.a1s[r], H, H, N, dict(a_trans=True, b_trans=True, C=C2w, accumulate=True, col_map=cm2,
+                                                     a_rowsum=slot(c2.bias))))
         gxn, gxon = e(N, H), e(N, H, dt=T)
         K.gemm(gh, w1, N, H, H, b_trans=True, pre=sv.xs[r], resid=gx, C=gxn, C2=gxon, c2_mode=3 if r > 0 else 2,
                drop2=(p_drop, sv.enc_seed[r - 1] if r > 0 else 0), seed_ptr=sv.ctr)
-        wgrads.append((gh, sv.a0s[r], H, H, N, dict(a_trans=True, b_trans=True, C=slot(c1.weight).view(H, 3 * H),
-                       accumulate=True, col_map=(0, 3, 1), a_rowsum=slot(c1.bias))))
+        C1w, cm1 = _centre_grad(slot(c1.weight))
+        wgrads.append((gh, sv.a0s[r], H, H, N, dict(a_trans=True, b_trans=True, C=C1w, accumulate=True, col_map=cm1,
+                                                    a_rowsum=slot(c1.bias))))
         gx, gxo = gxn, gxon
     K.gemm_grouped(wgrads)
 

@@ -203,6 +203,11 @@ static void plan(const aw_gemm_args& a, int ngroups, bool grouped, GemmP& P) {
       if (grouped && splits > 2) splits = 2;
       if (splits < 1) splits = 1;
     }
+    if (grouped && a.accumulate && nb > 512 && nb < 1024 && a.K >= 48 * BK) {
+      // 1.5 waves of 128-tiles (the decoder weight gradients: 768) -> 3 full waves of half-K units; the halves
+      // meet in the accumulating atomics the epilogue issues anyway (same-box A/B: +1.3 % windows/s)
+      splits = 2;
+    }
   }
   P.bm = bm;
   P.tiles_per_group = aw_cdiv(a.M, bm) * P.tiles_n;

@@ -167,8 +167,7 @@ class CNNBlock(nn.Module):
             c1, c2 = blk.block[1], blk.block[4]
             if self.seperate:
                 w1, w2 = (torch.empty(H, H, device=x.device, dtype=T) for _ in range(2))
-                K.weight_relayout(c1.weight, H, H, 3, 1, 0, w1)
-                K.weight_relayout(c2.weight, H, H, 3, 1, 0, w2)
+                K.weight_relayout_batch([engine._centre_job(c1.weight, w1), engine._centre_job(c2.weight, w2)])
                 kd, conv = H, None
             else:
                 w1, w2 = (torch.empty(H, 3 * H, device=x.device, dtype=T) for _ in range(2))
@@ -282,6 +281,12 @@ class VQVAEPatch(Autoencoder):
         self.log('train/recon_error', recon)
         self.last_recon = (x[:1], x_hat[:1])
         return loss
+
+    def centre_tap_parameters(self):
+        """The encoder ResBlock conv weights: k = 3, pad = 1 convs applied per token to length-1 inputs
+        (vq_vae_patch_embedd.py:93-114, loop :108-110), so only weight[:, :, 1] is used and the side taps receive
+        an exactly-zero gradient.  The optimizer keeps those taps out of the all-reduce, clip norm and update."""
+        return [blk.block[i].weight for blk in self.encoder[0].shared_conv for i in (1, 4)]
 
     def backward_split_parameter(self):
         """First parameter (in registration order) whose gradient is final at fused_train_step's mid_hook."""
