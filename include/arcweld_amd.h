@@ -181,7 +181,9 @@ int aw_mse_finalize(const double* sqerr, int64_t numel, float* out, void* stream
 /* ------------------------------------------------------------------------------------- optimizer
  * Multi-tensor RAdam over one flat parameter buffer (torch.optim.RAdam semantics, L2 weight decay):
  * segments [seg_off[s], seg_off[s]+seg_len[s]) (sorted, within [0,total)) with weight decay seg_wd[s]; seg_active[s]==0
- * are skipped (grad None: model/transformer_decoder.py heads under find_unused_parameters).
+ * are skipped (grad None: model/transformer_decoder.py heads under find_unused_parameters).  The buffers are 16-B
+ * aligned, total % 4 == 0 and every segment starts 16-B aligned; the padding after a segment (up to the next
+ * multiple of 4 elements) must be zero in all four buffers and stays zero (same for aw_grad_norm_clip's grad).
  * scalars come from host (step count, lr, betas, eps); `gscale` is a device scalar multiplying the gradient
  * first (clip coefficient; NULL = 1). */
 int aw_radam_step(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, const int64_t* seg_off,

@@ -241,12 +241,26 @@ struct Stager {
   // kernel orders the DMA itself with counted vmcnt waits and barriers.
   // Everything that does not depend on the K step is computed once (dma_init): per step a chunk costs one add,
   // a few compares and a select; the step-dependent parts (tap shift, k0 * ld) are wave-uniform scalars.
-  int doff[NCH];    // source byte offset of the chunk at K step 0 (tap-independent part)
+  int doff[NCH];    // source byte offset of the chunk at K step 0 (current tap), OOB_F folded in where masked
+  int rbase[NCH];   // ROWSHIFT: the unshifted, unmasked offset (doff is re-derived from it at every tap change)
   int dpos[NCH];    // logical k (K-contiguous image) or k-row (row-contiguous image) of the chunk within a step
   bool rok[NCH];    // the chunk's row (K-contiguous) / column block (row-contiguous) lies inside the operand
   uint32_t lds0;    // LDS byte address of this wave's first chunk in stage 0
+  int dj, dkc;      // ROWSHIFT: tap and channel offset of the next K step (cin % BK == 0; steps issue in order)
+  // A masked chunk carries OOB_F in its offset: OOB_F + any in-buffer delta (< 2^31) stays beyond num_records
+  // (< 2^31) as an unsigned 32-bit offset, so the buffer load returns zeros without a per-step select.
+  static constexpr uint32_t OOB_F = 0x80000000u;
 
-  __device__ __forceinline__ void dma_init(int tid, uint32_t img_lds) {
+  __device__ __forceinline__ void retap() {
+    const int sft = dir * (dj - 1);
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      const bool ok = rok[i] && (unsigned)(wpos[i] + sft) < (unsigned)seg;
+      doff[i] = ok ? rbase[i] + (int)((int64_t)sft * ld * (int)sizeof(T)) : (int)OOB_F;
+    }
+  }
+
+  __device__ __forceinline__ void dma_init(int tid, uint32_t img_lds, int kbeg) {
     lds0 = img_lds + __builtin_amdgcn_readfirstlane((uint32_t)(tid & ~63)) * 16u;
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
@@ -257,7 +271,8 @@ struct Stager {
         const int row = row0 + r;
         rok[i] = row < rows_total;
         dpos[i] = lc * EPC;
-        doff[i] = rok[i] ? (int)(((int64_t)row * ld + lc * EPC) * (int)sizeof(T)) : 0;
+        rbase[i] = rok[i] ? (int)(((int64_t)row * ld + lc * EPC) * (int)sizeof(T)) : 0;
+        doff[i] = rok[i] ? rbase[i] : (int)OOB_F;
       } else {
         const int kr = c / CPR;
         const int m = row0 + tr_logical_m(c, true);
@@ -266,34 +281,50 @@ struct Stager {
         if constexpr (CONV == CONV_KSHIFT)
           doff[i] = (int)(((int64_t)(kr + tapoff[i]) * ld + colin[i]) * (int)sizeof(T));
         else
-          doff[i] = rok[i] ? (int)(((int64_t)kr * ld + m) * (int)sizeof(T)) : 0;
+          doff[i] = rok[i] ? (int)(((int64_t)kr * ld + m) * (int)sizeof(T)) : (int)OOB_F;
       }
+    }
+    if constexpr (CONV == CONV_ROWSHIFT) {
+      dj = kbeg / cin;
+      dkc = kbeg - dj * cin;
+      retap();
     }
   }
 
+  // One K step's DMA.  Steps must be issued in increasing order, each once (ROWSHIFT keeps its tap state here).
+  // Interior steps cost one add per chunk: row / tap masks are folded into doff, and the K-range test is only
+  // evaluated on the (wave-uniform) partial last step.
   __device__ __forceinline__ void dma(int k0, uint32_t stage_off) {
     int delta;
-    int sft = 0;
-    if constexpr (!TR) {
-      const int jrow = (CONV == CONV_ROWSHIFT) ? k0 / cin : 0;   // tap of this step (cin % BK == 0)
-      sft = (CONV == CONV_ROWSHIFT) ? dir * (jrow - 1) : 0;
-      delta = (int)(((int64_t)sft * ld + (k0 - jrow * cin)) * (int)sizeof(T));
-    } else {
+    if constexpr (!TR)
+      delta = (CONV == CONV_ROWSHIFT ? dkc : k0) * (int)sizeof(T);
+    else
       delta = (int)((int64_t)k0 * ld * (int)sizeof(T));
-    }
+    const bool full = k0 + BK <= kend;
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
-      bool ok = rok[i] & (k0 + dpos[i] < kend);
-      if constexpr (CONV == CONV_ROWSHIFT) ok = ok & ((unsigned)(wpos[i] + sft) < (unsigned)seg);
+      int off;
       if constexpr (CONV == CONV_KSHIFT) {
+        bool ok = rok[i] & (k0 + dpos[i] < kend);
         ok = ok & ((unsigned)(wpos[i] + tapoff[i]) < (unsigned)seg);
         wpos[i] += BK % seg;                 // advance the window position to the next K step
         if (wpos[i] >= seg) wpos[i] -= seg;
+        off = ok ? doff[i] + delta : OOB;
+      } else {
+        off = doff[i] + delta;
+        if (!full) off = (k0 + dpos[i] < kend) ? off : OOB;
       }
-      const int off = ok ? doff[i] + delta : OOB;
       const uint32_t m0 = lds0 + stage_off + (uint32_t)(i * NTH * 16);
       asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" ::"s"(m0), "v"(off), "s"(desc)
                    : "memory", "m0");
+    }
+    if constexpr (CONV == CONV_ROWSHIFT) {
+      dkc += BK;
+      if (dkc >= cin) {
+        dkc = 0;
+        ++dj;
+        retap();
+      }
     }
   }
 };
@@ -432,8 +463,8 @@ __global__ __launch_bounds__(Cfg<BMT>::NTH, RAGGED ? 1 : Cfg<BMT>::MINB) void ge
   sb.init(kbeg, tid, P.b_bytes, use_dma);
   if constexpr (use_dma) {
     const uint32_t smem_lds = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
-    sa.dma_init(tid, smem_lds);
-    sb.dma_init(tid, smem_lds + A_IMG);
+    sa.dma_init(tid, smem_lds, kbeg);
+    sb.dma_init(tid, smem_lds + A_IMG, kbeg);
   }
   const bool do_rowsum = rowptr != nullptr && tn == 0;
 

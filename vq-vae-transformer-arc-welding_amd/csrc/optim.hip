@@ -46,6 +46,31 @@ __device__ __forceinline__ int find_seg(const int64_t* off, int nseg, int64_t e)
   return lo;
 }
 
+// Segment of element e for a thread whose elements only increase (grid-stride loops): advance from the last one
+// (amortised O(1); the binary search per element it replaces made both kernels ALU-bound).
+__device__ __forceinline__ int next_seg(const int64_t* off, int nseg, int s, int64_t e) {
+  while (s + 1 < nseg && off[s + 1] <= e) ++s;
+  return s;
+}
+
+__device__ __forceinline__ float radam_one(float gr, float& pv, float& mv, float& vv, float wd, float gs,
+                                           const RAdamScalars& S) {
+  gr = gs == 1.0f ? gr : gr * gs;
+  if (wd != 0.f) gr = gr + wd * pv;
+  mv = mv + (1.0f - S.beta1) * (gr - mv);  // exp_avg.lerp_(grad, 1-beta1)
+  vv = vv * S.beta2 + (1.0f - S.beta2) * (gr * gr);
+  const float mhat = mv / S.bc1;
+  if (S.rectified) {
+    const float adaptive = S.sqrt_bc2 / (sqrtf(vv) + S.eps);
+    pv = pv - ((mhat * S.lr) * adaptive) * S.rect;
+  } else {
+    pv = pv - mhat * S.lr;
+  }
+  return pv;
+}
+
+// float4 grid-stride over the flat buffers (segments are 256-B aligned: a float4 never straddles two; the
+// alignment padding past seg_len is zero in p, g, m and v and stays zero).
 __global__ __launch_bounds__(256) void radam_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                     float* __restrict__ m, float* __restrict__ v,
                                                     const int64_t* __restrict__ seg_off,
@@ -61,31 +86,28 @@ __global__ __launch_bounds__(256) void radam_kernel(float* __restrict__ p, const
   __syncthreads();
   if (step_ptr) S = s_S;
   const float gs = gscale ? gscale[0] : 1.0f;
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
-    const int s = find_seg(s_off, nseg, e);
+  const int64_t n4 = total >> 2;
+  int s = 0;
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n4; q += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t e = q << 2;
+    s = next_seg(s_off, nseg, s, e);
     if (e >= s_off[s] + seg_len[s] || !seg_active[s]) continue;
-    float gr = gs == 1.0f ? g[e] : g[e] * gs;
-    float pv = p[e];
     const float wd = seg_wd[s];
-    if (wd != 0.f) gr = gr + wd * pv;
-    float mv = m[e];
-    mv = mv + (1.0f - S.beta1) * (gr - mv);  // exp_avg.lerp_(grad, 1-beta1)
-    float vv = v[e] * S.beta2 + (1.0f - S.beta2) * (gr * gr);
-    m[e] = mv;
-    v[e] = vv;
-    const float mhat = mv / S.bc1;
-    if (S.rectified) {
-      const float adaptive = S.sqrt_bc2 / (sqrtf(vv) + S.eps);
-      pv = pv - ((mhat * S.lr) * adaptive) * S.rect;
-    } else {
-      pv = pv - mhat * S.lr;
-    }
-    p[e] = pv;
+    const float4 g4 = reinterpret_cast<const float4*>(g)[q];
+    float4 p4 = reinterpret_cast<const float4*>(p)[q];
+    float4 m4 = reinterpret_cast<const float4*>(m)[q];
+    float4 v4 = reinterpret_cast<const float4*>(v)[q];
+    radam_one(g4.x, p4.x, m4.x, v4.x, wd, gs, S);
+    radam_one(g4.y, p4.y, m4.y, v4.y, wd, gs, S);
+    radam_one(g4.z, p4.z, m4.z, v4.z, wd, gs, S);
+    radam_one(g4.w, p4.w, m4.w, v4.w, wd, gs, S);
+    reinterpret_cast<float4*>(p)[q] = p4;
+    reinterpret_cast<float4*>(m)[q] = m4;
+    reinterpret_cast<float4*>(v)[q] = v4;
   }
 }
 
-// Sum of squares of the active segments over the flat buffer: float4 grid-stride (segments are 256-B aligned,
-// so a float4 never straddles two), segment found by binary search over the offsets staged in LDS.
+// Sum of squares of the active segments over the flat buffer (float4 grid-stride as radam_kernel).
 __global__ __launch_bounds__(256) void sumsq_kernel(const float* __restrict__ g, const int64_t* __restrict__ seg_off,
                                                     const int64_t* __restrict__ seg_len,
                                                     const int* __restrict__ seg_active, int nseg, int64_t total,
@@ -95,13 +117,27 @@ __global__ __launch_bounds__(256) void sumsq_kernel(const float* __restrict__ g,
   __syncthreads();
   float acc = 0.f;
   const int64_t n4 = total >> 2;
-  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n4; q += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t e = q << 2;
-    const int s = find_seg(s_off, nseg, e);
-    if (!seg_active[s] || e >= s_off[s] + seg_len[s]) continue;
-    const float4 v = reinterpret_cast<const float4*>(g)[q];
-    acc += (v.x * v.x + v.y * v.y) + (v.z * v.z + v.w * v.w);   // past seg_len inside the float4: alignment
-  }                                                                 // padding, always zero
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  int s = 0;
+  // four float4 loads in flight per thread (one dependent load per iteration left the pass latency-bound)
+  for (int64_t q0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q0 < n4; q0 += 4 * stride) {
+    float4 v[4];
+    bool use[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t q = q0 + u * stride;
+      const int64_t e = q << 2;
+      use[u] = false;
+      if (q < n4) {
+        s = next_seg(s_off, nseg, s, e);
+        use[u] = seg_active[s] && e < s_off[s] + seg_len[s];
+      }
+      v[u] = use[u] ? reinterpret_cast<const float4*>(g)[q] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)   // past seg_len inside a float4: alignment padding, always zero
+      acc += (v[u].x * v[u].x + v[u].y * v[u].y) + (v[u].z * v[u].z + v[u].w * v[u].w);
+  }
   __shared__ double red[4];
   double d = wave_sum_d((double)acc);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = d;
@@ -135,9 +171,13 @@ extern "C" int aw_radam_step(float* param, const float* grad, float* exp_avg, fl
   // scalars in double, as torch's _single_tensor_radam computes them (python floats); on the device when the
   // step number lives there
   const RAdamScalars S = radam_scalars(step_ptr ? 1 : step, lr, beta1, beta2, eps);
+  AW_REQUIRE(total % 4 == 0 && ((uintptr_t)param & 15) == 0 && ((uintptr_t)grad & 15) == 0 &&
+                 ((uintptr_t)exp_avg & 15) == 0 && ((uintptr_t)exp_avg_sq & 15) == 0,
+             "aw_radam_step: flat buffers must be 16-B aligned with total %% 4 == 0");
   if (total == 0) return AW_OK;
-  int64_t g = (total + 255) / 256;
+  int64_t g = (total / 4 + 255) / 256;
   if (g > 4096) g = 4096;
+  if (g < 1) g = 1;
   hipLaunchKernelGGL(radam_kernel, dim3((int)g), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), param, grad,
                      exp_avg, exp_avg_sq, seg_off, seg_len, seg_wd, seg_active, nseg, total, S, gscale, step_ptr);
   return aw::check_launch("aw_radam_step");

@@ -1,3 +1,4 @@
+#include <stdlib.h>
 // VQ-VAE-Patch layout and un-patch head kernels (model/vq_vae_patch_embedd.py) for gfx950.
 // HBM-bound byte/elementwise work: coalesced float4 traffic, one wave per row where a row reduction is needed.
 #include "common.h"
@@ -218,11 +219,21 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(const float* __restrict__
   HeadParams<NS> hp;
   hp.load(st, w2, H, lane);
   const float bias = b2[0];
+  // software pipeline: the next row's loads are in flight while this row is reduced (one row per wave and
+  // iteration left the loads latency-bound at ~2 TB/s)
+  float4 nv[NS];
+  auto load_row = [&](int64_t r) {
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+      nv[s] = (hp.on[s] && r < R) ? *reinterpret_cast<const float4*>(y + r * H + lane * 4 + 256 * s)
+                                  : make_float4(0.f, 0.f, 0.f, 0.f);
+  };
+  load_row(wave);
   for (int64_t r = wave; r < R; r += nw) {
     float4 v[NS];
 #pragma unroll
-    for (int s = 0; s < NS; ++s)
-      v[s] = hp.on[s] ? *reinterpret_cast<const float4*>(y + r * H + lane * 4 + 256 * s) : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int s = 0; s < NS; ++s) v[s] = nv[s];
+    load_row(r + nw);
     float part[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
@@ -237,11 +248,7 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(const float* __restrict__
     }
 #pragma unroll
     for (int j = 0; j < 5; ++j) part[j] = wave_sum(part[j]);
-    if (lane < 5) {
-      const int64_t b = r / Q;
-      const int q = (int)(r - b * Q);
-      x_hat[b * (int64_t)Q * 5 + q * 5 + lane] = pick5(part, lane) + bias;
-    }
+    if (lane < 5) x_hat[r * 5 + lane] = pick5(part, lane) + bias;   // row r = b*Q + q -> x_hat[b][5q + j]
   }
 }
 
@@ -270,18 +277,34 @@ __global__ __launch_bounds__(256) void head_bwd1_kernel(const float* __restrict_
       for (int j = 0; j < 5; ++j) accw[s][e][j] = 0.f;
     }
   float gbsum = 0.f;
-  for (int64_t r = wave; r < R; r += nw) {
-    const int64_t b = r / Q;
-    const int q = (int)(r - b * Q);
-    const float* gp = gx + b * (int64_t)Q * 5 + q * 5;
-    float go[5];
+  // software pipeline over rows (see head_fwd_kernel): the next row's y and g are loaded before this row's math
+  float4 nv[NS];
+  float ngo[5];
+  auto load_row = [&](int64_t r) {
+    const bool in = r < R;
+    const int64_t rr = in ? r : 0;
+    const float* gp = gx + rr * 5;          // row r = b*Q + q -> g_xhat[b][5q + j]
 #pragma unroll
-    for (int j = 0; j < 5; ++j) go[j] = gp[j];
+    for (int j = 0; j < 5; ++j) ngo[j] = in ? gp[j] : 0.f;
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+      nv[s] = (hp.on[s] && in) ? *reinterpret_cast<const float4*>(y + rr * H + lane * 4 + 256 * s)
+                               : make_float4(0.f, 0.f, 0.f, 0.f);
+  };
+  load_row(wave);
+  for (int64_t r = wave; r < R; r += nw) {
+    float go[5];
+    float4 vrow[NS];
+#pragma unroll
+    for (int j = 0; j < 5; ++j) go[j] = ngo[j];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) vrow[s] = nv[s];
+    load_row(r + nw);
     gbsum += go[0] + go[1] + go[2] + go[3] + go[4];
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
       if (!hp.on[s]) continue;
-      const float4 v = *reinterpret_cast<const float4*>(y + r * H + lane * 4 + 256 * s);
+      const float4 v = vrow[s];
       const float vv[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
@@ -349,18 +372,33 @@ __global__ __launch_bounds__(256) void head_bwd2_kernel(const float* __restrict_
       sgx[s][e] = training ? (float)gsums[H + o] * invn : 0.f;
       accd[s][e] = 0.f;
     }
-  for (int64_t r = wave; r < R; r += nw) {
-    const int64_t b = r / Q;
-    const int q = (int)(r - b * Q);
-    const float* gp = gx + b * (int64_t)Q * 5 + q * 5;
-    float go[5];
+  float4 nv[NS];
+  float ngo[5];
+  auto load_row = [&](int64_t r) {   // software pipeline over rows, as in head_bwd1_kernel
+    const bool in = r < R;
+    const int64_t rr = in ? r : 0;
+    const float* gp = gx + rr * 5;          // row r = b*Q + q -> g_xhat[b][5q + j]
 #pragma unroll
-    for (int j = 0; j < 5; ++j) go[j] = gp[j];
+    for (int j = 0; j < 5; ++j) ngo[j] = in ? gp[j] : 0.f;
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+      nv[s] = (hp.on[s] && in) ? *reinterpret_cast<const float4*>(y + rr * H + lane * 4 + 256 * s)
+                               : make_float4(0.f, 0.f, 0.f, 0.f);
+  };
+  load_row(wave);
+  for (int64_t r = wave; r < R; r += nw) {
+    float go[5];
+    float4 vrow[NS];
+#pragma unroll
+    for (int j = 0; j < 5; ++j) go[j] = ngo[j];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) vrow[s] = nv[s];
+    load_row(r + nw);
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
       if (!hp.on[s]) continue;
       const int o4 = lane * 4 + 256 * s;
-      const float4 v = *reinterpret_cast<const float4*>(y + r * H + o4);
+      const float4 v = vrow[s];
       const float vv[4] = {v.x, v.y, v.z, v.w};
       float g4[4];
 #pragma unroll
@@ -395,6 +433,160 @@ __global__ __launch_bounds__(256) void head_bwd2_kernel(const float* __restrict_
   for (int o = threadIdx.x; o < H; o += blockDim.x) atomicAdd(dby + o, red[o]);
 }
 
+// Channel-split forms of the two backward passes (H a power of two, 64..2048): a row is covered by H/2
+// threads with two channels each, so the per-thread state (BN parameters, ConvT2 taps, accumulators of two
+// channels) stays small enough for 1024-thread workgroups: 16 waves per workgroup keep y streaming at HBM rate
+// while the number of workgroups -- each ends with its per-channel global atomics -- stays at 512.
+struct Head2 {
+  float mean[2], inv[2], gam[2], bet[2], w[2][5];
+  __device__ __forceinline__ void load(const float* st, const float* w2, int H, int c0) {
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int o = c0 + e;
+      mean[e] = st[o];
+      inv[e] = st[H + o];
+      gam[e] = st[2 * H + o];
+      bet[e] = st[3 * H + o];
+#pragma unroll
+      for (int j = 0; j < 5; ++j) w[e][j] = w2[o * 5 + j];
+    }
+  }
+};
+
+__global__ __launch_bounds__(1024) void head_bwd1_cs_kernel(const float* __restrict__ y, int64_t R, int H, int Q,
+                                                           const float* __restrict__ st, const float* __restrict__ w2,
+                                                           const float* __restrict__ gx, double* __restrict__ gsums,
+                                                           float* __restrict__ gw2, float* __restrict__ gb2,
+                                                           float* __restrict__ ggamma, float* __restrict__ gbeta) {
+  extern __shared__ float red[];  // 7*H floats: gw2 (5H), sum g (H), sum g*xn (H)
+  for (int i = threadIdx.x; i < 7 * H; i += blockDim.x) red[i] = 0.f;
+  __syncthreads();
+  const int tpr = H >> 1, rpb = blockDim.x / tpr;
+  const int c0 = (threadIdx.x % tpr) * 2, rg = threadIdx.x / tpr;
+  Head2 hp;
+  hp.load(st, w2, H, c0);
+  float accw[2][5] = {}, accg[2] = {0.f, 0.f}, accgx[2] = {0.f, 0.f};
+  float gbsum = 0.f;
+  const int64_t step = (int64_t)gridDim.x * rpb;
+  float2 nv;
+  float ngo[5];
+  auto load_row = [&](int64_t r) {
+    const bool in = r < R;
+    const int64_t rr = in ? r : 0;
+    const float* gp = gx + rr * 5;          // row r = b*Q + q -> g_xhat[b][5q + j]
+#pragma unroll
+    for (int j = 0; j < 5; ++j) ngo[j] = in ? gp[j] : 0.f;
+    nv = in ? *reinterpret_cast<const float2*>(y + rr * H + c0) : make_float2(0.f, 0.f);
+  };
+  load_row((int64_t)blockIdx.x * rpb + rg);
+  for (int64_t r = (int64_t)blockIdx.x * rpb + rg; r < R; r += step) {
+    float go[5];
+#pragma unroll
+    for (int j = 0; j < 5; ++j) go[j] = ngo[j];
+    const float vv[2] = {nv.x, nv.y};
+    load_row(r + step);
+    if (c0 == 0) gbsum += go[0] + go[1] + go[2] + go[3] + go[4];
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const float xn = (vv[e] - hp.mean[e]) * hp.inv[e];
+      const float bn = xn * hp.gam[e] + hp.bet[e];
+      const float a = gelu_erf_fast(bn);
+      float ga = 0.f;
+#pragma unroll
+      for (int j = 0; j < 5; ++j) {
+        ga = fmaf(go[j], hp.w[e][j], ga);
+        accw[e][j] = fmaf(a, go[j], accw[e][j]);
+      }
+      const float gbn = ga * gelu_erf_grad_fast(bn);
+      accg[e] += gbn;
+      accgx[e] = fmaf(gbn, xn, accgx[e]);
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 2; ++e) {
+    const int o = c0 + e;
+#pragma unroll
+    for (int j = 0; j < 5; ++j) atomicAdd(&red[o * 5 + j], accw[e][j]);
+    atomicAdd(&red[5 * H + o], accg[e]);
+    atomicAdd(&red[6 * H + o], accgx[e]);
+  }
+  if (c0 == 0) atomicAdd(gb2, gbsum);
+  __syncthreads();
+  for (int i = threadIdx.x; i < 5 * H; i += blockDim.x) atomicAdd(gw2 + i, red[i]);
+  for (int o = threadIdx.x; o < H; o += blockDim.x) {
+    atomicAdd(gsums + o, (double)red[5 * H + o]);
+    atomicAdd(gsums + H + o, (double)red[6 * H + o]);
+    if (gbeta) atomicAdd(gbeta + o, red[5 * H + o]);
+    if (ggamma) atomicAdd(ggamma + o, red[6 * H + o]);
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(1024) void head_bwd2_cs_kernel(const float* __restrict__ y, int64_t R, int H, int Q,
+                                                           const float* __restrict__ st, const float* __restrict__ w2,
+                                                           const float* __restrict__ gx,
+                                                           const double* __restrict__ gsums, int training,
+                                                           T* __restrict__ gy, float* __restrict__ dby) {
+  extern __shared__ float red[];  // H
+  for (int i = threadIdx.x; i < H; i += blockDim.x) red[i] = 0.f;
+  __syncthreads();
+  const int tpr = H >> 1, rpb = blockDim.x / tpr;
+  const int c0 = (threadIdx.x % tpr) * 2, rg = threadIdx.x / tpr;
+  Head2 hp;
+  hp.load(st, w2, H, c0);
+  const float invn = 1.0f / (float)R;
+  float sg[2], sgx[2], accd[2] = {0.f, 0.f};
+#pragma unroll
+  for (int e = 0; e < 2; ++e) {
+    sg[e] = training ? (float)gsums[c0 + e] * invn : 0.f;
+    sgx[e] = training ? (float)gsums[H + c0 + e] * invn : 0.f;
+  }
+  const int64_t step = (int64_t)gridDim.x * rpb;
+  float2 nv;
+  float ngo[5];
+  auto load_row = [&](int64_t r) {
+    const bool in = r < R;
+    const int64_t rr = in ? r : 0;
+    const float* gp = gx + rr * 5;          // row r = b*Q + q -> g_xhat[b][5q + j]
+#pragma unroll
+    for (int j = 0; j < 5; ++j) ngo[j] = in ? gp[j] : 0.f;
+    nv = in ? *reinterpret_cast<const float2*>(y + rr * H + c0) : make_float2(0.f, 0.f);
+  };
+  load_row((int64_t)blockIdx.x * rpb + rg);
+  for (int64_t r = (int64_t)blockIdx.x * rpb + rg; r < R; r += step) {
+    float go[5];
+#pragma unroll
+    for (int j = 0; j < 5; ++j) go[j] = ngo[j];
+    const float vv[2] = {nv.x, nv.y};
+    load_row(r + step);
+    float g2[2];
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const float xn = (vv[e] - hp.mean[e]) * hp.inv[e];
+      const float bn = xn * hp.gam[e] + hp.bet[e];
+      float ga = 0.f;
+#pragma unroll
+      for (int j = 0; j < 5; ++j) ga = fmaf(go[j], hp.w[e][j], ga);
+      const float gbn = ga * gelu_erf_grad_fast(bn);
+      const float g = hp.gam[e] * hp.inv[e] * (gbn - sg[e] - xn * sgx[e]);
+      accd[e] += g;
+      g2[e] = g;
+    }
+    if constexpr (sizeof(T) == 2) {
+      bf16 h[2] = {(bf16)g2[0], (bf16)g2[1]};
+      uint32_t u;
+      memcpy(&u, h, 4);
+      *reinterpret_cast<uint32_t*>(gy + r * H + c0) = u;
+    } else {
+      *reinterpret_cast<float2*>(gy + r * H + c0) = make_float2(g2[0], g2[1]);
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 2; ++e) atomicAdd(&red[c0 + e], accd[e]);
+  __syncthreads();
+  for (int o = threadIdx.x; o < H; o += blockDim.x) atomicAdd(dby + o, red[o]);
+}
+
 __global__ __launch_bounds__(256) void mse_fwd_kernel(const float* __restrict__ a, const float* __restrict__ b,
                                                       int64_t n, double* sqerr) {
   double acc = 0.0;
@@ -418,6 +610,16 @@ __global__ void mse_bwd_kernel(const float* __restrict__ a, const float* __restr
 
 __global__ void scalar_add_kernel(const float* a, const float* b, float* out) { out[0] = a[0] + b[0]; }
 __global__ void mse_finalize_kernel(const double* s, int64_t n, float* out) { out[0] = (float)(s[0] / (double)n); }
+
+// channel-split head backward: H / 2 threads per row must divide the 1024-thread workgroup
+int head_wgs() {   // workgroups of the channel-split head passes (AW_HEAD_WGS: tuning override)
+  // 256 measured best at H 512, B 1024: fewer starve the CUs of rows in flight, more serialise on the per-channel
+  // global atomics every workgroup ends with
+  static const int n = [] { const char* e = getenv("AW_HEAD_WGS"); return e ? atoi(e) : 256; }();
+  return n;
+}
+
+bool head_cs_ok(int H) { return H >= 64 && H <= 2048 && (H & (H - 1)) == 0; }
 
 int grid_for(int64_t n, int threads = 256, int cap = 8192) {
   int64_t g = (n + threads - 1) / threads;
@@ -539,8 +741,13 @@ extern "C" int aw_unpatch_head_bwd1(const float* y, int64_t R, int H, int Q, con
   AW_REQUIRE(H % 4 == 0 && H <= 256 * HEAD_MAXV && R % Q == 0, "aw_unpatch_head_bwd1: bad shape");
   if (R == 0) return AW_OK;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  dim3 grid(grid_for(R * 64, 256, 512));
   const size_t sh = 7 * H * sizeof(float);
+  if (head_cs_ok(H)) {
+    hipLaunchKernelGGL(head_bwd1_cs_kernel, dim3(grid_for(R * (H / 2), 1024, head_wgs())), dim3(1024), sh, s, y, R, H, Q,
+                       stats, w2, g_xhat, gsums, gw2, gb2, ggamma, gbeta);
+    return aw::check_launch("aw_unpatch_head_bwd1");
+  }
+  dim3 grid(grid_for(R * 64, 256, 512));
 #define AW_H1(NSV) \
   hipLaunchKernelGGL(head_bwd1_kernel<NSV>, grid, dim3(256), sh, s, y, R, H, Q, stats, w2, g_xhat, gsums, gw2, gb2, \
                      ggamma, gbeta)
@@ -561,8 +768,18 @@ extern "C" int aw_unpatch_head_bwd2(const float* y, int64_t R, int H, int Q, con
   AW_REQUIRE(H % 4 == 0 && H <= 256 * HEAD_MAXV && R % Q == 0, "aw_unpatch_head_bwd2: bad shape");
   if (R == 0) return AW_OK;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  dim3 grid(grid_for(R * 64, 256, 1024));
   const size_t sh = H * sizeof(float);
+  if (head_cs_ok(H)) {
+    dim3 g2(grid_for(R * (H / 2), 1024, head_wgs()));
+    if (gy_dtype == AW_BF16)
+      hipLaunchKernelGGL(head_bwd2_cs_kernel<bf16>, g2, dim3(1024), sh, s, y, R, H, Q, stats, w2, g_xhat, gsums,
+                         training, (bf16*)g_y, db_y);
+    else
+      hipLaunchKernelGGL(head_bwd2_cs_kernel<float>, g2, dim3(1024), sh, s, y, R, H, Q, stats, w2, g_xhat, gsums,
+                         training, (float*)g_y, db_y);
+    return aw::check_launch("aw_unpatch_head_bwd2");
+  }
+  dim3 grid(grid_for(R * 64, 256, 1024));
 #define AW_H2(TY, NSV) \
   hipLaunchKernelGGL((head_bwd2_kernel<TY, NSV>), grid, dim3(256), sh, s, y, R, H, Q, stats, w2, g_xhat, gsums, \
                      training, (TY*)g_y, db_y)
