@@ -195,7 +195,9 @@ int aw_radam_step(float* param, const float* grad, float* exp_avg, float* exp_av
  * corrections and rectification there, in double precision like torch's python-float scalars. */
 int aw_counter_add(int64_t* counter, int64_t v, void* stream);
 /* Global L2 norm of the active segments of `grad` -> out_norm (f32 device scalar) and the clip coefficient
- * min(max_norm/(norm+1e-6), 1) -> out_coef (Lightning gradient_clip_val -> clip_grad_norm_).  ws: f64[1]. */
+ * min(max_norm/(norm+1e-6), 1) -> out_coef (Lightning gradient_clip_val -> clip_grad_norm_).
+ * ws: f64[AW_NORM_WS] scratch (per-workgroup partial sums, reduced in a fixed order: the norm is deterministic). */
+#define AW_NORM_WS 1024
 int aw_grad_norm_clip(const float* grad, const int64_t* seg_off, const int64_t* seg_len, const int* seg_active,
                       int nseg, int64_t total, float max_norm, double* ws, float* out_norm, float* out_coef,
                       void* stream);

@@ -247,7 +247,12 @@ def counter_add(counter, v=1, stream=None):
     call("aw_counter_add", ptr(counter), int(v), stream_ptr(stream))
 
 
+NORM_WS = 1024      # AW_NORM_WS
+
+
 def grad_norm_clip(grad, seg_off, seg_len, seg_active, nseg, max_norm, ws, out_norm, out_coef, stream=None):
+    if ws.numel() < NORM_WS or ws.dtype != torch.float64:
+        raise nat.NativeError(f"grad_norm_clip: ws must hold {NORM_WS} float64")
     call("aw_grad_norm_clip", ptr(grad), ptr(seg_off), ptr(seg_len), ptr(seg_active), int(nseg), grad.numel(),
          float(max_norm), ptr(ws), ptr(out_norm), ptr(out_coef), stream_ptr(stream))
 

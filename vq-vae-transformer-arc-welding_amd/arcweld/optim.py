@@ -102,7 +102,7 @@ class RAdam(torch.optim.Optimizer):
                           off_d=torch.tensor(offs, device=dev, dtype=torch.int64),
                           len_d=torch.tensor(lens, device=dev, dtype=torch.int64),
                           wd_d=torch.tensor([s[3] for s in segs], device=dev, dtype=torch.float32),
-                          ws=torch.zeros(1, device=dev, dtype=torch.float64),
+                          ws=torch.zeros(K.NORM_WS, device=dev, dtype=torch.float64),
                           norm=torch.zeros((), device=dev), coef=torch.ones((), device=dev),
                           step=torch.full((1,), self._step_count, device=dev, dtype=torch.int64))
         self.set_active(self._pending_active)

@@ -142,11 +142,18 @@ __global__ __launch_bounds__(256) void sumsq_kernel(const float* __restrict__ g,
   double d = wave_sum_d((double)acc);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = d;
   __syncthreads();
-  if (threadIdx.x == 0) atomicAdd(ws, red[0] + red[1] + red[2] + red[3]);
+  // one partial per workgroup, summed in a fixed order by clip_coef_kernel: no same-address atomics (1024 of
+  // them serialised into ~40 us) and a deterministic norm
+  if (threadIdx.x == 0) ws[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
 }
 
-__global__ void clip_coef_kernel(const double* ws, float max_norm, float* out_norm, float* out_coef) {
-  const float norm = (float)sqrt(ws[0]);
+__global__ __launch_bounds__(64) void clip_coef_kernel(const double* ws, int nws, float max_norm, float* out_norm,
+                                                       float* out_coef) {
+  double a = 0.0;
+  for (int i = threadIdx.x; i < nws; i += 64) a += ws[i];
+  a = wave_sum_d(a);
+  if (threadIdx.x != 0) return;
+  const float norm = (float)sqrt(a);
   out_norm[0] = norm;
   float c = max_norm / (norm + 1e-6f);
   out_coef[0] = c < 1.0f ? c : 1.0f;
@@ -196,13 +203,12 @@ extern "C" int aw_grad_norm_clip(const float* grad, const int64_t* seg_off, cons
                  nseg <= MAXSEG_LDS && total >= 0 && total % 4 == 0 && ((uintptr_t)grad & 15) == 0,
              "aw_grad_norm_clip: bad args (segments <= %d, 16-B aligned, total %% 4 == 0)", MAXSEG_LDS);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  if (hipMemsetAsync(ws, 0, sizeof(double), s) != hipSuccess) return aw::check_launch("aw_grad_norm_clip memset");
   int64_t g = (total / 4 + 255) / 256;
-  if (g > 1024) g = 1024;
+  if (g > AW_NORM_WS) g = AW_NORM_WS;
   if (g < 1) g = 1;
   hipLaunchKernelGGL(sumsq_kernel, dim3((int)g), dim3(256), 0, s, grad, seg_off, seg_len, seg_active, nseg, total,
                      ws);
-  hipLaunchKernelGGL(clip_coef_kernel, dim3(1), dim3(1), 0, s, ws, max_norm, out_norm, out_coef);
+  hipLaunchKernelGGL(clip_coef_kernel, dim3(1), dim3(64), 0, s, ws, (int)g, max_norm, out_norm, out_coef);
   return aw::check_launch("aw_grad_norm_clip");
 }
 

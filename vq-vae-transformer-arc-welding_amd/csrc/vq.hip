@@ -51,7 +51,23 @@ __global__ __launch_bounds__(VQ_THREADS) void vq_fwd_kernel(const float* __restr
     const int kt = min(KT, K - t0);
     __syncthreads();
     const float4* src = reinterpret_cast<const float4*>(E + (int64_t)t0 * D);
-    for (int i = tid; i < kt * D / 4; i += VQ_THREADS) reinterpret_cast<float4*>(Es)[i] = src[i];
+    {
+      // all of this thread's tile loads first, then the LDS stores: a load -> store loop paid one L2 round trip
+      // per float4 (16 in a row per tile)
+      constexpr int PER = KT * D / 4 / VQ_THREADS;
+      const int n4 = kt * D / 4;
+      float4 tmp[PER];
+#pragma unroll
+      for (int u = 0; u < PER; ++u) {
+        const int i = tid + u * VQ_THREADS;
+        tmp[u] = i < n4 ? src[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int u = 0; u < PER; ++u) {
+        const int i = tid + u * VQ_THREADS;
+        if (i < n4) reinterpret_cast<float4*>(Es)[i] = tmp[u];
+      }
+    }
     for (int c = tid; c < kt; c += VQ_THREADS) {  // |e_k|^2 from global (L2) rows: avoids strided LDS reads
       const float4* ep = reinterpret_cast<const float4*>(E + (int64_t)(t0 + c) * D);
       float s = 0.f;

@@ -796,7 +796,8 @@ extern "C" int aw_unpatch_head_bwd2(const float* y, int64_t R, int H, int Q, con
 extern "C" int aw_mse_fwd(const float* a, const float* b, int64_t n, double* sqerr, void* stream) {
   AW_REQUIRE(a && b && sqerr && n >= 0, "aw_mse_fwd: bad args");
   if (n == 0) return AW_OK;
-  hipLaunchKernelGGL(mse_fwd_kernel, dim3(grid_for(n, 256, 1024)), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+  // few workgroups: each ends with one f64 atomic on the same address (1024 of them serialised into ~14 us)
+  hipLaunchKernelGGL(mse_fwd_kernel, dim3(grid_for(n, 256, 64)), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
                      a, b, n, sqerr);
   return aw::check_launch("aw_mse_fwd");
 }
