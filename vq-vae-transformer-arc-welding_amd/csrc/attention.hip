@@ -158,19 +158,18 @@ __global__ __launch_bounds__(256) void attn_fwd_mfma_kernel(const bf16* __restri
     }
     const bool edge = (k0 + TILE - 1 > qw) || (k0 + TILE > T_);
     float mx = -__builtin_huge_valf();
+    // causal / length mask as selects against one per-lane limit (the per-element `if` compiled to 32 branches)
+    const int lim = min(q, T_ - 1) - (k0 + 4 * hf);
 #pragma unroll
     for (int st = 0; st < 2; ++st)
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        if (edge) {
-          const int key = k0 + 32 * st + 8 * (i >> 2) + 4 * hf + (i & 3);
-          if (key > q || key >= T_) s[st][i] = -__builtin_huge_valf();
-        }
+        if (edge) s[st][i] = (32 * st + 8 * (i >> 2) + (i & 3) > lim) ? -__builtin_huge_valf() : s[st][i];
         mx = fmaxf(mx, s[st][i]);
       }
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
     const float mn = fmaxf(m, mx);
-    const float alpha = exp2f((m - mn) * c2);
+    const float alpha = __builtin_amdgcn_exp2f((m - mn) * c2);   // v_exp_f32: arguments <= 0, -inf -> 0
     const float mc = mn * c2;
     m = mn;
     float ls = 0.f;
@@ -178,7 +177,7 @@ __global__ __launch_bounds__(256) void attn_fwd_mfma_kernel(const bf16* __restri
     for (int st = 0; st < 2; ++st)
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        const float p = exp2f(s[st][i] * c2 - mc);
+        const float p = __builtin_amdgcn_exp2f(s[st][i] * c2 - mc);
         s[st][i] = p;
         ls += p;
       }
@@ -258,13 +257,11 @@ __global__ __launch_bounds__(256) void attn_dq_mfma_kernel(const bf16* __restric
         s = mfma32(row_frag(Ks, 32 * st + r, ks, hf), qf[ks], s);
         dp = mfma32(row_frag(Vs, 32 * st + r, ks, hf), gf[ks], dp);
       }
+      const int lim = min(q, T_ - 1) - (k0 + 32 * st + 4 * hf);
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        float p = exp2f(s[i] * c2 - L2);
-        if (edge) {
-          const int key = k0 + 32 * st + 8 * (i >> 2) + 4 * hf + (i & 3);
-          if (key > q || key >= T_) p = 0.f;
-        }
+        float p = __builtin_amdgcn_exp2f(s[i] * c2 - L2);
+        if (edge) p = (8 * (i >> 2) + (i & 3) > lim) ? 0.f : p;
         s[i] = p * (dp[i] - Dl);
       }
 #pragma unroll
@@ -353,10 +350,10 @@ __global__ __launch_bounds__(256) void attn_dkv_mfma_kernel(const bf16* __restri
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int i = 4 * g4 + e;
-          float pv = exp2f(s[i] * c2 - Lv[e]);
+          float pv = __builtin_amdgcn_exp2f(s[i] * c2 - Lv[e]);
           if (edge) {
             const int qq = q0 + ql + e;
-            if (qq < key || qq >= T_) pv = 0.f;
+            pv = (qq < key || qq >= T_) ? 0.f : pv;
           }
           p[i] = pv;
           s[i] = pv * (dp[i] - Dv[e]);
