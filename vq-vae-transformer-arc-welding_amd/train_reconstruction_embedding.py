@@ -1,8 +1,10 @@
 """VQ-VAE-Patch reconstruction training -- drop-in for the reference's train_reconstruction_embedding.py
 (same flags, model construction, Trainer(gradient_clip_val, early stopping on val/loss, best/last checkpoints),
-final test).  Differences: the ASIMoW data is not available offline, so the windows are synthetic N(0, 1) 200x2
-windows unless ``--data-npz`` points at an .npz with 'train'/'val'/'test' arrays of shape (n, 200, 2); the
-W&B / MLflow loggers are not available (CSVLogger only).
+final test).  Data: ``--data-dir`` reads the reference's ASIMoW CSV (``<dir>/processed_asimow_dataset.csv``,
+split by the reference's val/test (experiment, welding_run) ids, per-channel scaled; arcweld.asimow), or
+``--data-npz`` an .npz with 'train'/'val'/'test' arrays of shape (n, 200, 2); without either the windows are
+synthetic N(0, 1) 200x2 (the dataset is not available offline).  The W&B / MLflow loggers are not available
+(CSVLogger only).
 """
 import argparse
 import logging as log
@@ -33,6 +35,11 @@ def main(hparams):
     logger.log_hyperparams({"model_name": hparams.model_name, "clipping_value": hparams.clipping_value,
                             **vars(hparams)})
     data = load_windows(hparams.data_npz, dev) if hparams.data_npz else None
+    if hparams.data_dir:
+        from arcweld import asimow
+        ids = asimow.REFERENCE_SPLIT_IDS
+        ds = asimow.load(hparams.data_dir, ids["val_ids"], ids["test_ids"], task="reconstruction", seed=hparams.seed)
+        data = tuple(ds.tensors(s, device=dev)[0] for s in ("train", "val", "test"))
     data_module = ReconstructionDataModule(batch_size=hparams.batch_size, n_train=hparams.n_train,
                                            n_val=hparams.n_val, n_test=hparams.n_test, seed=hparams.seed,
                                            device=dev, data=data)
@@ -88,6 +95,7 @@ def parser():
     p.add_argument('--logging-project', type=str, default="asimow-vq-vae")
     # data source (this build): synthetic windows or an .npz of real windows
     p.add_argument('--data-npz', type=str, default="")
+    p.add_argument('--data-dir', type=str, default="", help="directory holding processed_asimow_dataset.csv")
     p.add_argument('--n-train', type=int, default=8192)
     p.add_argument('--n-val', type=int, default=1024)
     p.add_argument('--n-test', type=int, default=1024)
