@@ -234,6 +234,12 @@ int aw_attn_fwd(const void* qkv, int64_t B, int T, int n_head, int d, int dtype,
 /* dqkv (B*T, 3d, dtype) from dy (B*T, d, dtype), recomputing P from lse; ws: f32 B*n_head*T (delta). */
 int aw_attn_bwd(const void* qkv, const void* y, const void* dy, const float* lse, int64_t B, int T, int n_head,
                 int d, int dtype, void* dqkv, float* ws, void* stream);
+/* KV-cache decode attention (MyTransformerDecoder.generate, model/transformer_decoder.py:203-224):
+ * n_new query rows per sequence at absolute positions pos0 .. pos0+n_new-1 (qkv_new (B*n_new, 3d, dtype), row
+ * b*n_new + i).  Their K and V are appended to kv_cache (B, Tmax, 2d, dtype; row b*Tmax + t = [K | V]) and
+ * y (B*n_new, d, dtype) = softmax(q k^T / sqrt(hs)) v over the cached positions 0 .. pos0+i (causal). */
+int aw_attn_decode(const void* qkv_new, int64_t B, int n_new, int pos0, int n_head, int d, int dtype,
+                   void* kv_cache, int Tmax, void* y, void* stream);
 /* Cross entropy with ignore_index (transformer_decoder.py:226-230): logits (R, V) f32 with row stride ldl;
  * loss_sum (f64, zero on entry) += sum over kept rows of (lse - logit[y]); count (f64) += kept rows.
  * The backward writes dlogits = (softmax - onehot) * g / count (g device scalar) into dlogits (dtype) and zeros

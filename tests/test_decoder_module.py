@@ -202,3 +202,44 @@ def test_sequence_longer_than_mask_raises():
     with pytest.raises(RuntimeError):
         with torch.no_grad():
             m(torch.zeros(1, 40, dtype=torch.long, device="cuda"))
+
+
+@pytest.fixture
+def fp32_mode():
+    old = torch.get_float32_matmul_precision()
+    torch.set_float32_matmul_precision("highest")
+    yield
+    torch.set_float32_matmul_precision(old)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n_head", [4, 2])
+def test_kv_cache_prefill_and_decode_match_full_forward(fp32_mode, n_head):
+    """forward_cached: the prefill's last-position logits and each cached decode step equal the
+    reference's full recompute (forward over the whole prefix) within the fp32 tolerance."""
+    from arcweld import decoder as dec
+    m = make_model(SMALL, n_head, 401, device="cuda").eval()
+    B, T0 = 3, 7
+    x = torch.tensor(gen.randint(450, (B, 20), 0, SMALL["n_classes"]), device="cuda")
+    cache = dec.KVCache(m, B, SMALL["seq_len"])
+    got = dec.forward_cached(m, x[:, :T0], cache, 0)
+    with torch.no_grad():
+        ref = m(x[:, :T0])[:, -1]
+    torch.testing.assert_close(got, ref, rtol=1e-4, atol=1e-4)
+    for t in range(T0, 20):
+        got = dec.forward_cached(m, x[:, t:t + 1], cache, t)
+        with torch.no_grad():
+            ref = m(x[:, :t + 1])[:, -1]
+        torch.testing.assert_close(got, ref, rtol=1e-4, atol=1e-4, msg=f"position {t}")
+
+
+@pytest.mark.gpu
+def test_cached_generate_matches_reference_recompute(fp32_mode):
+    """generate(use_cache=True) produces the same greedy continuation as the reference's recompute loop,
+    including the steps after the context is cropped to seq_len (the cache is re-prefilled there)."""
+    m = make_model(SMALL, 4, 403, device="cuda").eval()
+    x = torch.tensor(gen.randint(451, (2, 9), 0, SMALL["n_classes"]), device="cuda")
+    a = m.generate(x, use_cache=True)
+    b = m.generate(x, use_cache=False)
+    assert a.shape == (2, 9 + SMALL["seq_len"])
+    assert torch.equal(a, b)

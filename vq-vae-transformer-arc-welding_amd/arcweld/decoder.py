@@ -261,3 +261,78 @@ def cross_entropy(logits2d, target, ignore_index=-100):
     if logits2d.stride(-1) != 1:
         raise ValueError("logits rows must be contiguous")
     return _CrossEntropy.apply(logits2d, target, ignore_index)
+
+
+class KVCache:
+    """Per-block key/value cache for incremental decoding: (B, Tmax, 2d) rows [K | V] in the operand dtype, plus
+    the operand copies of the block weights (cast once per generate call)."""
+
+    def __init__(self, m, B, Tmax, dtype=None):
+        self.T_ = operand_dtype(dtype)
+        dev = m.lm_head.weight.device
+        d = m.d_model
+        self.B, self.Tmax = B, Tmax
+        self.kv = [torch.empty(B, Tmax, 2 * d, device=dev, dtype=self.T_) for _ in m.transformer.h]
+        self.wops, casts = [], []
+        for blk in m.transformer.h:
+            ws = []
+            for lin in (blk.attn.c_attn, blk.attn.c_proj, blk.mlp.c_fc, blk.mlp.c_proj):
+                w = lin.weight
+                if self.T_ == w.dtype:
+                    ws.append(w)
+                else:
+                    o = torch.empty(w.shape, device=dev, dtype=self.T_)
+                    casts.append((w, w.shape[0], w.shape[1], 1, 0, 5, o))
+                    ws.append(o)
+            self.wops.append(ws)
+        K.weight_relayout_batch(casts)
+        V = m.n_classes
+        self.Wlm = torch.zeros(_pad8(V), d, device=dev, dtype=self.T_)
+        K.cast(m.lm_head.weight, self.Wlm[:V])
+
+
+@torch.no_grad()
+def forward_cached(m, ids_new, cache: KVCache, pos0: int):
+    """Eval forward of n_new tokens per sequence at positions pos0 .. pos0+n_new-1 against the cached keys and
+    values of positions < pos0 (appending their own); returns the logits of the LAST new position (B, V) f32.
+    pos0 = 0 with the whole prompt is the prefill; n_new = 1 the decode step (model/transformer_decoder.py:203-224
+    recomputes the whole prefix instead -- same values, the cached keys of a position never change while the
+    context is not cropped)."""
+    B, n = ids_new.shape
+    d, nh, V = m.d_model, m.n_head, m.n_classes
+    T_ = cache.T_
+    if pos0 + n > cache.Tmax:
+        raise RuntimeError(f"KV cache holds {cache.Tmax} positions, asked for {pos0 + n}")
+    pe = m.embedding.positional_embedding.pe
+    if pos0 + n > pe.shape[1]:
+        raise RuntimeError(f"positions beyond the positional table ({pe.shape[1]} rows, model/embedding.py:49-50)")
+    R = B * n
+    dev = ids_new.device
+    e = lambda *s, dt=F32: torch.empty(*s, device=dev, dtype=dt)  # noqa: E731
+    x = e(R, d)
+    K.embed_fwd(ids_new.contiguous(), m.embedding.latent_embedding.weight, pe[0, pos0:], x)
+    for i, blk in enumerate(m.transformer.h):
+        at, mlp = blk.attn, blk.mlp
+        Wqkv, Wo, Wfc, Wp = cache.wops[i]
+        a, mu, rs = e(R, d, dt=T_), e(R), e(R)
+        K.layernorm_fwd(x, blk.ln_1.weight, blk.ln_1.bias, blk.ln_1.eps, a, mu, rs)
+        qkv = e(R, 3 * d, dt=T_)
+        K.gemm(a, Wqkv, R, 3 * d, d, bias=at.c_attn.bias, C=qkv)
+        y = e(R, d, dt=T_)
+        K.attn_decode(qkv, B, n, pos0, nh, d, cache.kv[i], y)
+        x1 = e(R, d)
+        K.gemm(y, Wo, R, d, d, bias=at.c_proj.bias, resid=x, C=x1)
+        a2 = e(R, d, dt=T_)
+        K.layernorm_fwd(x1, blk.ln_2.weight, blk.ln_2.bias, blk.ln_2.eps, a2, mu, rs)
+        h, g = e(R, 4 * d, dt=T_), e(R, 4 * d, dt=T_)
+        K.gemm(a2, Wfc, R, 4 * d, d, bias=mlp.c_fc.bias, act=K.AW_ACT_GELU_TANH, C=h, C2=g, c2_mode=1)
+        x2 = e(R, d)
+        K.gemm(g, Wp, R, d, 4 * d, bias=mlp.c_proj.bias, resid=x1, C=x2)
+        x = x2
+    lnf = m.transformer.ln_f
+    xf, muf, rsf = e(R, d, dt=T_), e(R), e(R)
+    K.layernorm_fwd(x, lnf.weight, lnf.bias, lnf.eps, xf, muf, rsf)
+    last = xf.view(B, n, d)[:, n - 1]                     # (B, d) rows of stride n*d: the GEMM takes lda
+    logits = e(B, V)
+    K.gemm(last, cache.Wlm, B, V, d, C=logits)
+    return logits

@@ -305,6 +305,14 @@ def attn_bwd(qkv, y, dy, lse, B, T, n_head, d, dqkv, ws, stream=None):
          ptr(ws), stream_ptr(stream))
 
 
+def attn_decode(qkv_new, B, n_new, pos0, n_head, d, kv_cache, y, stream=None):
+    """KV-cache attention for n_new rows per sequence at positions pos0..; kv_cache (B, Tmax, 2d)."""
+    if kv_cache.dtype != qkv_new.dtype or y.dtype != qkv_new.dtype or kv_cache.shape[-1] != 2 * d:
+        raise nat.NativeError("attn_decode: qkv, cache and y share a dtype; cache rows are [K | V] (2d)")
+    call("aw_attn_decode", ptr(qkv_new), B, n_new, pos0, n_head, d, dtype_code(qkv_new.dtype), ptr(kv_cache),
+         kv_cache.shape[1], ptr(y), stream_ptr(stream))
+
+
 def ce_fwd(logits, V, y, ignore_index, loss_sum, count, lse, stream=None):
     R = y.numel()
     call("aw_ce_fwd", ptr(logits), R, V, logits.stride(0), ptr(y), int(ignore_index), ptr(loss_sum), ptr(count),

@@ -700,6 +700,90 @@ extern "C" int aw_embed_bwd(const int64_t* ids, int64_t B, int T, int D, const f
     else hipLaunchKernelGGL((KERNEL<float, HSV>), __VA_ARGS__);                                  \
   } while (0)
 
+// ---------------------------------------------------------------- KV-cache decode (generate)
+// cache (B, Tmax, 2d) rows [K | V]; the new rows' K and V are appended first (their own launch, so no wave reads
+// a cache row another wave of the same launch is writing), then one wave per (query row, head) attends over
+// positions 0..pos0+i: pass 1 scores one key per lane into LDS with the running max, pass 2 exponentiates and
+// sums, pass 3 gives each lane one head dimension and walks the keys (p broadcast from LDS).  f32 arithmetic.
+template <typename T>
+__global__ void kv_append_kernel(const T* __restrict__ qkv, int64_t B, int n_new, int pos0, int d,
+                                 T* __restrict__ cache, int Tmax) {
+  const int64_t total = B * n_new * 2 * (int64_t)d;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = e / (2 * d);                 // new row b*n_new + i
+    const int c = (int)(e - r * 2 * d);            // column within [K | V]
+    const int64_t b = r / n_new;
+    const int i = (int)(r - b * n_new);
+    cache[(b * Tmax + pos0 + i) * 2 * d + c] = qkv[r * 3 * d + d + c];
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(64) void attn_decode_kernel(const T* __restrict__ qkv, int n_new, int pos0, int nh,
+                                                         int d, const T* __restrict__ cache, int Tmax,
+                                                         T* __restrict__ y, float scale) {
+  extern __shared__ float sc[];                    // Tmax scores
+  const int lane = threadIdx.x;
+  const int64_t r = blockIdx.x;                    // new row b*n_new + i
+  const int h = blockIdx.y;
+  const int64_t b = r / n_new;
+  const int i = (int)(r - b * n_new);
+  const int hs = d / nh;
+  const int nk = pos0 + i + 1;                     // causal: keys 0 .. pos0 + i
+  const T* q = qkv + r * 3 * d + h * hs;
+  const T* kv = cache + b * (int64_t)Tmax * 2 * d;
+  float mx = -__builtin_huge_valf();
+  for (int j = lane; j < nk; j += 64) {
+    const T* k = kv + (int64_t)j * 2 * d + h * hs;
+    float dot = 0.f;
+    for (int e = 0; e < hs; ++e) dot = fmaf(to_f32<T>(q[e]), to_f32<T>(k[e]), dot);
+    const float s = dot * scale;
+    sc[j] = s;
+    mx = fmaxf(mx, s);
+  }
+  mx = wave_max(mx);
+  float sum = 0.f;
+  for (int j = lane; j < nk; j += 64) {
+    const float p = __expf(sc[j] - mx);
+    sc[j] = p;
+    sum += p;
+  }
+  sum = wave_sum(sum);
+  __syncthreads();
+  const float inv = 1.f / sum;
+  for (int e = lane; e < hs; e += 64) {
+    float acc = 0.f;
+    for (int j = 0; j < nk; ++j) acc = fmaf(sc[j], to_f32<T>(kv[(int64_t)j * 2 * d + d + h * hs + e]), acc);
+    y[r * d + h * hs + e] = from_f32<T>(acc * inv);
+  }
+}
+
+extern "C" int aw_attn_decode(const void* qkv_new, int64_t B, int n_new, int pos0, int n_head, int d, int dtype,
+                              void* kv_cache, int Tmax, void* y, void* stream) {
+  AW_REQUIRE(qkv_new && kv_cache && y && B >= 0 && n_new > 0 && pos0 >= 0 && n_head > 0 && d % n_head == 0 &&
+                 pos0 + n_new <= Tmax,
+             "aw_attn_decode: bad args (pos0 + n_new must fit the cache of Tmax positions)");
+  if (B == 0) return AW_OK;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const int64_t tot = B * n_new * 2 * (int64_t)d;
+  const int g = (int)((tot + 255) / 256 > 4096 ? 4096 : (tot + 255) / 256);
+  const float scale = 1.0f / sqrtf((float)(d / n_head));
+  dim3 grid((unsigned)(B * n_new), n_head);
+  const size_t sh = (size_t)Tmax * sizeof(float);
+  if (dtype == AW_BF16) {
+    hipLaunchKernelGGL(kv_append_kernel<bf16>, dim3(g), dim3(256), 0, s, (const bf16*)qkv_new, B, n_new, pos0, d,
+                       (bf16*)kv_cache, Tmax);
+    hipLaunchKernelGGL(attn_decode_kernel<bf16>, grid, dim3(64), sh, s, (const bf16*)qkv_new, n_new, pos0, n_head, d,
+                       (const bf16*)kv_cache, Tmax, (bf16*)y, scale);
+  } else {
+    hipLaunchKernelGGL(kv_append_kernel<float>, dim3(g), dim3(256), 0, s, (const float*)qkv_new, B, n_new, pos0, d,
+                       (float*)kv_cache, Tmax);
+    hipLaunchKernelGGL(attn_decode_kernel<float>, grid, dim3(64), sh, s, (const float*)qkv_new, n_new, pos0, n_head,
+                       d, (const float*)kv_cache, Tmax, (float*)y, scale);
+  }
+  return aw::check_launch("aw_attn_decode");
+}
+
 extern "C" int aw_attn_fwd(const void* qkv, int64_t B, int T, int n_head, int d, int dtype, void* y, float* lse,
                            void* stream) {
   AW_REQUIRE(qkv && y && lse && B >= 0 && T > 0 && n_head > 0 && d % n_head == 0, "aw_attn_fwd: bad args");

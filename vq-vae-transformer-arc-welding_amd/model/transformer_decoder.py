@@ -189,9 +189,16 @@ class MyTransformerDecoder(LightningModule):
             self.log_classification_results(loss, logits, labels, "test")
         return loss
 
-    def generate(self, x, do_sample=False, top_k=None):
+    def generate(self, x, do_sample=False, top_k=None, use_cache=True):
         """Autoregressive continuation by seq_len tokens (reference :203-224): greedy (top-1) or multinomial
-        sampling, context cropped to the last seq_len tokens."""
+        sampling, context cropped to the last seq_len tokens.
+
+        use_cache (default): the prompt is prefilled once and each new token is one cached decode step
+        (arcweld.decoder.forward_cached, aw_attn_decode); once the context is cropped every position moves, so
+        those steps re-prefill the window -- what the reference computes at every step.  use_cache=False runs
+        the reference's full recompute through forward()."""
+        if use_cache:
+            return self._generate_cached(x, do_sample, top_k)
         with torch.no_grad():
             for _ in range(self.seq_len):
                 x_cond = x if x.size(1) <= self.seq_len else x[:, -self.seq_len:]
@@ -206,6 +213,32 @@ class MyTransformerDecoder(LightningModule):
                 else:
                     _, idx_next = torch.topk(probs, k=1, dim=-1)
                 x = torch.cat([x, idx_next], dim=-1)
+        return x
+
+    @torch.no_grad()
+    def _generate_cached(self, x, do_sample, top_k):
+        cache = engine.KVCache(self, x.size(0), self.seq_len)
+        filled = 0                      # positions of x[:, :filled] are in the cache
+        for _ in range(self.seq_len):
+            L = x.size(1)
+            if L > self.seq_len:        # cropped window: every position shifted, prefill it again
+                logits = engine.forward_cached(self, x[:, -self.seq_len:], cache, 0)
+                filled = 0
+            elif filled == 0:
+                logits = engine.forward_cached(self, x, cache, 0)
+                filled = L
+            else:
+                logits = engine.forward_cached(self, x[:, filled:], cache, filled)
+                filled = L
+            if top_k is not None:
+                v, _ = torch.topk(logits, top_k)
+                logits = logits.masked_fill(logits < v[:, [-1]], -float('Inf'))
+            probs = torch.softmax(logits, dim=-1)
+            if do_sample:
+                idx_next = torch.multinomial(probs, num_samples=1)
+            else:
+                _, idx_next = torch.topk(probs, k=1, dim=-1)
+            x = torch.cat([x, idx_next], dim=-1)
         return x
 
     def loss_gen(self, logits, labels):
