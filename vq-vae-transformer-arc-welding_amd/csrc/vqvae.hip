@@ -81,30 +81,33 @@ __device__ __forceinline__ int64_t relayout_count(const aw_relayout_job& jb) {
 
 template <typename T>
 __global__ __launch_bounds__(256) void relayout_batch_kernel(RelayoutJobs J) {
+  // 32-bit unsigned index math (every job is < 2^31 elements, checked on the host): the int64 divisions by
+  // runtime extents cost more than the copy itself
   const aw_relayout_job& jb = J.j[blockIdx.y];
   const float* __restrict__ W = jb.W;
   T* __restrict__ out = reinterpret_cast<T*>(jb.out);
-  const int O = jb.O, I = jb.I, k = jb.k, tap = jb.tap, mode = jb.mode;
-  const int64_t ldo = jb.ldo, n = relayout_count(jb);
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
+  const uint32_t O = jb.O, I = jb.I, k = jb.k, tap = jb.tap, ldo = (uint32_t)jb.ldo;
+  const int mode = jb.mode;
+  const uint32_t n = (uint32_t)relayout_count(jb);
+  for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x) {
     float v;
     if (mode == 0) {
-      const int64_t o = e / I, i = e - o * I;
+      const uint32_t o = e / I, i = e - o * I;
       v = W[(o * I + i) * k + tap];
     } else if (mode == 1) {
-      const int64_t o = e / (3 * I), r = e - o * 3 * I;
-      const int64_t j = r / I, i = r - j * I;
+      const uint32_t o = e / (3 * I), r = e - o * 3 * I;
+      const uint32_t j = r / I, i = r - j * I;
       v = W[(o * I + i) * 3 + j];
     } else if (mode == 2) {
-      const int64_t jo = e / I, i = e - jo * I;
-      const int64_t j = jo / O, o = jo - j * O;
+      const uint32_t jo = e / I, i = e - jo * I;
+      const uint32_t j = jo / O, o = jo - j * O;
       v = W[(o * I + i) * 3 + j];
     } else if (mode == 3) {
-      const int64_t jo = e / I, i = e - jo * I;
-      const int64_t j = jo / O, o = jo - j * O;
+      const uint32_t jo = e / I, i = e - jo * I;
+      const uint32_t j = jo / O, o = jo - j * O;
       v = W[(i * O + o) * k + j];
     } else if (mode == 4) {
-      const int64_t o = e / ldo, j = e - o * ldo;
+      const uint32_t o = e / ldo, j = e - o * ldo;
       v = j < k ? W[o * k + j] : 0.f;
     } else {
       v = W[e];
@@ -670,6 +673,8 @@ extern "C" int aw_weight_relayout_batch(const aw_relayout_job* jobs, int n, int 
     AW_REQUIRE(jb.W && jb.out && jb.O > 0 && jb.I > 0 && jb.k > 0 && jb.mode >= 0 && jb.mode <= 5,
                "aw_weight_relayout_batch: bad job %d", i);
     AW_REQUIRE(!(jb.mode == 4 && jb.ldo < jb.k), "aw_weight_relayout_batch: job %d ldo < k", i);
+    AW_REQUIRE((int64_t)jb.O * jb.I * (jb.k > 3 ? jb.k : 3) < (1ll << 31) && (int64_t)jb.O * jb.ldo < (1ll << 31),
+               "aw_weight_relayout_batch: job %d exceeds 2^31 elements", i);
     J.j[i] = jb;
     const int64_t c = jb.mode == 4 ? (int64_t)jb.O * jb.ldo
                                     : (int64_t)jb.O * jb.I * (jb.mode == 0 || jb.mode == 5 ? 1 : (jb.mode == 3 ? jb.k : 3));
