@@ -115,7 +115,7 @@ __device__ __forceinline__ void store4_bf16(bf16* dst, const f32x16& a, int g4, 
 
 // ---------------------------------------------------------------- forward
 // grid (ceil(T/128), n_head, B), 256 threads; wave w owns queries qb*128 + 32w .. +31.
-__global__ __launch_bounds__(256) void attn_fwd_mfma_kernel(const bf16* __restrict__ qkv, int T_, int nh, int d,
+__global__ __launch_bounds__(256, 2) void attn_fwd_mfma_kernel(const bf16* __restrict__ qkv, int T_, int nh, int d,
                                                             bf16* __restrict__ y, float* __restrict__ lse,
                                                             float c2, float scale) {
   __shared__ __attribute__((aligned(16))) char Ks[IMG];
@@ -208,7 +208,7 @@ __global__ __launch_bounds__(256) void attn_fwd_mfma_kernel(const bf16* __restri
 }
 
 // ---------------------------------------------------------------- dQ (query-stationary)
-__global__ __launch_bounds__(256) void attn_dq_mfma_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ dy,
+__global__ __launch_bounds__(256, 2) void attn_dq_mfma_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ dy,
                                                            const float* __restrict__ lse,
                                                            const float* __restrict__ delta, int T_, int nh, int d,
                                                            bf16* __restrict__ dqkv, float c2, float scale) {
@@ -283,7 +283,7 @@ __global__ __launch_bounds__(256) void attn_dq_mfma_kernel(const bf16* __restric
 
 // ---------------------------------------------------------------- dK, dV (key-stationary)
 // grid (ceil(T/128), n_head, B); wave w owns keys kb*128 + 32w .. +31; query tiles from the block's first key on.
-__global__ __launch_bounds__(256) void attn_dkv_mfma_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ dy,
+__global__ __launch_bounds__(256, 2) void attn_dkv_mfma_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ dy,
                                                             const float* __restrict__ lse,
                                                             const float* __restrict__ delta, int T_, int nh, int d,
                                                             bf16* __restrict__ dqkv, float c2, float scale) {
