@@ -35,7 +35,15 @@ constexpr int ROWB = 128;                // bytes of K per operand row per step 
 constexpr int CPITCH = BN + 4;           // f32 pitch of the epilogue tile
 
 template <int BMT> struct Cfg;
+#ifndef AW_W8
+#define AW_W8 1
+#endif
+#if AW_W8
+// 128-row tile, 8 waves of 32x64: 4 waves per SIMD at two workgroups per CU (MINB = min waves per SIMD)
+template <> struct Cfg<128> { static constexpr int NTH = 512, NSTAGE = 2, MINB = 4; };
+#else
 template <> struct Cfg<128> { static constexpr int NTH = 256, NSTAGE = 2, MINB = 2; };
+#endif
 template <> struct Cfg<256> { static constexpr int NTH = 512, NSTAGE = 3, MINB = 1; };
 template <int BMT> constexpr int stage_bytes() { return (BMT + BN) * ROWB; }
 template <int BMT> constexpr int smem_bytes() {
@@ -437,6 +445,8 @@ __global__ __launch_bounds__(Cfg<BMT>::NTH, RAGGED ? 1 : Cfg<BMT>::MINB) void ge
   const int tid = threadIdx.x;
   const int lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
+  constexpr int WR = BMT / (NTH / 128);            // rows per wave (waves form (NTH/128) x 2)
+  constexpr int FM = WR / 16;                      // 16-row A fragments per wave
   int tile = xcd_remap(blockIdx.x, P.nblocks);
   const void* Aptr = p.A;
   const void* Bptr = p.B;
@@ -468,34 +478,33 @@ __global__ __launch_bounds__(Cfg<BMT>::NTH, RAGGED ? 1 : Cfg<BMT>::MINB) void ge
   }
   const bool do_rowsum = rowptr != nullptr && tn == 0;
 
-  f32x4 acc[4][4];
+  f32x4 acc[FM][4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < FM; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   // fused A-row sums (bias gradients) from the A fragments already in registers: waves wn == 0 of the tn == 0
   // tiles add their 8 (bf16) / 4 (f32) k-values per fragment; the lane groups are reduced once at the end
   constexpr bool ROWSUM_OK = (EPI & EP_GENERIC) || (EPI & EP_ACCUM);   // bias gradients: weight-gradient launches
   const bool wave_rowsum = ROWSUM_OK && do_rowsum && wn == 0;
-  float rowacc[4] = {0.f, 0.f, 0.f, 0.f};
+  float rowacc[FM] = {};
 
   auto compute = [&](const char* a_l) {
     const char* b_l = a_l + A_IMG;
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-      uint4 af[4], bfr[4];
+      uint4 af[FM], bfr[4];
 #pragma unroll
-      for (int f = 0; f < 4; ++f) {
-        af[f] = frag<T, ATR, BMT * (int)sizeof(T)>(a_l, wm * 64 + f * 16, lane, u);
-        bfr[f] = frag<T, BTR, BN * (int)sizeof(T)>(b_l, wn * 64 + f * 16, lane, u);
-      }
+      for (int f = 0; f < FM; ++f) af[f] = frag<T, ATR, BMT * (int)sizeof(T)>(a_l, wm * WR + f * 16, lane, u);
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int f = 0; f < 4; ++f) bfr[f] = frag<T, BTR, BN * (int)sizeof(T)>(b_l, wn * 64 + f * 16, lane, u);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) Mfma<T>::run(acc[i][j], af[i], bfr[j]);
       if (wave_rowsum) {
 #pragma unroll
-        for (int f = 0; f < 4; ++f) rowacc[f] += frag_sum<T>(af[f]);
+        for (int f = 0; f < FM; ++f) rowacc[f] += frag_sum<T>(af[f]);
       }
     }
   };
@@ -590,11 +599,11 @@ __global__ __launch_bounds__(Cfg<BMT>::NTH, RAGGED ? 1 : Cfg<BMT>::MINB) void ge
   AW_STAMP(2);
   if (wave_rowsum) {
 #pragma unroll
-    for (int f = 0; f < 4; ++f) {
+    for (int f = 0; f < FM; ++f) {
       float v = rowacc[f];
       v += __shfl_xor(v, 16, 64);
       v += __shfl_xor(v, 32, 64);
-      const int r = m0 + wm * 64 + f * 16 + lane;
+      const int r = m0 + wm * WR + f * 16 + lane;
       if (lane < 16 && r < M) atomicAdd(rowptr + r, v);
     }
   }
@@ -611,12 +620,12 @@ __global__ __launch_bounds__(Cfg<BMT>::NTH, RAGGED ? 1 : Cfg<BMT>::MINB) void ge
   {
     const int cq = lane & 15, rq = (lane >> 4) * 4;
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < FM; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j)
 #pragma unroll
         for (int r = 0; r < 4; ++r)
-          Cs[(wm * 64 + i * 16 + rq + r) * CPITCH + wn * 64 + j * 16 + cq] = acc[i][j][r];
+          Cs[(wm * WR + i * 16 + rq + r) * CPITCH + wn * 64 + j * 16 + cq] = acc[i][j][r];
   }
   __syncthreads();
   AW_STAMP(3);
