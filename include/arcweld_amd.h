@@ -168,6 +168,31 @@ int aw_unpatch_head_bwd1(const float* y, int64_t R, int H, int Q, const float* s
 int aw_unpatch_head_bwd2(const float* y, int64_t R, int H, int Q, const float* stats, const float* w2,
                          const float* g_xhat, const double* gsums, int training, void* g_y, int gy_dtype, float* db_y,
                          void* stream);
+/* BatchNorm1d of the `--batchnorm 1` ResBlocks (model/vq_vae_patch_embedd.py:60-74).  Activations h are
+ * [N rows][H channels] f32; statistics are per (group, channel), group = row % G (decoder G = 1; encoder G = S
+ * token positions, each its own batch of B rows: CNNBlock(seperate=True) runs the blocks per token slice).
+ * stats sums: double [2][G][H] (sum, sum of squares), zero on entry.
+ * finalize: stats f32 [4][G][H] = mean, invstd, gamma, beta; training: batch statistics (biased variance) and
+ *   the running statistics moved once per group in group order (unbiased variance, momentum), *nbt += G;
+ *   eval: the running statistics for every group.
+ * apply: mode 0: out = BN(h), op = GELU(out); mode 1: out = resid + dropout(BN(h)) (mask of element r*H + c
+ *   from aw_seed_mix(drop_seed, seed_ptr), as the GEMM epilogues), op = GELU(out) or NULL; mode 2: as mode 1
+ *   with op = out (no GELU).  op in op_dtype.
+ * bwd_reduce: t = g_in * dropout mask; sums [2][G][H] += (sum t, sum t * xhat), zero on entry.
+ * bwd_apply: dh (dh_dtype) = gamma*invstd*(t - S1/n - xhat*S2/n) (training) or gamma*invstd*t (eval);
+ *   dgamma += sum_g S2, dbeta += sum_g S1 (either may be NULL).  n = rows per group. */
+int aw_bn_group_stats(const float* h, int64_t N, int H, int G, double* sums, void* stream);
+int aw_bn_group_finalize(const double* sums, int64_t n, int H, int G, const float* gamma, const float* beta,
+                         float* running_mean, float* running_var, int64_t* nbt, float eps, float momentum,
+                         int training, float* stats, void* stream);
+int aw_bn_apply(const float* h, int64_t N, int H, int G, const float* stats, int mode, const float* resid,
+                float drop_p, uint64_t drop_seed, const uint64_t* seed_ptr, float* out, void* op, int op_dtype,
+                void* stream);
+int aw_bn_bwd_reduce(const float* h, int64_t N, int H, int G, const float* stats, const float* g_in, float drop_p,
+                     uint64_t drop_seed, const uint64_t* seed_ptr, double* sums, void* stream);
+int aw_bn_bwd_apply(const float* h, int64_t N, int H, int G, const float* stats, const float* g_in, float drop_p,
+                    uint64_t drop_seed, const uint64_t* seed_ptr, const double* sums, int64_t n, int training,
+                    void* dh, int dh_dtype, float* dgamma, float* dbeta, void* stream);
 /* Mean-squared error (F.mse_loss, autencoder_lightning_base.py:82): sqerr[0] (f64, zero on entry) += sum (a-b)^2;
  * backward: ga = 2(a-b)/n * g (device scalar g). */
 int aw_mse_fwd(const float* a, const float* b, int64_t n, double* sqerr, void* stream);

@@ -95,6 +95,41 @@ def test_vqvae_train_step_parity_fp32(fname, fp32_parity):
 
 
 @pytest.mark.gpu
+def test_vqvae_batchnorm_resblocks_parity_fp32(fp32_parity):
+    """`--batchnorm 1` ResBlocks (vq_vae_patch_embedd.py:60-74): per-token BatchNorm statistics in the encoder
+    (its blocks run on every token slice separately), per-channel in the decoder; one train step against the
+    reference's golden output, gradients (BN weights and biases included), running statistics and
+    num_batches_tracked (S per encoder BN, 1 per decoder BN), then the eval forward on the updated running stats."""
+    from arcweld.functional import mse_loss
+    kw = dict(hidden_dim=64, num_embeddings=64, embedding_dim=16, n_resblocks=2, patch_size=25)
+    g = golden("vqvae_small_bn.npz")
+    m = make_model(kw, 303, "cuda", batch_norm=True).train()
+    x = torch.tensor(gen.windows(304, 8), device="cuda")
+    emb, x_hat, perp = m(x)
+    recon = mse_loss(x_hat, x)
+    loss = recon + emb
+    loss.backward()
+    assert np.array_equal(m._last_indices.cpu().numpy(), g["idx"])
+    np.testing.assert_allclose(x_hat.detach().cpu().numpy(), g["x_hat"], rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(loss.item(), g["loss"], rtol=1e-4)
+    _check_grads(m, g)
+    sd = m.state_dict()
+    for k in g.files:
+        if k.startswith("state/"):
+            ref = g[k]
+            got = sd[k[6:]].cpu().numpy()
+            if "num_batches_tracked" in k:
+                assert int(got) == int(ref), k
+            else:
+                np.testing.assert_allclose(got, ref, rtol=1e-4, atol=1e-5, err_msg=k)
+    if "eval_x_hat" in g.files:
+        m.eval()
+        with torch.no_grad():
+            _, xh2, _ = m(x)
+        np.testing.assert_allclose(xh2.cpu().numpy(), g["eval_x_hat"], rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.gpu
 def test_vqvae_full_size_parity_fp32(fp32_parity):
     from arcweld.functional import mse_loss
     g = golden("vqvae_full_b4.npz")
@@ -253,3 +288,38 @@ def test_trainer_centre_tap_layout_matches_dense_layout(fp32_parity, monkeypatch
         out.append(sd)
     for k in out[0]:
         torch.testing.assert_close(out[0][k].float(), out[1][k].float(), rtol=1e-5, atol=1e-6, msg=k)
+
+
+@pytest.mark.gpu
+def test_batchnorm_model_tokenizes_and_trains_graphed(fp32_parity):
+    """BatchNorm ResBlocks on the other entry points: the fused tokenization gives the train-step indices of the
+    golden (batch statistics in train mode), the standalone encoder modules agree with it, and captured steps
+    follow eager steps."""
+    from arcweld.trainer import Trainer
+    kw = dict(hidden_dim=64, num_embeddings=64, embedding_dim=16, n_resblocks=2, patch_size=25)
+    g = golden("vqvae_small_bn.npz")
+    m = make_model(kw, 303, "cuda", batch_norm=True).train()
+    x = torch.tensor(gen.windows(304, 8), device="cuda")
+    ids = m.encode_ids(x)
+    assert np.array_equal(ids.reshape(-1).cpu().numpy(), g["idx"])
+    m2 = make_model(kw, 303, "cuda", batch_norm=True).eval()
+    with torch.no_grad():
+        z = m2.encoder(m2.patch_embed(x))           # standalone modules (latentspace_dataloader.py:154-161)
+        _, _, _, _, idx2 = m2.vector_quantization(z)
+    ids2 = m2.encode_ids(x)
+    assert torch.equal(idx2.reshape(-1).cpu(), ids2.reshape(-1).cpu())
+    xs = [torch.tensor(gen.windows(760 + i, 16), device="cuda") for i in range(4)]
+    runs = []
+    for graphed in (False, True):
+        mm = make_model(kw, 303, "cuda", batch_norm=True, dropout=0.1).train()
+        tr = Trainer(gradient_clip_val=0.7)
+        tr.setup_optimizer(mm)
+        for xx in xs:
+            if graphed:
+                tr.graphed_step(mm, xx, 1.0)
+            else:
+                tr.micro_step(mm, xx, 0, 1.0)
+                tr.optimizer_step(mm)
+        runs.append({k: v.detach().clone() for k, v in mm.state_dict().items()})
+    for k in runs[0]:
+        torch.testing.assert_close(runs[1][k].float(), runs[0][k].float(), rtol=1e-4, atol=1e-5, msg=k)

@@ -78,6 +78,12 @@ SIGNATURES = {
     "aw_bn_finalize": [c_p, c_i64, c_int, c_p, c_p, c_p, c_p, c_p, c_f, c_f, c_int, c_p, c_p],
     "aw_unpatch_head_bwd1": [c_p, c_i64, c_int, c_int, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p],
     "aw_unpatch_head_bwd2": [c_p, c_i64, c_int, c_int, c_p, c_p, c_p, c_p, c_int, c_p, c_int, c_p, c_p],
+    "aw_bn_group_stats": [c_p, c_i64, c_int, c_int, c_p, c_p],
+    "aw_bn_group_finalize": [c_p, c_i64, c_int, c_int, c_p, c_p, c_p, c_p, c_p, c_f, c_f, c_int, c_p, c_p],
+    "aw_bn_apply": [c_p, c_i64, c_int, c_int, c_p, c_int, c_p, c_f, ctypes.c_uint64, c_p, c_p, c_p, c_int, c_p],
+    "aw_bn_bwd_reduce": [c_p, c_i64, c_int, c_int, c_p, c_p, c_f, ctypes.c_uint64, c_p, c_p, c_p],
+    "aw_bn_bwd_apply": [c_p, c_i64, c_int, c_int, c_p, c_p, c_f, ctypes.c_uint64, c_p, c_p, c_i64, c_int, c_p, c_int,
+                        c_p, c_p, c_p],
     "aw_mse_fwd": [c_p, c_p, c_i64, c_p, c_p],
     "aw_mse_bwd": [c_p, c_p, c_i64, c_p, c_p, c_p],
     "aw_scalar_add": [c_p, c_p, c_p, c_p],

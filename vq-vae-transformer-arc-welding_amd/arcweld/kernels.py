@@ -305,6 +305,40 @@ def attn_bwd(qkv, y, dy, lse, B, T, n_head, d, dqkv, ws, stream=None):
          ptr(ws), stream_ptr(stream))
 
 
+# ------------------------------------------------------------------------------ ResBlock BatchNorm
+def bn_group_stats(h, G, sums, stream=None):
+    N, H = h.shape
+    call("aw_bn_group_stats", ptr(h), N, H, int(G), ptr(sums), stream_ptr(stream))
+
+
+def bn_group_finalize(sums, n, H, G, bn, training, stats, stream=None):
+    """stats [4][G][H] from the sums (training) or the running statistics (eval) of nn.BatchNorm1d ``bn``."""
+    mom = bn.momentum if bn.momentum is not None else 0.1
+    call("aw_bn_group_finalize", ptr(sums) if training else None, int(n), int(H), int(G), ptr(bn.weight),
+         ptr(bn.bias), ptr(bn.running_mean), ptr(bn.running_var), ptr(bn.num_batches_tracked) if training else None,
+         float(bn.eps), float(mom), int(bool(training)), ptr(stats), stream_ptr(stream))
+
+
+def bn_apply(h, G, stats, mode, out, op=None, resid=None, drop=(0.0, 0), seed_ptr=None, stream=None):
+    N, H = h.shape
+    call("aw_bn_apply", ptr(h), N, H, int(G), ptr(stats), int(mode), ptr(resid), float(drop[0]), int(drop[1]),
+         ptr(seed_ptr), ptr(out), ptr(op), dtype_code(op.dtype) if op is not None else AW_F32, stream_ptr(stream))
+
+
+def bn_bwd_reduce(h, G, stats, g_in, sums, drop=(0.0, 0), seed_ptr=None, stream=None):
+    N, H = h.shape
+    call("aw_bn_bwd_reduce", ptr(h), N, H, int(G), ptr(stats), ptr(g_in), float(drop[0]), int(drop[1]),
+         ptr(seed_ptr), ptr(sums), stream_ptr(stream))
+
+
+def bn_bwd_apply(h, G, stats, g_in, sums, n, training, dh, dgamma=None, dbeta=None, drop=(0.0, 0), seed_ptr=None,
+                 stream=None):
+    N, H = h.shape
+    call("aw_bn_bwd_apply", ptr(h), N, H, int(G), ptr(stats), ptr(g_in), float(drop[0]), int(drop[1]),
+         ptr(seed_ptr), ptr(sums), int(n), int(bool(training)), ptr(dh), dtype_code(dh.dtype), ptr(dgamma),
+         ptr(dbeta), stream_ptr(stream))
+
+
 def attn_decode(qkv_new, B, n_new, pos0, n_head, d, kv_cache, y, stream=None):
     """KV-cache attention for n_new rows per sequence at positions pos0..; kv_cache (B, Tmax, 2d)."""
     if kv_cache.dtype != qkv_new.dtype or y.dtype != qkv_new.dtype or kv_cache.shape[-1] != 2 * d:

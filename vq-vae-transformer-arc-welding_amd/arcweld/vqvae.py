@@ -72,9 +72,12 @@ def _params(m):
     """Reference-layout parameter tensors of a VQVAEPatch, by role."""
     enc = [(blk.block[1], blk.block[4]) for blk in m.encoder[0].shared_conv]
     dec = [(blk.block[1], blk.block[4]) for blk in m.decoder[1].shared_conv]
+    # --batchnorm 1: the BatchNorm1d after each ResBlock conv (block[2], block[5]); None with Identity
+    enc_bn = [(blk.block[2], blk.block[5]) if m.batch_norm else None for blk in m.encoder[0].shared_conv]
+    dec_bn = [(blk.block[2], blk.block[5]) if m.batch_norm else None for blk in m.decoder[1].shared_conv]
     rp = m.reverse_patch_embed.proj
     return dict(pe=m.patch_embed.proj, enc=enc, sep=m.encoder[1].shared_conv, E=m.vector_quantization.embedding.weight,
-                dec0=m.decoder[0], dec=dec, t1=rp[0], bn=rp[1], t2=rp[3])
+                dec0=m.decoder[0], dec=dec, t1=rp[0], bn=rp[1], t2=rp[3], enc_bn=enc_bn, dec_bn=dec_bn)
 
 
 class Saved:
@@ -103,6 +106,67 @@ def _centre_grad(g):
     if not c.is_contiguous():
         raise ValueError("encoder conv gradient: unsupported layout")
     return c, (0, 1, 0)
+
+
+def _bn_stats(h, G, bn, training):
+    """BatchNorm statistics [4][G][H] of h [N][H] (rows grouped by row % G); training moves the running stats."""
+    N, H = h.shape
+    sums = None
+    if training:
+        sums = torch.zeros(2, G, H, device=h.device, dtype=torch.float64)
+        K.bn_group_stats(h, G, sums)
+    st = torch.empty(4, G, H, device=h.device)
+    K.bn_group_finalize(sums, N // G, H, G, bn, training, st)
+    return st
+
+
+def _bn_block_fwd(a0, x, w1, w2, Kd, gemm_kw, c1, c2, bns, G, training, p_drop, seed, ctr, T, last=False):
+    """One `--batchnorm 1` ResBlock: x + Drop(BN2(Conv2(GELU(BN1(Conv1(GELU x)))))) (vq_vae_patch_embedd.py:60-74).
+    a0 = GELU(x) in the operand dtype.  Returns (y f32, operand copy of GELU(y) -- of y itself for the last block,
+    whose output feeds the next conv directly --, saved)."""
+    N, H = x.shape
+    bn1, bn2 = bns
+    e = lambda *s, dt=F32: torch.empty(*s, device=x.device, dtype=dt)  # noqa: E731
+    h1 = e(N, H)
+    K.gemm(a0, w1, N, H, Kd, bias=c1.bias, C=h1, **gemm_kw)
+    st1 = _bn_stats(h1, G, bn1, training)
+    hn1, a1 = e(N, H), e(N, H, dt=T)
+    K.bn_apply(h1, G, st1, 0, hn1, op=a1)
+    h2 = e(N, H)
+    K.gemm(a1, w2, N, H, Kd, bias=c2.bias, C=h2, **gemm_kw)
+    st2 = _bn_stats(h2, G, bn2, training)
+    y, an = e(N, H), e(N, H, dt=T)
+    K.bn_apply(h2, G, st2, 2 if last else 1, y, op=an, resid=x, drop=(p_drop, seed), seed_ptr=ctr)
+    return y, an, dict(h1=h1, hn1=hn1, a1=a1, h2=h2, st1=st1, st2=st2)
+
+
+def _bn_block_bwd(gy, x, a0, bs, w1d, w2d, Kd, dgemm_kw, wg, c1, c2, bns, G, training, p_drop, seed, ctr, T, slot,
+                  wgrads, need_copy):
+    """Backward of _bn_block_fwd from gy (f32 gradient of y).  Appends the two weight-gradient problems to
+    ``wgrads`` (wg(c, A, B) builds one) and returns (gx f32, bf16/f32 copy of gx or None)."""
+    N, H = gy.shape
+    bn1, bn2 = bns
+    dev = gy.device
+    e = lambda *s, dt=F32: torch.empty(*s, device=dev, dtype=dt)  # noqa: E731
+    n = N // G
+    sums2 = torch.zeros(2, G, H, device=dev, dtype=torch.float64)
+    K.bn_bwd_reduce(bs["h2"], G, bs["st2"], gy, sums2, drop=(p_drop, seed), seed_ptr=ctr)
+    dh2 = e(N, H, dt=T)
+    K.bn_bwd_apply(bs["h2"], G, bs["st2"], gy, sums2, n, training, dh2, slot(bn2.weight), slot(bn2.bias),
+                   drop=(p_drop, seed), seed_ptr=ctr)
+    t1 = e(N, H)   # gradient of BN1's output: (dh2 . W2) * GELU'(BN1(h1))
+    K.gemm(dh2, w2d, N, H, Kd, b_trans=True, pre=bs["hn1"], C=t1, **dgemm_kw)
+    wgrads.append(wg(c2, dh2, bs["a1"]))
+    sums1 = torch.zeros(2, G, H, device=dev, dtype=torch.float64)
+    K.bn_bwd_reduce(bs["h1"], G, bs["st1"], t1, sums1)
+    dh1 = e(N, H, dt=T)
+    K.bn_bwd_apply(bs["h1"], G, bs["st1"], t1, sums1, n, training, dh1, slot(bn1.weight), slot(bn1.bias))
+    gx = e(N, H)
+    gxo = e(N, H, dt=T) if need_copy else None
+    K.gemm(dh1, w1d, N, H, Kd, b_trans=True, pre=x, resid=gy, C=gx, C2=gxo, c2_mode=2 if need_copy else 0,
+           **dgemm_kw)
+    wgrads.append(wg(c1, dh1, a0))
+    return gx, gxo
 
 
 def forward(m, x, training: bool, need_backward: bool, dtype=None, seed: int = 0):
@@ -155,7 +219,15 @@ def forward(m, x, training: bool, need_backward: bool, dtype=None, seed: int = 0
 
     # ---- encoder ResBlocks (per-token: centre taps)
     xs, a0s, hs, a1s = [x0], [a0], [], []
+    sv.enc_bs, sv.dec_bs = [], []
     for r, (c1, c2) in enumerate(pr["enc"]):
+        if pr["enc_bn"][r] is not None:   # BatchNorm ResBlocks: per-token statistics (G = S)
+            xn, an, bs = _bn_block_fwd(a0s[r], xs[r], enc_w[r][0], enc_w[r][1], H, {}, c1, c2, pr["enc_bn"][r], S,
+                                       training, p_drop, sv.enc_seed[r], sv.ctr, T, last=r == R - 1)
+            xs.append(xn)
+            a0s.append(an)
+            sv.enc_bs.append(bs)
+            continue
         h, a1 = e(N, H, dt=T), e(N, H, dt=T)   # pre-activation kept in the operand dtype
         K.gemm(a0s[r], enc_w[r][0], N, H, H, bias=c1.bias, C=h, C2=a1, c2_mode=1)
         if r < R - 1:
@@ -194,6 +266,14 @@ def forward(m, x, training: bool, need_backward: bool, dtype=None, seed: int = 0
     conv = (H, S, 1, 0)
     ys, ya0s, dhs, da1s = [y0], [ya0], [], []
     for r, (c1, c2) in enumerate(pr["dec"]):
+        if pr["dec_bn"][r] is not None:   # BatchNorm ResBlocks: statistics over all B*S positions (G = 1)
+            yn, an, bs = _bn_block_fwd(ya0s[r], ys[r], dec_w[r][0], dec_w[r][1], 3 * H, dict(conv=conv), c1, c2,
+                                       pr["dec_bn"][r], 1, training, p_drop, sv.dec_seed[r], sv.ctr, T,
+                                       last=r == R - 1)
+            ys.append(yn)
+            ya0s.append(an)
+            sv.dec_bs.append(bs)
+            continue
         h, a1 = e(N, H, dt=T), e(N, H, dt=T)   # pre-activation kept in the operand dtype
         K.gemm(ya0s[r], dec_w[r][0], N, H, 3 * H, conv=conv, bias=c1.bias, C=h, C2=a1, c2_mode=1)
         if r < R - 1:
@@ -267,6 +347,10 @@ def encode(m, x, dtype=F32):
     h, a1 = e(N, H, dt=T), e(N, H, dt=T)   # pre-activation kept in the operand dtype
     for r, (c1, c2) in enumerate(pr["enc"]):
         w1, w2 = ew[r]
+        if pr["enc_bn"][r] is not None:   # BatchNorm ResBlocks (module mode decides batch vs running statistics)
+            xr, a, _ = _bn_block_fwd(a, xr, w1, w2, H, {}, c1, c2, pr["enc_bn"][r], sh.S, m.training, 0.0, 0, None,
+                                     T, last=r == R - 1)
+            continue
         K.gemm(a, w1, N, H, H, bias=c1.bias, C=h, C2=a1, c2_mode=1)
         if r < R - 1:   # x <- x + conv2(gelu(h)) in place (row-local epilogue), a <- gelu(x)
             K.gemm(a1, w2, N, H, H, bias=c2.bias, resid=xr, C=xr, C2=a, c2_mode=1)
@@ -315,8 +399,9 @@ def backward(m, sv, g_emb, g_xhat, slot, mid_hook=None):
     # ConvT1 input gradient -> grad of the decoder output, plus the dropout-masked operand for its last block
     gy, go = e(N, H), e(N, H, dt=T)
     last = R - 1
-    K.gemm(gY2, sv.Wt1, N, H, k1 * H, b_trans=True, C=gy, C2=go, c2_mode=3 if R > 0 else 2,
-           drop2=(p_drop, sv.dec_seed[last] if R > 0 else 0), seed_ptr=sv.ctr)
+    bnm = m.batch_norm and R > 0    # BatchNorm ResBlocks: each block applies its own dropout mask to gy
+    K.gemm(gY2, sv.Wt1, N, H, k1 * H, b_trans=True, C=gy, C2=None if bnm else go, c2_mode=0 if bnm else
+           (3 if R > 0 else 2), drop2=(p_drop, sv.dec_seed[last] if R > 0 else 0), seed_ptr=sv.ctr)
 
     # ---- decoder ResBlocks (reverse)
     dconv_in = (H, S, -1, 0)
@@ -327,9 +412,18 @@ def backward(m, sv, g_emb, g_xhat, slot, mid_hook=None):
     dgw = [(e(3 * H, H, dt=T), e(3 * H, H, dt=T)) for _ in range(R)]
     K.weight_relayout_batch([jb for r in range(R) for jb in ((pr["dec"][r][0].weight, H, H, 3, 0, 2, dgw[r][0]),
                                                              (pr["dec"][r][1].weight, H, H, 3, 0, 2, dgw[r][1]))])
+    def wg_dec(c, A, B):
+        return (A, B, H, 3 * H, N, dict(a_trans=True, b_trans=True, conv=wconv, C=slot(c.weight).view(H, 3 * H),
+                                        accumulate=True, col_map=(H, 3, 0), a_rowsum=slot(c.bias)))
+
     for r in reversed(range(R)):
         c1, c2 = pr["dec"][r]
         W1d, W2d = dgw[r]
+        if bnm:
+            gy, go = _bn_block_bwd(gy, sv.ys[r], sv.ya0s[r], sv.dec_bs[r], W1d, W2d, 3 * H, dict(conv=dconv_in),
+                                   wg_dec, c1, c2, pr["dec_bn"][r], 1, sv.training, p_drop, sv.dec_seed[r], sv.ctr,
+                                   T, slot, wgrads, need_copy=r == 0)
+            continue
         gh = e(N, H, dt=T)
         K.gemm(go, W2d, N, H, 3 * H, b_trans=True, conv=dconv_in, pre=sv.dhs[r], C=gh)
         wgrads.append((go, sv.da1s[r], H, 3 * H, N, dict(a_trans=True, b_trans=True, conv=wconv,
@@ -360,14 +454,25 @@ def backward(m, sv, g_emb, g_xhat, slot, mid_hook=None):
     K.gemm(dz_T, sv.xR_T, D, H, N, a_trans=True, b_trans=True, C=slot(pr["sep"].weight).view(D, H), accumulate=True,
            a_rowsum=slot(pr["sep"].bias))
     gx, gxo = e(N, H), e(N, H, dt=T)
-    K.gemm(dz_T, sv.Ws, N, H, D, b_trans=True, C=gx, C2=gxo, c2_mode=3 if R > 0 else 2,
-           drop2=(p_drop, sv.enc_seed[R - 1] if R > 0 else 0), seed_ptr=sv.ctr)
+    K.gemm(dz_T, sv.Ws, N, H, D, b_trans=True, C=gx, C2=None if bnm else gxo, c2_mode=0 if bnm else
+           (3 if R > 0 else 2), drop2=(p_drop, sv.enc_seed[R - 1] if R > 0 else 0), seed_ptr=sv.ctr)
 
     # ---- encoder ResBlocks (reverse); weight gradients deferred into one grouped launch as in the decoder
     wgrads = []
+
+    def wg_enc(c, A, B):
+        Cw, cm = _centre_grad(slot(c.weight))
+        return (A, B, H, H, N, dict(a_trans=True, b_trans=True, C=Cw, accumulate=True, col_map=cm,
+                                    a_rowsum=slot(c.bias)))
+
     for r in reversed(range(R)):
         c1, c2 = pr["enc"][r]
         w1, w2 = sv.enc_w[r]
+        if bnm:
+            gx, gxo = _bn_block_bwd(gx, sv.xs[r], sv.a0s[r], sv.enc_bs[r], w1, w2, H, {}, wg_enc, c1, c2,
+                                    pr["enc_bn"][r], S, sv.training, p_drop, sv.enc_seed[r], sv.ctr, T, slot, wgrads,
+                                    need_copy=r == 0)
+            continue
         gh = e(N, H, dt=T)
         K.gemm(gxo, w2, N, H, H, b_trans=True, pre=sv.hs[r], C=gh)
         C2w, cm2 = _centre_grad(slot(c2.weight))

@@ -154,8 +154,6 @@ class CNNBlock(nn.Module):
 
     def forward(self, x):
         _need_no_grad(self, x)
-        if self.batch_norm:
-            raise NotImplementedError("ResBlock BatchNorm (--batchnorm 1) is not on the HIP path yet")
         B, H, S = x.shape
         N = B * S
         T = engine.operand_dtype()
@@ -174,6 +172,12 @@ class CNNBlock(nn.Module):
                 K.weight_relayout(c1.weight, H, H, 3, 0, 1, w1)
                 K.weight_relayout(c2.weight, H, H, 3, 0, 1, w2)
                 kd, conv = 3 * H, (H, S, 1, 0)
+            if self.batch_norm:   # BatchNorm ResBlocks: per-token statistics when the tokens run separately
+                gk = {} if conv is None else dict(conv=conv)
+                cur, a0, _ = engine._bn_block_fwd(a0, cur, w1, w2, kd, gk, c1, c2, (blk.block[2], blk.block[5]),
+                                                  S if self.seperate else 1, self.training, p, engine._mix(seed, r),
+                                                  None, T)
+                continue
             a1 = torch.empty(N, H, device=x.device, dtype=T)
             K.gemm(a0, w1, N, H, kd, conv=conv, bias=c1.bias, C2=a1, c2_mode=1)
             nxt = torch.empty(N, H, device=x.device)
@@ -235,9 +239,6 @@ class VQVAEPatch(Autoencoder):
 
     def forward(self, x):
         """(B, seq_len, input_dim) -> (embedding_loss, x_hat (B, seq_len, input_dim), perplexity)."""
-        if self.batch_norm:
-            raise NotImplementedError("ResBlock BatchNorm (--batchnorm 1) is not on the HIP path yet; the reference "
-                                      "entry script default is --batchnorm 0")
         params = tuple(self.parameters())
         if torch.is_grad_enabled() and any(p.requires_grad for p in params):
             return engine.VQVAEPatchFunction.apply(self, x, self._next_seed(), *params)
@@ -253,8 +254,6 @@ class VQVAEPatch(Autoencoder):
         Gradients accumulate into each parameter's ``.grad`` (the flat optimizer views when a Trainer installed
         ``_grad_sink``).  ``mid_hook`` is called between the decoder-side and the encoder-side backward (see
         arcweld.vqvae.backward): the data-parallel step starts the decoder-side all-reduce there.  Returns the loss."""
-        if self.batch_norm:
-            raise NotImplementedError("ResBlock BatchNorm (--batchnorm 1) is not on the HIP path yet")
         x = x.contiguous()
         emb, x_hat, perp, idx, sv = engine.forward(self, x, self.training, need_backward=True, seed=self._next_seed())
         self._last_indices = idx
