@@ -78,13 +78,14 @@ def test_attention_bf16(T, hs, nh):
         assert (a - r).norm().item() <= 1e-2 * r.norm().item() + 1e-4, j   # dq is exactly 0 at T = 1
 
 
+@pytest.mark.parametrize("R", [1000, 5000])
 @pytest.mark.parametrize("D", [64, 512])
 @pytest.mark.parametrize("out_dtype", [torch.float32, torch.bfloat16])
-def test_layernorm_fwd_bwd(D, out_dtype):
+def test_layernorm_fwd_bwd(R, D, out_dtype):
     """aw_layernorm_fwd / aw_layernorm_bwd (vectorised at D % 256 == 0) vs torch layer_norm in fp32, including
-    the accumulate-into-dx form and the dropout-masked operand copy dx2 (regenerated mask)."""
+    the accumulate-into-dx form and the dropout-masked operand copy dx2 (regenerated mask).  R = 5000 exceeds
+    the backward's 2048 waves, so each wave walks several rows (the next-row prefetch path)."""
     from arcweld import kernels as K
-    R = 1000
     g = torch.Generator(device="cuda").manual_seed(D)
     x = torch.randn(R, D, device="cuda", generator=g) * 3 + 1
     w = torch.randn(D, device="cuda", generator=g)

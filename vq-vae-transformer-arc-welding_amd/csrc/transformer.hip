@@ -151,15 +151,47 @@ __global__ __launch_bounds__(256) void ln_bwd_vec_kernel(const float* __restrict
     w4[j] = *reinterpret_cast<const float4*>(w + 4 * lane + 256 * j);
     pdw[j] = pdb[j] = make_float4(0.f, 0.f, 0.f, 0.f);
   }
+  // Each wave walks ~R/nw rows; the next row's x / dy / statistics are loaded before this row's two wave
+  // reductions and stores, so the loads stay in flight across the dependent work.
+  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  float4 xc[NV], dc[NV], oc[NV];
+  float muc = 0.f, rsc = 0.f;
+  if (wave < R) {
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      xc[j] = *reinterpret_cast<const float4*>(x + wave * D + 4 * lane + 256 * j);
+      dc[j] = *reinterpret_cast<const float4*>(dy + wave * D + 4 * lane + 256 * j);
+      oc[j] = accumulate ? *reinterpret_cast<const float4*>(dx + wave * D + 4 * lane + 256 * j) : z4;
+    }
+    muc = mean[wave];
+    rsc = rstd[wave];
+  }
   for (int64_t r = wave; r < R; r += nw) {
-    const float mu = mean[r], rs = rstd[r];
+    const float mu = muc, rs = rsc;
+    float4 xcur[NV], dcur[NV], ocur[NV];
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      xcur[j] = xc[j];
+      dcur[j] = dc[j];
+      ocur[j] = oc[j];
+    }
+    const int64_t rn = r + nw;
+    if (rn < R) {
+#pragma unroll
+      for (int j = 0; j < NV; ++j) {
+        xc[j] = *reinterpret_cast<const float4*>(x + rn * D + 4 * lane + 256 * j);
+        dc[j] = *reinterpret_cast<const float4*>(dy + rn * D + 4 * lane + 256 * j);
+        oc[j] = accumulate ? *reinterpret_cast<const float4*>(dx + rn * D + 4 * lane + 256 * j) : z4;
+      }
+      muc = mean[rn];
+      rsc = rstd[rn];
+    }
     float4 xh[NV], g[NV];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int j = 0; j < NV; ++j) {
-      const int c = 4 * lane + 256 * j;
-      const float4 xv = *reinterpret_cast<const float4*>(x + r * D + c);
-      const float4 dv = *reinterpret_cast<const float4*>(dy + r * D + c);
+      const float4 xv = xcur[j];
+      const float4 dv = dcur[j];
       xh[j] = make_float4((xv.x - mu) * rs, (xv.y - mu) * rs, (xv.z - mu) * rs, (xv.w - mu) * rs);
       g[j] = make_float4(dv.x * w4[j].x, dv.y * w4[j].y, dv.z * w4[j].z, dv.w * w4[j].w);
       pdw[j].x += dv.x * xh[j].x; pdw[j].y += dv.y * xh[j].y; pdw[j].z += dv.z * xh[j].z; pdw[j].w += dv.w * xh[j].w;
@@ -175,8 +207,7 @@ __global__ __launch_bounds__(256) void ln_bwd_vec_kernel(const float* __restrict
       float v[4] = {rs * (g[j].x - s1 - xh[j].x * s2), rs * (g[j].y - s1 - xh[j].y * s2),
                     rs * (g[j].z - s1 - xh[j].z * s2), rs * (g[j].w - s1 - xh[j].w * s2)};
       if (accumulate) {
-        const float4 o = *reinterpret_cast<const float4*>(dx + r * D + c);
-        v[0] += o.x; v[1] += o.y; v[2] += o.z; v[3] += o.w;
+        v[0] += ocur[j].x; v[1] += ocur[j].y; v[2] += ocur[j].z; v[3] += ocur[j].w;
       }
       *reinterpret_cast<float4*>(dx + r * D + c) = make_float4(v[0], v[1], v[2], v[3]);
       if (dx2) {
