@@ -66,10 +66,9 @@ def test_active_parameters_follow_task():
 
 @pytest.fixture
 def fp32_parity():
-    old = torch.get_float32_matmul_precision()
-    torch.set_float32_matmul_precision("highest")
-    yield
-    torch.set_float32_matmul_precision(old)
+    from arcweld.precision import operands
+    with operands(torch.float32):
+        yield
 
 
 def _step(m, task, batch):
@@ -143,18 +142,15 @@ def test_eval_forward_matches_train_forward_without_dropout(fp32_parity):
 
 @pytest.mark.gpu
 def test_bf16_tracks_fp32():
-    """'medium' precision (what train_transformer_mtasks.py sets) -> bf16 MFMA operands, fp32 accumulation."""
+    """bf16 MFMA operands (the --precision bf16 opt-in), fp32 accumulation, track the fp32 step."""
+    from arcweld.precision import operands
     m = make_model(FULL, 8, 405, device="cuda").train()
     batch = inputs(2, 321, 514, 406, "cuda")
-    old = torch.get_float32_matmul_precision()
-    try:
-        torch.set_float32_matmul_precision("highest")
+    with operands(torch.float32):
         l32, lg32 = _step(m, "gen", batch)
         g32 = {n: p.grad.clone() for n, p in m.named_parameters() if p.grad is not None}
-        torch.set_float32_matmul_precision("medium")
+    with operands(torch.bfloat16):
         l16, lg16 = _step(m, "gen", batch)
-    finally:
-        torch.set_float32_matmul_precision(old)
     assert abs(l16.item() - l32.item()) < 2e-2 * abs(l32.item())
     err = (lg16 - lg32).abs().max().item()
     assert err < 5e-2 * lg32.abs().max().item() + 1e-2
@@ -206,10 +202,9 @@ def test_sequence_longer_than_mask_raises():
 
 @pytest.fixture
 def fp32_mode():
-    old = torch.get_float32_matmul_precision()
-    torch.set_float32_matmul_precision("highest")
-    yield
-    torch.set_float32_matmul_precision(old)
+    from arcweld.precision import operands
+    with operands(torch.float32):
+        yield
 
 
 @pytest.mark.gpu

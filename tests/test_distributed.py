@@ -168,3 +168,30 @@ def test_device_batches_shard_like_distributed_sampler(n, world, shuffle):
             assert db.indices().tolist() == list(ds)
             got = torch.cat(list(db)).tolist()
             assert got == list(ds)
+
+
+def _worker_devices1(rank, world, port, out):
+    """Trainer(devices=1) inside an initialised world-2 group: the rank trains alone on the whole split (no
+    broadcast, no sharding, no all-reduce), as Lightning's Trainer(devices=1) does."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from arcweld import trainer as T
+    from arcweld.data import DeviceBatches
+    try:
+        m = TinyModel()
+        tr = T.Trainer(devices=1, gradient_clip_val=None)
+        x, y = _data()
+        tr.fit(m, train_dataloaders=DeviceBatches((x, y), batch_size=4, shuffle=False))
+        out[rank] = {"w": m.lin.weight.detach().clone(), "steps": tr.global_step}
+    finally:
+        dist.destroy_process_group()
+
+
+def test_trainer_devices1_under_a_process_group_trains_alone():
+    port = _free_port()
+    out = mp.Manager().dict()
+    mp.spawn(_worker_devices1, args=(2, port, out), nprocs=2, join=True)
+    ref, steps = _reference_single_process(1, 1)
+    for r in range(2):
+        assert out[r]["steps"] == steps == 6
+        torch.testing.assert_close(out[r]["w"], ref.lin.weight.detach(), rtol=1e-5, atol=1e-6)

@@ -95,3 +95,48 @@ def test_centre_tap_layout_matches_dense_layout():
     np.testing.assert_allclose(n1, n0, rtol=1e-6)
     for a, b in zip(p0, p1):
         torch.testing.assert_close(b, a, rtol=1e-6, atol=1e-7)
+
+
+def test_state_dict_round_trip_resumes_the_trajectory():
+    """state_dict() / load_state_dict(): a fresh optimizer loaded mid-run (flat moments + device step counter)
+    continues exactly as the uninterrupted one -- the bias corrections depend on the restored step."""
+    from arcweld.optim import RAdam
+
+    def make():
+        ps = [torch.nn.Parameter(torch.tensor(gen.normal(950 + i, s, 0.3), device="cuda"))
+              for i, s in enumerate(SHAPES)]
+        return ps, RAdam([{"params": ps[:2], "weight_decay": 0.1}, {"params": ps[2:], "weight_decay": 0.0}],
+                         lr=1e-3, betas=(0.9, 0.95))
+
+    def grads(ps, step):
+        for i, p in enumerate(ps):
+            p.grad.copy_(torch.tensor(gen.normal(960 + 13 * step + i, p.shape, 1.0)))
+
+    ps, opt = make()
+    opt.flatten()
+    for step in range(6):
+        grads(ps, step)
+        opt.clip_grad_norm_(0.8)
+        opt.step()
+        opt.zero_grad()
+        if step == 2:
+            sd = opt.state_dict()
+            snap = [p.detach().clone() for p in ps]
+    assert sd["arcweld_flat"]["step"] == 3
+    qs, opt2 = make()
+    with torch.no_grad():
+        for q, s in zip(qs, snap):
+            q.copy_(s)
+    opt2.load_state_dict(sd)
+    for step in range(3, 6):
+        grads(qs, step)
+        opt2.clip_grad_norm_(0.8)
+        opt2.step()
+        opt2.zero_grad()
+    for p, q in zip(ps, qs):
+        assert torch.equal(p.detach(), q.detach())
+    bad = dict(sd)
+    bad["arcweld_flat"] = dict(sd["arcweld_flat"], m=sd["arcweld_flat"]["m"][:-64], v=sd["arcweld_flat"]["v"][:-64])
+    _, opt3 = make()
+    with pytest.raises(ValueError):
+        opt3.load_state_dict(bad)

@@ -1,0 +1,118 @@
+"""configs[1] at its real size: the VQ-VAE-Patch train step at B = 1024 windows (N = 16384 tokens: 128 row tiles
+x 4 column tiles per GEMM, the two-tile codebook of the VQ kernel, full-M grouped weight gradients) -- the exact
+shapes bench.py times (model/vq_vae_patch_embedd.py:155-167, model/autencoder_lightning_base.py:80-84).
+
+* fp32 operands against the CPU oracle (oracle/vqvae.py, itself pinned to the reference's golden fixtures) on the
+  same generator inputs: indices bit-exact over all 16384 rows, x_hat within 1e-4, loss / perplexity / BN running
+  statistics, and every gradient by its norm AND a strided sample of its elements.
+* bf16 operands (the bench's opt-in): fp32-vs-bf16 gradient agreement, and graphed steps == eager steps.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import gen
+from oracle import vqvae as ov
+
+pytestmark = pytest.mark.gpu
+
+KW = dict(hidden_dim=512, num_embeddings=512, embedding_dim=64, n_resblocks=8, patch_size=25)
+B = 1024
+
+
+def _model(wseed, dropout=0.0):
+    from model.vq_vae_patch_embedd import VQVAEPatch
+    m = VQVAEPatch(input_dim=2, learning_rate=1e-3, dropout_p=dropout, batch_norm=False, **KW)
+    sd = ov.det_state_dict(ov.VQVAEConfig(**KW), wseed)
+    m.load_state_dict({k: torch.tensor(v) for k, v in sd.items()})
+    return m.cuda().train(), sd
+
+
+def _sample(a, n=4096):
+    """A strided sample of a flattened gradient (every element class: rows, columns, taps, biases)."""
+    f = a.reshape(-1)
+    step = max(1, f.size // n)
+    return f[::step]
+
+
+def test_vqvae_b1024_train_step_matches_oracle_fp32():
+    from arcweld.functional import mse_loss
+    from arcweld.precision import operands
+    torch.set_num_threads(max(1, min(16, torch.get_num_threads())))
+    m, sd = _model(1701)
+    x_np = gen.windows(1702, B)
+    x = torch.tensor(x_np, device="cuda")
+    with operands(torch.float32):
+        emb, x_hat, perp = m(x)
+        recon = mse_loss(x_hat, x)
+        loss = recon + emb
+        loss.backward()
+    torch.cuda.synchronize()
+    out, grads, state = ov.vqvae_train_step_grads(sd, x_np, ov.VQVAEConfig(**KW))
+    idx = m._last_indices.cpu().numpy()
+    bad = np.flatnonzero(idx != out["idx"])
+    assert bad.size == 0, f"{bad.size} of {idx.size} indices differ (first rows {bad[:8].tolist()})"
+    np.testing.assert_allclose(x_hat.detach().cpu().numpy(), out["x_hat"], rtol=1e-4, atol=1e-4)
+    for k, v in (("emb_loss", emb), ("perplexity", perp), ("recon", recon), ("loss", loss)):
+        np.testing.assert_allclose(v.item(), out[k], rtol=1e-4, err_msg=k)
+    msd = m.state_dict()
+    for k, v in state.items():
+        np.testing.assert_allclose(msd[k].cpu().numpy(), v, rtol=1e-4, atol=1e-6, err_msg=k)
+    for name, p in m.named_parameters():
+        ref = grads[name]
+        got = p.grad.detach().cpu().numpy()
+        if name == "reverse_patch_embed.proj.0.bias":
+            # feeds a train-mode BatchNorm: analytically zero, both sides hold rounding noise only
+            assert np.abs(got).max() < 1e-6 and np.abs(ref).max() < 1e-6, name
+            continue
+        gn, rn = np.linalg.norm(got.astype(np.float64)), np.linalg.norm(ref.astype(np.float64))
+        np.testing.assert_allclose(gn, rn, rtol=2e-4, atol=1e-9, err_msg=name)
+        scale = np.abs(ref).max() + 1e-20
+        np.testing.assert_allclose(_sample(got), _sample(ref), rtol=1e-3, atol=2e-4 * scale, err_msg=name)
+
+
+def test_vqvae_b1024_bf16_step_tracks_fp32_and_graphs_match_eager():
+    """bf16 operands (fp32 accumulation, fp32 master weights) at the bench shape: the gradient of every parameter
+    within 5 % (relative Frobenius) of the fp32 step on the same weights and batch, the same indices on >= 97 % of
+    the rows; and three captured-graph optimizer steps equal three eager ones."""
+    from arcweld.functional import mse_loss
+    from arcweld.precision import operands
+    from arcweld.trainer import Trainer
+    m, _ = _model(1703)
+    x = torch.tensor(gen.windows(1704, B), device="cuda")
+    grads, idx = {}, {}
+    for dt in (torch.float32, torch.bfloat16):
+        m.zero_grad()
+        with operands(dt):
+            emb, x_hat, _ = m(x)
+            (mse_loss(x_hat, x) + emb).backward()
+        grads[dt] = {n: p.grad.detach().clone() for n, p in m.named_parameters()}
+        idx[dt] = m._last_indices.clone()
+    for n, g32 in grads[torch.float32].items():
+        if n == "reverse_patch_embed.proj.0.bias":
+            continue    # feeds a train-mode BatchNorm: zero up to rounding noise
+        rel = ((grads[torch.bfloat16][n] - g32).norm() / (g32.norm() + 1e-20)).item()
+        assert rel < 5e-2, (n, rel)
+    agree = (idx[torch.float32] == idx[torch.bfloat16]).float().mean().item()
+    assert agree >= 0.97, agree
+
+    xs = [torch.tensor(gen.windows(1710 + i, B), device="cuda") for i in range(5)]
+    runs = []
+    with operands(torch.bfloat16):
+        for graphed in (False, True):
+            mm, _ = _model(1703, dropout=0.1)
+            tr = Trainer(gradient_clip_val=0.7)
+            tr.setup_optimizer(mm)
+            losses = []
+            for xx in xs:
+                if graphed:
+                    losses.append(float(tr.graphed_step(mm, xx, 1.0)))
+                else:
+                    losses.append(float(tr.micro_step(mm, xx, 0, 1.0).detach()))
+                    tr.optimizer_step(mm)
+            runs.append((losses, {k: v.detach().clone() for k, v in mm.state_dict().items()}))
+    (l0, s0), (l1, s1) = runs
+    # same kernels and masks; only the order of floating-point atomics (bias-gradient row sums, BN sums) differs
+    np.testing.assert_allclose(l1, l0, rtol=1e-4)
+    for k in s0:
+        torch.testing.assert_close(s1[k].float(), s0[k].float(), rtol=1e-4, atol=1e-5, msg=k)

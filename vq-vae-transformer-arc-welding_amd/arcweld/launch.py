@@ -14,11 +14,12 @@ import torch
 import torch.distributed as dist
 
 
-def init_distributed(backend=None):
-    """-> (rank, world, device).  Initialises the default process group when launched with WORLD_SIZE > 1."""
+def init_distributed(backend=None, enable=True):
+    """-> (rank, world, device).  Initialises the default process group when launched with WORLD_SIZE > 1 (and
+    ``enable``; a process started by torchrun with enable=False trains alone on its LOCAL_RANK device)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1 and not dist.is_initialized():
+    if enable and world > 1 and not dist.is_initialized():
         backend = backend or ("nccl" if torch.cuda.is_available() else "gloo")
         dist.init_process_group(backend)
     rank = dist.get_rank() if dist.is_initialized() else 0

@@ -194,8 +194,29 @@ class RAdam(torch.optim.Optimizer):
         return [(k, F["act_group"][gi]) for gi, k in enumerate(keys)]
 
     def state_dict(self):
+        """torch's state_dict (param_groups; 'state' stays empty) plus 'arcweld_flat': the flat first/second moments
+        and the device step counter, in this optimizer's flat layout (same parameters, same groups, same order)."""
         sd = super().state_dict()
         if self._flat is not None:
             sd["arcweld_flat"] = {"m": self._flat["m"].cpu(), "v": self._flat["v"].cpu(),
-                                  "step": int(self._flat["step"].item())}
+                                  "step": int(self._flat["step"].item()), "total": int(self._flat["total"])}
         return sd
+
+    def load_state_dict(self, state_dict):
+        """Restores the hyper-parameters of every group and, when present, the flat RAdam moments and step count
+        (packing the parameters first).  The flat layout must be the one that wrote them."""
+        sd = dict(state_dict)
+        flat = sd.pop("arcweld_flat", None)
+        super().load_state_dict(sd)
+        if flat is None:
+            return
+        self.flatten()
+        F = self._flat
+        m, v = flat["m"], flat["v"]
+        if m.numel() != F["total"] or v.numel() != F["total"] or int(flat.get("total", F["total"])) != F["total"]:
+            raise ValueError(f"optimizer state holds a flat layout of {m.numel()} elements, this optimizer packs "
+                             f"{F['total']} (different parameters, groups or centre-tap declaration)")
+        F["m"].copy_(m.to(F["m"].device, torch.float32))
+        F["v"].copy_(v.to(F["v"].device, torch.float32))
+        self._step_count = int(flat["step"])
+        F["step"].fill_(self._step_count)

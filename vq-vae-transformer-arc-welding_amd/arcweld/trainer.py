@@ -73,11 +73,15 @@ def broadcast_params(model: torch.nn.Module, opt=None):
 
 
 class Trainer:
-    def __init__(self, devices=1, num_nodes=1, max_epochs=1, max_steps=-1, logger=None, callbacks=None,
+    def __init__(self, devices="auto", num_nodes=1, max_epochs=1, max_steps=-1, logger=None, callbacks=None,
                  gradient_clip_val=None, strategy="auto", accumulate_grad_batches=1, log_every_n_steps=50,
                  fused_grad_sink=True, hip_graphs=False, **_ignored):
         self.max_epochs = max_epochs
         self.max_steps = max_steps
+        # devices=1 under an initialised process group trains this rank alone (no sharding, no all-reduce), as a
+        # Lightning Trainer(devices=1) does; "auto" / N > 1 use every rank of the group
+        self.devices = devices
+        self.data_parallel = not (isinstance(devices, int) and devices == 1)
         self.logger = logger
         self.gradient_clip_val = gradient_clip_val
         self.accumulate = max(1, int(accumulate_grad_batches))
@@ -106,7 +110,8 @@ class Trainer:
         if self.fused_grad_sink:
             # fused autograd nodes accumulate straight into the flat gradient views (no extra add)
             model._grad_sink = {p: p.grad for p in model.parameters()}
-        broadcast_params(model, opt)
+        if self.data_parallel:
+            broadcast_params(model, opt)
         self.optimizer = opt
         self._graphs = None          # a captured step belongs to one optimizer
         self._graph_shape = None
@@ -125,8 +130,12 @@ class Trainer:
         opt.step()
         opt.zero_grad()
 
+    def world(self):
+        return world() if self.data_parallel else 1
+
     def optimizer_step(self, model):
-        for w in allreduce_spans(self.optimizer.flat_grad, _spans(self.optimizer)):
+        works = allreduce_spans(self.optimizer.flat_grad, _spans(self.optimizer)) if self.data_parallel else []
+        for w in works:
             w.wait()
         self._update(model)
         self.global_step += 1
@@ -144,6 +153,8 @@ class Trainer:
         "late" (that parameter onwards: final mid-backward) and "early" (the parameters before it)."""
         opt = self.optimizer
         flat = opt.flat_grad
+        if not self.data_parallel:
+            return []
         if region == "all" or not hasattr(model, "backward_split_parameter"):
             return allreduce_spans(flat, _spans(opt)) if region in ("all", "late") else []
         cut = opt.flat_offset(model.backward_split_parameter())
@@ -163,7 +174,11 @@ class Trainer:
         self.setup_optimizer(model)
         self.should_stop = False
         dev = next(model.parameters()).device
-        scale = 1.0 / (self.accumulate * world())
+        if not self.data_parallel:
+            for ld in (loader, val_loader):
+                if hasattr(ld, "rank") and hasattr(ld, "world"):
+                    ld.rank, ld.world = 0, 1
+        scale = 1.0 / (self.accumulate * self.world())
         t0 = time.time()
         for epoch in range(self.max_epochs):
             self.current_epoch = epoch
@@ -174,6 +189,12 @@ class Trainer:
                 batch = _to_device(batch, dev)
                 if self.hip_graphs and self.accumulate == 1 and _fixed_shape(self, batch):
                     loss = self.graphed_step(model, batch, scale)
+                    if self.global_step % self.log_every == 0:
+                        # the captured step's static loss tensor holds this replay's value
+                        lv = float(loss.detach())
+                        self.history.append((self.global_step, lv, time.time() - t0))
+                        if self.logger is not None and hasattr(self.logger, "log_metrics"):
+                            self.logger.log_metrics({"train/loss": lv}, step=self.global_step)
                     if 0 < self.max_steps <= self.global_step:
                         break
                     continue
@@ -182,7 +203,10 @@ class Trainer:
                 if (i + 1) % self.accumulate == 0 or (n is not None and i + 1 == n):
                     self.optimizer_step(model)
                     if self.global_step % self.log_every == 0:
-                        self.history.append((self.global_step, float(loss.detach()), time.time() - t0))
+                        lv = float(loss.detach())
+                        self.history.append((self.global_step, lv, time.time() - t0))
+                        if self.logger is not None and hasattr(self.logger, "log_metrics"):
+                            self.logger.log_metrics({"train/loss": lv}, step=self.global_step)
                     if 0 < self.max_steps <= self.global_step:
                         break
             if val_loader is not None:
@@ -219,7 +243,7 @@ class Trainer:
             return {}
         keys = sorted(sums)
         vec = torch.stack([sums[k] for k in keys] + [torch.tensor(float(total), device=dev)])
-        if world() > 1 and stage == "val":
+        if self.world() > 1 and stage == "val":
             dist.all_reduce(vec)
         vec = vec.cpu()
         return {k: float(vec[j] / vec[-1]) for j, k in enumerate(keys)}

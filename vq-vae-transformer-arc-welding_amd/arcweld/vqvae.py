@@ -14,24 +14,17 @@ one ``aw_gemm`` launch:
   head          BN -> GELU -> ConvT(H->1) -> x_hat, one wave per position
 
 The backward mirrors it (input-gradient GEMMs with the GELU' and dropout masks fused in the epilogues,
-weight-gradient GEMMs with the bias gradient fused as an A-row-sum).  Operand dtype follows
-``torch.get_float32_matmul_precision()`` unless the module overrides it: 'highest' -> exact fp32 MFMA
-(parity mode), 'high'/'medium' -> bf16 MFMA with fp32 accumulation (the reference scripts set 'medium',
-train_reconstruction_embedding.py:253).
+weight-gradient GEMMs with the bias gradient fused as an A-row-sum).  Operands are exact fp32 MFMA by default
+(the reference's numerics on MI355X); bf16 MFMA with fp32 accumulation is an explicit opt-in (arcweld.precision).
 """
 from __future__ import annotations
 
 import torch
 
 from . import kernels as K
+from .precision import operand_dtype  # noqa: F401  (re-exported: model/ and arcweld.decoder import it from here)
 
 F32 = torch.float32
-
-
-def operand_dtype(override=None):
-    if override is not None:
-        return override
-    return F32 if torch.get_float32_matmul_precision() == "highest" else torch.bfloat16
 
 
 def _mix(seed: int, salt: int) -> int:
@@ -112,6 +105,10 @@ def _bn_stats(h, G, bn, training):
     """BatchNorm statistics [4][G][H] of h [N][H] (rows grouped by row % G); training moves the running stats."""
     N, H = h.shape
     sums = None
+    if training and N // G <= 1:
+        # torch BatchNorm1d refuses it too (a ragged last batch of one window under --batchnorm 1)
+        raise ValueError(f"Expected more than 1 value per channel when training, got input size "
+                         f"torch.Size([{N // G}, {H}])")
     if training:
         sums = torch.zeros(2, G, H, device=h.device, dtype=torch.float64)
         K.bn_group_stats(h, G, sums)
@@ -320,10 +317,11 @@ def encode(m, x, dtype=F32):
     """Frozen-encoder tokenization: windows (W, L, C) f32 -> (codebook indices (W*S,) int64, z (W*S, D) f32).
 
     patch embed -> encoder ResBlocks (eval: no dropout) -> sep conv -> VQ argmin; the decoder is never run
-    (latentspace_dataloader.py:154-161 calls only patch_embed/encoder/vector_quantization).  Operands default to
-    exact fp32 so the indices are the reference's bit for bit; ``dtype=torch.bfloat16`` trades that for speed.
+    (latentspace_dataloader.py:154-161 calls only patch_embed/encoder/vector_quantization).  Operands are exact
+    fp32 unless ``dtype`` says otherwise, so the indices are the reference's bit for bit; ``dtype=torch.bfloat16``
+    trades that for speed.
     """
-    T = operand_dtype(dtype)
+    T = F32 if dtype is None else operand_dtype(dtype)
     if x.dtype != F32 or x.dim() != 3:
         raise ValueError("expected float32 windows of shape (W, seq_len, input_dim)")
     x = x.contiguous()

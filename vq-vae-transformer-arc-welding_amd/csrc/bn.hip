@@ -177,7 +177,11 @@ extern "C" int aw_bn_group_finalize(const double* sums, int64_t n, int H, int G,
                                     const float* beta, float* running_mean, float* running_var, int64_t* nbt,
                                     float eps, float momentum, int training, float* stats, void* stream) {
   AW_REQUIRE(stats && H > 0 && G > 0, "aw_bn_group_finalize: bad args");
-  AW_REQUIRE(!training || (sums && n > 0), "aw_bn_group_finalize: training needs the sums");
+  AW_REQUIRE(!training || sums, "aw_bn_group_finalize: training needs the sums");
+  // torch.nn.BatchNorm1d in training mode refuses a batch of one value per channel (nn.functional.batch_norm:
+  // "Expected more than 1 value per channel when training"); a zero variance would silently collapse to beta
+  AW_REQUIRE(!training || n > 1, "Expected more than 1 value per channel when training, got %lld per group",
+             (long long)n);
   AW_REQUIRE(training || (running_mean && running_var), "aw_bn_group_finalize: eval needs running statistics");
   hipLaunchKernelGGL(bn_finalize_groups_kernel, dim3(aw_cdiv(H, 256)), dim3(256), 0,
                      reinterpret_cast<hipStream_t>(stream), sums, n, H, G, gamma, beta, running_mean, running_var,

@@ -715,7 +715,8 @@ extern "C" int aw_bn_finalize(const double* colstats, int64_t n, int H, const fl
                               float* running_mean, float* running_var, int64_t* nbt, float eps, float momentum,
                               int training, float* stats, void* stream) {
   AW_REQUIRE(stats && H > 0, "aw_bn_finalize: bad args");
-  AW_REQUIRE(!training || (colstats && n > 0), "aw_bn_finalize: training needs colstats");
+  AW_REQUIRE(!training || colstats, "aw_bn_finalize: training needs colstats");
+  AW_REQUIRE(!training || n > 1, "Expected more than 1 value per channel when training, got %lld", (long long)n);
   AW_REQUIRE(training || (running_mean && running_var), "aw_bn_finalize: eval needs running stats");
   hipLaunchKernelGGL(bn_finalize_kernel, dim3(aw_cdiv(H, 256)), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
                      colstats, n, H, gamma, beta, running_mean, running_var, nbt, eps, momentum, training, stats);

@@ -4,7 +4,8 @@ final test).  Data: ``--data-dir`` reads the reference's ASIMoW CSV (``<dir>/pro
 split by the reference's val/test (experiment, welding_run) ids, per-channel scaled; arcweld.asimow), or
 ``--data-npz`` an .npz with 'train'/'val'/'test' arrays of shape (n, 200, 2); without either the windows are
 synthetic N(0, 1) 200x2 (the dataset is not available offline).  The W&B / MLflow loggers are not available
-(CSVLogger only).
+(CSVLogger only).  ``--precision`` picks the MFMA operand dtype: fp32 (default, the reference's numerics) or bf16
+(opt-in, fp32 accumulation; arcweld.precision).
 """
 import argparse
 import logging as log
@@ -18,6 +19,7 @@ import torch  # noqa: E402
 
 from arcweld.data import ReconstructionDataModule  # noqa: E402
 from arcweld.launch import CSVLogger, init_distributed, shutdown  # noqa: E402
+from arcweld.precision import set_operand_dtype  # noqa: E402
 from arcweld.trainer import EarlyStopping, ModelCheckpoint, Trainer  # noqa: E402
 from model.vq_vae_patch_embedd import VQVAEPatch  # noqa: E402
 
@@ -30,6 +32,7 @@ def load_windows(path, device):
 def main(hparams):
     if hparams.use_wandb or hparams.use_mlflow:
         raise SystemExit("W&B / MLflow logging is not available in this build (no network); use the CSV logger")
+    set_operand_dtype(hparams.precision)
     rank, world, dev = init_distributed()
     logger = CSVLogger("logs", name="vq-vae")
     logger.log_hyperparams({"model_name": hparams.model_name, "clipping_value": hparams.clipping_value,
@@ -100,6 +103,8 @@ def parser():
     p.add_argument('--n-val', type=int, default=1024)
     p.add_argument('--n-test', type=int, default=1024)
     p.add_argument('--seed', type=int, default=0)
+    p.add_argument('--precision', choices=["fp32", "bf16"], default="fp32",
+                   help="MFMA operand dtype (bf16: opt-in, fp32 accumulation and master weights)")
     return p
 
 

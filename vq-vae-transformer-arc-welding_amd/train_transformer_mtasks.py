@@ -9,6 +9,8 @@ Data: the frozen VQ-VAE (``--vqvae-model``: a checkpoint written by train_recons
 randomly initialised 512x64 VQ-VAE if the path does not exist) tokenizes synthetic welding sequences of n_cycles
 200x2 windows on the GPU (arcweld.tokenize); ``--data-npz`` may provide real windows ('train'/'val'/'test' of
 shape (n, n_cycles*200, 2) and '<split>_labels').  W&B / MLflow are not available (CSVLogger only).
+``--precision`` picks the MFMA operand dtype (fp32 default, bf16 opt-in; arcweld.precision).  Without
+``--use-all-gpus`` no process group is created (the reference trains on devices=1 then), even under torchrun.
 """
 import argparse
 import logging as log
@@ -22,6 +24,7 @@ import torch  # noqa: E402
 
 from arcweld.data import LatentPredDataModule, synthetic_labels, synthetic_windows  # noqa: E402
 from arcweld.launch import CSVLogger, init_distributed, shutdown  # noqa: E402
+from arcweld.precision import set_operand_dtype  # noqa: E402
 from arcweld.trainer import EarlyStopping, Trainer  # noqa: E402
 from model.transformer_decoder import MyTransformerDecoder  # noqa: E402
 from model.vq_vae_patch_embedd import VQVAEPatch  # noqa: E402
@@ -83,7 +86,9 @@ def main(hparams):
         raise SystemExit("W&B / MLflow are not available in this build (no network); use the CSV logger")
     if hparams.model_wandb_transformer and not os.path.exists(hparams.model_wandb_transformer):
         raise SystemExit("--model-wandb-transformer must be a local checkpoint path in this build")
-    rank, world, dev = init_distributed()
+    set_operand_dtype(hparams.precision)
+    # DDP only with --use-all-gpus (train_transformer_mtasks.py:149-153: otherwise Trainer(devices=1))
+    rank, world, dev = init_distributed(enable=bool(hparams.use_all_gpus))
     logger = CSVLogger("logs", name="vq-vae-transformer")
     logger.log_hyperparams(vars(hparams))
     num_embeddings, patch_size, cls_dm, gen_dm = load_dataset(hparams, dev, only_classify=hparams.classification_only)
@@ -162,6 +167,8 @@ def parser():
     p.add_argument('--n-test', type=int, default=128)
     p.add_argument('--data-npz', type=str, default="")
     p.add_argument('--seed', type=int, default=0)
+    p.add_argument('--precision', choices=["fp32", "bf16"], default="fp32",
+                   help="MFMA operand dtype (bf16: opt-in, fp32 accumulation and master weights)")
     return p
 
 
