@@ -1,167 +1,225 @@
 // Vector quantizer (model/vector_quantizer.py:59-131) for gfx950.
 //
-// Forward: one workgroup = 64 rows (one row per lane, the row held in VGPRs) x 4 waves that split the codes.
-// The codebook is staged through LDS in 64 KiB tiles (K=512 x D=64 is two tiles) and read as wave-uniform
-// float4 broadcasts.  Distances follow the reference expression exactly in fp32:
+// Forward: register-blocked distance tiles with the codebook streamed through LDS (see vq_fwd_kernel).
+// Distances follow the reference expression exactly in fp32:
 //     d_k = fl( fl(|z|^2 + |e_k|^2) - 2 * dot(z, e_k) ),  dot = k-ordered fmaf chain over the embedding dim
 // (torch's CPU sgemm on this shape is bit-identical to that chain -- measured), so the
 // argmin (lexicographic (d, k) minimum == torch.argmin first-index tie rule) is bit-exact.
-// No MFMA: the work is 1 MFLOP/window, dominated by staging, not arithmetic.
+// No MFMA (the north-star design): fp32 VALU, whose rate equals the f32-input MFMA's on gfx950.
 #include "common.h"
 
 namespace {
 
-constexpr int VQ_THREADS = 256;
+// ---------------------------------------------------------------- forward: register-blocked distance tiles
+// One workgroup = 64 rows (the z tile stays in LDS for the whole launch) x 8 waves (two per SIMD).  The codebook
+// streams through LDS in code tiles of 512 codes (64 per wave) x 16-float chunks of the embedding dim, stored
+// d-major ([d][code]) and register-prefetched one chunk ahead.  Lane (lr, lc) = (lane >> 3, lane & 7) of wave w
+// owns the 8 x 8 outer-product block rows {lr + 8i} x codes {64w + 8lc + j}: per embedding index it holds the
+// 8 code values as 4 register pairs and issues 32 packed FMAs (v_pk_fma_f32: the row value in both halves,
+// a pair of codes) -- the FP32 vector peak needs the packed form (a scalar v_fmac loop tops out near 70 TF,
+// tools/probe/valu_fma_probe.hip).  Per 4-deep step: 8 z reads (row broadcasts) + 8 e reads + 128 v_pk_fma.
+// Each (row, code) accumulator is the reference's dot product as an in-order fused-multiply-add chain over the
+// embedding dim; |z|^2 and |e_k|^2 are in-order sums of squares; the distance is fl(fl(|z|^2 + |e_k|^2) - 2 * dot)
+// and the argmin the lexicographic (d, k) minimum (torch.argmin's first-index tie rule).  The register footprint
+// does not depend on D, so the stress codebook (K 8192 x D 256) runs at the same occupancy.
+constexpr int VQ_THREADS = 512;
 constexpr int VQ_ROWS = 64;
+constexpr int VQ_CODES = 512;
+constexpr int VQ_DC = 16;           // embedding floats per staged chunk
+
+template <int D> struct VqLds {
+  static constexpr int ZP = D + 4;                                   // z image pitch (disjoint banks per row)
+  static constexpr int Z = VQ_ROWS * ZP;                             // floats
+  static constexpr int E = VQ_DC * VQ_CODES;                         // floats per stage, [d][code]
+  static constexpr int TOTAL = Z + 2 * E + 2 * VQ_CODES + VQ_ROWS;   // + ee[2][512] + zz[64]
+};
+
+__device__ __forceinline__ bool lex_less(float d, int k, float bd, int bk) { return d < bd || (d == bd && k < bk); }
 
 template <int D>
-__global__ __launch_bounds__(VQ_THREADS) void vq_fwd_kernel(const float* __restrict__ z, const float* __restrict__ E,
-                                                            int64_t N, int K, float* __restrict__ zq,
-                                                            int64_t* __restrict__ idx, float* __restrict__ counts,
-                                                            double* __restrict__ sqerr) {
-  constexpr int KT = 16384 / D;  // codes per 64 KiB LDS tile
-  __shared__ __attribute__((aligned(16))) float Es[KT * D];
-  __shared__ float ee[KT];
-  __shared__ float bd[4][VQ_ROWS];
-  __shared__ int bk[4][VQ_ROWS];
+__global__ __launch_bounds__(VQ_THREADS, 2) void vq_fwd_kernel(const float* __restrict__ z,
+                                                               const float* __restrict__ E, int64_t N, int K,
+                                                               float* __restrict__ zq, int64_t* __restrict__ idx,
+                                                               float* __restrict__ counts,
+                                                               double* __restrict__ sqerr) {
+  using L = VqLds<D>;
+  constexpr int ZP = L::ZP, ND = D / VQ_DC;
+  __shared__ __attribute__((aligned(16))) float smem[L::TOTAL];
+  float* zs = smem;
+  float* es = smem + L::Z;                 // [2][VQ_DC][VQ_CODES]
+  float* ees = es + 2 * L::E;              // [2][VQ_CODES]
+  float* zzs = ees + 2 * VQ_CODES;         // [VQ_ROWS]
 
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int64_t row = (int64_t)blockIdx.x * VQ_ROWS + lane;
-  const bool valid = row < N;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int lr = lane >> 3, lc = lane & 7;
+  const int64_t row0 = (int64_t)blockIdx.x * VQ_ROWS;
 
-  float zr[D];
-  {
-    const float4* zp = reinterpret_cast<const float4*>(z + (valid ? row : 0) * D);
-#pragma unroll
-    for (int q = 0; q < D / 4; ++q) {
-      float4 v = valid ? zp[q] : make_float4(0.f, 0.f, 0.f, 0.f);
-      zr[4 * q + 0] = v.x;
-      zr[4 * q + 1] = v.y;
-      zr[4 * q + 2] = v.z;
-      zr[4 * q + 3] = v.w;
-    }
+  // ---- z tile -> LDS (rows beyond N are zero), |z|^2 per row
+  for (int i = tid; i < VQ_ROWS * (D / 4); i += VQ_THREADS) {
+    const int r = i / (D / 4), q = i - r * (D / 4);
+    const int64_t gr = row0 + r;
+    const float4 v = gr < N ? reinterpret_cast<const float4*>(z + gr * D)[q] : make_float4(0.f, 0.f, 0.f, 0.f);
+    *reinterpret_cast<float4*>(zs + r * ZP + 4 * q) = v;
   }
-  float zz = 0.f;
-#pragma unroll
-  for (int d = 0; d < D; ++d) zz = __fadd_rn(zz, __fmul_rn(zr[d], zr[d]));
-
-  float best = __builtin_huge_valf();
-  int bestk = 0x7fffffff;
-  for (int t0 = 0; t0 < K; t0 += KT) {
-    const int kt = min(KT, K - t0);
-    __syncthreads();
-    const float4* src = reinterpret_cast<const float4*>(E + (int64_t)t0 * D);
-    {
-      // all of this thread's tile loads first, then the LDS stores: a load -> store loop paid one L2 round trip
-      // per float4 (16 in a row per tile)
-      constexpr int PER = KT * D / 4 / VQ_THREADS;
-      const int n4 = kt * D / 4;
-      float4 tmp[PER];
-#pragma unroll
-      for (int u = 0; u < PER; ++u) {
-        const int i = tid + u * VQ_THREADS;
-        tmp[u] = i < n4 ? src[i] : make_float4(0.f, 0.f, 0.f, 0.f);
-      }
-#pragma unroll
-      for (int u = 0; u < PER; ++u) {
-        const int i = tid + u * VQ_THREADS;
-        if (i < n4) reinterpret_cast<float4*>(Es)[i] = tmp[u];
-      }
-    }
-    for (int c = tid; c < kt; c += VQ_THREADS) {  // |e_k|^2 from global (L2) rows: avoids strided LDS reads
-      const float4* ep = reinterpret_cast<const float4*>(E + (int64_t)(t0 + c) * D);
-      float s = 0.f;
-#pragma unroll 4
-      for (int q = 0; q < D / 4; ++q) {
-        float4 v = ep[q];
-        s = __fadd_rn(s, __fmul_rn(v.x, v.x));
-        s = __fadd_rn(s, __fmul_rn(v.y, v.y));
-        s = __fadd_rn(s, __fmul_rn(v.z, v.z));
-        s = __fadd_rn(s, __fmul_rn(v.w, v.w));
-      }
-      ee[c] = s;
-    }
-    __syncthreads();
-    const int per = (kt + 3) / 4;
-    const int kb = wid * per, ke = min(kt, kb + per);
-    // four codes per iteration: four independent in-order fmaf chains (each chain is the reference's dot
-    // product bit for bit; the chains only interleave to hide the fma latency), compared in code order
-    int k = kb;
-    constexpr int NC = D <= 64 ? 4 : 1;   // wide embeddings: the row itself fills the register file
-    for (; NC == 4 && k + 4 <= ke; k += 4) {
-      const float4* e0 = reinterpret_cast<const float4*>(Es + k * D);
-      float dt[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int q = 0; q < D / 4; ++q) {
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          const float4 e = e0[c * (D / 4) + q];
-          dt[c] = fmaf(zr[4 * q + 0], e.x, dt[c]);
-          dt[c] = fmaf(zr[4 * q + 1], e.y, dt[c]);
-          dt[c] = fmaf(zr[4 * q + 2], e.z, dt[c]);
-          dt[c] = fmaf(zr[4 * q + 3], e.w, dt[c]);
-        }
-      }
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const float dist = __fsub_rn(__fadd_rn(zz, ee[k + c]), __fmul_rn(2.f, dt[c]));
-        const int gk = t0 + k + c;
-        if (dist < best || (dist == best && gk < bestk)) {
-          best = dist;
-          bestk = gk;
-        }
-      }
-    }
-    for (; k < ke; ++k) {
-      const float4* e4 = reinterpret_cast<const float4*>(Es + k * D);
-      float dot = 0.f;
-#pragma unroll
-      for (int q = 0; q < D / 4; ++q) {
-        const float4 e = e4[q];
-        dot = fmaf(zr[4 * q + 0], e.x, dot);
-        dot = fmaf(zr[4 * q + 1], e.y, dot);
-        dot = fmaf(zr[4 * q + 2], e.z, dot);
-        dot = fmaf(zr[4 * q + 3], e.w, dot);
-      }
-      const float dist = __fsub_rn(__fadd_rn(zz, ee[k]), __fmul_rn(2.f, dot));
-      const int gk = t0 + k;
-      if (dist < best || (dist == best && gk < bestk)) {
-        best = dist;
-        bestk = gk;
-      }
-    }
-  }
-  bd[wid][lane] = best;
-  bk[wid][lane] = bestk;
   __syncthreads();
-  if (wid != 0) return;
+  if (tid < VQ_ROWS) {
+    float s = 0.f;
+    for (int d = 0; d < D; ++d) s = __fadd_rn(s, __fmul_rn(zs[tid * ZP + d], zs[tid * ZP + d]));
+    zzs[tid] = s;
+  }
+
+  // ---- codebook stream: step s = (code tile s / ND, chunk s % ND); thread t stages code t of the tile
+  const int ntiles = (K + VQ_CODES - 1) / VQ_CODES;
+  const int nsteps = ntiles * ND;
+  float4 pre[VQ_DC / 4];
+  float ee_acc = 0.f;
+  auto load = [&](int st) {
+    const int ct = st / ND, dc = st - ct * ND;
+    const int code = ct * VQ_CODES + tid;
+    const float4* src = reinterpret_cast<const float4*>(E + (int64_t)code * D + dc * VQ_DC);
 #pragma unroll
-  for (int w = 1; w < 4; ++w) {
-    const float d = bd[w][lane];
-    const int k = bk[w][lane];
-    if (d < best || (d == best && k < bestk)) {
-      best = d;
-      bestk = k;
+    for (int u = 0; u < VQ_DC / 4; ++u) pre[u] = code < K ? src[u] : make_float4(0.f, 0.f, 0.f, 0.f);
+  };
+  auto store = [&](int st) {
+    const int ct = st / ND, dc = st - ct * ND;
+    float* dst = es + (st & 1) * L::E + tid;       // transposed: element d of code t at [d][t]
+    if (dc == 0) ee_acc = 0.f;
+#pragma unroll
+    for (int u = 0; u < VQ_DC / 4; ++u) {
+      dst[(4 * u + 0) * VQ_CODES] = pre[u].x;
+      dst[(4 * u + 1) * VQ_CODES] = pre[u].y;
+      dst[(4 * u + 2) * VQ_CODES] = pre[u].z;
+      dst[(4 * u + 3) * VQ_CODES] = pre[u].w;
+      ee_acc = __fadd_rn(ee_acc, __fmul_rn(pre[u].x, pre[u].x));
+      ee_acc = __fadd_rn(ee_acc, __fmul_rn(pre[u].y, pre[u].y));
+      ee_acc = __fadd_rn(ee_acc, __fmul_rn(pre[u].z, pre[u].z));
+      ee_acc = __fadd_rn(ee_acc, __fmul_rn(pre[u].w, pre[u].w));
+    }
+    if (dc == ND - 1) ees[(ct & 1) * VQ_CODES + tid] = ee_acc;
+  };
+
+  f32x2 acc[8][4];                 // [row i][code pair jp]: codes 8lc + 2jp, 8lc + 2jp + 1
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x2{0.f, 0.f};
+  float best[8];
+  int bestk[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    best[i] = __builtin_huge_valf();
+    bestk[i] = 0x7fffffff;
+  }
+
+  load(0);
+  store(0);
+  __syncthreads();
+  float zz[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) zz[i] = zzs[lr + 8 * i];
+
+  for (int st = 0; st < nsteps; ++st) {
+    if (st + 1 < nsteps) load(st + 1);
+    const int ct = st / ND, dc = st - ct * ND;
+    const float* eb = es + (st & 1) * L::E + w * 64 + 8 * lc;
+    const float* zb = zs + lr * ZP + dc * VQ_DC;
+#pragma unroll 1
+    for (int q = 0; q < VQ_DC / 4; ++q) {   // not unrolled: hoisted operand reads of four steps would spill
+      float4 zv[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) zv[i] = *reinterpret_cast<const float4*>(zb + 8 * i * ZP + 4 * q);
+#pragma unroll
+      for (int dd = 0; dd < 4; ++dd) {
+        const float4 e0 = *reinterpret_cast<const float4*>(eb + (4 * q + dd) * VQ_CODES);
+        const float4 e1 = *reinterpret_cast<const float4*>(eb + (4 * q + dd) * VQ_CODES + 4);
+        const f32x2 ep[4] = {f32x2{e0.x, e0.y}, f32x2{e0.z, e0.w}, f32x2{e1.x, e1.y}, f32x2{e1.z, e1.w}};
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const float zi = dd == 0 ? zv[i].x : dd == 1 ? zv[i].y : dd == 2 ? zv[i].z : zv[i].w;
+          const f32x2 zp = f32x2{zi, zi};
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_elementwise_fma(zp, ep[j], acc[i][j]);
+        }
+      }
+    }
+    if (dc == ND - 1) {   // the tile's dot products are complete: distances, running argmin, reset
+      const float* eet = ees + (ct & 1) * VQ_CODES + w * 64 + 8 * lc;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int gk = ct * VQ_CODES + w * 64 + 8 * lc + j;
+        const float e2 = eet[j];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const float dot = (j & 1) ? acc[i][j >> 1].y : acc[i][j >> 1].x;
+          const float dist = __fsub_rn(__fadd_rn(zz[i], e2), __fmul_rn(2.f, dot));
+          if (gk < K && lex_less(dist, gk, best[i], bestk[i])) {
+            best[i] = dist;
+            bestk[i] = gk;
+          }
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x2{0.f, 0.f};
+    }
+    if (st + 1 < nsteps) store(st + 1);
+    __syncthreads();
+  }
+
+  // ---- argmin across the 8 code lanes of a row group, then across the 8 waves (LDS, the e stages are free)
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+#pragma unroll
+    for (int o = 1; o < 8; o <<= 1) {
+      const float d = __shfl_xor(best[i], o, 64);
+      const int k = __shfl_xor(bestk[i], o, 64);
+      if (lex_less(d, k, best[i], bestk[i])) {
+        best[i] = d;
+        bestk[i] = k;
+      }
     }
   }
+  float* rd = es;                                        // [8 waves][64 rows]
+  int* rk = reinterpret_cast<int*>(es + 8 * VQ_ROWS);
+  if (lc == 0) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      rd[w * VQ_ROWS + lr + 8 * i] = best[i];
+      rk[w * VQ_ROWS + lr + 8 * i] = bestk[i];
+    }
+  }
+  __syncthreads();
+  if (w != 0) return;
+  const int r = lane;
+  const int64_t row = row0 + r;
+  float bd = rd[r];
+  int bk = rk[r];
+#pragma unroll
+  for (int v = 1; v < 8; ++v)
+    if (lex_less(rd[v * VQ_ROWS + r], rk[v * VQ_ROWS + r], bd, bk)) {
+      bd = rd[v * VQ_ROWS + r];
+      bk = rk[v * VQ_ROWS + r];
+    }
   double se = 0.0;
-  if (valid) {
-    if (bestk < 0 || bestk >= K) bestk = 0;  // all-NaN row guard (torch would return the NaN position)
-    idx[row] = bestk;
-    atomicAdd(counts + bestk, 1.0f);
-    const float4* ep = reinterpret_cast<const float4*>(E + (int64_t)bestk * D);
+  if (row < N) {
+    if (bk < 0 || bk >= K) bk = 0;  // all-NaN row guard (torch would return the NaN position)
+    idx[row] = bk;
+    atomicAdd(counts + bk, 1.0f);
+    const float4* ep = reinterpret_cast<const float4*>(E + (int64_t)bk * D);
+    const float* zr = zs + r * ZP;
     float4* op = reinterpret_cast<float4*>(zq + row * D);
     float s = 0.f;
-#pragma unroll
     for (int q = 0; q < D / 4; ++q) {
       const float4 e = ep[q];
+      const float4 zv = *reinterpret_cast<const float4*>(zr + 4 * q);
+      const float d0 = __fsub_rn(e.x, zv.x), d1 = __fsub_rn(e.y, zv.y);
+      const float d2 = __fsub_rn(e.z, zv.z), d3 = __fsub_rn(e.w, zv.w);
       float4 o;
-      float d0 = __fsub_rn(e.x, zr[4 * q + 0]), d1 = __fsub_rn(e.y, zr[4 * q + 1]);
-      float d2 = __fsub_rn(e.z, zr[4 * q + 2]), d3 = __fsub_rn(e.w, zr[4 * q + 3]);
-      o.x = __fadd_rn(zr[4 * q + 0], d0);  // z + (z_q - z).detach()
-      o.y = __fadd_rn(zr[4 * q + 1], d1);
-      o.z = __fadd_rn(zr[4 * q + 2], d2);
-      o.w = __fadd_rn(zr[4 * q + 3], d3);
+      o.x = __fadd_rn(zv.x, d0);  // z + (z_q - z).detach()
+      o.y = __fadd_rn(zv.y, d1);
+      o.z = __fadd_rn(zv.z, d2);
+      o.w = __fadd_rn(zv.w, d3);
       op[q] = o;
       s += d0 * d0 + d1 * d1 + d2 * d2 + d3 * d3;
     }
