@@ -45,6 +45,8 @@ def parse():
     ap.add_argument("--no-transformer", action="store_true",
                     help="skip the secondary configs[2]/[3] line items (tokenize + 8-block Transformer train step)")
     ap.add_argument("--no-fp32", action="store_true", help="skip the exact-fp32 operand line of configs[1]")
+    ap.add_argument("--no-stress", action="store_true",
+                    help="skip the configs[4] line (codebook 8192x256, T 1025, 16-block Transformer)")
     ap.add_argument("--seqs", type=int, default=51, help="Transformer sequences per GPU per step (configs[2])")
     ap.add_argument("--n-cycles", type=int, default=20)
     ap.add_argument("--gemm-tile", type=int, default=0, choices=[0, 128, 256],
@@ -52,10 +54,10 @@ def parse():
     return ap.parse_args()
 
 
-def build_model(dev):
+def build_model(dev, K=512, D=64):
     from model.vq_vae_patch_embedd import VQVAEPatch
     torch.manual_seed(1)
-    m = VQVAEPatch(hidden_dim=512, input_dim=2, num_embeddings=512, embedding_dim=64, n_resblocks=8,
+    m = VQVAEPatch(hidden_dim=512, input_dim=2, num_embeddings=K, embedding_dim=D, n_resblocks=8,
                    learning_rate=1e-3, dropout_p=0.1, patch_size=25, seq_len=200, batch_norm=False)
     return m.to(dev).train()
 
@@ -86,7 +88,8 @@ def transformer_flops_per_seq(T, n_blocks=8, d=512, V=514):
     return 3 * (n_blocks * (24 * d * d * T + 2 * d * T * (T + 1)) + 2 * d * V * T)
 
 
-def transformer_workload(dev, rank, world, args, seqs, n_cycles, accumulate=1, label="configs[2]"):
+def transformer_workload(dev, rank, world, args, seqs, n_cycles, accumulate=1, label="configs[2]", K=512, D=64,
+                         n_blocks=8):
     """Per optimizer step the frozen VQ-VAE encoder tokenizes seqs x n_cycles windows per micro-batch (fused
     encoder + VQ, exact fp32 operands), then the 8-block/8-head d512 decoder trains on the generation task
     (T = 16*n_cycles + 1, V = 514, clip 0.8, RAdam betas (0.9, 0.95) wd 0.1 on Linear weights) over `accumulate`
@@ -94,12 +97,13 @@ def transformer_workload(dev, rank, world, args, seqs, n_cycles, accumulate=1, l
     from arcweld import tokenize
     from arcweld.trainer import Trainer
     from model.transformer_decoder import MyTransformerDecoder
-    vq = build_model(dev).eval()
+    vq = build_model(dev, K, D).eval()
     nc = n_cycles
     T = 16 * nc + 1
+    V = K + 2
     torch.manual_seed(2)
-    dec = MyTransformerDecoder(d_model=512, n_classes=514, seq_len=T, n_blocks=8, n_head=8,
-                               res_dropout=0.1).to(dev).train()
+    dec = MyTransformerDecoder(d_model=512, n_classes=V, seq_len=T, n_blocks=n_blocks, n_head=8, res_dropout=0.1,
+                               pe_len=max(512, T)).to(dev).train()
     tr = Trainer(gradient_clip_val=0.8, accumulate_grad_batches=accumulate)
     tr.setup_optimizer(dec)
     g = torch.Generator(device=dev)
@@ -111,7 +115,7 @@ def transformer_workload(dev, rank, world, args, seqs, n_cycles, accumulate=1, l
 
     def train(w):
         ids = tokenize.encode_ids(vq, w)
-        x, y, _ = tokenize.autoregressive_pairs(ids, start_token=512)
+        x, y, _ = tokenize.autoregressive_pairs(ids, start_token=K)
         return (x, cond, y)
 
     def step(i):
@@ -125,15 +129,19 @@ def transformer_workload(dev, rank, world, args, seqs, n_cycles, accumulate=1, l
             tr.optimizer_step(dec)
 
     if use_graph:
-        orig = dec.training_step
+        # the captured step tokenizes its static window buffer itself (warm-up calls: training_step; captured
+        # replays: the fused step with the mid-backward all-reduce split)
+        orig, orig_fused = dec.training_step, dec.fused_train_step
         dec.training_step = lambda w, i: orig(train(w), i)
+        dec.fused_train_step = lambda w, scale, mid_hook=None: orig_fused(train(w), scale, mid_hook=mid_hook)
     el = _timed_steps(step, max(args.warmup, 1 if use_graph else 0), args.steps, world)
     windows = world * seqs * accumulate * nc * args.steps
-    flops = transformer_flops_per_seq(T) * seqs * accumulate * world * args.steps
+    flops = transformer_flops_per_seq(T, n_blocks, 512, V) * seqs * accumulate * world * args.steps
     return {"value": round(windows / el, 2), "unit": "windows/s", "ms_per_step": round(el * 1e3 / args.steps, 3),
             "config": {"workload": f"tokenize (frozen VQ-VAE encoder, fp32 exact) + Transformer train step ({label})",
                        "seqs_per_gpu_per_micro_batch": seqs, "accumulate_grad_batches": accumulate,
-                       "n_cycles": nc, "T": T, "d_model": 512, "n_blocks": 8, "n_head": 8, "V": 514,
+                       "n_cycles": nc, "T": T, "d_model": 512, "n_blocks": n_blocks, "n_head": 8, "V": V,
+                       "codebook": f"{K}x{D}",
                        "global_batch_windows": windows // args.steps, "operands": "bf16"},
             "transformer_tflops": round(flops / el / 1e12, 2),
             "launch": "hip-graph" if use_graph else "eager"}
@@ -215,7 +223,7 @@ def cpu_baseline(seconds):
             "reference": REFERENCE_CPU}
 
 
-def vqvae_workload(dev, rank, world, args, dtype, steps, warmup, profile=True):
+def vqvae_workload(dev, rank, world, args, dtype, steps, warmup, profile=True, K=512, D=64):
     """configs[1]: one step = fwd + bwd (mse + VQ loss) + clip 0.7 + RAdam over B windows per GPU, inputs resident
     in HBM, captured as HIP graphs; operands `dtype` (bf16 opt-in or exact fp32).  Returns (elapsed seconds,
     per-GEMM profile list or None, eager seconds/step of the profiled pass)."""
@@ -223,7 +231,7 @@ def vqvae_workload(dev, rank, world, args, dtype, steps, warmup, profile=True):
     from arcweld.precision import operands
     from arcweld.trainer import Trainer
     with operands(dtype):
-        model = build_model(dev)
+        model = build_model(dev, K, D)
         trainer = Trainer(gradient_clip_val=0.7)
         trainer.setup_optimizer(model)
         scale = 1.0 / world
@@ -278,6 +286,57 @@ def gemm_roofline(prof, prof_el, elapsed, steps, peak, dtype_name, traffic=None,
             "eager_ms_per_step_with_events": round(prof_el * 1e3, 3)}
 
 
+def vq_kernel_roofline(dev, N, K, D, iters=10):
+    """aw_vq_forward alone at (N, K, D): HIP events around each launch on its stream; 2*N*K*D FP32 FLOPs against the
+    157.3 TF fp32 vector peak (the north star's "FP32-VALU-bound" kernel), plus its algorithmic HBM bytes
+    (z + E + idx + z_q + counts)."""
+    from arcweld import kernels
+    g = torch.Generator(device=dev).manual_seed(5)
+    z = torch.randn(N, D, device=dev, generator=g) * 0.08
+    E = torch.randn(K, D, device=dev, generator=g) * 0.08
+    zq, idx = torch.empty_like(z), torch.empty(N, dtype=torch.int64, device=dev)
+    counts, sq = torch.zeros(K, device=dev), torch.zeros(1, device=dev, dtype=torch.float64)
+    s = torch.cuda.current_stream()
+    kernels.vq_forward(z, E, zq, idx, counts, sq)
+    evs = []
+    for _ in range(iters):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        kernels.vq_forward(z, E, zq, idx, counts, sq)
+        e1.record(s)
+        evs.append((e0, e1))
+    torch.cuda.synchronize()
+    us = sum(a.elapsed_time(b) for a, b in evs) * 1e3 / iters
+    tf = 2.0 * N * K * D / (us * 1e-6) / 1e12
+    byts = N * D * 4 * 2 + K * D * 4 + N * 8 + K * 4
+    return {"kernel": "vq_fwd_kernel<D> (aw_vq_forward)", "bound": "fp32-valu", "N": N, "K": K, "D": D,
+            "avg_launch_us": round(us, 2), "achieved": round(tf, 2), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(tf / FP32_PEAK_TFLOPS, 4), "algorithmic_bytes": byts,
+            "hbm_gbs": round(byts / (us * 1e-6) / 1e9, 1)}
+
+
+def stress_workload(dev, rank, world, args):
+    """configs[4]: the VQ-VAE with the 8192 x 256 codebook (B = 1024 windows per GPU, bf16 operands, graphed step)
+    and the 16-block Transformer at T = 1025 (n_cycles 64, V 8194; 16 sequences = 1024 windows per GPU, tokenized
+    by that VQ-VAE), each reported as windows/s with its roofline."""
+    from arcweld.precision import operands
+    n = max(2, args.steps // 4)
+    el, prof, pel = vqvae_workload(dev, rank, world, args, torch.bfloat16, n, 2, profile=not args.no_profile,
+                                   K=8192, D=256)
+    out = {"vqvae": {"value": round(world * args.batch * n / el, 2), "unit": "windows/s",
+                     "ms_per_step": round(el * 1e3 / n, 3), "steps": n,
+                     "config": {"workload": "VQ-VAE-Patch train step, stress codebook (configs[4])",
+                                "per_gpu_batch": args.batch, "codebook": "8192x256", "operands": "bf16"},
+                     "roofline": gemm_roofline(prof, pel, el, n, BF16_PEAK_TFLOPS, "bf16") if prof else None,
+                     "vq_kernel": vq_kernel_roofline(dev, args.batch * 16, 8192, 256)}}
+    sargs = argparse.Namespace(**vars(args))
+    sargs.steps = n
+    with operands(torch.bfloat16):
+        out["transformer"] = transformer_workload(dev, rank, world, sargs, 16, 64, K=8192, D=256, n_blocks=16,
+                                                  label="configs[4] stress: 16 blocks, T 1025, codebook 8192x256")
+    return out
+
+
 def _transformer_lines(extra, dev, rank, world, args):
     """configs[2] at 51 sequences per step (1020 windows), configs[2] at the reference's own batch (16 sequences x
     accumulate_grad_batches 5, train_transformer_mtasks.py:32) and the configs[3](ii) shape (n_cycles 16, T = 257,
@@ -314,7 +373,7 @@ def main():
     roofline = gemm_roofline(prof, prof_el, elapsed, args.steps, BF16_PEAK_TFLOPS, "bf16", traffic,
                              traffic_src) if prof else None
 
-    extra = {}
+    extra = {"vq_kernel": vq_kernel_roofline(dev, args.batch * 16, 512, 64)}
     if not args.no_fp32:
         # the same step with exact-fp32 operands (the default numerics, the reference's): priced against the
         # 157.3 TF fp32 MFMA roof
@@ -323,6 +382,8 @@ def main():
         extra["fp32"] = {"value": round(world * args.batch * n32 / el32, 2), "unit": "windows/s",
                          "ms_per_step": round(el32 * 1e3 / n32, 3), "steps": n32, "dtype": "f32",
                          "roofline": gemm_roofline(prof32, pel32, el32, n32, FP32_PEAK_TFLOPS, "f32") if prof32 else None}
+    if not args.no_stress:
+        extra["stress"] = stress_workload(dev, rank, world, args)
     if not args.no_transformer:
         from arcweld.precision import operands
         with operands(torch.bfloat16):

@@ -238,3 +238,34 @@ def test_cached_generate_matches_reference_recompute(fp32_mode):
     b = m.generate(x, use_cache=False)
     assert a.shape == (2, 9 + SMALL["seq_len"])
     assert torch.equal(a, b)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("task", ["gen", "cls"])
+def test_fused_train_step_matches_autograd_and_split_point_is_final(fp32_parity, task):
+    """fused_train_step (no autograd; what a captured data-parallel step runs) gives the autograd step's loss and
+    gradients, and at its mid_hook every gradient of backward_late_parameters() is final while every other one is
+    still untouched -- the invariant the overlapped all-reduce of the later blocks relies on."""
+    m = make_model(dict(SMALL, n_blocks=4), 4, 411, device="cuda").train()
+    batch = inputs(4, 33, 34, 412, "cuda")
+    x, y, cond = batch
+    loss_ref, _ = _step(m, task, batch)
+    ref = {n: p.grad.clone() for n, p in m.named_parameters() if p.grad is not None}
+    for p in m.parameters():
+        p.grad = torch.zeros_like(p)
+    names = [n for n, _ in m.named_parameters()]
+    params = list(m.parameters())
+    late = set(id(p) for p in m.backward_late_parameters())
+    snap = []
+    loss = m.fused_train_step((x, cond, y), 1.0, mid_hook=lambda: snap.append([p.grad.clone() for p in params]))
+    assert len(snap) == 1
+    np.testing.assert_allclose(loss.item(), loss_ref.item(), rtol=1e-6)
+    for i, (n, p) in enumerate(zip(names, params)):
+        if n in ref:
+            torch.testing.assert_close(p.grad, ref[n], rtol=1e-5, atol=1e-7, msg=n)
+            if id(p) in late:
+                assert torch.equal(snap[0][i], p.grad), n
+            else:
+                assert not snap[0][i].any(), n
+        else:
+            assert not p.grad.any(), n

@@ -131,8 +131,21 @@ def forward(m, ids, generate: bool, training: bool, need_backward: bool, seed: i
     return out, (sv if need_backward else None)
 
 
-def backward(m, sv, g_out, slot):
-    """g_out: gradient of the logits (B, T, V) f32 or of the class logits (B, 2)."""
+def late_parameters(m, generate):
+    """Parameters whose gradients are final at backward()'s mid_hook: the task head, ln_f and blocks
+    nb//2 .. nb-1 (the backward reaches them first; their weight gradients are issued before the hook)."""
+    nb = len(m.transformer.h)
+    ps = [m.lm_head.weight] if generate else list(m.class_head.parameters())
+    ps += list(m.transformer.ln_f.parameters())
+    for blk in list(m.transformer.h)[nb // 2:]:
+        ps += list(blk.parameters())
+    return ps
+
+
+def backward(m, sv, g_out, slot, mid_hook=None):
+    """g_out: gradient of the logits (B, T, V) f32 or of the class logits (B, 2).  ``mid_hook()`` runs once the
+    gradients of late_parameters(m, generate) are final (a data-parallel step starts their all-reduce there, which
+    then overlaps the backward of the earlier blocks)."""
     B, T, R, d, nh, V, T_ = sv.B, sv.T, sv.R, sv.d, sv.nh, sv.V, sv.Tdt
     dev = g_out.device
     e = lambda *s, dt=F32: torch.empty(*s, device=dev, dtype=dt)  # noqa: E731
@@ -161,8 +174,10 @@ def backward(m, sv, g_out, slot):
     last = nb - 1
     K.layernorm_bwd(sv.x_last, gxf, lnf.weight, sv.muf, sv.rsf, gx, False, slot(lnf.weight), slot(lnf.bias),
                     dx2=go, drop=(sv.p_drop, sv.seed_mlp[last] if nb else 0), seed_ptr=sv.ctr)
-    # per-layer-kind weight gradients are deferred and issued as one grouped launch per kind over all blocks
+    # per-layer-kind weight gradients are deferred and issued as grouped launches per kind: once for the later
+    # half of the blocks (before the mid-backward hook), once for the rest
     wg = {"fc2": [], "fc1": [], "proj": [], "qkv": []}
+    half = nb // 2
     for i in reversed(range(nb)):
         blk = m.transformer.h[i]
         at, mlp = blk.attn, blk.mlp
@@ -196,8 +211,16 @@ def backward(m, sv, g_out, slot):
         K.layernorm_bwd(c["x"], ga, blk.ln_1.weight, c["mu1"], c["rs1"], gx, True, slot(blk.ln_1.weight),
                         slot(blk.ln_1.bias), dx2=go, drop=(sv.p_drop, sv.seed_mlp[i - 1] if i > 0 else 0),
                         seed_ptr=sv.ctr)
+        if i == half:
+            for kind in wg:
+                K.gemm_grouped(wg[kind])
+                wg[kind] = []
+            if mid_hook is not None:
+                mid_hook()
     for probs in wg.values():
         K.gemm_grouped(probs)
+    if nb == 0 and mid_hook is not None:
+        mid_hook()
     K.embed_bwd(sv_ids(sv), gx, slot(m.embedding.latent_embedding.weight))
 
 
@@ -255,6 +278,33 @@ class _CrossEntropy(torch.autograd.Function):
         dl = torch.empty(R, V, device=logits2d.device)
         K.ce_bwd(logits2d, V, target.contiguous(), ctx.ignore, lse, s[1:2], g.reshape(1).contiguous(), dl)
         return dl, None, None
+
+
+def fused_step(m, batch, scale, slot, mid_hook=None):
+    """forward + cross-entropy + backward of one micro-batch of the current task, without autograd: the work of
+    training_step followed by (loss * scale).backward() (model/transformer_decoder.py:139-155, 226-230).  Returns
+    (loss, logits)."""
+    x, cond, y = batch
+    generate = m.task == "generate"
+    out, sv = forward(m, x, generate, m.training, need_backward=True, seed=m._next_seed())
+    sv.ids = x.contiguous()
+    dev = x.device
+    if generate:
+        logits2d = out.view(-1, out.shape[-1])          # rows of stride Vp (the padded logits buffer)
+        target, ignore = y.reshape(-1).contiguous(), -1
+    else:
+        logits2d, target, ignore = out, cond.reshape(-1).contiguous(), -100
+    R, V = logits2d.shape
+    lse = torch.empty(R, device=dev)
+    sums = torch.zeros(2, device=dev, dtype=torch.float64)
+    K.ce_fwd(logits2d, V, target, ignore, sums[0:1], sums[1:2], lse)
+    loss = torch.empty((), device=dev)
+    K.ce_finalize(sums[0:1], sums[1:2], loss)
+    g = torch.full((1,), float(scale), device=dev)
+    dl = torch.empty(R, V, device=dev)
+    K.ce_bwd(logits2d, V, target, ignore, lse, sums[1:2], g, dl)
+    backward(m, sv, dl.view(out.shape), slot, mid_hook=mid_hook)
+    return loss, out
 
 
 def cross_entropy(logits2d, target, ignore_index=-100):

@@ -4,9 +4,10 @@ A step is captured as graphs on the current stream:
   g_fwd_bwd : forward + backward of one micro-batch (gradients accumulate into the flat buffer)
   g_update  : clip-norm + RAdam + zero_grad
 With data parallelism the RCCL all-reduce of the flat gradient buffer runs eagerly between the two.  A model
-with ``fused_train_step`` (VQVAEPatch) is captured as TWO forward/backward graphs split where its decoder-side
-gradients are final: the decoder-side all-reduce is launched (async, RCCL stream) between them and overlaps the
-encoder-side backward; the encoder-side all-reduce follows.  Replay needs no host values: dropout masks come from
+with ``fused_train_step`` (VQVAEPatch, MyTransformerDecoder) is captured as TWO forward/backward graphs split
+where its ``backward_late_parameters()`` are final (VQ-VAE: the decoder side; Transformer: the task head, ln_f and
+the later half of the blocks): their all-reduce is launched (async, RCCL stream) between the two replays and
+overlaps the rest of the backward; the remaining gradients' all-reduce follows.  Replay needs no host values: dropout masks come from
 a device counter (aw_gemm_args.seed_ptr), the RAdam step number and clip coefficient live on the device.  Inputs
 are copied into static buffers before each replay.
 
@@ -42,7 +43,7 @@ class StepGraphs:
         self.warmup = warmup
         self.calls = 0
         self.static = None
-        self.split = hasattr(model, "fused_train_step") and hasattr(model, "backward_split_parameter")
+        self.split = hasattr(model, "fused_train_step") and hasattr(model, "backward_late_parameters")
 
     def _capture(self, batch):
         self.static = _clone_static(batch)

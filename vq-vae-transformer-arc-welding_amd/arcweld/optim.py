@@ -142,6 +142,37 @@ class RAdam(torch.optim.Optimizer):
         hi = self._flat["total"] if hi is None else hi
         return [(max(a, lo), min(b, hi)) for a, b in self._flat["spans"] if min(b, hi) > max(a, lo)]
 
+    def param_spans(self, params):
+        """Merged [a, b) ranges of the flat buffers holding the (live) segments of ``params``: what an all-reduce
+        of just those gradients moves (alignment padding between adjacent segments included)."""
+        self.flatten()
+        keep = set(id(p) for p in params)
+        al = lambda n: (n + 63) // 64 * 64   # noqa: E731
+        spans = []
+        for p, o, n, _, _ in self._flat["segs"]:
+            if id(p) not in keep:
+                continue
+            if spans and o <= al(spans[-1][1]):
+                spans[-1][1] = max(spans[-1][1], o + n)
+            else:
+                spans.append([o, o + n])
+        return [tuple(x) for x in spans]
+
+    def live_spans_excluding(self, spans):
+        """live_spans() minus the given [a, b) ranges."""
+        out = []
+        for a, b in self.live_spans():
+            cur = a
+            for x, y in sorted(spans):
+                if y <= cur or x >= b:
+                    continue
+                if x > cur:
+                    out.append((cur, x))
+                cur = max(cur, y)
+            if cur < b:
+                out.append((cur, b))
+        return out
+
     @property
     def flat_grad(self):
         return self.flatten()[1]

@@ -149,18 +149,20 @@ class Trainer:
         return self._graphs.run(batch)
 
     def _allreduce_region(self, model, region):
-        """Async all-reduce of the flat gradients: "all", or split at the model's backward_split_parameter into
-        "late" (that parameter onwards: final mid-backward) and "early" (the parameters before it)."""
+        """Async all-reduce of the flat gradients: "all", or split by the model's backward_late_parameters() into
+        "late" (those parameters: final at the fused step's mid-backward hook, reduced while the rest of the
+        backward runs) and "early" (every other live gradient)."""
         opt = self.optimizer
         flat = opt.flat_grad
         if not self.data_parallel:
             return []
-        if region == "all" or not hasattr(model, "backward_split_parameter"):
+        if region == "all" or not hasattr(model, "backward_late_parameters"):
             return allreduce_spans(flat, _spans(opt)) if region in ("all", "late") else []
-        cut = opt.flat_offset(model.backward_split_parameter())
-        if region == "late":
-            return allreduce_spans(flat, _spans(opt, lo=cut))
-        return allreduce_spans(flat, _spans(opt, hi=cut))
+        key = (id(model), getattr(model, "task", None))      # the late set of the decoder follows its task
+        if getattr(self, "_late_key", None) != key:
+            late = opt.param_spans(model.backward_late_parameters())
+            self._late_spans, self._early_spans, self._late_key = late, opt.live_spans_excluding(late), key
+        return allreduce_spans(flat, self._late_spans if region == "late" else self._early_spans)
 
     def fit(self, model, datamodule=None, train_dataloaders=None, val_dataloaders=None):
         if datamodule is not None:

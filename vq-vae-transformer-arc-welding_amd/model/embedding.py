@@ -8,17 +8,16 @@ from arcweld import kernels as K
 
 
 class PositionalEmbedding(nn.Module):
-    """Fixed sinusoidal table (reference :6-24), buffer 'pe' of shape (1, max_len, d_model)."""
+    """Fixed sinusoidal table (reference :6-24): buffer 'pe' (1, max_len, d_model) with
+    pe[p, 2i] = sin(p * w_i), pe[p, 2i+1] = cos(p * w_i), w_i = exp(2i * -(ln 10000 / d_model)), evaluated in fp32
+    exactly as the reference does (same operations, same rounding), so the buffer is bit-identical."""
 
     def __init__(self, d_model, max_len=5000):
         super().__init__()
-        pe = torch.zeros(max_len, d_model).float()
-        pe.require_grad = False
-        position = torch.arange(0, max_len).float().unsqueeze(1)
-        div_term = (torch.arange(0, d_model, 2).float() * -(math.log(10000.0) / d_model)).exp()
-        pe[:, 0::2] = torch.sin(position * div_term)
-        pe[:, 1::2] = torch.cos(position * div_term)
-        self.register_buffer('pe', pe.unsqueeze(0))
+        inv_freq = (torch.arange(0, d_model, 2).float() * -(math.log(10000.0) / d_model)).exp()
+        angle = torch.arange(max_len, dtype=torch.float32)[:, None] * inv_freq[None, :]
+        table = torch.stack((angle.sin(), angle.cos()), dim=-1).reshape(max_len, -1)[:, :d_model]
+        self.register_buffer('pe', table.contiguous().unsqueeze(0))
 
     def forward(self, x):
         return self.pe[:, :x.size(1)]
@@ -38,7 +37,8 @@ class LatentEmbeddingCond(nn.Module):
 
 
 class LatentEmbedding(nn.Module):
-    """latent_embedding(ids) + pe[:T] (reference :45-59); the PE table is capped at seq_len rows (default 512)."""
+    """latent_embedding(ids) + pe[:T] (reference :45-59); the PE table has seq_len rows (the decoder passes 512,
+    reference model/transformer_decoder.py:22-23, unless its pe_len opt-in asks for more)."""
 
     def __init__(self, input_size: int, d_model: int, seq_len: int = 512) -> None:
         super().__init__()

@@ -1,7 +1,9 @@
 """Latent-token Transformer decoder -- drop-in for model/transformer_decoder.py:13-230 of the reference.
 
 Same constructor, module tree / state_dict keys, initialisation, optimizer groups, task switching, step methods
-and log keys.  forward() runs the fused HIP engine (arcweld.decoder): embedding, the pre-LN blocks (flash-style
+and log keys.  One opt-in extension: ``pe_len`` (default 512, the reference's hard-coded positional table,
+:22-23) sizes the sinusoidal table from its closed form (model/embedding.py:10-18) so that sequences longer than
+512 tokens -- the stress configuration's T = 1025 -- can run; at the default the state_dict is the reference's.  forward() runs the fused HIP engine (arcweld.decoder): embedding, the pre-LN blocks (flash-style
 causal attention, GEMM epilogues carrying bias/GELU/dropout/residual), ln_f and the task head; the losses are the
 HIP cross-entropy kernels.
 """
@@ -32,7 +34,7 @@ class MyTransformerDecoder(LightningModule):
 
     def __init__(self, d_model: int = 64, n_classes: int = 131, seq_len: int = 100, n_blocks: int = 2,
                  n_head: int = 6, res_dropout=0.1, att_dropout=0.0, learning_rate: float = 1e-3,
-                 class_h_bias: bool = False, class_h_dropout: bool = False):
+                 class_h_bias: bool = False, class_h_dropout: bool = False, pe_len: int = 512):
         super().__init__()
         self.task = "generate"
         self.learning_rate = learning_rate
@@ -43,7 +45,7 @@ class MyTransformerDecoder(LightningModule):
         self.n_head = n_head
         self.n_classes = n_classes
         self.res_dropout = res_dropout
-        self.embedding = LatentEmbedding(input_size=n_classes, d_model=d_model, seq_len=512)
+        self.embedding = LatentEmbedding(input_size=n_classes, d_model=d_model, seq_len=int(pe_len))
         self.transformer = nn.ModuleDict(dict(
             drop=nn.Dropout(res_dropout),
             h=nn.ModuleList([Block(d_model=d_model, seq_len=seq_len, n_head=n_head, res_dropout=res_dropout,
@@ -132,6 +134,33 @@ class MyTransformerDecoder(LightningModule):
             return engine.DecoderFunction.apply(self, x, generate, self._next_seed(), *params)
         out, _ = engine.forward(self, x, generate, self.training, need_backward=False, seed=self._next_seed())
         return out
+
+    @torch.no_grad()
+    def fused_train_step(self, batch, scale, mid_hook=None):
+        """One training micro-step on the kernels without autograd: training_step followed by
+        ``(loss * scale).backward()``.  Gradients accumulate into each parameter's ``.grad`` (the flat optimizer
+        views when a Trainer installed ``_grad_sink``); ``mid_hook`` runs once backward_late_parameters() are final
+        (arcweld.decoder.backward).  Returns the loss."""
+        sink = getattr(self, "_grad_sink", None)
+
+        def slot(p):
+            if sink is not None and p in sink:
+                return sink[p]
+            if p.grad is None:
+                p.grad = torch.zeros_like(p)
+            return p.grad
+
+        loss, logits = engine.fused_step(self, batch, scale, slot, mid_hook=mid_hook)
+        if self.task == "generate":
+            self.log('train/loss', loss, prog_bar=True)
+        else:
+            self.log_classification_results(loss, logits, batch[1], "train")
+        return loss
+
+    def backward_late_parameters(self):
+        """Parameters whose gradients are final at fused_train_step's mid_hook (the task head, ln_f, the later half
+        of the blocks): a data-parallel step all-reduces them while the earlier blocks' backward runs."""
+        return engine.late_parameters(self, self.task == "generate")
 
     def switch_to_generate(self):
         self.task = "generate"

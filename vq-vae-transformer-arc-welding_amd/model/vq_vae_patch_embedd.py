@@ -291,6 +291,13 @@ class VQVAEPatch(Autoencoder):
         """First parameter (in registration order) whose gradient is final at fused_train_step's mid_hook."""
         return self.vector_quantization.embedding.weight
 
+    def backward_late_parameters(self):
+        """Parameters whose gradients are final at fused_train_step's mid_hook: the codebook and everything after
+        it in registration order (decoder 1x1 conv, decoder ResBlocks, un-patch head)."""
+        ps = list(self.parameters())
+        cut = next(i for i, p in enumerate(ps) if p is self.backward_split_parameter())
+        return ps[cut:]
+
     @torch.no_grad()
     def encode_ids(self, x):
         """Frozen-encoder tokenization (latentspace_dataloader.py:154-161): windows (B, L, C) -> ids (B, S) int64,
