@@ -62,6 +62,8 @@ _SHIM = {
             def __init__(self, *a, **k):
                 raise RuntimeError('improved VQ is out of scope (vector-quantize-pytorch not installed)')
         """),
+    # dataloader/utils.py reads the data path from a .env file; every call here passes data_directory_path
+    "dotenv/__init__.py": "def dotenv_values(*a, **k):\n    return {}\n",
 }
 
 
@@ -272,18 +274,149 @@ def case_radam():
     save("radam.npz", **out)
 
 
-def main():
+# ----------------------------------------------------------------------------- training regime
+REGIME_KW = dict(d_model=32, n_classes=20, seq_len=17, n_blocks=2, n_head=4, res_dropout=0.0, att_dropout=0.0)
+REGIME_STAGES = (("generate", 3), ("classification", 2))    # (task, optimizer steps); 5 micro-batches per step
+
+
+def regime_batch(stage: int, step: int, micro: int):
+    """Micro-batch (x, cond, y) of 4 sequences: ids in [0, 18) with start/end tokens 18/19 as
+    MyLatentAutoregressiveDataset builds them (dataloader/base_dataloader.py:74-110)."""
+    seed = 1000 + 100 * stage + 10 * step + micro
+    ids = gen.randint(seed, (4, 16), 0, 18)
+    x = np.concatenate([np.full((4, 1), 18), ids], axis=1)
+    y = np.concatenate([ids, np.full((4, 1), 19)], axis=1)
+    cond = gen.randint(seed + 7, (4,), 0, 2)
+    return torch.from_numpy(x), torch.from_numpy(cond), torch.from_numpy(y)
+
+
+def case_training_regime(MyTransformerDecoder):
+    """train_transformer_mtasks.py:23-33,178-190 on the reference module: per stage a new Trainer and so a new
+    optimizer (the module's own configure_optimizers: torch.optim.RAdam, betas (0.9, 0.95), wd 0.1 on Linear
+    weights); Lightning automatic optimisation with accumulate_grad_batches=5 (each micro-batch loss / 5, one
+    backward each), gradient_clip_val=0.8 (clip_grad_norm_ over the optimizer's parameters -- the unused head has
+    grad None and is skipped), optimizer.step(), zero_grad(set_to_none=True).  Generate stage, then a
+    classification stage on the same module."""
+    torch.manual_seed(0)
+    m = MyTransformerDecoder(**REGIME_KW)
+    load_det_state(m, 1001)
+    m.train()
+    out = {}
+    for si, (task, nsteps) in enumerate(REGIME_STAGES):
+        (m.switch_to_generate if task == "generate" else m.switch_to_classification)()
+        opt = m.configure_optimizers()
+        params = [p for g in opt.param_groups for p in g["params"]]
+        for step in range(nsteps):
+            losses = []
+            for micro in range(5):
+                loss, _, _ = m._step(regime_batch(si, step, micro))
+                (loss / 5).backward()
+                losses.append(loss.item())
+            out[f"s{si}/loss_{step}"] = np.array(losses, dtype=np.float32)
+            out[f"s{si}/gradnorm_{step}"] = torch.nn.utils.clip_grad_norm_(params, 0.8).numpy()
+            out[f"s{si}/unused_grad_is_none_{step}"] = np.array(
+                (m.class_head.linear_1.weight.grad is None) if task == "generate" else (m.lm_head.weight.grad is None))
+            opt.step()
+            opt.zero_grad(set_to_none=True)
+        for n, p in m.named_parameters():
+            out[f"s{si}/param/{n}"] = p.detach().numpy().copy()
+    save("training_regime.npz", **out)
+
+
+# ------------------------------------------------------------------------- ASIMoW CSV format (SURVEY §8 f3)
+ASIMOW_VAL = ((1, 2), (3, 1))
+ASIMOW_TEST = ((2, 3),)
+ASIMOW_CASES = (("reconstruction", 1), ("classification", 1), ("classification", 3))
+
+
+def asimow_frame(n=90):
+    """A synthetic processed_asimow_dataset.csv in the reference's column layout (experiment, welding_run, labels,
+    V_0..V_199, I_0..I_199); values on a 1e-3 grid so the CSV text round-trips exactly."""
+    import pandas as pd
+    exp = gen.randint(1501, (n,), 1, 4)
+    run = gen.randint(1502, (n,), 1, 5)
+    lab = gen.randint(1503, (n,), -1, 2)
+    v = np.round(gen.normal(1504, (n, 200), 3.0, 20.0).astype(np.float64), 3)
+    i = np.round(gen.normal(1505, (n, 200), 30.0, 150.0).astype(np.float64), 3)
+    cols = {"experiment": exp, "welding_run": run, "labels": lab}
+    cols.update({f"V_{k}": v[:, k] for k in range(200)})
+    cols.update({f"I_{k}": i[:, k] for k in range(200)})
+    return pd.DataFrame(cols)
+
+
+def case_asimow():
+    """The reference's own ASIMoWDataLoader (dataloader/asimow_dataloader.py:28-206) on a synthetic CSV: CSV parse,
+    (experiment, welding_run) split, per-channel StandardScaler fitted on train, cycle sequences, numpy-global-RNG
+    shuffle.  Its pickle cache is written and read back by the reference inside a temporary directory (our own
+    synthetic data); nothing shipped with the reference is unpickled."""
+    from dataloader.asimow_dataloader import ASIMoWDataLoader, DataSplitId
+    out = {}
+    for task, seq in ASIMOW_CASES:
+        with tempfile.TemporaryDirectory() as d:
+            asimow_frame().to_csv(os.path.join(d, "processed_asimow_dataset.csv"), index=False)
+            dl = ASIMoWDataLoader([DataSplitId(e, r) for e, r in ASIMOW_VAL], [DataSplitId(e, r) for e, r in ASIMOW_TEST],
+                                  task=task, cycle_seq_number=seq, seed=7, data_directory_path=d)
+            for name, ds in zip(("train", "val", "test"), dl.get_dataset()):
+                out[f"{task}_{seq}/{name}/x"] = np.asarray(ds.data, dtype=np.float64)
+                if hasattr(ds, "labels"):
+                    out[f"{task}_{seq}/{name}/y"] = np.asarray(ds.labels, dtype=np.float64)
+    save("asimow_split.npz", **out)
+
+
+# ------------------------------------------------------------------------ Lightning checkpoint (SURVEY §5)
+def case_checkpoints(VQVAEPatch, MyTransformerDecoder):
+    """Checkpoints in Lightning's .ckpt layout ({state_dict, hyper_parameters, epoch, global_step, ...}) built from
+    the reference modules' own state_dicts and constructor arguments (what ModelCheckpoint writes and
+    load_from_checkpoint reads, utils.py:30, train_transformer_mtasks.py:171), with the reference's eval outputs
+    on fixed inputs.  Tensors and plain Python values only: torch.load(weights_only=True) reads them."""
+    vq_kw = vqvae_kwargs(64, 64, 16, 2, 25, False, dropout=0.1)
+    torch.manual_seed(0)
+    m = VQVAEPatch(**vq_kw)
+    load_det_state(m, 1601)
+    ck = {"epoch": 3, "global_step": 120, "pytorch-lightning_version": "2.1.0",
+          "state_dict": {k: v.detach().clone() for k, v in m.state_dict().items()},
+          "hyper_parameters": dict(vq_kw, use_improved_vq=False, kmeans_iters=0, threshold_ema_dead_code=2),
+          "loops": {}, "callbacks": {}, "optimizer_states": [], "lr_schedulers": []}
+    torch.save(ck, os.path.join(HERE, "ref_vqvae_small.ckpt"))
+    m.eval()
+    x = torch.from_numpy(gen.windows(1602, 4))
+    with torch.no_grad():
+        e, xh, p = m(x)
+        _, _, _, _, idx = m.vector_quantization(m.encoder(m.patch_embed(x)))
+    dec_kw = dict(d_model=32, n_classes=20, seq_len=17, n_blocks=2, n_head=4, res_dropout=0.1, att_dropout=0.0,
+                  learning_rate=1e-3, class_h_bias=True, class_h_dropout=False)
+    torch.manual_seed(0)
+    d = MyTransformerDecoder(**dec_kw)
+    load_det_state(d, 1603)
+    ck = {"epoch": 9, "global_step": 50, "pytorch-lightning_version": "2.1.0",
+          "state_dict": {k: v.detach().clone() for k, v in d.state_dict().items()},
+          "hyper_parameters": dec_kw, "loops": {}, "callbacks": {}, "optimizer_states": [], "lr_schedulers": []}
+    torch.save(ck, os.path.join(HERE, "ref_decoder_small.ckpt"))
+    d.eval()
+    ids = torch.from_numpy(gen.randint(1604, (3, 17), 0, 20))
+    with torch.no_grad():
+        lg = d(ids)
+        cl = d(ids, generate=False)
+    save("ref_ckpt_outputs.npz", vq_x_hat=xh.numpy(), vq_emb_loss=e.numpy(), vq_perplexity=p.numpy(),
+         vq_idx=idx.view(-1).numpy().astype(np.int64), dec_logits=lg.numpy(), dec_class_logits=cl.numpy())
+
+
+def main(only=()):
+    """python tests/golden/make_golden.py [case ...]: every case, or only the named ones (vq_small vq_idx vqvae
+    decoder radam regime asimow ckpt)."""
     install_shim()
     torch.set_num_threads(8)
     from model.vector_quantizer import VectorQuantizer
     from model.vq_vae_patch_embedd import VQVAEPatch
     from model.transformer_decoder import MyTransformerDecoder
-    case_vq_small(VectorQuantizer)
-    case_vq_idx(VectorQuantizer)
-    case_vqvae(VQVAEPatch)
-    case_decoder(MyTransformerDecoder)
-    case_radam()
+    cases = {"vq_small": lambda: case_vq_small(VectorQuantizer), "vq_idx": lambda: case_vq_idx(VectorQuantizer),
+             "vqvae": lambda: case_vqvae(VQVAEPatch), "decoder": lambda: case_decoder(MyTransformerDecoder),
+             "radam": case_radam, "regime": lambda: case_training_regime(MyTransformerDecoder),
+             "asimow": case_asimow, "ckpt": lambda: case_checkpoints(VQVAEPatch, MyTransformerDecoder)}
+    for name, fn in cases.items():
+        if not only or name in only:
+            fn()
 
 
 if __name__ == "__main__":
-    main()
+    main(tuple(sys.argv[1:]))

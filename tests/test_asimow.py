@@ -120,3 +120,28 @@ def test_window_offset_and_weights(csv):
     np.testing.assert_allclose(w, [2 / 3, 2 / 3, 1 / 3, 1 / 3, 1 / 3, 0.0], rtol=1e-6)   # ratio = P(label 0)
     x, lab = data.tensors("val", device="cpu")
     assert x.dtype.is_floating_point and x.dtype.itemsize == 4 and lab.dtype.itemsize == 8
+
+
+def test_reference_loader_fixture(tmp_path):
+    """Against the reference's own ASIMoWDataLoader (tests/golden/asimow_split.npz, written by
+    tests/golden/make_golden.py from the same synthetic CSV): every split's windows and labels, for
+    reconstruction, classification and 3-cycle classification sequences (asimow_dataloader.py:56-206)."""
+    import os
+    import sys
+    from conftest import golden
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
+    import make_golden as mg
+    mg.asimow_frame().to_csv(tmp_path / "processed_asimow_dataset.csv", index=False)
+    g = golden("asimow_split.npz")
+    val = [A.DataSplitId(e, r) for e, r in mg.ASIMOW_VAL]
+    test = [A.DataSplitId(e, r) for e, r in mg.ASIMOW_TEST]
+    for task, seq in mg.ASIMOW_CASES:
+        data = A.load(str(tmp_path), val, test, task=task, cycle_seq_number=seq, seed=7, cache=False)
+        for name in ("train", "val", "test"):
+            x, y = data.splits[name]
+            rx = g[f"{task}_{seq}/{name}/x"]
+            assert x.shape == rx.shape, (task, seq, name)
+            np.testing.assert_allclose(x, rx, rtol=1e-12, atol=1e-12, err_msg=f"{task} {seq} {name}")
+            key = f"{task}_{seq}/{name}/y"
+            if key in g.files:
+                np.testing.assert_array_equal(np.asarray(y, dtype=np.float64), g[key])

@@ -112,3 +112,29 @@ def test_layernorm_fwd_bwd(R, D, out_dtype):
     frac = kept.float().mean().item()
     assert 0.72 < frac < 0.78
     torch.testing.assert_close(dx2.float()[kept], (dx / 0.75)[kept], rtol=tol, atol=tol)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("hs,T", [(8, 17), (12, 33), (24, 70), (40, 65), (6, 5)])
+def test_attention_any_head_size_fp32(hs, T):
+    """Head sizes outside 16/32/64/128 (the reference allows any d_model % n_head == 0) run the runtime-size
+    kernels: forward and every input gradient against the torch fp32 reference."""
+    from arcweld import kernels as K
+    torch.manual_seed(hs * 100 + T)
+    B, nh = 2, 3
+    d = nh * hs
+    qkv = torch.randn(B * T, 3 * d, device="cuda")
+    y, lse = torch.empty(B * T, d, device="cuda"), torch.empty(B * nh * T, device="cuda")
+    K.attn_fwd(qkv, B, T, nh, d, y, lse)
+    dy = torch.randn(B * T, d, device="cuda")
+    dqkv, ws = torch.empty_like(qkv), torch.empty(B * nh * T, device="cuda")
+    K.attn_bwd(qkv, y, dy, lse, B, T, nh, d, dqkv, ws)
+    ref_in = qkv.detach().clone().requires_grad_(True)
+    q, k, v = ref_in.view(B, T, 3 * d).split(d, dim=2)
+    q, k, v = (t.reshape(B, T, nh, hs).transpose(1, 2) for t in (q, k, v))
+    att = (q @ k.transpose(-2, -1)) / math.sqrt(hs)
+    att = att.masked_fill(~torch.ones(T, T, dtype=torch.bool, device="cuda").tril(), float("-inf")).softmax(-1)
+    ref = (att @ v).transpose(1, 2).reshape(B * T, d)
+    ref.backward(dy)
+    torch.testing.assert_close(y, ref.detach(), rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(dqkv, ref_in.grad, rtol=1e-4, atol=1e-4)

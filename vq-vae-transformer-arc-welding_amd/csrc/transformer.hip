@@ -263,20 +263,35 @@ __global__ void embed_bwd_kernel(const int64_t* __restrict__ ids, int64_t B, int
 }
 
 // ---------------------------------------------------------------- causal attention
-// Two lanes per query (or key) row, each holding half of the head dimension (HS/2 values); partial dot
-// products are combined with one xor-1 shuffle.  Key/value (resp. query) tiles of 32 rows are staged in LDS
-// and read as broadcasts.  64 rows per 128-thread workgroup; grid = (ceil(T/64), n_head, B).
+// Two lanes per query (or key) row, each holding half of the head dimension; partial dot products are combined
+// with one xor-1 shuffle.  Key/value (resp. query) tiles of 32 rows are staged in LDS and read as broadcasts.
+// 64 rows per 128-thread workgroup; grid = (ceil(T/64), n_head, B).  EXACT kernels are compiled for head sizes
+// 16/32/64/128; any other head size (hs <= 128, e.g. d_model 32 with 4 heads) runs the HS-capacity kernel with
+// the runtime size: lane 0 of a pair holds ceil(hs/2) values, lane 1 the rest.
 constexpr int ATT_ROWS = 64;
 constexpr int ATT_TILE = 32;
 
-template <typename T, int HS>
-__global__ __launch_bounds__(128) void attn_fwd_kernel(const T* __restrict__ qkv, int T_, int nh, int d,
+template <int HS, bool EXACT> struct HeadSplit {
+  int hs, h2, mine, off;    // head size, lane-0 share, this lane's share, this lane's first element
+  __device__ __forceinline__ HeadSplit(int hs_rt, int half) {
+    hs = EXACT ? HS : hs_rt;
+    h2 = EXACT ? HS / 2 : (hs + 1) / 2;
+    mine = half ? hs - h2 : h2;
+    off = half * h2;
+  }
+  __device__ __forceinline__ bool has(int e) const { return EXACT || e < mine; }
+};
+
+template <typename T, int HS, bool EXACT = true>
+__global__ __launch_bounds__(128) void attn_fwd_kernel(const T* __restrict__ qkv, int T_, int nh, int d, int hs_rt,
                                                        T* __restrict__ y, float* __restrict__ lse, float scale) {
   constexpr int H2 = HS / 2;
   __shared__ float Ks[ATT_TILE][HS + 1];
   __shared__ float Vs[ATT_TILE][HS + 1];
   const int b = blockIdx.z, h = blockIdx.y;
   const int tid = threadIdx.x, half = tid & 1;
+  const HeadSplit<HS, EXACT> hd(hs_rt, half);
+  const int hs = hd.hs;
   const int qi = blockIdx.x * ATT_ROWS + (tid >> 1);
   const int64_t ld = 3 * (int64_t)d;
   const T* base = qkv + (int64_t)b * T_ * ld;
@@ -284,20 +299,20 @@ __global__ __launch_bounds__(128) void attn_fwd_kernel(const T* __restrict__ qkv
   float q[H2], o[H2];
 #pragma unroll
   for (int e = 0; e < H2; ++e) {
-    q[e] = valid ? to_f32<T>(base[(int64_t)qi * ld + h * HS + half * H2 + e]) * scale : 0.f;
+    q[e] = valid && hd.has(e) ? to_f32<T>(base[(int64_t)qi * ld + h * hs + hd.off + e]) * scale : 0.f;
     o[e] = 0.f;
   }
   float m = -__builtin_huge_valf(), l = 0.f;
   const int kend = min(T_, (blockIdx.x + 1) * ATT_ROWS);  // keys beyond the block's last query are masked
   for (int k0 = 0; k0 < kend; k0 += ATT_TILE) {
     __syncthreads();
-    for (int i = tid; i < ATT_TILE * HS; i += 128) {
-      const int kr = i / HS, e = i - kr * HS;
+    for (int i = tid; i < ATT_TILE * hs; i += 128) {
+      const int kr = i / hs, e = i - kr * hs;
       const int kk = k0 + kr;
       float kv = 0.f, vv = 0.f;
       if (kk < T_) {
-        kv = to_f32<T>(base[(int64_t)kk * ld + d + h * HS + e]);
-        vv = to_f32<T>(base[(int64_t)kk * ld + 2 * d + h * HS + e]);
+        kv = to_f32<T>(base[(int64_t)kk * ld + d + h * hs + e]);
+        vv = to_f32<T>(base[(int64_t)kk * ld + 2 * d + h * hs + e]);
       }
       Ks[kr][e] = kv;
       Vs[kr][e] = vv;
@@ -309,7 +324,8 @@ __global__ __launch_bounds__(128) void attn_fwd_kernel(const T* __restrict__ qkv
     for (int j = 0; j < ATT_TILE; ++j) {
       float a = 0.f;
 #pragma unroll
-      for (int e = 0; e < H2; ++e) a = fmaf(q[e], Ks[j][half * H2 + e], a);
+      for (int e = 0; e < H2; ++e)
+        if (hd.has(e)) a = fmaf(q[e], Ks[j][hd.off + e], a);
       a += __shfl_xor(a, 1, 64);
       const bool ok = (k0 + j) <= qi && (k0 + j) < T_;
       s[j] = ok ? a : -__builtin_huge_valf();
@@ -326,57 +342,62 @@ __global__ __launch_bounds__(128) void attn_fwd_kernel(const T* __restrict__ qkv
       const float pj = __expf(s[j] - mn);
       l += pj;
 #pragma unroll
-      for (int e = 0; e < H2; ++e) o[e] = fmaf(pj, Vs[j][half * H2 + e], o[e]);
+      for (int e = 0; e < H2; ++e)
+        if (hd.has(e)) o[e] = fmaf(pj, Vs[j][hd.off + e], o[e]);
     }
     m = mn;
   }
   if (!valid) return;
   const float inv = 1.f / l;
-  T* yr = y + ((int64_t)b * T_ + qi) * d + h * HS + half * H2;
+  T* yr = y + ((int64_t)b * T_ + qi) * d + h * hs + hd.off;
 #pragma unroll
-  for (int e = 0; e < H2; ++e) yr[e] = from_f32<T>(o[e] * inv);
+  for (int e = 0; e < H2; ++e)
+    if (hd.has(e)) yr[e] = from_f32<T>(o[e] * inv);
   if (half == 0) lse[((int64_t)b * nh + h) * T_ + qi] = m + logf(l);
 }
 
 // delta_i = sum_e dy_i,e * y_i,e   (per (b, h, i))
-template <typename T, int HS>
+template <typename T>
 __global__ void attn_delta_kernel(const T* __restrict__ y, const T* __restrict__ dy, int64_t B, int T_, int nh, int d,
                                   float* __restrict__ delta) {
   const int64_t n = B * nh * T_;
+  const int hs = d / nh;
   for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
     const int64_t bh = r / T_;
     const int t = (int)(r - bh * T_);
     const int64_t b = bh / nh;
     const int h = (int)(bh - b * nh);
-    const int64_t off = (b * T_ + t) * d + h * HS;
+    const int64_t off = (b * T_ + t) * d + h * hs;
     float s = 0.f;
 #pragma unroll 8
-    for (int e = 0; e < HS; ++e) s += to_f32<T>(dy[off + e]) * to_f32<T>(y[off + e]);
+    for (int e = 0; e < hs; ++e) s += to_f32<T>(dy[off + e]) * to_f32<T>(y[off + e]);
     delta[r] = s;
   }
 }
 
 // dq_i = scale * sum_{j<=i} P_ij (dP_ij - delta_i) k_j     (query-stationary)
-template <typename T, int HS>
+template <typename T, int HS, bool EXACT = true>
 __global__ __launch_bounds__(128) void attn_bwd_dq_kernel(const T* __restrict__ qkv, const T* __restrict__ dy,
                                                           const float* __restrict__ lse,
                                                           const float* __restrict__ delta, int T_, int nh, int d,
-                                                          T* __restrict__ dqkv, float scale) {
+                                                          int hs_rt, T* __restrict__ dqkv, float scale) {
   constexpr int H2 = HS / 2;
   __shared__ float Ks[ATT_TILE][HS + 1];
   __shared__ float Vs[ATT_TILE][HS + 1];
   const int b = blockIdx.z, h = blockIdx.y;
   const int tid = threadIdx.x, half = tid & 1;
+  const HeadSplit<HS, EXACT> hd(hs_rt, half);
+  const int hs = hd.hs;
   const int qi = blockIdx.x * ATT_ROWS + (tid >> 1);
   const int64_t ld = 3 * (int64_t)d;
   const T* base = qkv + (int64_t)b * T_ * ld;
   const bool valid = qi < T_;
   float q[H2], g[H2], dq[H2];
-  const int64_t yo = ((int64_t)b * T_ + (valid ? qi : 0)) * d + h * HS + half * H2;
+  const int64_t yo = ((int64_t)b * T_ + (valid ? qi : 0)) * d + h * hs + hd.off;
 #pragma unroll
   for (int e = 0; e < H2; ++e) {
-    q[e] = valid ? to_f32<T>(base[(int64_t)qi * ld + h * HS + half * H2 + e]) * scale : 0.f;
-    g[e] = valid ? to_f32<T>(dy[yo + e]) : 0.f;
+    q[e] = valid && hd.has(e) ? to_f32<T>(base[(int64_t)qi * ld + h * hs + hd.off + e]) * scale : 0.f;
+    g[e] = valid && hd.has(e) ? to_f32<T>(dy[yo + e]) : 0.f;
     dq[e] = 0.f;
   }
   const int64_t st = ((int64_t)b * nh + h) * T_ + (valid ? qi : 0);
@@ -384,13 +405,13 @@ __global__ __launch_bounds__(128) void attn_bwd_dq_kernel(const T* __restrict__ 
   const int kend = min(T_, (blockIdx.x + 1) * ATT_ROWS);
   for (int k0 = 0; k0 < kend; k0 += ATT_TILE) {
     __syncthreads();
-    for (int i = tid; i < ATT_TILE * HS; i += 128) {
-      const int kr = i / HS, e = i - kr * HS;
+    for (int i = tid; i < ATT_TILE * hs; i += 128) {
+      const int kr = i / hs, e = i - kr * hs;
       const int kk = k0 + kr;
       float kv = 0.f, vv = 0.f;
       if (kk < T_) {
-        kv = to_f32<T>(base[(int64_t)kk * ld + d + h * HS + e]);
-        vv = to_f32<T>(base[(int64_t)kk * ld + 2 * d + h * HS + e]);
+        kv = to_f32<T>(base[(int64_t)kk * ld + d + h * hs + e]);
+        vv = to_f32<T>(base[(int64_t)kk * ld + 2 * d + h * hs + e]);
       }
       Ks[kr][e] = kv;
       Vs[kr][e] = vv;
@@ -400,37 +421,42 @@ __global__ __launch_bounds__(128) void attn_bwd_dq_kernel(const T* __restrict__ 
     for (int j = 0; j < ATT_TILE; ++j) {
       float a = 0.f, dp = 0.f;
 #pragma unroll
-      for (int e = 0; e < H2; ++e) {
-        a = fmaf(q[e], Ks[j][half * H2 + e], a);
-        dp = fmaf(g[e], Vs[j][half * H2 + e], dp);
-      }
+      for (int e = 0; e < H2; ++e)
+        if (hd.has(e)) {
+          a = fmaf(q[e], Ks[j][hd.off + e], a);
+          dp = fmaf(g[e], Vs[j][hd.off + e], dp);
+        }
       a += __shfl_xor(a, 1, 64);
       dp += __shfl_xor(dp, 1, 64);
       const bool ok = valid && (k0 + j) <= qi && (k0 + j) < T_;
       const float p = ok ? __expf(a - L) : 0.f;
       const float ds = p * (dp - Dl);
 #pragma unroll
-      for (int e = 0; e < H2; ++e) dq[e] = fmaf(ds, Ks[j][half * H2 + e], dq[e]);
+      for (int e = 0; e < H2; ++e)
+        if (hd.has(e)) dq[e] = fmaf(ds, Ks[j][hd.off + e], dq[e]);
     }
   }
   if (!valid) return;
-  T* out = dqkv + ((int64_t)b * T_ + qi) * ld + h * HS + half * H2;
+  T* out = dqkv + ((int64_t)b * T_ + qi) * ld + h * hs + hd.off;
 #pragma unroll
-  for (int e = 0; e < H2; ++e) out[e] = from_f32<T>(dq[e] * scale);
+  for (int e = 0; e < H2; ++e)
+    if (hd.has(e)) out[e] = from_f32<T>(dq[e] * scale);
 }
 
 // dk_j = scale * sum_{i>=j} dS_ij q_i ;  dv_j = sum_{i>=j} P_ij dy_i      (key-stationary)
-template <typename T, int HS>
+template <typename T, int HS, bool EXACT = true>
 __global__ __launch_bounds__(128) void attn_bwd_dkv_kernel(const T* __restrict__ qkv, const T* __restrict__ dy,
                                                            const float* __restrict__ lse,
                                                            const float* __restrict__ delta, int T_, int nh, int d,
-                                                           T* __restrict__ dqkv, float scale) {
+                                                           int hs_rt, T* __restrict__ dqkv, float scale) {
   constexpr int H2 = HS / 2;
   __shared__ float Qs[ATT_TILE][HS + 1];
   __shared__ float Gs[ATT_TILE][HS + 1];
   __shared__ float Ls[ATT_TILE], Ds[ATT_TILE];
   const int b = blockIdx.z, h = blockIdx.y;
   const int tid = threadIdx.x, half = tid & 1;
+  const HeadSplit<HS, EXACT> hd(hs_rt, half);
+  const int hs = hd.hs;
   const int kj = blockIdx.x * ATT_ROWS + (tid >> 1);
   const int64_t ld = 3 * (int64_t)d;
   const T* base = qkv + (int64_t)b * T_ * ld;
@@ -438,20 +464,20 @@ __global__ __launch_bounds__(128) void attn_bwd_dkv_kernel(const T* __restrict__
   float k[H2], v[H2], dk[H2], dv[H2];
 #pragma unroll
   for (int e = 0; e < H2; ++e) {
-    k[e] = valid ? to_f32<T>(base[(int64_t)kj * ld + d + h * HS + half * H2 + e]) : 0.f;
-    v[e] = valid ? to_f32<T>(base[(int64_t)kj * ld + 2 * d + h * HS + half * H2 + e]) : 0.f;
+    k[e] = valid && hd.has(e) ? to_f32<T>(base[(int64_t)kj * ld + d + h * hs + hd.off + e]) : 0.f;
+    v[e] = valid && hd.has(e) ? to_f32<T>(base[(int64_t)kj * ld + 2 * d + h * hs + hd.off + e]) : 0.f;
     dk[e] = dv[e] = 0.f;
   }
   const int qstart = blockIdx.x * ATT_ROWS;  // queries before the block's first key see none of its keys
   for (int q0 = (qstart / ATT_TILE) * ATT_TILE; q0 < T_; q0 += ATT_TILE) {
     __syncthreads();
-    for (int i = tid; i < ATT_TILE * HS; i += 128) {
-      const int qr = i / HS, e = i - qr * HS;
+    for (int i = tid; i < ATT_TILE * hs; i += 128) {
+      const int qr = i / hs, e = i - qr * hs;
       const int qq = q0 + qr;
       float qv = 0.f, gv = 0.f;
       if (qq < T_) {
-        qv = to_f32<T>(base[(int64_t)qq * ld + h * HS + e]) * scale;
-        gv = to_f32<T>(dy[((int64_t)b * T_ + qq) * d + h * HS + e]);
+        qv = to_f32<T>(base[(int64_t)qq * ld + h * hs + e]) * scale;
+        gv = to_f32<T>(dy[((int64_t)b * T_ + qq) * d + h * hs + e]);
       }
       Qs[qr][e] = qv;
       Gs[qr][e] = gv;
@@ -467,10 +493,11 @@ __global__ __launch_bounds__(128) void attn_bwd_dkv_kernel(const T* __restrict__
     for (int i = 0; i < ATT_TILE; ++i) {
       float a = 0.f, dp = 0.f;
 #pragma unroll
-      for (int e = 0; e < H2; ++e) {
-        a = fmaf(Qs[i][half * H2 + e], k[e], a);
-        dp = fmaf(Gs[i][half * H2 + e], v[e], dp);
-      }
+      for (int e = 0; e < H2; ++e)
+        if (hd.has(e)) {
+          a = fmaf(Qs[i][hd.off + e], k[e], a);
+          dp = fmaf(Gs[i][hd.off + e], v[e], dp);
+        }
       a += __shfl_xor(a, 1, 64);
       dp += __shfl_xor(dp, 1, 64);
       const int qq = q0 + i;
@@ -478,19 +505,21 @@ __global__ __launch_bounds__(128) void attn_bwd_dkv_kernel(const T* __restrict__
       const float p = ok ? __expf(a - Ls[i]) : 0.f;
       const float ds = p * (dp - Ds[i]);
 #pragma unroll
-      for (int e = 0; e < H2; ++e) {
-        dv[e] = fmaf(p, Gs[i][half * H2 + e], dv[e]);
-        dk[e] = fmaf(ds, Qs[i][half * H2 + e], dk[e]);  // Qs already carries the scale
-      }
+      for (int e = 0; e < H2; ++e)
+        if (hd.has(e)) {
+          dv[e] = fmaf(p, Gs[i][hd.off + e], dv[e]);
+          dk[e] = fmaf(ds, Qs[i][hd.off + e], dk[e]);  // Qs already carries the scale
+        }
     }
   }
   if (!valid) return;
-  T* out = dqkv + ((int64_t)b * T_ + kj) * ld + h * HS + half * H2;
+  T* out = dqkv + ((int64_t)b * T_ + kj) * ld + h * hs + hd.off;
 #pragma unroll
-  for (int e = 0; e < H2; ++e) {
-    out[d + e] = from_f32<T>(dk[e]);
-    out[2 * d + e] = from_f32<T>(dv[e]);
-  }
+  for (int e = 0; e < H2; ++e)
+    if (hd.has(e)) {
+      out[d + e] = from_f32<T>(dk[e]);
+      out[2 * d + e] = from_f32<T>(dv[e]);
+    }
 }
 
 // ---------------------------------------------------------------- cross entropy (one wave per row)
@@ -819,7 +848,7 @@ extern "C" int aw_attn_fwd(const void* qkv, int64_t B, int T, int n_head, int d,
                            void* stream) {
   AW_REQUIRE(qkv && y && lse && B >= 0 && T > 0 && n_head > 0 && d % n_head == 0, "aw_attn_fwd: bad args");
   const int hs = d / n_head;
-  AW_REQUIRE(hs == 16 || hs == 32 || hs == 64 || hs == 128, "aw_attn_fwd: head size %d unsupported", hs);
+  AW_REQUIRE(hs >= 1 && hs <= 128, "aw_attn_fwd: head size %d unsupported (1..128)", hs);
   if (B == 0) return AW_OK;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (aw::attn_mfma_supported(dtype, hs, d)) {
@@ -828,18 +857,21 @@ extern "C" int aw_attn_fwd(const void* qkv, int64_t B, int T, int n_head, int d,
   }
   dim3 grid(aw_cdiv(T, ATT_ROWS), n_head, (unsigned)B);
   const float scale = 1.0f / sqrtf((float)hs);
-#define AW_F(HSV)                                                                                          \
-  if (dtype == AW_BF16)                                                                                    \
-    hipLaunchKernelGGL((attn_fwd_kernel<bf16, HSV>), grid, dim3(128), 0, s, (const bf16*)qkv, T, n_head, d, \
-                       (bf16*)y, lse, scale);                                                              \
-  else                                                                                                     \
-    hipLaunchKernelGGL((attn_fwd_kernel<float, HSV>), grid, dim3(128), 0, s, (const float*)qkv, T, n_head, d, \
-                       (float*)y, lse, scale);
+#define AW_F(HSV, EX)                                                                                         \
+  if (dtype == AW_BF16)                                                                                       \
+    hipLaunchKernelGGL((attn_fwd_kernel<bf16, HSV, EX>), grid, dim3(128), 0, s, (const bf16*)qkv, T, n_head, d, \
+                       hs, (bf16*)y, lse, scale);                                                             \
+  else                                                                                                        \
+    hipLaunchKernelGGL((attn_fwd_kernel<float, HSV, EX>), grid, dim3(128), 0, s, (const float*)qkv, T, n_head, \
+                       d, hs, (float*)y, lse, scale);
   switch (hs) {
-    case 16: AW_F(16) break;
-    case 32: AW_F(32) break;
-    case 64: AW_F(64) break;
-    default: AW_F(128) break;
+    case 16: AW_F(16, true) break;
+    case 32: AW_F(32, true) break;
+    case 64: AW_F(64, true) break;
+    case 128: AW_F(128, true) break;
+    default:
+      if (hs < 16) { AW_F(16, false) } else if (hs < 32) { AW_F(32, false) } else if (hs < 64) { AW_F(64, false) }
+      else { AW_F(128, false) }
   }
 #undef AW_F
   return aw::check_launch("aw_attn_fwd");
@@ -850,39 +882,42 @@ extern "C" int aw_attn_bwd(const void* qkv, const void* y, const void* dy, const
   AW_REQUIRE(qkv && y && dy && lse && dqkv && ws && B >= 0 && T > 0 && n_head > 0 && d % n_head == 0,
              "aw_attn_bwd: bad args");
   const int hs = d / n_head;
-  AW_REQUIRE(hs == 16 || hs == 32 || hs == 64 || hs == 128, "aw_attn_bwd: head size %d unsupported", hs);
+  AW_REQUIRE(hs >= 1 && hs <= 128, "aw_attn_bwd: head size %d unsupported (1..128)", hs);
   if (B == 0) return AW_OK;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   dim3 grid(aw_cdiv(T, ATT_ROWS), n_head, (unsigned)B);
   const float scale = 1.0f / sqrtf((float)hs);
   const int64_t nrows = B * n_head * T;
   if (aw::attn_mfma_supported(dtype, hs, d)) {
-    hipLaunchKernelGGL((attn_delta_kernel<bf16, 64>), dim3(gridcap(nrows)), dim3(256), 0, s, (const bf16*)y,
+    hipLaunchKernelGGL((attn_delta_kernel<bf16>), dim3(gridcap(nrows)), dim3(256), 0, s, (const bf16*)y,
                        (const bf16*)dy, B, T, n_head, d, ws);
     aw::attn_bwd_mfma(qkv, dy, lse, ws, B, T, n_head, d, dqkv, s);
     return aw::check_launch("aw_attn_bwd");
   }
-#define AW_B(HSV)                                                                                                  \
+#define AW_B(HSV, EX)                                                                                              \
   if (dtype == AW_BF16) {                                                                                          \
-    hipLaunchKernelGGL((attn_delta_kernel<bf16, HSV>), dim3(gridcap(nrows)), dim3(256), 0, s, (const bf16*)y,       \
+    hipLaunchKernelGGL((attn_delta_kernel<bf16>), dim3(gridcap(nrows)), dim3(256), 0, s, (const bf16*)y,             \
                        (const bf16*)dy, B, T, n_head, d, ws);                                                      \
-    hipLaunchKernelGGL((attn_bwd_dq_kernel<bf16, HSV>), grid, dim3(128), 0, s, (const bf16*)qkv, (const bf16*)dy,   \
-                       lse, ws, T, n_head, d, (bf16*)dqkv, scale);                                                 \
-    hipLaunchKernelGGL((attn_bwd_dkv_kernel<bf16, HSV>), grid, dim3(128), 0, s, (const bf16*)qkv, (const bf16*)dy,  \
-                       lse, ws, T, n_head, d, (bf16*)dqkv, scale);                                                 \
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<bf16, HSV, EX>), grid, dim3(128), 0, s, (const bf16*)qkv,                 \
+                       (const bf16*)dy, lse, ws, T, n_head, d, hs, (bf16*)dqkv, scale);                            \
+    hipLaunchKernelGGL((attn_bwd_dkv_kernel<bf16, HSV, EX>), grid, dim3(128), 0, s, (const bf16*)qkv,                \
+                       (const bf16*)dy, lse, ws, T, n_head, d, hs, (bf16*)dqkv, scale);                            \
   } else {                                                                                                         \
-    hipLaunchKernelGGL((attn_delta_kernel<float, HSV>), dim3(gridcap(nrows)), dim3(256), 0, s, (const float*)y,     \
+    hipLaunchKernelGGL((attn_delta_kernel<float>), dim3(gridcap(nrows)), dim3(256), 0, s, (const float*)y,           \
                        (const float*)dy, B, T, n_head, d, ws);                                                     \
-    hipLaunchKernelGGL((attn_bwd_dq_kernel<float, HSV>), grid, dim3(128), 0, s, (const float*)qkv,                  \
-                       (const float*)dy, lse, ws, T, n_head, d, (float*)dqkv, scale);                              \
-    hipLaunchKernelGGL((attn_bwd_dkv_kernel<float, HSV>), grid, dim3(128), 0, s, (const float*)qkv,                 \
-                       (const float*)dy, lse, ws, T, n_head, d, (float*)dqkv, scale);                              \
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<float, HSV, EX>), grid, dim3(128), 0, s, (const float*)qkv,               \
+                       (const float*)dy, lse, ws, T, n_head, d, hs, (float*)dqkv, scale);                          \
+    hipLaunchKernelGGL((attn_bwd_dkv_kernel<float, HSV, EX>), grid, dim3(128), 0, s, (const float*)qkv,              \
+                       (const float*)dy, lse, ws, T, n_head, d, hs, (float*)dqkv, scale);                          \
   }
   switch (hs) {
-    case 16: AW_B(16) break;
-    case 32: AW_B(32) break;
-    case 64: AW_B(64) break;
-    default: AW_B(128) break;
+    case 16: AW_B(16, true) break;
+    case 32: AW_B(32, true) break;
+    case 64: AW_B(64, true) break;
+    case 128: AW_B(128, true) break;
+    default:
+      if (hs < 16) { AW_B(16, false) } else if (hs < 32) { AW_B(32, false) } else if (hs < 64) { AW_B(64, false) }
+      else { AW_B(128, false) }
   }
 #undef AW_B
   return aw::check_launch("aw_attn_bwd");
