@@ -259,6 +259,15 @@ int aw_attn_fwd(const void* qkv, int64_t B, int T, int n_head, int d, int dtype,
 /* dqkv (B*T, 3d, dtype) from dy (B*T, d, dtype), recomputing P from lse; ws: f32 B*n_head*T (delta). */
 int aw_attn_bwd(const void* qkv, const void* y, const void* dy, const float* lse, int64_t B, int T, int n_head,
                 int d, int dtype, void* dqkv, float* ws, void* stream);
+/* The same two with attention-probability dropout (CausalSelfAttention.attn_dropout, transformer_block.py:44-57;
+ * the reference default is 0.0): P_ij kept with probability 1 - drop_p and scaled by 1/(1 - drop_p); the mask of
+ * element ((b*n_head + h)*T + i)*T + j comes from the counter hash of (drop_seed mixed with *seed_ptr when given),
+ * so the backward regenerates the forward's mask.  drop_p = 0 is exactly aw_attn_fwd / aw_attn_bwd. */
+int aw_attn_fwd_dropout(const void* qkv, int64_t B, int T, int n_head, int d, int dtype, void* y, float* lse,
+                        float drop_p, uint64_t drop_seed, const uint64_t* seed_ptr, void* stream);
+int aw_attn_bwd_dropout(const void* qkv, const void* y, const void* dy, const float* lse, int64_t B, int T,
+                        int n_head, int d, int dtype, void* dqkv, float* ws, float drop_p, uint64_t drop_seed,
+                        const uint64_t* seed_ptr, void* stream);
 /* KV-cache decode attention (MyTransformerDecoder.generate, model/transformer_decoder.py:203-224):
  * n_new query rows per sequence at absolute positions pos0 .. pos0+n_new-1 (qkv_new (B*n_new, 3d, dtype), row
  * b*n_new + i).  Their K and V are appended to kv_cache (B, Tmax, 2d, dtype; row b*Tmax + t = [K | V]) and

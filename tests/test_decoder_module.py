@@ -269,3 +269,35 @@ def test_fused_train_step_matches_autograd_and_split_point_is_final(fp32_parity,
                 assert not snap[0][i].any(), n
         else:
             assert not p.grad.any(), n
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_kv_cache_full_size_decode_matches_full_forward(dtype):
+    """The KV-cache path at the full size (d 512, 8 heads of 64, 8 blocks, T 321, V 514): a 300-token prefill,
+    then 20 cached decode steps up to position 320, each against the full-recompute forward (fp32: 1e-4; bf16
+    operands: the same kernels' bf16 recompute, 2e-2), and greedy generation identical to the recompute loop."""
+    from arcweld import decoder as dec
+    from arcweld.precision import operands
+    dt = torch.float32 if dtype == "fp32" else torch.bfloat16
+    tol = 1e-4 if dtype == "fp32" else 2e-2
+    m = make_model(FULL, 8, 405, device="cuda").eval()
+    B, T0 = 2, 300
+    x = torch.tensor(gen.randint(452, (B, 321), 0, FULL["n_classes"]), device="cuda")
+    with operands(dt):
+        cache = dec.KVCache(m, B, FULL["seq_len"])
+        got = dec.forward_cached(m, x[:, :T0], cache, 0)
+        with torch.no_grad():
+            ref = m(x[:, :T0])[:, -1]
+        torch.testing.assert_close(got, ref, rtol=tol, atol=tol)
+        for t in range(T0, 321):
+            got = dec.forward_cached(m, x[:, t:t + 1], cache, t)
+            if t % 5 == 0 or t == 320:
+                with torch.no_grad():
+                    ref = m(x[:, :t + 1])[:, -1]
+                torch.testing.assert_close(got, ref, rtol=tol, atol=tol, msg=f"position {t}")
+    if dtype == "fp32":
+        with operands(torch.float32):
+            m2 = make_model(dict(FULL, seq_len=24), 8, 405, device="cuda").eval()
+            p = torch.tensor(gen.randint(453, (2, 5), 0, FULL["n_classes"]), device="cuda")
+            assert torch.equal(m2.generate(p, use_cache=True), m2.generate(p, use_cache=False))

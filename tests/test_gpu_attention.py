@@ -138,3 +138,76 @@ def test_attention_any_head_size_fp32(hs, T):
     ref.backward(dy)
     torch.testing.assert_close(y, ref.detach(), rtol=1e-4, atol=1e-4)
     torch.testing.assert_close(dqkv, ref_in.grad, rtol=1e-4, atol=1e-4)
+
+
+def _dropout_keep(seed, B, nh, T, p):
+    """The kernels' counter-based mask (common.h aw_hash_group / aw_dropout_scale), restated in numpy: element
+    e = ((b*nh + h)*T + i)*T + j is dropped iff its 16-bit slice of splitmix64(seed, e >> 2) < round(p * 65536)."""
+    import numpy as np
+    M = np.uint64(0xFFFFFFFFFFFFFFFF)
+    e = np.arange(B * nh * T * T, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        z = np.uint64(seed) + (e // np.uint64(4) + np.uint64(1)) * np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z = z ^ (z >> np.uint64(31))
+    u = (z >> (np.uint64(16) * (e & np.uint64(3)))) & np.uint64(0xFFFF)
+    keep = u >= np.uint64(int(p * 65536 + 0.5))
+    del M
+    return torch.tensor(keep.reshape(B, nh, T, T))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("hs,T,dtype", [(16, 40, torch.float32), (64, 70, torch.float32), (64, 45, torch.bfloat16),
+                                        (12, 33, torch.float32)])
+def test_attention_probability_dropout_fp32(hs, T, dtype):
+    """att_dropout > 0 (model/transformer_block.py:44-57): the kernels' output and input gradients equal torch's
+    attention with the same mask (regenerated here from the counter hash) applied after the softmax and 1/(1-p)
+    scaling."""
+    from arcweld import kernels as K
+    torch.manual_seed(hs + T)
+    B, nh, p, seed = 2, 2, 0.2, 12345
+    d = nh * hs
+    qkv = torch.randn(B * T, 3 * d, device="cuda").to(dtype)
+    y, lse = torch.empty(B * T, d, device="cuda", dtype=dtype), torch.empty(B * nh * T, device="cuda")
+    K.attn_fwd(qkv, B, T, nh, d, y, lse, drop=(p, seed))
+    dy = torch.randn(B * T, d, device="cuda").to(dtype)
+    dqkv, ws = torch.empty_like(qkv), torch.empty(B * nh * T, device="cuda")
+    K.attn_bwd(qkv, y, dy, lse, B, T, nh, d, dqkv, ws, drop=(p, seed))
+    keep = _dropout_keep(seed, B, nh, T, p).cuda()
+    assert 0.7 < keep.float().mean().item() < 0.9
+    ref_in = qkv.float().detach().clone().requires_grad_(True)
+    q, k, v = ref_in.view(B, T, 3 * d).split(d, dim=2)
+    q, k, v = (t.reshape(B, T, nh, hs).transpose(1, 2) for t in (q, k, v))
+    att = (q @ k.transpose(-2, -1)) / math.sqrt(hs)
+    att = att.masked_fill(~torch.ones(T, T, dtype=torch.bool, device="cuda").tril(), float("-inf")).softmax(-1)
+    att = att * keep / (1 - p)
+    ref = (att @ v).transpose(1, 2).reshape(B * T, d)
+    ref.backward(dy.float())
+    tol = 1e-4 if dtype == torch.float32 else 3e-2
+    torch.testing.assert_close(y.float(), ref.detach(), rtol=tol, atol=tol)
+    torch.testing.assert_close(dqkv.float(), ref_in.grad, rtol=tol, atol=tol)
+
+
+@pytest.mark.gpu
+def test_decoder_trains_with_attention_dropout():
+    """MyTransformerDecoder(att_dropout > 0) trains through the fused path: the masks change per step (device
+    counter), eval mode is deterministic and equals the att_dropout = 0 model."""
+    from arcweld.precision import operands
+    from model.transformer_decoder import MyTransformerDecoder
+    with operands(torch.float32):
+        torch.manual_seed(0)
+        m = MyTransformerDecoder(d_model=64, n_classes=34, seq_len=33, n_blocks=2, n_head=4, res_dropout=0.0,
+                                 att_dropout=0.3).cuda().train()
+        x = torch.randint(0, 34, (3, 33), device="cuda")
+        a = m(x)
+        b = m(x)
+        assert not torch.equal(a, b)
+        a.sum().backward()
+        assert all(torch.isfinite(p.grad).all() for p in m.parameters() if p.grad is not None)
+        m.eval()
+        ref = MyTransformerDecoder(d_model=64, n_classes=34, seq_len=33, n_blocks=2, n_head=4, res_dropout=0.0,
+                                   att_dropout=0.0).cuda().eval()
+        ref.load_state_dict(m.state_dict())
+        with torch.no_grad():
+            torch.testing.assert_close(m(x), ref(x), rtol=0, atol=0)

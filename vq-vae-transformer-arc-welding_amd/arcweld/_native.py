@@ -102,6 +102,9 @@ SIGNATURES = {
     "aw_embed_bwd": [c_p, c_i64, c_int, c_int, c_p, c_p, c_p],
     "aw_attn_fwd": [c_p, c_i64, c_int, c_int, c_int, c_int, c_p, c_p, c_p],
     "aw_attn_bwd": [c_p, c_p, c_p, c_p, c_i64, c_int, c_int, c_int, c_int, c_p, c_p, c_p],
+    "aw_attn_fwd_dropout": [c_p, c_i64, c_int, c_int, c_int, c_int, c_p, c_p, c_f, ctypes.c_uint64, c_p, c_p],
+    "aw_attn_bwd_dropout": [c_p, c_p, c_p, c_p, c_i64, c_int, c_int, c_int, c_int, c_p, c_p, c_f, ctypes.c_uint64,
+                            c_p, c_p],
     "aw_attn_decode": [c_p, c_i64, c_int, c_int, c_int, c_int, c_int, c_p, c_int, c_p, c_p],
     "aw_ce_fwd": [c_p, c_i64, c_int, c_i64, c_p, c_int, c_p, c_p, c_p, c_p],
     "aw_ce_bwd": [c_p, c_i64, c_int, c_i64, c_p, c_int, c_p, c_p, c_p, c_p, c_i64, c_int, c_p],

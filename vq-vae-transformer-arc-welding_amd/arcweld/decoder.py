@@ -64,9 +64,12 @@ def forward(m, ids, generate: bool, training: bool, need_backward: bool, seed: i
     sv.B, sv.T, sv.R, sv.d, sv.nh, sv.V, sv.Tdt, sv.generate = B, T, R, d, nh, V, T_, generate
     sv.p_drop = p_drop
     nb = len(m.transformer.h)
+    # attention-probability dropout (CausalSelfAttention.attn_dropout; reference default 0.0)
+    sv.p_att = float(m.transformer.h[0].attn.attn_pdrop) if (training and nb) else 0.0
     sv.seed_attn = [_mix(seed, 300 + i) for i in range(nb)]
     sv.seed_mlp = [_mix(seed, 400 + i) for i in range(nb)]
-    sv.ctr = rng_snapshot(m, dev, p_drop)
+    sv.seed_probs = [_mix(seed, 500 + i) for i in range(nb)]
+    sv.ctr = rng_snapshot(m, dev, max(p_drop, sv.p_att))
     ids = ids.contiguous()
 
     x = e(R, d)
@@ -95,7 +98,7 @@ def forward(m, ids, generate: bool, training: bool, need_backward: bool, seed: i
         qkv = e(R, 3 * d, dt=T_)
         K.gemm(a, Wqkv, R, 3 * d, d, bias=at.c_attn.bias, C=qkv)
         y, lse = e(R, d, dt=T_), e(B * nh * T)
-        K.attn_fwd(qkv, B, T, nh, d, y, lse)
+        K.attn_fwd(qkv, B, T, nh, d, y, lse, drop=(sv.p_att, sv.seed_probs[i]), seed_ptr=sv.ctr)
         x1 = e(R, d)
         K.gemm(y, Wo, R, d, d, bias=at.c_proj.bias, drop=(p_drop, sv.seed_attn[i]), resid=x, C=x1,
                seed_ptr=sv.ctr)
@@ -202,7 +205,8 @@ def backward(m, sv, g_out, slot, mid_hook=None):
                                                        accumulate=True, a_rowsum=slot(at.c_proj.bias))))
         dqkv = e(R, 3 * d, dt=T_)
         ws = e(B * nh * T)
-        K.attn_bwd(c["qkv"], c["y"], gy, c["lse"], B, T, nh, d, dqkv, ws)
+        K.attn_bwd(c["qkv"], c["y"], gy, c["lse"], B, T, nh, d, dqkv, ws, drop=(sv.p_att, sv.seed_probs[i]),
+                   seed_ptr=sv.ctr)
         wg["qkv"].append((dqkv, c["a"], 3 * d, d, R, dict(a_trans=True, b_trans=True, C=slot(at.c_attn.weight),
                                                            accumulate=True, a_rowsum=slot(at.c_attn.bias))))
         ga = e(R, d)

@@ -296,11 +296,20 @@ def embed_bwd(ids, dx, dwtok, stream=None):
     call("aw_embed_bwd", ptr(ids), B, T, dwtok.shape[1], ptr(dx), ptr(dwtok), stream_ptr(stream))
 
 
-def attn_fwd(qkv, B, T, n_head, d, y, lse, stream=None):
+def attn_fwd(qkv, B, T, n_head, d, y, lse, drop=(0.0, 0), seed_ptr=None, stream=None):
+    """drop = (p, seed): attention-probability dropout (aw_attn_fwd_dropout); p = 0 is plain aw_attn_fwd."""
+    if drop[0] > 0:
+        call("aw_attn_fwd_dropout", ptr(qkv), B, T, n_head, d, dtype_code(qkv.dtype), ptr(y), ptr(lse), float(drop[0]),
+             int(drop[1]) & 0xFFFFFFFFFFFFFFFF, ptr(seed_ptr), stream_ptr(stream))
+        return
     call("aw_attn_fwd", ptr(qkv), B, T, n_head, d, dtype_code(qkv.dtype), ptr(y), ptr(lse), stream_ptr(stream))
 
 
-def attn_bwd(qkv, y, dy, lse, B, T, n_head, d, dqkv, ws, stream=None):
+def attn_bwd(qkv, y, dy, lse, B, T, n_head, d, dqkv, ws, drop=(0.0, 0), seed_ptr=None, stream=None):
+    if drop[0] > 0:
+        call("aw_attn_bwd_dropout", ptr(qkv), ptr(y), ptr(dy), ptr(lse), B, T, n_head, d, dtype_code(qkv.dtype),
+             ptr(dqkv), ptr(ws), float(drop[0]), int(drop[1]) & 0xFFFFFFFFFFFFFFFF, ptr(seed_ptr), stream_ptr(stream))
+        return
     call("aw_attn_bwd", ptr(qkv), ptr(y), ptr(dy), ptr(lse), B, T, n_head, d, dtype_code(qkv.dtype), ptr(dqkv),
          ptr(ws), stream_ptr(stream))
 

@@ -282,9 +282,22 @@ template <int HS, bool EXACT> struct HeadSplit {
   __device__ __forceinline__ bool has(int e) const { return EXACT || e < mine; }
 };
 
-template <typename T, int HS, bool EXACT = true>
+// Attention-probability dropout (CausalSelfAttention.attn_dropout, model/transformer_block.py:44-57; DROP): P_ij of
+// (b, h) is kept with probability 1 - p and scaled by 1/(1 - p), the mask of element ((b*nh + h)*T + i)*T + j
+// regenerated from (seed, element) by the backward; the row normaliser and delta_i = dy_i . y_i are unchanged.
+struct AttnDrop {
+  float p;
+  uint64_t seed;
+  __device__ __forceinline__ float scale(int64_t bh, int T_, int i, int j) const {
+    return aw_dropout_scale(seed, ((uint64_t)bh * T_ + i) * T_ + j, p);
+  }
+};
+
+template <typename T, int HS, bool EXACT = true, bool DROP = false>
 __global__ __launch_bounds__(128) void attn_fwd_kernel(const T* __restrict__ qkv, int T_, int nh, int d, int hs_rt,
-                                                       T* __restrict__ y, float* __restrict__ lse, float scale) {
+                                                       T* __restrict__ y, float* __restrict__ lse, float scale,
+                                                       float drop_p, uint64_t drop_seed,
+                                                       const uint64_t* __restrict__ seed_ptr) {
   constexpr int H2 = HS / 2;
   __shared__ float Ks[ATT_TILE][HS + 1];
   __shared__ float Vs[ATT_TILE][HS + 1];
@@ -296,6 +309,8 @@ __global__ __launch_bounds__(128) void attn_fwd_kernel(const T* __restrict__ qkv
   const int64_t ld = 3 * (int64_t)d;
   const T* base = qkv + (int64_t)b * T_ * ld;
   const bool valid = qi < T_;
+  AttnDrop dr{drop_p, DROP ? aw_seed_mix(drop_seed, seed_ptr) : 0ull};
+  const int64_t bh = (int64_t)b * nh + h;
   float q[H2], o[H2];
 #pragma unroll
   for (int e = 0; e < H2; ++e) {
@@ -341,9 +356,10 @@ __global__ __launch_bounds__(128) void attn_fwd_kernel(const T* __restrict__ qkv
     for (int j = 0; j < ATT_TILE; ++j) {
       const float pj = __expf(s[j] - mn);
       l += pj;
+      const float pv = DROP ? pj * dr.scale(bh, T_, qi, k0 + j) : pj;
 #pragma unroll
       for (int e = 0; e < H2; ++e)
-        if (hd.has(e)) o[e] = fmaf(pj, Vs[j][hd.off + e], o[e]);
+        if (hd.has(e)) o[e] = fmaf(pv, Vs[j][hd.off + e], o[e]);
     }
     m = mn;
   }
@@ -376,11 +392,12 @@ __global__ void attn_delta_kernel(const T* __restrict__ y, const T* __restrict__
 }
 
 // dq_i = scale * sum_{j<=i} P_ij (dP_ij - delta_i) k_j     (query-stationary)
-template <typename T, int HS, bool EXACT = true>
+template <typename T, int HS, bool EXACT = true, bool DROP = false>
 __global__ __launch_bounds__(128) void attn_bwd_dq_kernel(const T* __restrict__ qkv, const T* __restrict__ dy,
                                                           const float* __restrict__ lse,
                                                           const float* __restrict__ delta, int T_, int nh, int d,
-                                                          int hs_rt, T* __restrict__ dqkv, float scale) {
+                                                          int hs_rt, T* __restrict__ dqkv, float scale, float drop_p,
+                                                          uint64_t drop_seed, const uint64_t* __restrict__ seed_ptr) {
   constexpr int H2 = HS / 2;
   __shared__ float Ks[ATT_TILE][HS + 1];
   __shared__ float Vs[ATT_TILE][HS + 1];
@@ -392,6 +409,8 @@ __global__ __launch_bounds__(128) void attn_bwd_dq_kernel(const T* __restrict__ 
   const int64_t ld = 3 * (int64_t)d;
   const T* base = qkv + (int64_t)b * T_ * ld;
   const bool valid = qi < T_;
+  AttnDrop dr{drop_p, DROP ? aw_seed_mix(drop_seed, seed_ptr) : 0ull};
+  const int64_t bh = (int64_t)b * nh + h;
   float q[H2], g[H2], dq[H2];
   const int64_t yo = ((int64_t)b * T_ + (valid ? qi : 0)) * d + h * hs + hd.off;
 #pragma unroll
@@ -430,7 +449,7 @@ __global__ __launch_bounds__(128) void attn_bwd_dq_kernel(const T* __restrict__ 
       dp += __shfl_xor(dp, 1, 64);
       const bool ok = valid && (k0 + j) <= qi && (k0 + j) < T_;
       const float p = ok ? __expf(a - L) : 0.f;
-      const float ds = p * (dp - Dl);
+      const float ds = p * ((DROP ? dp * dr.scale(bh, T_, qi, k0 + j) : dp) - Dl);
 #pragma unroll
       for (int e = 0; e < H2; ++e)
         if (hd.has(e)) dq[e] = fmaf(ds, Ks[j][hd.off + e], dq[e]);
@@ -444,11 +463,12 @@ __global__ __launch_bounds__(128) void attn_bwd_dq_kernel(const T* __restrict__ 
 }
 
 // dk_j = scale * sum_{i>=j} dS_ij q_i ;  dv_j = sum_{i>=j} P_ij dy_i      (key-stationary)
-template <typename T, int HS, bool EXACT = true>
+template <typename T, int HS, bool EXACT = true, bool DROP = false>
 __global__ __launch_bounds__(128) void attn_bwd_dkv_kernel(const T* __restrict__ qkv, const T* __restrict__ dy,
                                                            const float* __restrict__ lse,
                                                            const float* __restrict__ delta, int T_, int nh, int d,
-                                                           int hs_rt, T* __restrict__ dqkv, float scale) {
+                                                           int hs_rt, T* __restrict__ dqkv, float scale, float drop_p,
+                                                           uint64_t drop_seed, const uint64_t* __restrict__ seed_ptr) {
   constexpr int H2 = HS / 2;
   __shared__ float Qs[ATT_TILE][HS + 1];
   __shared__ float Gs[ATT_TILE][HS + 1];
@@ -461,6 +481,8 @@ __global__ __launch_bounds__(128) void attn_bwd_dkv_kernel(const T* __restrict__
   const int64_t ld = 3 * (int64_t)d;
   const T* base = qkv + (int64_t)b * T_ * ld;
   const bool valid = kj < T_;
+  AttnDrop dr{drop_p, DROP ? aw_seed_mix(drop_seed, seed_ptr) : 0ull};
+  const int64_t bh = (int64_t)b * nh + h;
   float k[H2], v[H2], dk[H2], dv[H2];
 #pragma unroll
   for (int e = 0; e < H2; ++e) {
@@ -503,11 +525,13 @@ __global__ __launch_bounds__(128) void attn_bwd_dkv_kernel(const T* __restrict__
       const int qq = q0 + i;
       const bool ok = valid && qq >= kj && qq < T_;
       const float p = ok ? __expf(a - Ls[i]) : 0.f;
-      const float ds = p * (dp - Ds[i]);
+      const float ms = DROP ? dr.scale(bh, T_, qq, kj) : 1.f;
+      const float ds = p * (dp * ms - Ds[i]);
+      const float pd = p * ms;
 #pragma unroll
       for (int e = 0; e < H2; ++e)
         if (hd.has(e)) {
-          dv[e] = fmaf(p, Gs[i][hd.off + e], dv[e]);
+          dv[e] = fmaf(pd, Gs[i][hd.off + e], dv[e]);
           dk[e] = fmaf(ds, Qs[i][hd.off + e], dk[e]);  // Qs already carries the scale
         }
     }
@@ -844,43 +868,57 @@ extern "C" int aw_attn_decode(const void* qkv_new, int64_t B, int n_new, int pos
   return aw::check_launch("aw_attn_decode");
 }
 
-extern "C" int aw_attn_fwd(const void* qkv, int64_t B, int T, int n_head, int d, int dtype, void* y, float* lse,
-                           void* stream) {
+extern "C" int aw_attn_fwd_dropout(const void* qkv, int64_t B, int T, int n_head, int d, int dtype, void* y,
+                                   float* lse, float drop_p, uint64_t drop_seed, const uint64_t* seed_ptr,
+                                   void* stream) {
   AW_REQUIRE(qkv && y && lse && B >= 0 && T > 0 && n_head > 0 && d % n_head == 0, "aw_attn_fwd: bad args");
+  AW_REQUIRE(drop_p >= 0.f && drop_p < 1.f, "aw_attn_fwd: dropout probability must be in [0, 1)");
   const int hs = d / n_head;
   AW_REQUIRE(hs >= 1 && hs <= 128, "aw_attn_fwd: head size %d unsupported (1..128)", hs);
   if (B == 0) return AW_OK;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  if (aw::attn_mfma_supported(dtype, hs, d)) {
+  if (drop_p == 0.f && aw::attn_mfma_supported(dtype, hs, d)) {
     aw::attn_fwd_mfma(qkv, B, T, n_head, d, y, lse, s);
     return aw::check_launch("aw_attn_fwd");
   }
   dim3 grid(aw_cdiv(T, ATT_ROWS), n_head, (unsigned)B);
   const float scale = 1.0f / sqrtf((float)hs);
-#define AW_F(HSV, EX)                                                                                         \
-  if (dtype == AW_BF16)                                                                                       \
-    hipLaunchKernelGGL((attn_fwd_kernel<bf16, HSV, EX>), grid, dim3(128), 0, s, (const bf16*)qkv, T, n_head, d, \
-                       hs, (bf16*)y, lse, scale);                                                             \
-  else                                                                                                        \
-    hipLaunchKernelGGL((attn_fwd_kernel<float, HSV, EX>), grid, dim3(128), 0, s, (const float*)qkv, T, n_head, \
-                       d, hs, (float*)y, lse, scale);
-  switch (hs) {
-    case 16: AW_F(16, true) break;
-    case 32: AW_F(32, true) break;
-    case 64: AW_F(64, true) break;
-    case 128: AW_F(128, true) break;
-    default:
-      if (hs < 16) { AW_F(16, false) } else if (hs < 32) { AW_F(32, false) } else if (hs < 64) { AW_F(64, false) }
-      else { AW_F(128, false) }
+#define AW_F(HSV, EX, DR)                                                                                          \
+  if (dtype == AW_BF16)                                                                                            \
+    hipLaunchKernelGGL((attn_fwd_kernel<bf16, HSV, EX, DR>), grid, dim3(128), 0, s, (const bf16*)qkv, T, n_head, d, \
+                       hs, (bf16*)y, lse, scale, drop_p, drop_seed, seed_ptr);                                     \
+  else                                                                                                             \
+    hipLaunchKernelGGL((attn_fwd_kernel<float, HSV, EX, DR>), grid, dim3(128), 0, s, (const float*)qkv, T, n_head, \
+                       d, hs, (float*)y, lse, scale, drop_p, drop_seed, seed_ptr);
+  if (drop_p > 0.f) {         // dropout: the runtime-size kernels (non-default; reference att_dropout = 0.0)
+    if (hs <= 16) { AW_F(16, false, true) } else if (hs <= 32) { AW_F(32, false, true) }
+    else if (hs <= 64) { AW_F(64, false, true) } else { AW_F(128, false, true) }
+  } else {
+    switch (hs) {
+      case 16: AW_F(16, true, false) break;
+      case 32: AW_F(32, true, false) break;
+      case 64: AW_F(64, true, false) break;
+      case 128: AW_F(128, true, false) break;
+      default:
+        if (hs < 16) { AW_F(16, false, false) } else if (hs < 32) { AW_F(32, false, false) }
+        else if (hs < 64) { AW_F(64, false, false) } else { AW_F(128, false, false) }
+    }
   }
 #undef AW_F
   return aw::check_launch("aw_attn_fwd");
 }
 
-extern "C" int aw_attn_bwd(const void* qkv, const void* y, const void* dy, const float* lse, int64_t B, int T,
-                           int n_head, int d, int dtype, void* dqkv, float* ws, void* stream) {
+extern "C" int aw_attn_fwd(const void* qkv, int64_t B, int T, int n_head, int d, int dtype, void* y, float* lse,
+                           void* stream) {
+  return aw_attn_fwd_dropout(qkv, B, T, n_head, d, dtype, y, lse, 0.f, 0ull, nullptr, stream);
+}
+
+extern "C" int aw_attn_bwd_dropout(const void* qkv, const void* y, const void* dy, const float* lse, int64_t B, int T,
+                                   int n_head, int d, int dtype, void* dqkv, float* ws, float drop_p,
+                                   uint64_t drop_seed, const uint64_t* seed_ptr, void* stream) {
   AW_REQUIRE(qkv && y && dy && lse && dqkv && ws && B >= 0 && T > 0 && n_head > 0 && d % n_head == 0,
              "aw_attn_bwd: bad args");
+  AW_REQUIRE(drop_p >= 0.f && drop_p < 1.f, "aw_attn_bwd: dropout probability must be in [0, 1)");
   const int hs = d / n_head;
   AW_REQUIRE(hs >= 1 && hs <= 128, "aw_attn_bwd: head size %d unsupported (1..128)", hs);
   if (B == 0) return AW_OK;
@@ -888,39 +926,51 @@ extern "C" int aw_attn_bwd(const void* qkv, const void* y, const void* dy, const
   dim3 grid(aw_cdiv(T, ATT_ROWS), n_head, (unsigned)B);
   const float scale = 1.0f / sqrtf((float)hs);
   const int64_t nrows = B * n_head * T;
-  if (aw::attn_mfma_supported(dtype, hs, d)) {
+  if (drop_p == 0.f && aw::attn_mfma_supported(dtype, hs, d)) {
     hipLaunchKernelGGL((attn_delta_kernel<bf16>), dim3(gridcap(nrows)), dim3(256), 0, s, (const bf16*)y,
                        (const bf16*)dy, B, T, n_head, d, ws);
     aw::attn_bwd_mfma(qkv, dy, lse, ws, B, T, n_head, d, dqkv, s);
     return aw::check_launch("aw_attn_bwd");
   }
-#define AW_B(HSV, EX)                                                                                              \
+#define AW_B(HSV, EX, DR)                                                                                          \
   if (dtype == AW_BF16) {                                                                                          \
     hipLaunchKernelGGL((attn_delta_kernel<bf16>), dim3(gridcap(nrows)), dim3(256), 0, s, (const bf16*)y,             \
                        (const bf16*)dy, B, T, n_head, d, ws);                                                      \
-    hipLaunchKernelGGL((attn_bwd_dq_kernel<bf16, HSV, EX>), grid, dim3(128), 0, s, (const bf16*)qkv,                 \
-                       (const bf16*)dy, lse, ws, T, n_head, d, hs, (bf16*)dqkv, scale);                            \
-    hipLaunchKernelGGL((attn_bwd_dkv_kernel<bf16, HSV, EX>), grid, dim3(128), 0, s, (const bf16*)qkv,                \
-                       (const bf16*)dy, lse, ws, T, n_head, d, hs, (bf16*)dqkv, scale);                            \
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<bf16, HSV, EX, DR>), grid, dim3(128), 0, s, (const bf16*)qkv,             \
+                       (const bf16*)dy, lse, ws, T, n_head, d, hs, (bf16*)dqkv, scale, drop_p, drop_seed, seed_ptr); \
+    hipLaunchKernelGGL((attn_bwd_dkv_kernel<bf16, HSV, EX, DR>), grid, dim3(128), 0, s, (const bf16*)qkv,            \
+                       (const bf16*)dy, lse, ws, T, n_head, d, hs, (bf16*)dqkv, scale, drop_p, drop_seed, seed_ptr); \
   } else {                                                                                                         \
     hipLaunchKernelGGL((attn_delta_kernel<float>), dim3(gridcap(nrows)), dim3(256), 0, s, (const float*)y,           \
                        (const float*)dy, B, T, n_head, d, ws);                                                     \
-    hipLaunchKernelGGL((attn_bwd_dq_kernel<float, HSV, EX>), grid, dim3(128), 0, s, (const float*)qkv,               \
-                       (const float*)dy, lse, ws, T, n_head, d, hs, (float*)dqkv, scale);                          \
-    hipLaunchKernelGGL((attn_bwd_dkv_kernel<float, HSV, EX>), grid, dim3(128), 0, s, (const float*)qkv,              \
-                       (const float*)dy, lse, ws, T, n_head, d, hs, (float*)dqkv, scale);                          \
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<float, HSV, EX, DR>), grid, dim3(128), 0, s, (const float*)qkv,           \
+                       (const float*)dy, lse, ws, T, n_head, d, hs, (float*)dqkv, scale, drop_p, drop_seed,         \
+                       seed_ptr);                                                                                  \
+    hipLaunchKernelGGL((attn_bwd_dkv_kernel<float, HSV, EX, DR>), grid, dim3(128), 0, s, (const float*)qkv,          \
+                       (const float*)dy, lse, ws, T, n_head, d, hs, (float*)dqkv, scale, drop_p, drop_seed,         \
+                       seed_ptr);                                                                                  \
   }
-  switch (hs) {
-    case 16: AW_B(16, true) break;
-    case 32: AW_B(32, true) break;
-    case 64: AW_B(64, true) break;
-    case 128: AW_B(128, true) break;
-    default:
-      if (hs < 16) { AW_B(16, false) } else if (hs < 32) { AW_B(32, false) } else if (hs < 64) { AW_B(64, false) }
-      else { AW_B(128, false) }
+  if (drop_p > 0.f) {
+    if (hs <= 16) { AW_B(16, false, true) } else if (hs <= 32) { AW_B(32, false, true) }
+    else if (hs <= 64) { AW_B(64, false, true) } else { AW_B(128, false, true) }
+  } else {
+    switch (hs) {
+      case 16: AW_B(16, true, false) break;
+      case 32: AW_B(32, true, false) break;
+      case 64: AW_B(64, true, false) break;
+      case 128: AW_B(128, true, false) break;
+      default:
+        if (hs < 16) { AW_B(16, false, false) } else if (hs < 32) { AW_B(32, false, false) }
+        else if (hs < 64) { AW_B(64, false, false) } else { AW_B(128, false, false) }
+    }
   }
 #undef AW_B
   return aw::check_launch("aw_attn_bwd");
+}
+
+extern "C" int aw_attn_bwd(const void* qkv, const void* y, const void* dy, const float* lse, int64_t B, int T,
+                           int n_head, int d, int dtype, void* dqkv, float* ws, void* stream) {
+  return aw_attn_bwd_dropout(qkv, y, dy, lse, B, T, n_head, d, dtype, dqkv, ws, 0.f, 0ull, nullptr, stream);
 }
 
 extern "C" int aw_ce_fwd(const float* logits, int64_t R, int V, int64_t ldl, const int64_t* y, int ignore_index,

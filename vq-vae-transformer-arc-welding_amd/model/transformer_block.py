@@ -28,9 +28,9 @@ class CausalSelfAttention(nn.Module):
         self.register_buffer("bias", torch.tril(torch.ones(seq_len, seq_len)).view(1, 1, seq_len, seq_len))
         self.n_head = n_head
         self.n_embd = d_model
-        if attn_pdrop > 0:
-            raise NotImplementedError("attention-probability dropout > 0 is not on the HIP path (reference default "
-                                      "att_dropout=0.0)")
+        # the probability dropout runs inside the flash attention kernels (aw_attn_fwd_dropout): a counter-based
+        # mask per (b, h, i, j) the backward regenerates; p > 0 takes the runtime-size VALU kernels
+        self.attn_pdrop = float(attn_pdrop)
 
 
 class Block(nn.Module):
