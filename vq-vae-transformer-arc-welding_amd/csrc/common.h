@@ -89,11 +89,13 @@ __device__ __forceinline__ uint64_t aw_hash_group(uint64_t seed, uint64_t g) {
 }
 __device__ __forceinline__ uint32_t aw_drop_threshold(float p) { return (uint32_t)(p * 65536.f + 0.5f); }
 // Effective seed when a device-side per-step counter is supplied (seed_ptr in the ABI).
-__device__ __forceinline__ uint64_t aw_seed_mix(uint64_t salt, const uint64_t* ctr) {
-  if (!ctr) return salt;
-  uint64_t z = salt ^ (*ctr * 0xD1B54A32D192ED03ull + 0x8CB92BA72F3D8DD7ull);
+__device__ __forceinline__ uint64_t aw_seed_mix_value(uint64_t salt, uint64_t ctr) {
+  uint64_t z = salt ^ (ctr * 0xD1B54A32D192ED03ull + 0x8CB92BA72F3D8DD7ull);
   z = (z ^ (z >> 32)) * 0xD6E8FEB86659FD93ull;
   return z ^ (z >> 32);
+}
+__device__ __forceinline__ uint64_t aw_seed_mix(uint64_t salt, const uint64_t* ctr) {
+  return ctr ? aw_seed_mix_value(salt, *ctr) : salt;
 }
 __device__ __forceinline__ float aw_dropout_scale(uint64_t seed, uint64_t e, float p) {
   if (p <= 0.f) return 1.f;
