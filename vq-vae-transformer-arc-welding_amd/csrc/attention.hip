@@ -35,6 +35,22 @@ constexpr int WROWS = 32;    // rows (queries or keys) per wave
 constexpr int BLK = 128;     // rows per workgroup (4 waves)
 constexpr int IMG = TILE * ROWB;
 
+// One-dimensional grid of nqb * nh * B workgroups; the nqb row blocks of one (b, h) get consecutive logical ids and
+// the logical ids of one XCD are contiguous (hardware blocks i, i+8, i+16, ... run on one XCD), so the blocks that
+// re-read the same K/V (or Q/dO) tiles share that XCD's L2 and run at the same time.
+struct BlockId {
+  int x, h, b;
+  __device__ __forceinline__ BlockId(int nqb, int nh) {
+    const int n = (int)gridDim.x, bid = (int)blockIdx.x;
+    const int q = n / 8, r = n % 8, xcd = bid % 8, slot = bid / 8;
+    const int L = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + slot;
+    x = L % nqb;
+    const int bh = L / nqb;
+    h = bh % nh;
+    b = bh / nh;
+  }
+};
+
 __device__ __forceinline__ int swz(int r) { return (((r >> 1) & 1) << 2) | ((r >> 2) & 3); }
 __device__ __forceinline__ int img_off(int r, int c) { return r * ROWB + ((c ^ swz(r)) << 4); }
 
@@ -121,8 +137,9 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_mfma_kernel(const bf16* __res
   __shared__ __attribute__((aligned(16))) char Ks[IMG];
   __shared__ __attribute__((aligned(16))) char Vs[IMG];
   const int nqb = (T_ + BLK - 1) / BLK;
-  const int qb = nqb - 1 - (int)blockIdx.x;  // longest key ranges first
-  const int h = blockIdx.y, b = blockIdx.z;
+  const BlockId id(nqb, nh);
+  const int qb = nqb - 1 - id.x;  // longest key ranges first
+  const int h = id.h, b = id.b;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = lane & 31, hf = lane >> 5;
   const int64_t ld = 3 * (int64_t)d;
   const bf16* base = qkv + (int64_t)b * T_ * ld;
@@ -208,15 +225,17 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_mfma_kernel(const bf16* __res
 }
 
 // ---------------------------------------------------------------- dQ (query-stationary)
+// Also computes delta_i = dO_i . O_i (rows it owns, from dy and y) and writes it for the dK/dV launch that follows.
 __global__ __launch_bounds__(256, 2) void attn_dq_mfma_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ dy,
-                                                           const float* __restrict__ lse,
-                                                           const float* __restrict__ delta, int T_, int nh, int d,
+                                                           const bf16* __restrict__ y, const float* __restrict__ lse,
+                                                           float* __restrict__ delta, int T_, int nh, int d,
                                                            bf16* __restrict__ dqkv, float c2, float scale) {
   __shared__ __attribute__((aligned(16))) char Ks[IMG];
   __shared__ __attribute__((aligned(16))) char Vs[IMG];
   const int nqb = (T_ + BLK - 1) / BLK;
-  const int qb = nqb - 1 - (int)blockIdx.x;
-  const int h = blockIdx.y, b = blockIdx.z;
+  const BlockId id(nqb, nh);
+  const int qb = nqb - 1 - id.x;
+  const int h = id.h, b = id.b;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = lane & 31, hf = lane >> 5;
   const int64_t ld = 3 * (int64_t)d;
   const bf16* base = qkv + (int64_t)b * T_ * ld;
@@ -230,7 +249,20 @@ __global__ __launch_bounds__(256, 2) void attn_dq_mfma_kernel(const bf16* __rest
     gf[s] = *reinterpret_cast<const uint4*>(gbase + (int64_t)qc * d + h * HS + 16 * s + 8 * hf);
   }
   const int64_t st_i = ((int64_t)b * nh + h) * T_ + qc;
-  const float L2 = lse[st_i] * 1.4426950408889634f, Dl = delta[st_i];
+  float Dl = 0.f;
+  {
+    const bf16* yb = y + (int64_t)b * T_ * d + (int64_t)qc * d + h * HS + 8 * hf;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const bf16x8 yv = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(yb + 16 * s));
+      const bf16x8 gv = __builtin_bit_cast(bf16x8, gf[s]);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) Dl = fmaf((float)gv[e], (float)yv[e], Dl);
+    }
+    Dl += __shfl_xor(Dl, 32, 64);
+    if (hf == 0 && q < T_) delta[st_i] = Dl;
+  }
+  const float L2 = lse[st_i] * 1.4426950408889634f;
   f32x16 acc[2] = {zero16(), zero16()};
   const int kend = min(T_, qb * BLK + BLK);
   const int nt = (kend + TILE - 1) / TILE;
@@ -291,8 +323,9 @@ __global__ __launch_bounds__(256, 2) void attn_dkv_mfma_kernel(const bf16* __res
   __shared__ __attribute__((aligned(16))) char Gs[IMG];
   __shared__ __attribute__((aligned(16))) float Ls[TILE];
   __shared__ __attribute__((aligned(16))) float Ds[TILE];
-  const int kb = blockIdx.x;  // early key blocks see the most queries: launched first
-  const int h = blockIdx.y, b = blockIdx.z;
+  const BlockId id((T_ + BLK - 1) / BLK, nh);
+  const int kb = id.x;  // early key blocks see the most queries: launched first
+  const int h = id.h, b = id.b;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = lane & 31, hf = lane >> 5;
   const int64_t ld = 3 * (int64_t)d;
   const bf16* base = qkv + (int64_t)b * T_ * ld;
@@ -393,17 +426,17 @@ bool attn_mfma_supported(int dtype, int hs, int d) {
 
 void attn_fwd_mfma(const void* qkv, int64_t B, int T, int nh, int d, void* y, float* lse, hipStream_t s) {
   const float scale = 1.0f / sqrtf((float)HS);
-  dim3 grid((T + BLK - 1) / BLK, nh, (unsigned)B);
+  dim3 grid((unsigned)(((T + BLK - 1) / BLK) * (int64_t)nh * B));
   hipLaunchKernelGGL(attn_fwd_mfma_kernel, grid, dim3(256), 0, s, (const bf16*)qkv, T, nh, d, (bf16*)y, lse,
                      scale * 1.4426950408889634f, scale);
 }
 
-void attn_bwd_mfma(const void* qkv, const void* dy, const float* lse, const float* delta, int64_t B, int T, int nh,
-                   int d, void* dqkv, hipStream_t s) {
+void attn_bwd_mfma(const void* qkv, const void* y, const void* dy, const float* lse, float* delta, int64_t B, int T,
+                   int nh, int d, void* dqkv, hipStream_t s) {
   const float scale = 1.0f / sqrtf((float)HS);
-  dim3 grid((T + BLK - 1) / BLK, nh, (unsigned)B);
-  hipLaunchKernelGGL(attn_dq_mfma_kernel, grid, dim3(256), 0, s, (const bf16*)qkv, (const bf16*)dy, lse, delta, T,
-                     nh, d, (bf16*)dqkv, scale * 1.4426950408889634f, scale);
+  dim3 grid((unsigned)(((T + BLK - 1) / BLK) * (int64_t)nh * B));
+  hipLaunchKernelGGL(attn_dq_mfma_kernel, grid, dim3(256), 0, s, (const bf16*)qkv, (const bf16*)dy, (const bf16*)y,
+                     lse, delta, T, nh, d, (bf16*)dqkv, scale * 1.4426950408889634f, scale);
   hipLaunchKernelGGL(attn_dkv_mfma_kernel, grid, dim3(256), 0, s, (const bf16*)qkv, (const bf16*)dy, lse, delta, T,
                      nh, d, (bf16*)dqkv, scale * 1.4426950408889634f, scale);
 }

@@ -7,8 +7,8 @@
 namespace aw {  // attention.hip: MFMA path for bf16, head size 64
 bool attn_mfma_supported(int dtype, int hs, int d);
 void attn_fwd_mfma(const void* qkv, int64_t B, int T, int nh, int d, void* y, float* lse, hipStream_t s);
-void attn_bwd_mfma(const void* qkv, const void* dy, const float* lse, const float* delta, int64_t B, int T, int nh,
-                   int d, void* dqkv, hipStream_t s);
+void attn_bwd_mfma(const void* qkv, const void* y, const void* dy, const float* lse, float* delta, int64_t B, int T,
+                   int nh, int d, void* dqkv, hipStream_t s);   // delta computed by its dQ launch
 }  // namespace aw
 
 namespace {
@@ -927,9 +927,7 @@ extern "C" int aw_attn_bwd_dropout(const void* qkv, const void* y, const void* d
   const float scale = 1.0f / sqrtf((float)hs);
   const int64_t nrows = B * n_head * T;
   if (drop_p == 0.f && aw::attn_mfma_supported(dtype, hs, d)) {
-    hipLaunchKernelGGL((attn_delta_kernel<bf16>), dim3(gridcap(nrows)), dim3(256), 0, s, (const bf16*)y,
-                       (const bf16*)dy, B, T, n_head, d, ws);
-    aw::attn_bwd_mfma(qkv, dy, lse, ws, B, T, n_head, d, dqkv, s);
+    aw::attn_bwd_mfma(qkv, y, dy, lse, ws, B, T, n_head, d, dqkv, s);
     return aw::check_launch("aw_attn_bwd");
   }
 #define AW_B(HSV, EX, DR)                                                                                          \
