@@ -142,6 +142,31 @@ int aw_vq_finalize(const float* counts, const double* sqerr, int64_t N, int K, i
  * g_zq may be NULL (treated as 0); g_loss is a device scalar.  dE is accumulated (not overwritten). */
 int aw_vq_backward(const float* z, const float* E, const int64_t* idx, const float* g_zq, const float* g_loss,
                    int64_t N, int K, int D, float beta, float* dz, float* dE, void* stream);
+/* ------------------------------------------------------------------ residual VQ with EMA codebooks (csrc/rvq.hip)
+ * ResidualVQLightning (model/vector_quantizer.py:9-56) wraps vector-quantize-pytorch's ResidualVQ (third-party, not
+ * installed here: its published algorithm is restated, parity unpinned).  Per layer i: aw_vq_forward on residual r_i
+ * (counts = the EMA's bins, sqerr -> commitment loss via aw_vq_finalize with beta 0), then these:
+ * sums[idx[n]][:] += z[n][:] (accumulated; zero on entry), f32, D % 4 == 0 (vector_quantizer.py:20-21 ema update). */
+int aw_vq_cluster_sums(const float* z, const int64_t* idx, int64_t N, int K, int D, float* sums, void* stream);
+/* One Lloyd step of the k-means init: means[k] = sums[k] / counts[k] where counts[k] > 0 (else unchanged);
+ * avg (may be NULL) = the new means * counts (the init's embed_avg, written on the last step). */
+int aw_kmeans_update(float* means, const float* sums, const float* counts, int K, int D, float* avg, void* stream);
+/* EMA codebook update + dead-code replacement, in place (EuclideanCodebook training branch):
+ *   cs = decay cs + (1-decay) counts;  avg = decay avg + (1-decay) sums;
+ *   embed = avg / ((cs + eps) / (sum cs + K eps) * sum cs);
+ *   codes with cs < threshold (threshold > 0) take a batch row z[r]: embed = z[r], avg = threshold z[r], cs = threshold.
+ * Rows: the expired code of rank j (of n) draws uniformly from the j-th of n equal strata of the N rows (distinct rows),
+ * hash seed mix(salt, *seed_ptr) (seed_ptr may be NULL).  ws: 2K floats of scratch. */
+int aw_rvq_ema_update(float* embed, float* embed_avg, float* cluster_size, const float* counts, const float* sums,
+                      const float* z, int64_t N, int K, int D, float decay, float eps, float threshold, uint64_t salt,
+                      const uint64_t* seed_ptr, float* ws, void* stream);
+/* out = (first ? 0 : out) + zq;  r_next = r - zq (r_next may be NULL).  n elements. */
+int aw_rvq_residual(const float* r, const float* zq, int64_t n, float* out, int first, float* r_next, void* stream);
+/* Backward of the stack: dz = nq * g_zq + sum_i g_loss[i] * commitment * 2 (res_i - q_i) / (N D);
+ * res, q: (nq, N, D) -- each layer's input residual and its straight-through output; g_zq may be NULL. */
+int aw_rvq_backward(const float* res, const float* q, const float* g_zq, const float* g_loss, int nq, int64_t N,
+                    int D, float commitment, float* dz, void* stream);
+
 /* min_encodings one-hot (N,K) f32 (vector_quantizer.py:98-100). */
 int aw_vq_onehot(const int64_t* idx, int64_t N, int K, float* onehot, void* stream);
 /* Gather E[idx] -> out (N, D) (get_embedding_from_one_hot, vector_quantizer.py:121-131). */

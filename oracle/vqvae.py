@@ -112,8 +112,10 @@ def _resblock(x, sd, pre, taps, cfg, train, token_axis_conv):
     return x + o
 
 
-def vqvae_forward(sd, x, cfg: VQVAEConfig, train=True, capture=None):
-    """Returns (embedding_loss, x_hat, perplexity) like VQVAEPatch.forward (vq_vae_patch_embedd.py:155-167)."""
+def vqvae_forward(sd, x, cfg: VQVAEConfig, train=True, capture=None, quantizer=None):
+    """Returns (embedding_loss, x_hat, perplexity) like VQVAEPatch.forward (vq_vae_patch_embedd.py:155-167).
+    ``quantizer(z) -> (loss, z_q_ste, perplexity, idx)`` replaces the VectorQuantizer (e.g. the residual VQ of
+    oracle/residual_vq.torch_quantizer for --use-improved-vq)."""
     B = x.shape[0]
     flat = x.transpose(1, 2).reshape(B, cfg.L * cfg.C)                         # channel-major
     patches = flat.view(B, cfg.S, cfg.P)
@@ -121,7 +123,10 @@ def vqvae_forward(sd, x, cfg: VQVAEConfig, train=True, capture=None):
     for r in range(cfg.R):
         h = _resblock(h, sd, f"encoder.0.shared_conv.{r}", None, cfg, train, token_axis_conv=False)
     z = h @ sd["encoder.1.shared_conv.weight"][:, :, 0].t() + sd["encoder.1.shared_conv.bias"]  # (B,S,D)
-    emb_loss, zq, perplexity, idx, _ = vq_quantize(z, sd["vector_quantization.embedding.weight"], cfg.beta)
+    if quantizer is None:
+        emb_loss, zq, perplexity, idx, _ = vq_quantize(z, sd["vector_quantization.embedding.weight"], cfg.beta)
+    else:
+        emb_loss, zq, perplexity, idx = quantizer(z)
     if capture is not None:
         capture["z_e"] = z
         capture["idx"] = idx
@@ -141,7 +146,7 @@ def vqvae_forward(sd, x, cfg: VQVAEConfig, train=True, capture=None):
     return emb_loss, x_hat, perplexity
 
 
-def vqvae_train_step_grads(sd_np, x_np, cfg: VQVAEConfig, train=True):
+def vqvae_train_step_grads(sd_np, x_np, cfg: VQVAEConfig, train=True, quantizer=None):
     """fwd + bwd of loss = mse(x_hat, x) + emb_loss (autencoder_lightning_base.py:80-84). Returns outputs,
     gradients keyed by reference parameter name, and the post-forward state (BN running stats)."""
     sd = {k: torch.tensor(v).clone() for k, v in sd_np.items()}
@@ -149,14 +154,15 @@ def vqvae_train_step_grads(sd_np, x_np, cfg: VQVAEConfig, train=True):
               if not (k.endswith("running_mean") or k.endswith("running_var") or k.endswith("num_batches_tracked"))}
     x = torch.tensor(x_np)
     cap = {}
-    emb_loss, x_hat, perp = vqvae_forward(sd, x, cfg, train=train, capture=cap)
+    emb_loss, x_hat, perp = vqvae_forward(sd, x, cfg, train=train, capture=cap, quantizer=quantizer)
     recon = F.mse_loss(x_hat, x)
     loss = recon + emb_loss
     loss.backward()
     grads = {k: (p.grad.numpy() if p.grad is not None else None) for k, p in params.items()}
     state = {k: v.detach().numpy() for k, v in sd.items()
              if k.endswith("running_mean") or k.endswith("running_var")}
-    out = dict(x_hat=x_hat.detach().numpy(), emb_loss=emb_loss.detach().numpy(), perplexity=perp.detach().numpy(),
+    out = dict(x_hat=x_hat.detach().numpy(), emb_loss=emb_loss.detach().numpy(),
+               perplexity=None if perp is None else perp.detach().numpy(),
                recon=recon.detach().numpy(), loss=loss.detach().numpy(), idx=cap["idx"].numpy(),
                z_e=cap["z_e"].detach().numpy())
     return out, grads, state

@@ -126,6 +126,12 @@ SIGNATURES = {
     "aw_ce_fwd": [c_p, c_i64, c_int, c_i64, c_p, c_int, c_p, c_p, c_p, c_p],
     "aw_ce_bwd": [c_p, c_i64, c_int, c_i64, c_p, c_int, c_p, c_p, c_p, c_p, c_i64, c_int, c_p],
     "aw_ce_finalize": [c_p, c_p, c_p, c_p],
+    "aw_vq_cluster_sums": [c_p, c_p, c_i64, c_int, c_int, c_p, c_p],
+    "aw_kmeans_update": [c_p, c_p, c_p, c_int, c_int, c_p, c_p],
+    "aw_rvq_ema_update": [c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_int, c_int, c_f, c_f, c_f, ctypes.c_uint64, c_p, c_p,
+                          c_p],
+    "aw_rvq_residual": [c_p, c_p, c_i64, c_p, c_int, c_p, c_p],
+    "aw_rvq_backward": [c_p, c_p, c_p, c_p, c_int, c_i64, c_int, c_f, c_p, c_p],
 }
 
 RET_I64 = {"aw_gemm_workspace"}

@@ -165,6 +165,37 @@ def vq_backward(z2d, E, idx, g_zq, g_loss, beta, dz, dE, stream=None):
          ptr(dz), ptr(dE), stream_ptr(stream))
 
 
+# ------------------------------------------------------------------------ residual VQ (EMA codebooks)
+def vq_cluster_sums(z2d, idx, K, sums, stream=None):
+    """sums[idx[n]] += z[n] (sums zeroed by the caller)."""
+    _dense(z2d, "vq_cluster_sums")
+    call("aw_vq_cluster_sums", ptr(z2d), ptr(idx), z2d.shape[0], K, z2d.shape[1], ptr(sums), stream_ptr(stream))
+
+
+def kmeans_update(means, sums, counts, avg=None, stream=None):
+    call("aw_kmeans_update", ptr(means), ptr(sums), ptr(counts), means.shape[0], means.shape[1], ptr(avg),
+         stream_ptr(stream))
+
+
+def rvq_ema_update(embed, embed_avg, cluster_size, counts, sums, z2d, decay, eps, threshold, salt, seed_ptr, ws,
+                   stream=None):
+    K, D = embed.shape
+    call("aw_rvq_ema_update", ptr(embed), ptr(embed_avg), ptr(cluster_size), ptr(counts), ptr(sums), ptr(z2d),
+         z2d.shape[0], K, D, float(decay), float(eps), float(threshold), int(salt) & 0xFFFFFFFFFFFFFFFF,
+         ptr(seed_ptr), ptr(ws), stream_ptr(stream))
+
+
+def rvq_residual(r, zq, out, first, r_next=None, stream=None):
+    call("aw_rvq_residual", ptr(r), ptr(zq), zq.numel(), ptr(out), int(bool(first)), ptr(r_next), stream_ptr(stream))
+
+
+def rvq_backward(res, q, g_zq, g_loss, dz, commitment=1.0, stream=None):
+    """res, q: (nq, N, D); dz (N, D)."""
+    nq, N, D = res.shape
+    call("aw_rvq_backward", ptr(res), ptr(q), ptr(g_zq), ptr(g_loss), nq, N, D, float(commitment), ptr(dz),
+         stream_ptr(stream))
+
+
 def vq_onehot(idx, K, out, stream=None):
     call("aw_vq_onehot", ptr(idx), idx.numel(), K, ptr(out), stream_ptr(stream))
 

@@ -189,7 +189,10 @@ class Trainer:
             n = len(loader) if hasattr(loader, "__len__") else None
             for i, batch in enumerate(loader):
                 batch = _to_device(batch, dev)
-                if self.hip_graphs and self.accumulate == 1 and _fixed_shape(self, batch):
+                # a residual-VQ model synchronises its codebooks with host-issued collectives in the forward
+                # (arcweld/residual_vq.py): eager steps when data parallel
+                graphable = not (getattr(model, "use_improved_vq", False) and self.world() > 1)
+                if self.hip_graphs and graphable and self.accumulate == 1 and _fixed_shape(self, batch):
                     loss = self.graphed_step(model, batch, scale)
                     if self.global_step % self.log_every == 0:
                         # the captured step's static loss tensor holds this replay's value

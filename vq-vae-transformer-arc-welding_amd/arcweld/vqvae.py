@@ -79,7 +79,9 @@ def _params(m):
     enc_bn = [(blk.block[2], blk.block[5]) if m.batch_norm else None for blk in m.encoder[0].shared_conv]
     dec_bn = [(blk.block[2], blk.block[5]) if m.batch_norm else None for blk in m.decoder[1].shared_conv]
     rp = m.reverse_patch_embed.proj
-    return dict(pe=m.patch_embed.proj, enc=enc, sep=m.encoder[1].shared_conv, E=m.vector_quantization.embedding.weight,
+    # the residual VQ (--use-improved-vq) keeps EMA codebook buffers, no codebook parameter
+    E = None if getattr(m, "use_improved_vq", False) else m.vector_quantization.embedding.weight
+    return dict(pe=m.patch_embed.proj, enc=enc, sep=m.encoder[1].shared_conv, E=E,
                 dec0=m.decoder[0], dec=dec, t1=rp[0], bn=rp[1], t2=rp[3], enc_bn=enc_bn, dec_bn=dec_bn)
 
 
@@ -272,13 +274,21 @@ def forward(m, x, training: bool, need_backward: bool, dtype=None, seed: int = 0
 
     # ---- vector quantizer
     Kc = sh.K
-    zq = e(N, D)
-    idx = e(N, dt=torch.int64)
-    counts = torch.zeros(Kc, device=dev)
-    sq = torch.zeros(1, device=dev, dtype=torch.float64)
-    K.vq_forward(z, pr["E"], zq, idx, counts, sq)
-    emb_loss, perplexity = e(()), e(())
-    K.vq_finalize(counts, sq, N, Kc, D, m.vector_quantization.beta, emb_loss, perplexity)
+    if pr["E"] is None:
+        # residual VQ with EMA codebooks (vector_quantizer.py:9-56): commitment loss, no perplexity (:39)
+        rvq = m.vector_quantization.vq
+        zq, idx2, losses, sv.rvq = rvq.quantize_rows(z, training, save=need_backward)
+        idx = idx2[:, 0] if rvq.num_quantizers == 1 else idx2
+        emb_loss = losses.view(()) if rvq.num_quantizers == 1 else losses.sum()
+        perplexity = None
+    else:
+        zq = e(N, D)
+        idx = e(N, dt=torch.int64)
+        counts = torch.zeros(Kc, device=dev)
+        sq = torch.zeros(1, device=dev, dtype=torch.float64)
+        K.vq_forward(z, pr["E"], zq, idx, counts, sq)
+        emb_loss, perplexity = e(()), e(())
+        K.vq_finalize(counts, sq, N, Kc, D, m.vector_quantization.beta, emb_loss, perplexity)
     zq_T = zq if T == F32 else _cast(zq, T)
 
     # ---- decoder: 1x1 conv + ResBlocks with k=3 convs along the window
@@ -381,6 +391,12 @@ def encode(m, x, dtype=F32):
     xR_T = a if R > 0 else (xr if T == F32 else _cast(xr, T))
     z = e(N, D)
     K.gemm(xR_T, Ws, N, D, H, bias=pr["sep"].bias, C=z)
+    if pr["E"] is None:   # residual VQ: eval-mode assignment (no EMA), one token per position needs nq == 1
+        rvq = m.vector_quantization.vq
+        if rvq.num_quantizers != 1:
+            raise ValueError("tokenization needs a single quantizer (ResidualVQ num_quantizers == 1)")
+        _, idx2, _, _ = rvq.quantize_rows(z, False)
+        return idx2[:, 0].contiguous(), z
     zq, idx = e(N, D), e(N, dt=torch.int64)
     counts = torch.zeros(sh.K, device=x.device)
     sq = torch.zeros(1, device=x.device, dtype=torch.float64)
@@ -467,7 +483,12 @@ def backward(m, sv, g_emb, g_xhat, slot, mid_hook=None):
 
     # ---- vector quantizer (straight-through + codebook/commitment loss)
     dz = e(N, D)
-    K.vq_backward(sv.z, pr["E"], sv.idx, gzq, g_emb, m.vector_quantization.beta, dz, slot(pr["E"]))
+    if pr["E"] is None:   # residual VQ: straight-through + commitment terms, codebooks are EMA buffers
+        res, qs = sv.rvq
+        nq = res.shape[0]
+        K.rvq_backward(res, qs, gzq, g_emb if nq == 1 else g_emb.expand(nq).contiguous(), dz)
+    else:
+        K.vq_backward(sv.z, pr["E"], sv.idx, gzq, g_emb, m.vector_quantization.beta, dz, slot(pr["E"]))
     if mid_hook is not None:
         mid_hook()
     dz_T = dz if T == F32 else _cast(dz, T)
@@ -523,7 +544,8 @@ class VQVAEPatchFunction(torch.autograd.Function):
         need = torch.is_grad_enabled() or any(p.requires_grad for p in params)
         emb, x_hat, perp, idx, sv = forward(m, x, training, need_backward=True, seed=seed)
         ctx.m, ctx.sv, ctx.params = m, sv, params
-        ctx.mark_non_differentiable(perp)
+        if perp is not None:          # None for the residual VQ (vector_quantizer.py:39)
+            ctx.mark_non_differentiable(perp)
         m._last_indices = idx
         return emb, x_hat, perp
 

@@ -15,7 +15,7 @@ from torch import nn
 from arcweld import kernels as K
 from arcweld import vqvae as engine
 from model.autencoder_lightning_base import Autoencoder
-from model.vector_quantizer import VectorQuantizer
+from model.vector_quantizer import ResidualVQLightning, VectorQuantizer
 
 
 def _need_no_grad(mod, *tensors):
@@ -208,15 +208,18 @@ class VQVAEPatch(Autoencoder):
         super().__init__(hidden_dim=hidden_dim, input_dim=input_dim, num_embeddings=num_embeddings,
                          embedding_dim=embedding_dim, n_resblocks=n_resblocks, learning_rate=learning_rate,
                          seq_len=seq_len, dropout_p=dropout_p)
-        if use_improved_vq:
-            raise NotImplementedError("use_improved_vq (vector-quantize-pytorch ResidualVQ) is out of scope: the "
-                                      "third-party library is not available and its parity is unpinned")
+        self.use_improved_vq = bool(use_improved_vq)
         self.patch_embed = PatchEmbedding(patch_size=patch_size, embed_dim=hidden_dim)
         self.encoder = nn.Sequential(
             CNNBlock(embed_dim=hidden_dim, n_resblocks=n_resblocks, dropout_p=dropout_p, batch_norm=batch_norm),
             SepCNNBlock(hidden_dim=hidden_dim, embedding_dim=embedding_dim),
         )
-        self.vector_quantization = VectorQuantizer(n_e=num_embeddings, e_dim=embedding_dim, beta=beta)
+        if use_improved_vq:   # vq_vae_patch_embedd.py:132-136: one EMA quantizer, k-means init, dead-code reset
+            self.vector_quantization = ResidualVQLightning(num_quantizers=1, e_dim=embedding_dim, n_e=num_embeddings,
+                                                           kmeans_init=True, kmeans_iters=kmeans_iters,
+                                                           threshold_ema_dead_code=threshold_ema_dead_code)
+        else:
+            self.vector_quantization = VectorQuantizer(n_e=num_embeddings, e_dim=embedding_dim, beta=beta)
         self.decoder = nn.Sequential(
             nn.Conv1d(embedding_dim, hidden_dim, kernel_size=1, stride=1, padding=0),
             CNNBlock(embed_dim=hidden_dim, seperate=False, n_resblocks=n_resblocks, dropout_p=dropout_p,
@@ -288,7 +291,10 @@ class VQVAEPatch(Autoencoder):
         return [blk.block[i].weight for blk in self.encoder[0].shared_conv for i in (1, 4)]
 
     def backward_split_parameter(self):
-        """First parameter (in registration order) whose gradient is final at fused_train_step's mid_hook."""
+        """First parameter (in registration order) whose gradient is final at fused_train_step's mid_hook (the
+        residual VQ's codebooks are EMA buffers: the decoder's 1x1 conv comes first then)."""
+        if self.use_improved_vq:
+            return self.decoder[0].weight
         return self.vector_quantization.embedding.weight
 
     def backward_late_parameters(self):
