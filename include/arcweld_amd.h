@@ -274,6 +274,21 @@ int aw_radam_step(float* param, const float* grad, float* exp_avg, float* exp_av
                   const int64_t* seg_len, const float* seg_wd, const int* seg_active, int nseg, int64_t total, int64_t step,
                   float lr, float beta1, float beta2, float eps, const float* gscale, const int64_t* step_ptr,
                   void* stream);
+/* aw_radam_step that also writes the operand copies of the updated weights (what aw_weight_relayout_batch would
+ * produce from the new values), so the training step needs no relayout launch.  ops: device array of
+ * AW_OPS_PER_SEG descriptors per segment (ops[AW_OPS_PER_SEG*s + j]; mode -1 = none): flat element l of segment s
+ * (the parameter in its storage order: (O, I, k) contiguous; a declare_centre_tap segment is its [O][I] centre,
+ * described as k = 1, tap = 0) goes to `out` at the index of relayout mode `mode` (0-6), cast to `dtype`. */
+#define AW_OPS_PER_SEG 2
+typedef struct {
+  void* out;
+  int O, I, k, tap, mode, dtype;
+  int64_t ldo;
+} aw_operand_desc;
+int aw_radam_step_ops(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, const int64_t* seg_off,
+                      const int64_t* seg_len, const float* seg_wd, const int* seg_active, int nseg, int64_t total,
+                      int64_t step, float lr, float beta1, float beta2, float eps, const float* gscale,
+                      const int64_t* step_ptr, const aw_operand_desc* ops, void* stream);
 /* Device step counter / RNG counter: *counter += v (one thread; graph-capture safe).  With step_ptr != NULL,
  * aw_radam_step reads the step number from the device (the host `step` is ignored) and derives the bias
  * corrections and rectification there, in double precision like torch's python-float scalars. */

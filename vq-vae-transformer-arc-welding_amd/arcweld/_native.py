@@ -72,6 +72,14 @@ class RelayoutJob(ctypes.Structure):
                 ("mode", c_int), ("ldo", c_i64)]
 
 
+class OperandDesc(ctypes.Structure):
+    """aw_operand_desc (include/arcweld_amd.h)."""
+    _fields_ = [("out", c_p), ("O", c_int), ("I", c_int), ("k", c_int), ("tap", c_int), ("mode", c_int),
+                ("dtype", c_int), ("ldo", c_i64)]
+
+
+OPS_PER_SEG = 2     # AW_OPS_PER_SEG
+
 # name -> argtypes (every entry returns int status except aw_last_error)
 SIGNATURES = {
     "aw_version": [],
@@ -106,6 +114,8 @@ SIGNATURES = {
     "aw_mse_finalize": [c_p, c_i64, c_p, c_p],
     "aw_radam_step": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_int, c_i64, c_i64, c_f, c_f, c_f, c_f, c_p, c_p,
                       c_p],
+    "aw_radam_step_ops": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_int, c_i64, c_i64, c_f, c_f, c_f, c_f, c_p, c_p,
+                          c_p, c_p],
     "aw_counter_add": [c_p, c_i64, c_p],
     "aw_grad_norm_clip": [c_p, c_p, c_p, c_p, c_int, c_i64, c_f, c_p, c_p, c_p, c_p],
     "aw_scale": [c_p, c_i64, c_p, c_p],

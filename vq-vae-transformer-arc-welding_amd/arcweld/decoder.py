@@ -21,6 +21,7 @@ from __future__ import annotations
 import torch
 
 from . import kernels as K
+from . import operands
 from .vqvae import _mix, operand_dtype, rng_snapshot
 
 F32 = torch.float32
@@ -40,6 +41,29 @@ def _cast(t, T):
     out = torch.empty(t.shape, device=t.device, dtype=T)
     K.cast(t, out)
     return out
+
+
+def _operand_jobs(m, T_):
+    """Operand copies of the training step: the blocks' Linear weights in the operand dtype (when it is not f32)
+    and the lm head zero-padded to a multiple of 8 rows."""
+    from .operands import OperandJob as J
+    jobs = []
+    for i, blk in enumerate(m.transformer.h):
+        for nm, lin in (("qkv", blk.attn.c_attn), ("o", blk.attn.c_proj), ("fc", blk.mlp.c_fc), ("p", blk.mlp.c_proj)):
+            w = lin.weight
+            if w.dtype != T_:
+                jobs.append(J(f"b{i}_{nm}", w, w, w.shape[0], w.shape[1], 1, 0, 5,
+                              torch.empty(w.shape, device=w.device, dtype=T_)))
+    w = m.lm_head.weight
+    jobs.append(J("Wlm", w, w, w.shape[0], w.shape[1], 1, 0, 5,
+                  torch.zeros(_pad8(w.shape[0]), w.shape[1], device=w.device, dtype=T_)))
+    return jobs
+
+
+def operand_set(m, T=None):
+    """The OperandSet the training step of `m` reads (for arcweld.optim.RAdam.attach_operands)."""
+    T_ = operand_dtype(T)
+    return operands.peek(m, ("decoder", T_), lambda: _operand_jobs(m, T_))
 
 
 def forward(m, ids, generate: bool, training: bool, need_backward: bool, seed: int = 0, dtype=None):
@@ -74,21 +98,12 @@ def forward(m, ids, generate: bool, training: bool, need_backward: bool, seed: i
 
     x = e(R, d)
     K.embed_fwd(ids, m.embedding.latent_embedding.weight, pe[0], x)
-    # operand copies of every block's Linear weights: one batched cast launch (f32 operands are used as they are)
-    wops = []
-    casts = []
-    for blk in m.transformer.h:
-        ws = []
-        for lin in (blk.attn.c_attn, blk.attn.c_proj, blk.mlp.c_fc, blk.mlp.c_proj):
-            w = lin.weight
-            if T_ == w.dtype:
-                ws.append(w)
-            else:
-                o = torch.empty(w.shape, device=dev, dtype=T_)
-                casts.append((w, w.shape[0], w.shape[1], 1, 0, 5, o))
-                ws.append(o)
-        wops.append(ws)
-    K.weight_relayout_batch(casts)
+    # operand copies of every block's Linear weights and the padded lm head (f32 Linear operands are used as they
+    # are): persistent, re-cast only when a weight changed outside the optimizer (arcweld/operands.py)
+    ops = operands.get(m, ("decoder", T_), lambda: _operand_jobs(m, T_))
+    wops = [[ops.get(f"b{i}_{nm}", lin.weight)
+             for nm, lin in (("qkv", blk.attn.c_attn), ("o", blk.attn.c_proj), ("fc", blk.mlp.c_fc),
+                             ("p", blk.mlp.c_proj))] for i, blk in enumerate(m.transformer.h)]
     blocks = []
     for i, blk in enumerate(m.transformer.h):
         at, mlp = blk.attn, blk.mlp
@@ -119,8 +134,7 @@ def forward(m, ids, generate: bool, training: bool, need_backward: bool, seed: i
     sv.blocks, sv.x_last, sv.xf, sv.muf, sv.rsf = blocks, x, xf, muf, rsf
     if generate:
         Vp = _pad8(V)
-        Wlm = torch.zeros(Vp, d, device=dev, dtype=T_)        # padded rows stay zero (K padding of the dgrad)
-        K.cast(m.lm_head.weight, Wlm[:V])
+        Wlm = ops["Wlm"]        # [Vp][d]: padded rows stay zero (K padding of the dgrad)
         logits_buf = e(R, Vp)
         logits = logits_buf[:, :V]
         K.gemm(xf, Wlm, R, V, d, C=logits)

@@ -290,10 +290,15 @@ def mse_finalize(sqerr, numel, out, stream=None):
 
 # ------------------------------------------------------------------------------------------ optimizer
 def radam_step(param, grad, m, v, seg_off, seg_len, seg_wd, seg_active, nseg, total, step, lr, beta1, beta2, eps,
-               gscale=None, stream=None, step_ptr=None):
-    call("aw_radam_step", ptr(param), ptr(grad), ptr(m), ptr(v), ptr(seg_off), ptr(seg_len), ptr(seg_wd),
-         ptr(seg_active), int(nseg), int(total), int(step), float(lr), float(beta1), float(beta2), float(eps),
-         ptr(gscale), ptr(step_ptr), stream_ptr(stream))
+               gscale=None, stream=None, step_ptr=None, ops=None):
+    """aw_radam_step, or aw_radam_step_ops when `ops` (device table of aw_operand_desc, AW_OPS_PER_SEG per
+    segment) is given: the update also writes the operand copies of the updated weights."""
+    args = (ptr(param), ptr(grad), ptr(m), ptr(v), ptr(seg_off), ptr(seg_len), ptr(seg_wd), ptr(seg_active), int(nseg),
+            int(total), int(step), float(lr), float(beta1), float(beta2), float(eps), ptr(gscale), ptr(step_ptr))
+    if ops is None:
+        call("aw_radam_step", *args, stream_ptr(stream))
+    else:
+        call("aw_radam_step_ops", *args, ptr(ops), stream_ptr(stream))
 
 
 def counter_add(counter, v=1, stream=None):

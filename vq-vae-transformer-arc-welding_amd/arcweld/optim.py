@@ -173,6 +173,45 @@ class RAdam(torch.optim.Optimizer):
                 out.append((cur, b))
         return out
 
+    def attach_operands(self, opset):
+        """Keep the GEMM operand copies of ``opset`` (arcweld.operands.OperandSet) current from the update kernel
+        (aw_radam_step_ops): each updated element is also cast into the copies of its parameter, so the step needs no
+        relayout launch.  Returns False (and leaves the set refreshed per forward) when a copy's parameter is not in
+        this optimizer or one parameter feeds more than AW_OPS_PER_SEG copies."""
+        import ctypes
+        from . import _native as nat
+        self.flatten()
+        F = self._flat
+        seg_of = {id(sg[0]): i for i, sg in enumerate(F["segs"])}
+        per = [[] for _ in F["segs"]]
+        for j in opset.jobs:
+            i = seg_of.get(id(j.param))
+            if i is None:
+                return False
+            per[i].append(j)
+        if any(len(x) > nat.OPS_PER_SEG for x in per):
+            return False
+        table = (nat.OperandDesc * (nat.OPS_PER_SEG * len(per)))()
+        for i, js in enumerate(per):
+            for k in range(nat.OPS_PER_SEG):
+                d = table[nat.OPS_PER_SEG * i + k]
+                if k >= len(js):
+                    d.mode = -1
+                    continue
+                j = js[k]
+                # the segment stores the parameter (O, I, k) contiguous, or only its [O][I] centre (declared
+                # centre-tap: the job's source is then that centre view, k = 1)
+                if j.src.numel() != F["segs"][i][2]:
+                    return False
+                d.out = j.out.data_ptr()
+                d.O, d.I, d.k, d.tap, d.mode, d.ldo = j.O, j.I, j.k, j.tap, j.mode, j.ldo
+                d.dtype = K.dtype_code(j.out.dtype)
+        raw = torch.frombuffer(bytearray(bytes(table)), dtype=torch.uint8)
+        F["ops_d"] = raw.to(F["p"].device)
+        F["opset"] = opset
+        opset.maintained = True
+        return True
+
     @property
     def flat_grad(self):
         return self.flatten()[1]
@@ -213,7 +252,8 @@ class RAdam(torch.optim.Optimizer):
         # groups that differ only in weight decay (per segment already) share one launch
         for (lr, (b1, b2), eps), act in self._launch_groups():
             K.radam_step(F["p"], F["g"], F["m"], F["v"], F["off_d"], F["len_d"], F["wd_d"], act, len(F["segs"]),
-                         F["total"], self._step_count, lr, b1, b2, eps, gscale=self._coef, step_ptr=F["step"])
+                         F["total"], self._step_count, lr, b1, b2, eps, gscale=self._coef, step_ptr=F["step"],
+                         ops=F.get("ops_d"))
         self._coef = None
         return loss
 

@@ -70,6 +70,8 @@ def broadcast_params(model: torch.nn.Module, opt=None):
     for t in list(model.parameters()) + list(model.buffers()):
         if id(t) not in packed:
             dist.broadcast(t.data, src=0)
+    from . import operands
+    operands.invalidate(model)      # the flat buffer changed behind the parameters' version counters
 
 
 class Trainer:
@@ -112,6 +114,8 @@ class Trainer:
             model._grad_sink = {p: p.grad for p in model.parameters()}
         if self.data_parallel:
             broadcast_params(model, opt)
+        if hasattr(model, "operand_set") and hasattr(opt, "attach_operands"):
+            opt.attach_operands(model.operand_set())     # the update kernel keeps the GEMM operand copies current
         self.optimizer = opt
         self._graphs = None          # a captured step belongs to one optimizer
         self._graph_shape = None

@@ -22,6 +22,7 @@ from __future__ import annotations
 import torch
 
 from . import kernels as K
+from . import operands
 from .precision import operand_dtype  # noqa: F401  (re-exported: model/ and arcweld.decoder import it from here)
 
 F32 = torch.float32
@@ -100,6 +101,40 @@ def _centre_job(w, out):
     if not c.is_contiguous():
         raise ValueError("encoder conv weight: unsupported layout")
     return (c, O, I, 1, 0, 0, out)
+
+
+def _operand_jobs(m, T, chain):
+    """Every weight operand of the training step (forward and backward): arcweld.operands.OperandJob list."""
+    from .operands import OperandJob as J
+    sh = VQVAEShapes(m, 1)
+    H, D, R, P, k1 = sh.H, sh.D, sh.R, sh.P, sh.k1
+    pr = _params(m)
+    dev = pr["pe"].weight.device
+    e = lambda *s: torch.empty(*s, device=dev, dtype=T)  # noqa: E731
+    jobs = [J("Wp", pr["pe"].weight, pr["pe"].weight, H, 1, P, 0, 4, torch.zeros(H, sh.ldp, device=dev, dtype=T),
+              sh.ldp)]
+    for r, (c1, c2) in enumerate(pr["enc"]):
+        for nm, c in (("1", c1), ("2", c2)):
+            src, O, I, k, tap, mode, _ = _centre_job(c.weight, None)
+            jobs.append(J(f"enc{r}_{nm}", c.weight, src, O, I, k, tap, mode, e(H, H)))
+            if chain:   # K-step-major copies for the fused chain's weight stream (the backward reads enc_w)
+                jobs.append(J(f"chain{r}_{nm}", c.weight, src, O, I, k, tap, 6, e(H, H)))
+    jobs.append(J("Ws", pr["sep"].weight, pr["sep"].weight, D, H, 1, 0, 0, e(D, H)))
+    jobs.append(J("Wd0", pr["dec0"].weight, pr["dec0"].weight, H, D, 1, 0, 0, e(H, D)))
+    for r, (c1, c2) in enumerate(pr["dec"]):
+        for nm, c in (("1", c1), ("2", c2)):
+            jobs.append(J(f"dec{r}_{nm}", c.weight, c.weight, H, H, 3, 0, 1, e(H, 3 * H)))     # forward [O][3I]
+            jobs.append(J(f"dgw{r}_{nm}", c.weight, c.weight, H, H, 3, 0, 2, e(3 * H, H)))     # dgrad [3O][I]
+    jobs.append(J("Wt1", pr["t1"].weight, pr["t1"].weight, H, H, k1, 0, 3, e(k1 * H, H)))
+    return jobs
+
+
+def operand_set(m, T=None):
+    """The OperandSet the training step of `m` reads (for arcweld.optim.RAdam.attach_operands)."""
+    T = operand_dtype(T)
+    sh = VQVAEShapes(m, 1)
+    chain = use_encoder_chain(m, T, sh.H, sh.R)
+    return operands.peek(m, ("vqvae", T, chain), lambda: _operand_jobs(m, T, chain))
 
 
 def _centre_grad(g):
@@ -198,32 +233,15 @@ def forward(m, x, training: bool, need_backward: bool, dtype=None, seed: int = 0
     sv.dec_seed = [_mix(seed, 200 + r) for r in range(R)]
     sv.ctr = rng_snapshot(m, dev, p_drop)
 
-    # ---- operand copies of the weights (relayout + cast), one batched launch
-    jobs = []
-    Wp = e(H, sh.ldp, dt=T)
-    jobs.append((pr["pe"].weight, H, 1, P, 0, 4, Wp, sh.ldp))
-    enc_w, chain_w = [], []
+    # ---- operand copies of the weights (relayout + cast): persistent, refreshed by one batched relayout only when
+    #      a weight changed outside the optimizer (the flat RAdam rewrites them in its update kernel)
     chain = use_encoder_chain(m, T, H, R)
-    for c1, c2 in pr["enc"]:
-        w1, w2 = e(H, H, dt=T), e(H, H, dt=T)
-        jobs += [_centre_job(c1.weight, w1), _centre_job(c2.weight, w2)]
-        enc_w.append((w1, w2))
-        if chain:   # K-step-major copies for the fused chain's weight stream (the backward reads enc_w)
-            s1, s2 = e(H, H, dt=T), e(H, H, dt=T)
-            jobs += [_centre_job(c1.weight, s1)[:5] + (6, s1), _centre_job(c2.weight, s2)[:5] + (6, s2)]
-            chain_w.append((s1, s2))
-    Ws = e(D, H, dt=T)
-    jobs.append((pr["sep"].weight, D, H, 1, 0, 0, Ws))
-    Wd0 = e(H, D, dt=T)
-    jobs.append((pr["dec0"].weight, H, D, 1, 0, 0, Wd0))
-    dec_w = []
-    for c1, c2 in pr["dec"]:
-        w1, w2 = e(H, 3 * H, dt=T), e(H, 3 * H, dt=T)
-        jobs += [(c1.weight, H, H, 3, 0, 1, w1), (c2.weight, H, H, 3, 0, 1, w2)]
-        dec_w.append((w1, w2))
-    Wt1 = e(k1 * H, H, dt=T)
-    jobs.append((pr["t1"].weight, H, H, k1, 0, 3, Wt1))
-    K.weight_relayout_batch(jobs)
+    ops = operands.get(m, ("vqvae", T, chain), lambda: _operand_jobs(m, T, chain))
+    Wp, Ws, Wd0, Wt1 = ops["Wp"], ops["Ws"], ops["Wd0"], ops["Wt1"]
+    enc_w = [(ops[f"enc{r}_1"], ops[f"enc{r}_2"]) for r in range(R)]
+    chain_w = [(ops[f"chain{r}_1"], ops[f"chain{r}_2"]) for r in range(R)] if chain else []
+    dec_w = [(ops[f"dec{r}_1"], ops[f"dec{r}_2"]) for r in range(R)]
+    sv.ops = ops
 
     # ---- patch embed
     patches = e(N, sh.ldp, dt=T)
@@ -447,9 +465,7 @@ def backward(m, sv, g_emb, g_xhat, slot, mid_hook=None):
     # weight gradients of the whole ResBlock stack are deferred and issued as ONE grouped launch (every tile runs
     # the full token reduction: no split-K, no slab reduce); their operands stay alive until then
     wgrads = []
-    dgw = [(e(3 * H, H, dt=T), e(3 * H, H, dt=T)) for _ in range(R)]
-    K.weight_relayout_batch([jb for r in range(R) for jb in ((pr["dec"][r][0].weight, H, H, 3, 0, 2, dgw[r][0]),
-                                                             (pr["dec"][r][1].weight, H, H, 3, 0, 2, dgw[r][1]))])
+    dgw = [(sv.ops[f"dgw{r}_1"], sv.ops[f"dgw{r}_2"]) for r in range(R)]
     def wg_dec(c, A, B):
         return (A, B, H, 3 * H, N, dict(a_trans=True, b_trans=True, conv=wconv, C=slot(c.weight).view(H, 3 * H),
                                         accumulate=True, col_map=(H, 3, 0), a_rowsum=slot(c.bias)))

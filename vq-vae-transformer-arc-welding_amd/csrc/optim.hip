@@ -107,6 +107,104 @@ __global__ __launch_bounds__(256) void radam_kernel(float* __restrict__ p, const
   }
 }
 
+// Operand copy of an updated element: index of flat element l of a segment (the parameter in its storage order,
+// (O, I, k) contiguous) in the operand `d` (aw_weight_relayout modes), or -1 when the element is not part of it.
+__device__ __forceinline__ int64_t op_dst(const aw_operand_desc& d, uint32_t l) {
+  const uint32_t O = (uint32_t)d.O, I = (uint32_t)d.I, k = (uint32_t)d.k;
+  switch (d.mode) {
+    case 0: {   // (O, I, k) tap t -> [O][I]
+      const uint32_t oi = l / k, j = l - oi * k;
+      return j == (uint32_t)d.tap ? (int64_t)oi : -1;
+    }
+    case 1: {   // (O, I, 3) -> [O][3 I], col j I + i
+      const uint32_t oi = l / 3u, j = l - oi * 3u, o = oi / I, i = oi - o * I;
+      return (int64_t)o * 3 * I + (int64_t)j * I + i;
+    }
+    case 2: {   // (O, I, 3) -> [3 O][I], row j O + o
+      const uint32_t oi = l / 3u, j = l - oi * 3u, o = oi / I, i = oi - o * I;
+      return ((int64_t)j * O + o) * I + i;
+    }
+    case 3: {   // convT (I_in, O, k) -> [k O][I_in], row j O + o
+      const uint32_t io = l / k, j = l - io * k, i = io / O, o = io - i * O;
+      return ((int64_t)j * O + o) * I + i;
+    }
+    case 4: {   // (O, 1, k) -> [O][ldo] (the zero padding columns are never touched)
+      const uint32_t o = l / k, j = l - o * k;
+      return (int64_t)o * d.ldo + j;
+    }
+    case 5:
+      return (int64_t)l;
+    case 6: {   // (O, I, k) tap t -> K-step-major [I / 32][O][32]
+      const uint32_t oi = l / k, j = l - oi * k;
+      if (j != (uint32_t)d.tap) return -1;
+      const uint32_t o = oi / I, i = oi - o * I;
+      return ((int64_t)(i >> 5) * O + o) * 32 + (i & 31);
+    }
+    default:
+      return -1;
+  }
+}
+
+__device__ __forceinline__ void op_store(const aw_operand_desc& d, uint32_t l, float v) {
+  const int64_t t = op_dst(d, l);
+  if (t < 0) return;
+  if (d.dtype == AW_BF16)
+    reinterpret_cast<bf16*>(d.out)[t] = (bf16)v;
+  else
+    reinterpret_cast<float*>(d.out)[t] = v;
+}
+
+// radam_kernel that also refreshes the operand copies of every updated element (up to AW_OPS_PER_SEG per segment,
+// ops[AW_OPS_PER_SEG * s + j], mode < 0 = unused): the per-step relayout launch of the forward disappears and the
+// updated weights are cast while still in registers.
+__global__ __launch_bounds__(256) void radam_ops_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                        float* __restrict__ m, float* __restrict__ v,
+                                                        const int64_t* __restrict__ seg_off,
+                                                        const int64_t* __restrict__ seg_len,
+                                                        const float* __restrict__ seg_wd,
+                                                        const int* __restrict__ seg_active, int nseg, int64_t total,
+                                                        RAdamScalars S, const float* __restrict__ gscale,
+                                                        const int64_t* __restrict__ step_ptr,
+                                                        const aw_operand_desc* __restrict__ ops) {
+  __shared__ int64_t s_off[MAXSEG_LDS];
+  __shared__ RAdamScalars s_S;
+  for (int i = threadIdx.x; i < nseg; i += blockDim.x) s_off[i] = seg_off[i];
+  if (step_ptr && threadIdx.x == 0) s_S = radam_scalars(*step_ptr, S.lr, S.beta1, S.beta2, S.eps);
+  __syncthreads();
+  if (step_ptr) S = s_S;
+  const float gs = gscale ? gscale[0] : 1.0f;
+  const int64_t n4 = total >> 2;
+  int s = 0;
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n4; q += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t e = q << 2;
+    s = next_seg(s_off, nseg, s, e);
+    const int64_t len = seg_len[s];
+    if (e >= s_off[s] + len || !seg_active[s]) continue;
+    const float wd = seg_wd[s];
+    const float4 g4 = reinterpret_cast<const float4*>(g)[q];
+    float4 p4 = reinterpret_cast<const float4*>(p)[q];
+    float4 m4 = reinterpret_cast<const float4*>(m)[q];
+    float4 v4 = reinterpret_cast<const float4*>(v)[q];
+    radam_one(g4.x, p4.x, m4.x, v4.x, wd, gs, S);
+    radam_one(g4.y, p4.y, m4.y, v4.y, wd, gs, S);
+    radam_one(g4.z, p4.z, m4.z, v4.z, wd, gs, S);
+    radam_one(g4.w, p4.w, m4.w, v4.w, wd, gs, S);
+    reinterpret_cast<float4*>(p)[q] = p4;
+    reinterpret_cast<float4*>(m)[q] = m4;
+    reinterpret_cast<float4*>(v)[q] = v4;
+    const uint32_t l0 = (uint32_t)(e - s_off[s]);
+    const float pv[4] = {p4.x, p4.y, p4.z, p4.w};
+#pragma unroll
+    for (int j = 0; j < AW_OPS_PER_SEG; ++j) {
+      const aw_operand_desc d = ops[AW_OPS_PER_SEG * s + j];
+      if (d.mode < 0) continue;
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        if ((int64_t)l0 + c < len) op_store(d, l0 + c, pv[c]);   // past seg_len: alignment padding
+    }
+  }
+}
+
 // Sum of squares of the active segments over the flat buffer (float4 grid-stride as radam_kernel).
 __global__ __launch_bounds__(256) void sumsq_kernel(const float* __restrict__ g, const int64_t* __restrict__ seg_off,
                                                     const int64_t* __restrict__ seg_len,
@@ -188,6 +286,29 @@ extern "C" int aw_radam_step(float* param, const float* grad, float* exp_avg, fl
   hipLaunchKernelGGL(radam_kernel, dim3((int)g), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), param, grad,
                      exp_avg, exp_avg_sq, seg_off, seg_len, seg_wd, seg_active, nseg, total, S, gscale, step_ptr);
   return aw::check_launch("aw_radam_step");
+}
+
+extern "C" int aw_radam_step_ops(float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
+                                 const int64_t* seg_off, const int64_t* seg_len, const float* seg_wd,
+                                 const int* seg_active, int nseg, int64_t total, int64_t step, float lr, float beta1,
+                                 float beta2, float eps, const float* gscale, const int64_t* step_ptr,
+                                 const aw_operand_desc* ops, void* stream) {
+  AW_REQUIRE(param && grad && exp_avg && exp_avg_sq && seg_off && seg_len && seg_wd && seg_active && ops,
+             "aw_radam_step_ops: null pointer");
+  AW_REQUIRE(nseg > 0 && nseg <= MAXSEG_LDS, "aw_radam_step_ops: nseg must be in [1, %d]", MAXSEG_LDS);
+  AW_REQUIRE((step_ptr || step >= 1) && total >= 0, "aw_radam_step_ops: step counts from 1");
+  AW_REQUIRE(total % 4 == 0 && ((uintptr_t)param & 15) == 0 && ((uintptr_t)grad & 15) == 0 &&
+                 ((uintptr_t)exp_avg & 15) == 0 && ((uintptr_t)exp_avg_sq & 15) == 0,
+             "aw_radam_step_ops: flat buffers must be 16-B aligned with total %% 4 == 0");
+  const RAdamScalars S = radam_scalars(step_ptr ? 1 : step, lr, beta1, beta2, eps);
+  if (total == 0) return AW_OK;
+  int64_t g = (total / 4 + 255) / 256;
+  if (g > 4096) g = 4096;
+  if (g < 1) g = 1;
+  hipLaunchKernelGGL(radam_ops_kernel, dim3((int)g), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), param,
+                     grad, exp_avg, exp_avg_sq, seg_off, seg_len, seg_wd, seg_active, nseg, total, S, gscale, step_ptr,
+                     ops);
+  return aw::check_launch("aw_radam_step_ops");
 }
 
 extern "C" int aw_counter_add(int64_t* counter, int64_t v, void* stream) {

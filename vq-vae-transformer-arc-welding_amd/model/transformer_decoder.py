@@ -157,6 +157,11 @@ class MyTransformerDecoder(LightningModule):
             self.log_classification_results(loss, logits, batch[1], "train")
         return loss
 
+    def operand_set(self):
+        """The persistent GEMM operand copies of the training step (arcweld.operands), for the optimizer to keep
+        current (arcweld.optim.RAdam.attach_operands)."""
+        return engine.operand_set(self)
+
     def backward_late_parameters(self):
         """Parameters whose gradients are final at fused_train_step's mid_hook (the task head, ln_f, the later half
         of the blocks): a data-parallel step all-reduces them while the earlier blocks' backward runs."""

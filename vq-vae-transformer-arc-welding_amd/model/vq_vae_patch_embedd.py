@@ -284,6 +284,11 @@ class VQVAEPatch(Autoencoder):
         self.last_recon = (x[:1], x_hat[:1])
         return loss
 
+    def operand_set(self):
+        """The persistent GEMM operand copies of the training step (arcweld.operands), for the optimizer to keep
+        current (arcweld.optim.RAdam.attach_operands)."""
+        return engine.operand_set(self)
+
     def centre_tap_parameters(self):
         """The encoder ResBlock conv weights: k = 3, pad = 1 convs applied per token to length-1 inputs
         (vq_vae_patch_embedd.py:93-114, loop :108-110), so only weight[:, :, 1] is used and the side taps receive
