@@ -18,7 +18,10 @@ XCDS = 8
 
 
 def family(name):
-    n = re.sub(r"\(.*", "", name)
+    """Kernel name without its argument list (and without the '(anonymous namespace)::' qualifier, whose own
+    parenthesis would otherwise cut the whole name)."""
+    n = name.replace("(anonymous namespace)::", "")
+    n = re.sub(r"\(.*", "", n)
     n = re.sub(r"^void ", "", n)
     return n[:140]
 
