@@ -270,10 +270,12 @@ int aw_mse_finalize(const double* sqerr, int64_t numel, float* out, void* stream
  * multiple of 4 elements) must be zero in all four buffers and stays zero (same for aw_grad_norm_clip's grad).
  * scalars come from host (step count, lr, betas, eps); `gscale` is a device scalar multiplying the gradient
  * first (clip coefficient; NULL = 1). */
-int aw_radam_step(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, const int64_t* seg_off,
+int aw_radam_step(float* param, float* grad, float* exp_avg, float* exp_avg_sq, const int64_t* seg_off,
                   const int64_t* seg_len, const float* seg_wd, const int* seg_active, int nseg, int64_t total, int64_t step,
                   float lr, float beta1, float beta2, float eps, const float* gscale, const int64_t* step_ptr,
-                  void* stream);
+                  int zero_grad, void* stream);
+/* zero_grad != 0: the gradient of every updated element is zeroed after use (optimizer.zero_grad() fused into the
+ * update; inactive segments are left as they are). */
 /* aw_radam_step that also writes the operand copies of the updated weights (what aw_weight_relayout_batch would
  * produce from the new values), so the training step needs no relayout launch.  ops: device array of
  * AW_OPS_PER_SEG descriptors per segment (ops[AW_OPS_PER_SEG*s + j]; mode -1 = none): flat element l of segment s
@@ -285,14 +287,16 @@ typedef struct {
   int O, I, k, tap, mode, dtype;
   int64_t ldo;
 } aw_operand_desc;
-int aw_radam_step_ops(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, const int64_t* seg_off,
+int aw_radam_step_ops(float* param, float* grad, float* exp_avg, float* exp_avg_sq, const int64_t* seg_off,
                       const int64_t* seg_len, const float* seg_wd, const int* seg_active, int nseg, int64_t total,
                       int64_t step, float lr, float beta1, float beta2, float eps, const float* gscale,
-                      const int64_t* step_ptr, const aw_operand_desc* ops, void* stream);
+                      const int64_t* step_ptr, const aw_operand_desc* ops, int zero_grad, void* stream);
 /* Device step counter / RNG counter: *counter += v (one thread; graph-capture safe).  With step_ptr != NULL,
  * aw_radam_step reads the step number from the device (the host `step` is ignored) and derives the bias
  * corrections and rectification there, in double precision like torch's python-float scalars. */
 int aw_counter_add(int64_t* counter, int64_t v, void* stream);
+/* The same, also copying the new value to *snapshot (the per-forward dropout seed the backward re-reads). */
+int aw_counter_add_snapshot(int64_t* counter, int64_t v, int64_t* snapshot, void* stream);
 /* Global L2 norm of the active segments of `grad` -> out_norm (f32 device scalar) and the clip coefficient
  * min(max_norm/(norm+1e-6), 1) -> out_coef (Lightning gradient_clip_val -> clip_grad_norm_).
  * ws: f64[AW_NORM_WS] scratch (per-workgroup partial sums, reduced in a fixed order: the norm is deterministic). */

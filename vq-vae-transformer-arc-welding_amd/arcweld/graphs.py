@@ -47,6 +47,9 @@ class StepGraphs:
 
     def _capture(self, batch):
         self.static = _clone_static(batch)
+        if hasattr(self.model, "_loss_scale_tensor"):       # persistent scalars are made outside the capture
+            dev = next(self.model.parameters()).device
+            self.model._loss_scale_tensor(float(self.scale), dev)
         torch.cuda.synchronize()
         pool = torch.cuda.graph_pool_handle()
         self.g2 = torch.cuda.CUDAGraph()

@@ -290,15 +290,21 @@ def mse_finalize(sqerr, numel, out, stream=None):
 
 # ------------------------------------------------------------------------------------------ optimizer
 def radam_step(param, grad, m, v, seg_off, seg_len, seg_wd, seg_active, nseg, total, step, lr, beta1, beta2, eps,
-               gscale=None, stream=None, step_ptr=None, ops=None):
+               gscale=None, stream=None, step_ptr=None, ops=None, zero_grad=False):
     """aw_radam_step, or aw_radam_step_ops when `ops` (device table of aw_operand_desc, AW_OPS_PER_SEG per
-    segment) is given: the update also writes the operand copies of the updated weights."""
+    segment) is given: the update also writes the operand copies of the updated weights.  zero_grad: the updated
+    elements' gradients are zeroed in the same pass."""
     args = (ptr(param), ptr(grad), ptr(m), ptr(v), ptr(seg_off), ptr(seg_len), ptr(seg_wd), ptr(seg_active), int(nseg),
             int(total), int(step), float(lr), float(beta1), float(beta2), float(eps), ptr(gscale), ptr(step_ptr))
     if ops is None:
-        call("aw_radam_step", *args, stream_ptr(stream))
+        call("aw_radam_step", *args, int(bool(zero_grad)), stream_ptr(stream))
     else:
-        call("aw_radam_step_ops", *args, ptr(ops), stream_ptr(stream))
+        call("aw_radam_step_ops", *args, ptr(ops), int(bool(zero_grad)), stream_ptr(stream))
+
+
+def counter_add_snapshot(counter, snapshot, v=1, stream=None):
+    """counter += v and snapshot = the new value, in one launch."""
+    call("aw_counter_add_snapshot", ptr(counter), int(v), ptr(snapshot), stream_ptr(stream))
 
 
 def counter_add(counter, v=1, stream=None):

@@ -29,6 +29,7 @@ class RAdam(torch.optim.Optimizer):
         self._step_count = 0
         self._coef = None
         self._pending_active = None
+        self._grads_zeroed = False
 
     # ------------------------------------------------------------------ flat layout
     def declare_centre_tap(self, params):
@@ -120,6 +121,7 @@ class RAdam(torch.optim.Optimizer):
             self._pending_active = params
             return
         F = self._flat
+        self._grads_zeroed = False       # the fused zeroing covered the previous active set only
         keep = None if params is None else set(id(p) for p in params)
         act = [1 if keep is None or id(s[0]) in keep else 0 for s in F["segs"]]
         dev = F["p"].device
@@ -223,6 +225,10 @@ class RAdam(torch.optim.Optimizer):
                 for p in g["params"]:
                     p.grad = None
             return
+        if self._grads_zeroed:
+            # the last step(zero_grad=True) zeroed every active segment; inactive ones carry no gradient
+            self._grads_zeroed = False
+            return
         g = self._flat["g"]
         for a, b in self._flat["spans"]:
             g[a:b].zero_()
@@ -238,7 +244,9 @@ class RAdam(torch.optim.Optimizer):
         return F["norm"]
 
     @torch.no_grad()
-    def step(self, closure=None):
+    def step(self, closure=None, zero_grad=False):
+        """torch.optim.RAdam.step; zero_grad=True also zeroes the gradients of the updated (active) segments in the
+        same kernel pass, and the next zero_grad() call is then free (the Trainer's step + zero_grad pair)."""
         loss = None
         if closure is not None:
             with torch.enable_grad():
@@ -253,8 +261,9 @@ class RAdam(torch.optim.Optimizer):
         for (lr, (b1, b2), eps), act in self._launch_groups():
             K.radam_step(F["p"], F["g"], F["m"], F["v"], F["off_d"], F["len_d"], F["wd_d"], act, len(F["segs"]),
                          F["total"], self._step_count, lr, b1, b2, eps, gscale=self._coef, step_ptr=F["step"],
-                         ops=F.get("ops_d"))
+                         ops=F.get("ops_d"), zero_grad=zero_grad)
         self._coef = None
+        self._grads_zeroed = bool(zero_grad)
         return loss
 
     def _launch_groups(self):

@@ -131,7 +131,10 @@ class Trainer:
         opt = self.optimizer
         if self.gradient_clip_val:
             opt.clip_grad_norm_(float(self.gradient_clip_val))
-        opt.step()
+        if hasattr(opt, "attach_operands"):     # arcweld RAdam: zero_grad fused into the update pass
+            opt.step(zero_grad=True)
+        else:
+            opt.step()
         opt.zero_grad()
 
     def world(self):

@@ -45,8 +45,24 @@ def rng_snapshot(m, dev, p_drop):
     if ctr is None or ctr.device != dev:
         ctr = torch.zeros(1, dtype=torch.int64, device=dev)
         m._rng_counter = ctr
-    K.counter_add(ctr, 1)
-    return ctr.clone()
+    snap = torch.empty(1, dtype=torch.int64, device=dev)
+    K.counter_add_snapshot(ctr, snap)      # advance and snapshot in one launch
+    return snap
+
+
+def accumulators(m, dev, K, H):
+    """Zeroed device accumulators of one forward, carved from one persistent block with ONE fill launch: VQ sqerr
+    (f64), MSE sqerr (f64, fused_train_step), BN column statistics (2H f64) and the VQ code counts (K f32).  Each is
+    consumed inside the call that filled it (never across a forward/backward boundary)."""
+    key = (dev, K, H)
+    st = m.__dict__.get("_acc_block")
+    if st is None or st[0] != key:
+        st = (key, torch.empty(2 + 4 * H + (K + 1) // 2, dtype=torch.float64, device=dev))
+        m.__dict__["_acc_block"] = st
+    buf = st[1]
+    buf.zero_()
+    return dict(vq_sq=buf[0:1], mse_sq=buf[1:2], colstats=buf[2:2 + 2 * H], head_gsums=buf[2 + 2 * H:2 + 4 * H],
+                counts=buf[2 + 4 * H:].view(torch.float32)[:K])
 
 
 class VQVAEShapes:
@@ -232,6 +248,13 @@ def forward(m, x, training: bool, need_backward: bool, dtype=None, seed: int = 0
     sv.enc_seed = [_mix(seed, 100 + r) for r in range(R)]
     sv.dec_seed = [_mix(seed, 200 + r) for r in range(R)]
     sv.ctr = rng_snapshot(m, dev, p_drop)
+    acc = accumulators(m, dev, sh.K, H)
+    sv.acc = acc
+    # the head-backward sums of the block are this forward's only while no other forward awaits its backward
+    pending = m.__dict__.get("_acc_pending", 0)
+    sv.head_gsums = acc["head_gsums"] if pending == 0 else torch.zeros(2 * H, device=dev, dtype=torch.float64)
+    if need_backward:
+        m.__dict__["_acc_pending"] = pending + 1
 
     # ---- operand copies of the weights (relayout + cast): persistent, refreshed by one batched relayout only when
     #      a weight changed outside the optimizer (the flat RAdam rewrites them in its update kernel)
@@ -302,8 +325,7 @@ def forward(m, x, training: bool, need_backward: bool, dtype=None, seed: int = 0
     else:
         zq = e(N, D)
         idx = e(N, dt=torch.int64)
-        counts = torch.zeros(Kc, device=dev)
-        sq = torch.zeros(1, device=dev, dtype=torch.float64)
+        counts, sq = acc["counts"], acc["vq_sq"]
         K.vq_forward(z, pr["E"], zq, idx, counts, sq)
         emb_loss, perplexity = e(()), e(())
         K.vq_finalize(counts, sq, N, Kc, D, m.vector_quantization.beta, emb_loss, perplexity)
@@ -344,7 +366,7 @@ def forward(m, x, training: bool, need_backward: bool, dtype=None, seed: int = 0
     # ---- un-patch: ConvT(H->H, k1) with BN statistics in the epilogue, then the fused head
     bn = pr["bn"]
     Y = e(N, k1 * H)
-    colstats = torch.zeros(2 * H, device=dev, dtype=torch.float64) if training else None
+    colstats = acc["colstats"] if training else None
     K.gemm(yR_T, Wt1, N, k1 * H, H, bias=pr["t1"].bias, bias_mod=H, C=Y, colstats=colstats, stats_mod=H)
     stats = e(4 * H)
     K.bn_finalize(colstats, N * k1, H, bn.weight, bn.bias, bn.running_mean if training else bn.running_mean,
@@ -442,7 +464,8 @@ def backward(m, sv, g_emb, g_xhat, slot, mid_hook=None):
     bn = pr["bn"]
 
     # ---- head + BN backward
-    gsums = torch.zeros(2 * H, device=dev, dtype=torch.float64)
+    gsums = sv.head_gsums
+    m.__dict__["_acc_pending"] = max(0, m.__dict__.get("_acc_pending", 1) - 1)
     K.unpatch_head_bwd1(sv.Y2, sh.Q, sv.stats, pr["t2"].weight.view(H, 5), g_xhat, gsums,
                         slot(pr["t2"].weight).view(H, 5), slot(pr["t2"].bias), slot(bn.weight), slot(bn.bias))
     gY = e(N * k1, H, dt=T)

@@ -34,7 +34,11 @@ __host__ __device__ inline RAdamScalars radam_scalars(int64_t step, float lr, fl
   return S;
 }
 
-__global__ void counter_add_kernel(int64_t* c, int64_t v) { c[0] += v; }
+__global__ void counter_add_kernel(int64_t* c, int64_t v, int64_t* snap) {
+  const int64_t n = c[0] + v;
+  c[0] = n;
+  if (snap) snap[0] = n;
+}
 
 __device__ __forceinline__ int find_seg(const int64_t* off, int nseg, int64_t e) {
   int lo = 0, hi = nseg - 1;
@@ -71,14 +75,14 @@ __device__ __forceinline__ float radam_one(float gr, float& pv, float& mv, float
 
 // float4 grid-stride over the flat buffers (segments are 256-B aligned: a float4 never straddles two; the
 // alignment padding past seg_len is zero in p, g, m and v and stays zero).
-__global__ __launch_bounds__(256) void radam_kernel(float* __restrict__ p, const float* __restrict__ g,
+__global__ __launch_bounds__(256) void radam_kernel(float* __restrict__ p, float* __restrict__ g,
                                                     float* __restrict__ m, float* __restrict__ v,
                                                     const int64_t* __restrict__ seg_off,
                                                     const int64_t* __restrict__ seg_len,
                                                     const float* __restrict__ seg_wd, const int* __restrict__ seg_active,
                                                     int nseg, int64_t total, RAdamScalars S,
                                                     const float* __restrict__ gscale,
-                                                    const int64_t* __restrict__ step_ptr) {
+                                                    const int64_t* __restrict__ step_ptr, int zero_g) {
   __shared__ int64_t s_off[MAXSEG_LDS];
   __shared__ RAdamScalars s_S;
   for (int i = threadIdx.x; i < nseg; i += blockDim.x) s_off[i] = seg_off[i];
@@ -104,6 +108,7 @@ __global__ __launch_bounds__(256) void radam_kernel(float* __restrict__ p, const
     reinterpret_cast<float4*>(p)[q] = p4;
     reinterpret_cast<float4*>(m)[q] = m4;
     reinterpret_cast<float4*>(v)[q] = v4;
+    if (zero_g) reinterpret_cast<float4*>(g)[q] = make_float4(0.f, 0.f, 0.f, 0.f);   // zero_grad, fused
   }
 }
 
@@ -157,7 +162,7 @@ __device__ __forceinline__ void op_store(const aw_operand_desc& d, uint32_t l, f
 // radam_kernel that also refreshes the operand copies of every updated element (up to AW_OPS_PER_SEG per segment,
 // ops[AW_OPS_PER_SEG * s + j], mode < 0 = unused): the per-step relayout launch of the forward disappears and the
 // updated weights are cast while still in registers.
-__global__ __launch_bounds__(256) void radam_ops_kernel(float* __restrict__ p, const float* __restrict__ g,
+__global__ __launch_bounds__(256) void radam_ops_kernel(float* __restrict__ p, float* __restrict__ g,
                                                         float* __restrict__ m, float* __restrict__ v,
                                                         const int64_t* __restrict__ seg_off,
                                                         const int64_t* __restrict__ seg_len,
@@ -165,7 +170,7 @@ __global__ __launch_bounds__(256) void radam_ops_kernel(float* __restrict__ p, c
                                                         const int* __restrict__ seg_active, int nseg, int64_t total,
                                                         RAdamScalars S, const float* __restrict__ gscale,
                                                         const int64_t* __restrict__ step_ptr,
-                                                        const aw_operand_desc* __restrict__ ops) {
+                                                        const aw_operand_desc* __restrict__ ops, int zero_g) {
   __shared__ int64_t s_off[MAXSEG_LDS];
   __shared__ RAdamScalars s_S;
   for (int i = threadIdx.x; i < nseg; i += blockDim.x) s_off[i] = seg_off[i];
@@ -192,6 +197,7 @@ __global__ __launch_bounds__(256) void radam_ops_kernel(float* __restrict__ p, c
     reinterpret_cast<float4*>(p)[q] = p4;
     reinterpret_cast<float4*>(m)[q] = m4;
     reinterpret_cast<float4*>(v)[q] = v4;
+    if (zero_g) reinterpret_cast<float4*>(g)[q] = make_float4(0.f, 0.f, 0.f, 0.f);   // zero_grad, fused
     const uint32_t l0 = (uint32_t)(e - s_off[s]);
     const float pv[4] = {p4.x, p4.y, p4.z, p4.w};
 #pragma unroll
@@ -265,10 +271,10 @@ __global__ void scale_kernel(float* x, int64_t n, const float* s) {
 
 }  // namespace
 
-extern "C" int aw_radam_step(float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
+extern "C" int aw_radam_step(float* param, float* grad, float* exp_avg, float* exp_avg_sq,
                              const int64_t* seg_off, const int64_t* seg_len, const float* seg_wd, const int* seg_active,
                              int nseg, int64_t total, int64_t step, float lr, float beta1, float beta2, float eps,
-                             const float* gscale, const int64_t* step_ptr, void* stream) {
+                             const float* gscale, const int64_t* step_ptr, int zero_grad, void* stream) {
   AW_REQUIRE(param && grad && exp_avg && exp_avg_sq && seg_off && seg_len && seg_wd && seg_active,
              "aw_radam_step: null pointer");
   AW_REQUIRE(nseg > 0 && nseg <= MAXSEG_LDS, "aw_radam_step: nseg must be in [1, %d]", MAXSEG_LDS);
@@ -284,15 +290,16 @@ extern "C" int aw_radam_step(float* param, const float* grad, float* exp_avg, fl
   if (g > 4096) g = 4096;
   if (g < 1) g = 1;
   hipLaunchKernelGGL(radam_kernel, dim3((int)g), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), param, grad,
-                     exp_avg, exp_avg_sq, seg_off, seg_len, seg_wd, seg_active, nseg, total, S, gscale, step_ptr);
+                     exp_avg, exp_avg_sq, seg_off, seg_len, seg_wd, seg_active, nseg, total, S, gscale, step_ptr,
+                     zero_grad);
   return aw::check_launch("aw_radam_step");
 }
 
-extern "C" int aw_radam_step_ops(float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
+extern "C" int aw_radam_step_ops(float* param, float* grad, float* exp_avg, float* exp_avg_sq,
                                  const int64_t* seg_off, const int64_t* seg_len, const float* seg_wd,
                                  const int* seg_active, int nseg, int64_t total, int64_t step, float lr, float beta1,
                                  float beta2, float eps, const float* gscale, const int64_t* step_ptr,
-                                 const aw_operand_desc* ops, void* stream) {
+                                 const aw_operand_desc* ops, int zero_grad, void* stream) {
   AW_REQUIRE(param && grad && exp_avg && exp_avg_sq && seg_off && seg_len && seg_wd && seg_active && ops,
              "aw_radam_step_ops: null pointer");
   AW_REQUIRE(nseg > 0 && nseg <= MAXSEG_LDS, "aw_radam_step_ops: nseg must be in [1, %d]", MAXSEG_LDS);
@@ -307,14 +314,22 @@ extern "C" int aw_radam_step_ops(float* param, const float* grad, float* exp_avg
   if (g < 1) g = 1;
   hipLaunchKernelGGL(radam_ops_kernel, dim3((int)g), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), param,
                      grad, exp_avg, exp_avg_sq, seg_off, seg_len, seg_wd, seg_active, nseg, total, S, gscale, step_ptr,
-                     ops);
+                     ops, zero_grad);
   return aw::check_launch("aw_radam_step_ops");
 }
 
 extern "C" int aw_counter_add(int64_t* counter, int64_t v, void* stream) {
   AW_REQUIRE(counter, "aw_counter_add: null counter");
-  hipLaunchKernelGGL(counter_add_kernel, dim3(1), dim3(1), 0, reinterpret_cast<hipStream_t>(stream), counter, v);
+  hipLaunchKernelGGL(counter_add_kernel, dim3(1), dim3(1), 0, reinterpret_cast<hipStream_t>(stream), counter, v,
+                     nullptr);
   return aw::check_launch("aw_counter_add");
+}
+
+extern "C" int aw_counter_add_snapshot(int64_t* counter, int64_t v, int64_t* snapshot, void* stream) {
+  AW_REQUIRE(counter && snapshot, "aw_counter_add_snapshot: null pointer");
+  hipLaunchKernelGGL(counter_add_kernel, dim3(1), dim3(1), 0, reinterpret_cast<hipStream_t>(stream), counter, v,
+                     snapshot);
+  return aw::check_launch("aw_counter_add_snapshot");
 }
 
 extern "C" int aw_grad_norm_clip(const float* grad, const int64_t* seg_off, const int64_t* seg_len,

@@ -260,13 +260,13 @@ class VQVAEPatch(Autoencoder):
         x = x.contiguous()
         emb, x_hat, perp, idx, sv = engine.forward(self, x, self.training, need_backward=True, seed=self._next_seed())
         self._last_indices = idx
-        sq = torch.zeros(1, device=x.device, dtype=torch.float64)
+        sq = sv.acc["mse_sq"]            # zeroed with the forward's other accumulators (one fill launch)
         K.mse_fwd(x_hat, x, sq)
         recon = torch.empty((), device=x.device)
         K.mse_finalize(sq, x.numel(), recon)
         loss = torch.empty((), device=x.device)
         K.scalar_add(recon.reshape(1), emb.reshape(1), loss)
-        g = torch.full((1,), float(scale), device=x.device)
+        g = self._loss_scale_tensor(float(scale), x.device)
         g_xhat = torch.empty_like(x_hat)
         K.mse_bwd(x_hat, x, g, g_xhat)
         sink = getattr(self, "_grad_sink", None)
@@ -283,6 +283,14 @@ class VQVAEPatch(Autoencoder):
         self.log('train/recon_error', recon)
         self.last_recon = (x[:1], x_hat[:1])
         return loss
+
+    def _loss_scale_tensor(self, scale, dev):
+        """Persistent device scalar holding the loss scale (refilled only when the value changes)."""
+        st = self.__dict__.get("_gscale")
+        if st is None or st[0] != scale or st[1].device != dev:
+            st = (scale, torch.full((1,), scale, device=dev))
+            self.__dict__["_gscale"] = st
+        return st[1]
 
     def operand_set(self):
         """The persistent GEMM operand copies of the training step (arcweld.operands), for the optimizer to keep
