@@ -247,3 +247,49 @@ def test_improved_vq_trains_graphed_and_tokenizes():
         torch.testing.assert_close(s1[k].float(), s0[k].float(), rtol=1e-4, atol=1e-5, msg=k)
     ids = m1.eval().encode_ids(xs[0])
     assert ids.shape == (16, 16) and int(ids.max()) < 64
+
+
+def _rvq_dp_worker(rank, world, port, z, init_rows, out):
+    import os
+    import torch.distributed as dist
+    from arcweld.residual_vq import ResidualVQ
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        rvq = ResidualVQ(1, 32, 64, kmeans_init=True, kmeans_iters=3, threshold_ema_dead_code=2).cuda().train()
+        rvq.layers[0]._codebook.init_rows = torch.tensor(init_rows)      # rank 0's rows seed the broadcast means
+        n = z.shape[0] // world
+        half = torch.tensor(z[rank * n:(rank + 1) * n], device="cuda")
+        for _ in range(3):
+            rvq.quantize_rows(half, True)
+        torch.cuda.synchronize()
+        c = rvq.layers[0]._codebook
+        out[rank] = {k: getattr(c, k).cpu().clone() for k in ("embed", "embed_avg", "cluster_size")}
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_residual_vq_data_parallel_world2_matches_full_batch():
+    """Data parallel (two ranks over gloo sharing cuda:0): k-means and the EMA all-reduce bins and per-code sums, so
+    both ranks hold the codebook a single process gets from the whole batch."""
+    import socket
+    import torch.multiprocessing as mp
+    from arcweld.residual_vq import ResidualVQ
+    z, l1, _, _, _ = _clustered(1, seed=7)
+    init = np.array([np.flatnonzero(l1[:2048] == c)[0] for c in range(64)])     # rows of rank 0's half
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    out = mp.Manager().dict()
+    mp.spawn(_rvq_dp_worker, args=(2, port, z, init, out), nprocs=2, join=True)
+    ref = ResidualVQ(1, 32, 64, kmeans_init=True, kmeans_iters=3, threshold_ema_dead_code=2).cuda().train()
+    ref.layers[0]._codebook.init_rows = torch.tensor(init)
+    full = torch.tensor(z, device="cuda")
+    for _ in range(3):
+        ref.quantize_rows(full, True)
+    c = ref.layers[0]._codebook
+    for k in ("embed", "embed_avg", "cluster_size"):
+        torch.testing.assert_close(out[0][k], out[1][k], rtol=0, atol=0, msg=k)
+        torch.testing.assert_close(out[0][k], getattr(c, k).cpu(), rtol=1e-5, atol=1e-5, msg=k)
