@@ -2,6 +2,8 @@
 // for gfx950: LayerNorm, token+position embedding, causal attention (flash-style: the T x T score matrix is
 // never materialised, softmax statistics are kept per query row and the backward recomputes P from the
 // saved log-sum-exp), and cross-entropy with ignore_index.
+#include <stdlib.h>
+
 #include "common.h"
 
 namespace aw {  // attention.hip: MFMA path for bf16, head size 64
@@ -737,7 +739,11 @@ extern "C" int aw_layernorm_bwd(const float* x, const float* dy, int64_t R, int 
              "aw_layernorm_bwd: bad args");
   if (R == 0) return AW_OK;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  dim3 grid(gridcap(R * 64, 256, 512));
+  // workgroups of the row walk (AW_LN_BWD_BLOCKS: tuning override); each ends with one atomic per dw / db column,
+  // so more workgroups contend on those 2D addresses: 256 measured best at 16371 x 512 (29.4 us, 5.1 TB/s; 512:
+  // 32.5 us, 1024: 40.1 us; tools/probe/ln_probe.py)
+  static const int cap = [] { const char* e = getenv("AW_LN_BWD_BLOCKS"); return e ? atoi(e) : 256; }();
+  dim3 grid(gridcap(R * 64, 256, cap));
 #define AW_LNB(NV)                                                                                               \
   if (dx2_dtype == AW_BF16)                                                                                      \
     hipLaunchKernelGGL((ln_bwd_vec_kernel<bf16, NV>), grid, dim3(256), 0, s, x, dy, R, D, w, mean, rstd, dx,      \
