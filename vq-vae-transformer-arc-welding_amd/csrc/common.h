@@ -63,6 +63,43 @@ __device__ __forceinline__ float gelu_erf_grad_fast(float x) {
   return aw_phi_cdf(x) + x * AW_INV_SQRT2PI * __expf(-0.5f * x * x);
 }
 
+// The same functions on a pair of values (the two channels a thread owns): the polynomial and the products run as
+// v_pk_fma_f32 / v_pk_mul_f32 (two values per instruction), only rcp / exp / the sign select stay scalar.  Same
+// operations in the same order per element as the scalar forms above (up to FMA contraction).
+__device__ __forceinline__ f32x2 aw_splat2(float c) { return (f32x2){c, c}; }
+__device__ __forceinline__ f32x2 aw_phi_cdf2(f32x2 x) {
+  const f32x2 z = (f32x2){fabsf(x.x), fabsf(x.y)} * aw_splat2(AW_INV_SQRT2);
+  const f32x2 d = __builtin_elementwise_fma(aw_splat2(0.5f), z, aw_splat2(1.0f));
+  const f32x2 t = {__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+  f32x2 p = aw_splat2(0.17087277f);
+  p = __builtin_elementwise_fma(p, t, aw_splat2(-0.82215223f));
+  p = __builtin_elementwise_fma(p, t, aw_splat2(1.48851587f));
+  p = __builtin_elementwise_fma(p, t, aw_splat2(-1.13520398f));
+  p = __builtin_elementwise_fma(p, t, aw_splat2(0.27886807f));
+  p = __builtin_elementwise_fma(p, t, aw_splat2(-0.18628806f));
+  p = __builtin_elementwise_fma(p, t, aw_splat2(0.09678418f));
+  p = __builtin_elementwise_fma(p, t, aw_splat2(0.37409196f));
+  p = __builtin_elementwise_fma(p, t, aw_splat2(1.00002368f));
+  p = __builtin_elementwise_fma(p, t, aw_splat2(-1.26551223f));
+  const f32x2 e = __builtin_elementwise_fma(-z, z, p);
+  const f32x2 r = aw_splat2(0.5f) * (t * (f32x2){__expf(e.x), __expf(e.y)});
+  const f32x2 q = aw_splat2(1.0f) - r;
+  return (f32x2){x.x >= 0.f ? q.x : r.x, x.y >= 0.f ? q.y : r.y};
+}
+__device__ __forceinline__ f32x2 gelu_erf_fast2(f32x2 x) { return x * aw_phi_cdf2(x); }
+// GELU and its derivative from one Phi evaluation
+__device__ __forceinline__ void gelu_erf_fast2_and_grad(f32x2 x, f32x2& g, f32x2& dg) {
+  const f32x2 phi = aw_phi_cdf2(x);
+  const f32x2 h = aw_splat2(-0.5f) * x * x;
+  g = x * phi;
+  dg = __builtin_elementwise_fma(x * aw_splat2(AW_INV_SQRT2PI), (f32x2){__expf(h.x), __expf(h.y)}, phi);
+}
+__device__ __forceinline__ f32x2 gelu_erf_grad_fast2(f32x2 x) {
+  f32x2 g, dg;
+  gelu_erf_fast2_and_grad(x, g, dg);
+  return dg;
+}
+
 // GELU tanh form (model/transformer_block.py:8-15): 0.5*x*(1 + tanh(u)) == x * sigmoid(2u), u = sqrt(2/pi)(x +
 // 0.044715 x^3) -- one exp and one division instead of tanhf (same value to fp32 rounding).
 #define AW_SQRT_2_OVER_PI 0.79788456080286535588f

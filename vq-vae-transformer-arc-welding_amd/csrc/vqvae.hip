@@ -216,31 +216,63 @@ __device__ __forceinline__ float pick5(const float (&v)[5], int lane) {
   return r;
 }
 
+// Sum over the wave into lane 63 with DPP adds (quad xor 1/2, row rotate 4/8, row_bcast 15/31): six VALU ops per
+// value, against six LDS-crossbar ds_bpermute round trips (plus their index math) for the shfl_xor butterfly.
+template <int CTRL, int ROWMASK = 0xF>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, ROWMASK, 0xF, false));
+}
+__device__ __forceinline__ float wave_sum_to_last(float v) {
+  v += dpp_f<0xB1>(v);         // quad_perm [1,0,3,2]
+  v += dpp_f<0x4E>(v);         // quad_perm [2,3,0,1]
+  v += dpp_f<0x124>(v);        // row_ror:4
+  v += dpp_f<0x128>(v);        // row_ror:8   -> every lane holds its 16-lane row sum
+  v += dpp_f<0x142, 0xA>(v);   // row_bcast:15 into rows 1, 3
+  v += dpp_f<0x143, 0xC>(v);   // row_bcast:31 into rows 2, 3 -> lane 63 holds the wave sum
+  return v;
+}
+
 template <int NS>
 __global__ __launch_bounds__(256) void head_fwd_kernel(const float* __restrict__ y, int64_t R, int H, int Q,
                                                        const float* __restrict__ st, const float* __restrict__ w2,
                                                        const float* __restrict__ b2, float* __restrict__ x_hat) {
   const int lane = threadIdx.x & 63;
-  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  // the row index is wave-uniform: kept in SGPRs, the y loads are SGPR base + lane offset
+  const int64_t wave = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6));
   const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
   HeadParams<NS> hp;
   hp.load(st, w2, H, lane);
+  // BN folded into one FMA per element: bn = v * A + B with A = inv * gam, B = bet - mean * A
+  float A[NS][4], B[NS][4];
+#pragma unroll
+  for (int s = 0; s < NS; ++s)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      A[s][e] = hp.inv[s][e] * hp.gam[s][e];
+      B[s][e] = fmaf(-hp.mean[s][e], A[s][e], hp.bet[s][e]);
+    }
   const float bias = b2[0];
-  // software pipeline: the next row's loads are in flight while this row is reduced (one row per wave and
-  // iteration left the loads latency-bound at ~2 TB/s)
-  float4 nv[NS];
-  auto load_row = [&](int64_t r) {
+  // software pipeline: the next FD rows' loads are in flight while this row is reduced (no look-ahead left the
+  // loads latency-bound at ~2 TB/s; FD 2 measured no better than 1 at 5 waves/SIMD)
+  constexpr int FD = 1;
+  float4 nv[FD][NS];
+  auto load_row = [&](int d, int64_t r) {
 #pragma unroll
     for (int s = 0; s < NS; ++s)
-      nv[s] = (hp.on[s] && r < R) ? *reinterpret_cast<const float4*>(y + r * H + lane * 4 + 256 * s)
-                                  : make_float4(0.f, 0.f, 0.f, 0.f);
+      nv[d][s] = (hp.on[s] && r < R) ? *reinterpret_cast<const float4*>(y + r * H + lane * 4 + 256 * s)
+                                     : make_float4(0.f, 0.f, 0.f, 0.f);
   };
-  load_row(wave);
-  for (int64_t r = wave; r < R; r += nw) {
+#pragma unroll
+  for (int d = 0; d < FD; ++d) load_row(d, wave + d * nw);
+  for (int64_t rb = wave; rb < R; rb += FD * nw)
+#pragma unroll
+  for (int d = 0; d < FD; ++d) {
+    const int64_t r = rb + d * nw;
     float4 v[NS];
 #pragma unroll
-    for (int s = 0; s < NS; ++s) v[s] = nv[s];
-    load_row(r + nw);
+    for (int s = 0; s < NS; ++s) v[s] = nv[d][s];
+    load_row(d, r + FD * nw);
+    if (r >= R) continue;    // wave-uniform
     float part[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
@@ -248,14 +280,17 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(const float* __restrict__
       const float vv[4] = {v[s].x, v[s].y, v[s].z, v[s].w};
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const float a = gelu_erf_fast((vv[e] - hp.mean[s][e]) * hp.inv[s][e] * hp.gam[s][e] + hp.bet[s][e]);
+        const float a = gelu_erf_fast(fmaf(vv[e], A[s][e], B[s][e]));
 #pragma unroll
         for (int j = 0; j < 5; ++j) part[j] = fmaf(a, hp.w[s][e][j], part[j]);
       }
     }
 #pragma unroll
-    for (int j = 0; j < 5; ++j) part[j] = wave_sum(part[j]);
-    if (lane < 5) x_hat[r * 5 + lane] = pick5(part, lane) + bias;   // row r = b*Q + q -> x_hat[b][5q + j]
+    for (int j = 0; j < 5; ++j) part[j] = wave_sum_to_last(part[j]);
+    if (lane == 63) {   // row r = b*Q + q -> x_hat[b][5q + j]
+#pragma unroll
+      for (int j = 0; j < 5; ++j) x_hat[r * 5 + j] = part[j] + bias;
+    }
   }
 }
 
@@ -444,21 +479,22 @@ __global__ __launch_bounds__(256) void head_bwd2_kernel(const float* __restrict_
 // threads with two channels each, so the per-thread state (BN parameters, ConvT2 taps, accumulators of two
 // channels) stays small enough for 1024-thread workgroups: 16 waves per workgroup keep y streaming at HBM rate
 // while the number of workgroups -- each ends with its per-channel global atomics -- stays at 512.
-struct Head2 {
-  float mean[2], inv[2], gam[2], bet[2], w[2][5];
+struct Head2 {   // the two channels c0, c0+1 of a thread as register pairs
+  f32x2 inv, c, gam, bet, w[5];   // c = -mean * inv: xn = v * inv + c in one packed FMA
   __device__ __forceinline__ void load(const float* st, const float* w2, int H, int c0) {
+    const f32x2 mean = {st[c0], st[c0 + 1]};
+    inv = (f32x2){st[H + c0], st[H + c0 + 1]};
+    gam = (f32x2){st[2 * H + c0], st[2 * H + c0 + 1]};
+    bet = (f32x2){st[3 * H + c0], st[3 * H + c0 + 1]};
+    c = -mean * inv;
 #pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      const int o = c0 + e;
-      mean[e] = st[o];
-      inv[e] = st[H + o];
-      gam[e] = st[2 * H + o];
-      bet[e] = st[3 * H + o];
-#pragma unroll
-      for (int j = 0; j < 5; ++j) w[e][j] = w2[o * 5 + j];
-    }
+    for (int j = 0; j < 5; ++j) w[j] = (f32x2){w2[c0 * 5 + j], w2[(c0 + 1) * 5 + j]};
   }
 };
+
+// Rows in flight per thread in the channel-split passes: each thread streams only 8 bytes of y per row, so one row
+// of look-ahead kept ~8 KB per CU in flight (1.9-3.3 TB/s); HEAD_CS_DEPTH rows are loaded ahead instead.
+constexpr int HEAD_CS_DEPTH = 2;
 
 __global__ __launch_bounds__(1024) void head_bwd1_cs_kernel(const float* __restrict__ y, int64_t R, int H, int Q,
                                                            const float* __restrict__ st, const float* __restrict__ w2,
@@ -472,48 +508,56 @@ __global__ __launch_bounds__(1024) void head_bwd1_cs_kernel(const float* __restr
   const int c0 = (threadIdx.x % tpr) * 2, rg = threadIdx.x / tpr;
   Head2 hp;
   hp.load(st, w2, H, c0);
-  float accw[2][5] = {}, accg[2] = {0.f, 0.f}, accgx[2] = {0.f, 0.f};
+  f32x2 accw[5], accg = aw_splat2(0.f), accgx = aw_splat2(0.f);
+#pragma unroll
+  for (int j = 0; j < 5; ++j) accw[j] = aw_splat2(0.f);
   float gbsum = 0.f;
   const int64_t step = (int64_t)gridDim.x * rpb;
-  float2 nv;
-  float ngo[5];
-  auto load_row = [&](int64_t r) {
+  constexpr int D = HEAD_CS_DEPTH;
+  float2 nv[D];
+  float ngo[D][5];
+  auto load_row = [&](int d, int64_t r) {   // rows past R load as zeros
     const bool in = r < R;
     const int64_t rr = in ? r : 0;
     const float* gp = gx + rr * 5;          // row r = b*Q + q -> g_xhat[b][5q + j]
 #pragma unroll
-    for (int j = 0; j < 5; ++j) ngo[j] = in ? gp[j] : 0.f;
-    nv = in ? *reinterpret_cast<const float2*>(y + rr * H + c0) : make_float2(0.f, 0.f);
+    for (int j = 0; j < 5; ++j) ngo[d][j] = in ? gp[j] : 0.f;
+    nv[d] = in ? *reinterpret_cast<const float2*>(y + rr * H + c0) : make_float2(0.f, 0.f);
   };
-  load_row((int64_t)blockIdx.x * rpb + rg);
-  for (int64_t r = (int64_t)blockIdx.x * rpb + rg; r < R; r += step) {
+  const int64_t r0 = (int64_t)blockIdx.x * rpb + rg;
+#pragma unroll
+  for (int d = 0; d < D; ++d) load_row(d, r0 + d * step);
+  for (int64_t rb = r0; rb < R; rb += D * step)
+#pragma unroll
+  for (int d = 0; d < D; ++d) {
+    const int64_t r = rb + d * step;
     float go[5];
 #pragma unroll
-    for (int j = 0; j < 5; ++j) go[j] = ngo[j];
-    const float vv[2] = {nv.x, nv.y};
-    load_row(r + step);
+    for (int j = 0; j < 5; ++j) go[j] = ngo[d][j];
+    const f32x2 v = {nv[d].x, nv[d].y};
+    load_row(d, r + D * step);
+    __builtin_amdgcn_sched_barrier(0);   // one row's math at a time: the unrolled rows must not interleave (spills)
+    // a row past R has g = 0 and y = 0: every accumulator below gains exactly zero from it
     if (c0 == 0) gbsum += go[0] + go[1] + go[2] + go[3] + go[4];
+    const f32x2 xn = __builtin_elementwise_fma(v, hp.inv, hp.c);
+    const f32x2 bn = __builtin_elementwise_fma(xn, hp.gam, hp.bet);
+    f32x2 a, dg;
+    gelu_erf_fast2_and_grad(bn, a, dg);
+    f32x2 ga = aw_splat2(0.f);
 #pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      const float xn = (vv[e] - hp.mean[e]) * hp.inv[e];
-      const float bn = xn * hp.gam[e] + hp.bet[e];
-      const float a = gelu_erf_fast(bn);
-      float ga = 0.f;
-#pragma unroll
-      for (int j = 0; j < 5; ++j) {
-        ga = fmaf(go[j], hp.w[e][j], ga);
-        accw[e][j] = fmaf(a, go[j], accw[e][j]);
-      }
-      const float gbn = ga * gelu_erf_grad_fast(bn);
-      accg[e] += gbn;
-      accgx[e] = fmaf(gbn, xn, accgx[e]);
+    for (int j = 0; j < 5; ++j) {
+      ga = __builtin_elementwise_fma(aw_splat2(go[j]), hp.w[j], ga);
+      accw[j] = __builtin_elementwise_fma(a, aw_splat2(go[j]), accw[j]);
     }
+    const f32x2 gbn = ga * dg;
+    accg += gbn;
+    accgx = __builtin_elementwise_fma(gbn, xn, accgx);
   }
 #pragma unroll
   for (int e = 0; e < 2; ++e) {
     const int o = c0 + e;
 #pragma unroll
-    for (int j = 0; j < 5; ++j) atomicAdd(&red[o * 5 + j], accw[e][j]);
+    for (int j = 0; j < 5; ++j) atomicAdd(&red[o * 5 + j], accw[j][e]);
     atomicAdd(&red[5 * H + o], accg[e]);
     atomicAdd(&red[6 * H + o], accgx[e]);
   }
@@ -542,50 +586,53 @@ __global__ __launch_bounds__(1024) void head_bwd2_cs_kernel(const float* __restr
   Head2 hp;
   hp.load(st, w2, H, c0);
   const float invn = 1.0f / (float)R;
-  float sg[2], sgx[2], accd[2] = {0.f, 0.f};
-#pragma unroll
-  for (int e = 0; e < 2; ++e) {
-    sg[e] = training ? (float)gsums[c0 + e] * invn : 0.f;
-    sgx[e] = training ? (float)gsums[H + c0 + e] * invn : 0.f;
+  f32x2 sg = aw_splat2(0.f), sgx = aw_splat2(0.f), accd = aw_splat2(0.f);
+  if (training) {
+    sg = (f32x2){(float)gsums[c0], (float)gsums[c0 + 1]} * aw_splat2(invn);
+    sgx = (f32x2){(float)gsums[H + c0], (float)gsums[H + c0 + 1]} * aw_splat2(invn);
   }
+  const f32x2 P = hp.gam * hp.inv;
   const int64_t step = (int64_t)gridDim.x * rpb;
-  float2 nv;
-  float ngo[5];
-  auto load_row = [&](int64_t r) {
+  constexpr int D = HEAD_CS_DEPTH;
+  float2 nv[D];
+  float ngo[D][5];
+  auto load_row = [&](int d, int64_t r) {   // rows past R load as zeros
     const bool in = r < R;
     const int64_t rr = in ? r : 0;
     const float* gp = gx + rr * 5;          // row r = b*Q + q -> g_xhat[b][5q + j]
 #pragma unroll
-    for (int j = 0; j < 5; ++j) ngo[j] = in ? gp[j] : 0.f;
-    nv = in ? *reinterpret_cast<const float2*>(y + rr * H + c0) : make_float2(0.f, 0.f);
+    for (int j = 0; j < 5; ++j) ngo[d][j] = in ? gp[j] : 0.f;
+    nv[d] = in ? *reinterpret_cast<const float2*>(y + rr * H + c0) : make_float2(0.f, 0.f);
   };
-  load_row((int64_t)blockIdx.x * rpb + rg);
-  for (int64_t r = (int64_t)blockIdx.x * rpb + rg; r < R; r += step) {
+  const int64_t r0 = (int64_t)blockIdx.x * rpb + rg;
+#pragma unroll
+  for (int d = 0; d < D; ++d) load_row(d, r0 + d * step);
+  for (int64_t rb = r0; rb < R; rb += D * step)
+#pragma unroll
+  for (int d = 0; d < D; ++d) {
+    const int64_t r = rb + d * step;
     float go[5];
 #pragma unroll
-    for (int j = 0; j < 5; ++j) go[j] = ngo[j];
-    const float vv[2] = {nv.x, nv.y};
-    load_row(r + step);
-    float g2[2];
+    for (int j = 0; j < 5; ++j) go[j] = ngo[d][j];
+    const f32x2 v = {nv[d].x, nv[d].y};
+    load_row(d, r + D * step);
+    __builtin_amdgcn_sched_barrier(0);   // one row's math at a time: the unrolled rows must not interleave (spills)
+    const f32x2 xn = __builtin_elementwise_fma(v, hp.inv, hp.c);
+    const f32x2 bn = __builtin_elementwise_fma(xn, hp.gam, hp.bet);
+    f32x2 ga = aw_splat2(0.f);
 #pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      const float xn = (vv[e] - hp.mean[e]) * hp.inv[e];
-      const float bn = xn * hp.gam[e] + hp.bet[e];
-      float ga = 0.f;
-#pragma unroll
-      for (int j = 0; j < 5; ++j) ga = fmaf(go[j], hp.w[e][j], ga);
-      const float gbn = ga * gelu_erf_grad_fast(bn);
-      const float g = hp.gam[e] * hp.inv[e] * (gbn - sg[e] - xn * sgx[e]);
-      accd[e] += g;
-      g2[e] = g;
-    }
+    for (int j = 0; j < 5; ++j) ga = __builtin_elementwise_fma(aw_splat2(go[j]), hp.w[j], ga);
+    const f32x2 gbn = ga * gelu_erf_grad_fast2(bn);
+    const f32x2 g = P * (gbn - __builtin_elementwise_fma(xn, sgx, sg));
+    if (r >= R) continue;
+    accd += g;
     if constexpr (sizeof(T) == 2) {
-      bf16 h[2] = {(bf16)g2[0], (bf16)g2[1]};
+      bf16 h[2] = {(bf16)g.x, (bf16)g.y};
       uint32_t u;
       memcpy(&u, h, 4);
       *reinterpret_cast<uint32_t*>(gy + r * H + c0) = u;
     } else {
-      *reinterpret_cast<float2*>(gy + r * H + c0) = make_float2(g2[0], g2[1]);
+      *reinterpret_cast<float2*>(gy + r * H + c0) = make_float2(g.x, g.y);
     }
   }
 #pragma unroll
@@ -734,7 +781,19 @@ extern "C" int aw_unpatch_head_fwd(const float* y, int64_t R, int H, int Q, cons
   AW_REQUIRE(R % Q == 0, "aw_unpatch_head_fwd: rows must be whole windows");
   if (R == 0) return AW_OK;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  dim3 grid(grid_for(R * 64, 256, 2048));
+  // one resident round of workgroups: a grid larger than what fits at the kernel's occupancy runs a second, partly
+  // filled round of row-loop waves (2048 workgroups at 5 waves/SIMD left ~40% of the chip idle in the tail)
+  static const int fwd_wgs = [] {
+    const char* e = getenv("AW_HEAD_FWD_WGS");
+    if (e) return atoi(e);
+    int dev = 0, cus = 0, per = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, head_fwd_kernel<2>, 256, 0) != hipSuccess)
+      return 2048;
+    return per > 0 && cus > 0 ? per * cus : 2048;
+  }();
+  dim3 grid(grid_for(R * 64, 256, fwd_wgs));
   switch ((H + 255) / 256) {
     case 1: hipLaunchKernelGGL(head_fwd_kernel<1>, grid, dim3(256), 0, s, y, R, H, Q, stats, w2, b2, x_hat); break;
     case 2: hipLaunchKernelGGL(head_fwd_kernel<2>, grid, dim3(256), 0, s, y, R, H, Q, stats, w2, b2, x_hat); break;
@@ -753,8 +812,9 @@ extern "C" int aw_unpatch_head_bwd1(const float* y, int64_t R, int H, int Q, con
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const size_t sh = 7 * H * sizeof(float);
   if (head_cs_ok(H)) {
-    hipLaunchKernelGGL(head_bwd1_cs_kernel, dim3(grid_for(R * (H / 2), 1024, head_wgs())), dim3(1024), sh, s, y, R, H, Q,
-                       stats, w2, g_xhat, gsums, gw2, gb2, ggamma, gbeta);
+    const dim3 g1(grid_for(R * (H / 2), 1024, head_wgs()));
+    hipLaunchKernelGGL(head_bwd1_cs_kernel, g1, dim3(1024), sh, s, y, R, H, Q, stats, w2, g_xhat, gsums, gw2, gb2,
+                       ggamma, gbeta);
     return aw::check_launch("aw_unpatch_head_bwd1");
   }
   dim3 grid(grid_for(R * 64, 256, 512));
