@@ -117,9 +117,7 @@ def vqvae_forward(sd, x, cfg: VQVAEConfig, train=True, capture=None, quantizer=N
     ``quantizer(z) -> (loss, z_q_ste, perplexity, idx)`` replaces the VectorQuantizer (e.g. the residual VQ of
     oracle/residual_vq.torch_quantizer for --use-improved-vq)."""
     B = x.shape[0]
-    flat = x.transpose(1, 2).reshape(B, cfg.L * cfg.C)                         # channel-major
-    patches = flat.view(B, cfg.S, cfg.P)
-    h = patches @ sd["patch_embed.proj.weight"][:, 0, :].t() + sd["patch_embed.proj.bias"]   # (B,S,H)
+    h = patch_embed(sd, x, cfg, "patch_embed.")                                 # (B,S,H)
     for r in range(cfg.R):
         h = _resblock(h, sd, f"encoder.0.shared_conv.{r}", None, cfg, train, token_axis_conv=False)
     z = h @ sd["encoder.1.shared_conv.weight"][:, :, 0].t() + sd["encoder.1.shared_conv.bias"]  # (B,S,D)
@@ -133,17 +131,31 @@ def vqvae_forward(sd, x, cfg: VQVAEConfig, train=True, capture=None, quantizer=N
     h = zq @ sd["decoder.0.weight"][:, :, 0].t() + sd["decoder.0.bias"]
     for r in range(cfg.R):
         h = _resblock(h, sd, f"decoder.1.shared_conv.{r}", None, cfg, train, token_axis_conv=True)
+    x_hat = unpatch(sd, h, cfg, train, "reverse_patch_embed.")
+    return emb_loss, x_hat, perplexity
+
+
+def patch_embed(sd, x, cfg: VQVAEConfig, p):
+    """PatchEmbedding (vq_vae_patch_embedd.py:7-17): windows (B, L, C) -> token-major (B, S, H)."""
+    B = x.shape[0]
+    flat = x.transpose(1, 2).reshape(B, cfg.L * cfg.C)                         # channel-major
+    patches = flat.view(B, cfg.S, cfg.P)
+    return patches @ sd[p + "proj.weight"][:, 0, :].t() + sd[p + "proj.bias"]
+
+
+def unpatch(sd, h, cfg: VQVAEConfig, train, p):
+    """PatchEmbeddingInverse (vq_vae_patch_embedd.py:19-57): token-major (B, S, H) -> (B, L, C)."""
+    B = h.shape[0]
     # ConvT(H->H, k=k1, s=k1): position k1*t + j, channel o
-    w1 = sd["reverse_patch_embed.proj.0.weight"]                               # (H_in, H_out, k1)
-    y = torch.einsum("bti,ioj->btjo", h, w1).reshape(B, cfg.S * cfg.k1, -1) + sd["reverse_patch_embed.proj.0.bias"]
-    g, bb = sd["reverse_patch_embed.proj.1.weight"], sd["reverse_patch_embed.proj.1.bias"]
-    rm, rv = sd["reverse_patch_embed.proj.1.running_mean"], sd["reverse_patch_embed.proj.1.running_var"]
+    w1 = sd[p + "proj.0.weight"]                                               # (H_in, H_out, k1)
+    y = torch.einsum("bti,ioj->btjo", h, w1).reshape(B, h.shape[1] * cfg.k1, -1) + sd[p + "proj.0.bias"]
+    g, bb = sd[p + "proj.1.weight"], sd[p + "proj.1.bias"]
+    rm, rv = sd[p + "proj.1.running_mean"], sd[p + "proj.1.running_var"]
     y = _bn_train(y, g, bb, rm, rv, axes=(0, 1)) if train else _bn_eval(y, g, bb, rm, rv)
     a = gelu_erf(y)
-    w2 = sd["reverse_patch_embed.proj.3.weight"]                               # (H, 1, 5)
-    out = torch.einsum("bqo,oj->bqj", a, w2[:, 0, :]).reshape(B, -1) + sd["reverse_patch_embed.proj.3.bias"]
-    x_hat = out.view(B, -1, cfg.C)                                             # interleaved reshape
-    return emb_loss, x_hat, perplexity
+    w2 = sd[p + "proj.3.weight"]                                               # (H, 1, 5)
+    out = torch.einsum("bqo,oj->bqj", a, w2[:, 0, :]).reshape(B, -1) + sd[p + "proj.3.bias"]
+    return out.view(B, -1, cfg.C)                                              # interleaved reshape
 
 
 def vqvae_train_step_grads(sd_np, x_np, cfg: VQVAEConfig, train=True, quantizer=None):

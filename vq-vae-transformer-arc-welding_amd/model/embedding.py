@@ -4,7 +4,7 @@ import math
 import torch
 from torch import nn
 
-from arcweld import kernels as K
+from arcweld import modules
 
 
 class PositionalEmbedding(nn.Module):
@@ -24,7 +24,7 @@ class PositionalEmbedding(nn.Module):
 
 
 class LatentEmbeddingCond(nn.Module):
-    """Reference :27-43 (unused by the entry points); kept for state_dict/API compatibility."""
+    """Reference :27-43 (unused by the entry points): token + positional + per-window condition embedding."""
 
     def __init__(self, input_size: int, d_model: int, cond_size: int) -> None:
         super().__init__()
@@ -33,7 +33,8 @@ class LatentEmbeddingCond(nn.Module):
         self.cond_embedding = nn.Embedding(num_embeddings=cond_size, embedding_dim=d_model)
 
     def forward(self, x, cond):
-        raise NotImplementedError("LatentEmbeddingCond is unused by the reference entry points (out of scope)")
+        """latent_embedding(x) + pe[:T] + cond_embedding(cond) on every position (reference :38-43)."""
+        return modules.latent_embedding(self, x, cond.contiguous(), self.cond_embedding.weight)
 
 
 class LatentEmbedding(nn.Module):
@@ -49,14 +50,5 @@ class LatentEmbedding(nn.Module):
         self.seq_len = seq_len
 
     def forward(self, x):
-        if torch.is_grad_enabled() and self.latent_embedding.weight.requires_grad:
-            raise NotImplementedError("LatentEmbedding alone is inference-only on the HIP path; train through "
-                                      "MyTransformerDecoder.forward")
-        B, T = x.shape
-        if T > self.positional_embedding.pe.shape[1]:
-            raise RuntimeError(f"The size of tensor a ({T}) must match the size of tensor b "
-                               f"({self.positional_embedding.pe.shape[1]}) at non-singleton dimension 1")
-        out = torch.empty(B, T, self.d_model, device=x.device)
-        K.embed_fwd(x.contiguous(), self.latent_embedding.weight, self.positional_embedding.pe[0],
-                    out.view(B * T, self.d_model))
-        return out
+        """latent_embedding(x) + pe[:T] (reference :57-59); trainable on its own (scatter-add backward)."""
+        return modules.latent_embedding(self, x)

@@ -1,13 +1,12 @@
 """minGPT pre-LN block -- drop-in for model/transformer_block.py of the reference (same module tree and keys:
 ln_1, attn.{c_attn, c_proj, bias}, ln_2, mlp.{c_fc, c_proj}).  Training runs through the fused decoder path
-(arcweld.decoder); a Block used on its own runs the same kernels for inference."""
+(arcweld.decoder); a Block used on its own runs the same kernels, with its own autograd node."""
 import math
 
 import torch
 from torch import nn, Tensor
 
-from arcweld import kernels as K
-from arcweld.vqvae import operand_dtype
+from arcweld import modules
 
 
 class NewGELUActivation(nn.Module):
@@ -49,30 +48,7 @@ class Block(nn.Module):
         ))
         self.res_dropout = res_dropout
 
-    @torch.no_grad()
     def forward(self, x):
-        """(B, T, d) -> (B, T, d), inference semantics (dropout inactive unless training)."""
-        if torch.is_grad_enabled():
-            raise NotImplementedError("Block alone is inference-only on the HIP path; train via MyTransformerDecoder")
-        B, T, d = x.shape
-        R = B * T
-        Td = operand_dtype()
-        e = lambda *s, dt=torch.float32: torch.empty(*s, device=x.device, dtype=dt)  # noqa: E731
-        xr = x.reshape(R, d).contiguous().float()
-        cast = (lambda w: w) if Td == torch.float32 else (lambda w: w.to(Td))
-        a, mu, rs = e(R, d, dt=Td), e(R), e(R)
-        K.layernorm_fwd(xr, self.ln_1.weight, self.ln_1.bias, self.ln_1.eps, a, mu, rs)
-        qkv = e(R, 3 * d, dt=Td)
-        K.gemm(a, cast(self.attn.c_attn.weight), R, 3 * d, d, bias=self.attn.c_attn.bias, C=qkv)
-        y, lse = e(R, d, dt=Td), e(B * self.attn.n_head * T)
-        K.attn_fwd(qkv, B, T, self.attn.n_head, d, y, lse)
-        x1 = e(R, d)
-        K.gemm(y, cast(self.attn.c_proj.weight), R, d, d, bias=self.attn.c_proj.bias, resid=xr, C=x1)
-        a2 = e(R, d, dt=Td)
-        K.layernorm_fwd(x1, self.ln_2.weight, self.ln_2.bias, self.ln_2.eps, a2, mu, rs)
-        g = e(R, 4 * d, dt=Td)
-        K.gemm(a2, cast(self.mlp.c_fc.weight), R, 4 * d, d, bias=self.mlp.c_fc.bias, act=K.AW_ACT_GELU_TANH, C2=g,
-               c2_mode=1)
-        x2 = e(R, d)
-        K.gemm(g, cast(self.mlp.c_proj.weight), R, d, 4 * d, bias=self.mlp.c_proj.bias, resid=x1, C=x2)
-        return x2.view(B, T, d)
+        """(B, T, d) -> (B, T, d); dropout active in training mode.  An autograd node of its own when anything
+        requires grad (arcweld.modules.block: the fused decoder's per-block kernels)."""
+        return modules.block(self, x)

@@ -5,36 +5,19 @@ patch_embed.proj, encoder.0.shared_conv.{r}.block.{1,4}, encoder.1.shared_conv, 
 decoder.0, decoder.1.shared_conv.{r}.block.{1,4}, reverse_patch_embed.proj.{0,1,3}.
 
 ``VQVAEPatch.forward`` runs the whole network as ONE fused HIP pass (arcweld.vqvae) behind a single autograd
-Function.  The sub-modules keep working on their own in the reference's channel-major layout (B, C, S) for
-inference (the latent tokenizer calls patch_embed -> encoder -> vector_quantization,
-dataloader/latentspace_dataloader.py:154-161); their standalone forwards run the same kernels.
+Function.  The sub-modules also work on their own in the reference's channel-major layout (B, C, S) -- the latent
+tokenizer calls patch_embed -> encoder -> vector_quantization (dataloader/latentspace_dataloader.py:154-161) -- and
+are trainable there too: each records its own autograd node whose backward runs the same kernels
+(arcweld.modules).
 """
 import torch
 from torch import nn
 
 from arcweld import kernels as K
+from arcweld import modules
 from arcweld import vqvae as engine
 from model.autencoder_lightning_base import Autoencoder
 from model.vector_quantizer import ResidualVQLightning, VectorQuantizer
-
-
-def _need_no_grad(mod, *tensors):
-    if torch.is_grad_enabled() and (any(t.requires_grad for t in tensors) or
-                                    any(p.requires_grad for p in mod.parameters())):
-        raise NotImplementedError(
-            f"{type(mod).__name__}.forward on its own is inference-only on the HIP path; train through "
-            "VQVAEPatch.forward (one fused autograd node) or wrap the call in torch.no_grad()")
-
-
-def _tokens(x_bcs, T):
-    """(B, C, S) channel-major -> token-major (B*S, C) contiguous in operand dtype T."""
-    B, C, S = x_bcs.shape
-    t = x_bcs.permute(0, 2, 1)
-    if t.dtype != T or not t.is_contiguous():
-        out = torch.empty(B * S, C, device=x_bcs.device, dtype=T)
-        out.view(B, S, C).copy_(t)
-        return out
-    return t.reshape(B * S, C)
 
 
 class PatchEmbedding(nn.Module):
@@ -46,19 +29,7 @@ class PatchEmbedding(nn.Module):
         self.proj = nn.Conv1d(1, embed_dim, kernel_size=patch_size, stride=patch_size)
 
     def forward(self, x):
-        _need_no_grad(self, x)
-        B, L, C = x.shape
-        P, H = self.patch_size, self.proj.out_channels
-        S = L * C // P
-        ldp = (P + 7) // 8 * 8
-        T = engine.operand_dtype()
-        patches = torch.empty(B * S, ldp, device=x.device, dtype=T)
-        K.patchify(x.contiguous(), P, patches)
-        W = torch.empty(H, ldp, device=x.device, dtype=T)
-        K.weight_relayout(self.proj.weight, H, 1, P, 0, 4, W, ldo=ldp)
-        out = torch.empty(B * S, H, device=x.device)
-        K.gemm(patches, W, B * S, H, ldp, bias=self.proj.bias, C=out)
-        return out.view(B, S, H).permute(0, 2, 1)
+        return modules.patch_embed(self, x)
 
 
 class PatchEmbeddingInverse(nn.Module):
@@ -81,24 +52,7 @@ class PatchEmbeddingInverse(nn.Module):
         self.input_dim = input_dim
 
     def forward(self, x):
-        _need_no_grad(self, x)
-        B, H, S = x.shape
-        T = engine.operand_dtype()
-        xt = _tokens(x, T)
-        N, k1 = B * S, self.k1
-        W = torch.empty(k1 * H, H, device=x.device, dtype=T)
-        K.weight_relayout(self.proj[0].weight, H, H, k1, 0, 3, W)
-        Y = torch.empty(N, k1 * H, device=x.device)
-        bn = self.proj[1]
-        cs = torch.zeros(2 * H, device=x.device, dtype=torch.float64) if self.training else None
-        K.gemm(xt, W, N, k1 * H, H, bias=self.proj[0].bias, bias_mod=H, C=Y, colstats=cs, stats_mod=H)
-        stats = torch.empty(4 * H, device=x.device)
-        K.bn_finalize(cs, N * k1, H, bn.weight, bn.bias, bn.running_mean, bn.running_var,
-                      bn.num_batches_tracked if self.training else None, bn.eps, bn.momentum or 0.1, self.training,
-                      stats)
-        out = torch.empty(B, S * k1 * 5 // self.input_dim, self.input_dim, device=x.device)
-        K.unpatch_head_fwd(Y.view(N * k1, H), S * k1, stats, self.proj[3].weight.view(H, 5), self.proj[3].bias, out)
-        return out
+        return modules.patch_unembed(self, x)
 
 
 class ResBlock(nn.Module):
@@ -126,16 +80,7 @@ class SepCNNBlock(nn.Module):
         self.shared_conv = nn.Conv1d(hidden_dim, embedding_dim, kernel_size=1, stride=1, padding=0)
 
     def forward(self, x):
-        _need_no_grad(self, x)
-        B, H, S = x.shape
-        D = self.shared_conv.out_channels
-        T = engine.operand_dtype()
-        xt = _tokens(x, T)
-        W = torch.empty(D, H, device=x.device, dtype=T)
-        K.weight_relayout(self.shared_conv.weight, D, H, 1, 0, 0, W)
-        z = torch.empty(B * S, D, device=x.device)
-        K.gemm(xt, W, B * S, D, H, bias=self.shared_conv.bias, C=z)
-        return z.view(B, S, D)
+        return modules.sep_cnn(self, x)
 
 
 class CNNBlock(nn.Module):
@@ -153,49 +98,7 @@ class CNNBlock(nn.Module):
                      batch_norm=batch_norm) for _ in range(n_resblocks)])
 
     def forward(self, x):
-        _need_no_grad(self, x)
-        B, H, S = x.shape
-        N = B * S
-        T = engine.operand_dtype()
-        cur = x.permute(0, 2, 1).contiguous().view(N, H)
-        a0 = _gelu_operand(cur, T)
-        p = self.dropout_p if self.training else 0.0
-        seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if p > 0 else 0
-        for r, blk in enumerate(self.shared_conv):
-            c1, c2 = blk.block[1], blk.block[4]
-            if self.seperate:
-                w1, w2 = (torch.empty(H, H, device=x.device, dtype=T) for _ in range(2))
-                K.weight_relayout_batch([engine._centre_job(c1.weight, w1), engine._centre_job(c2.weight, w2)])
-                kd, conv = H, None
-            else:
-                w1, w2 = (torch.empty(H, 3 * H, device=x.device, dtype=T) for _ in range(2))
-                K.weight_relayout(c1.weight, H, H, 3, 0, 1, w1)
-                K.weight_relayout(c2.weight, H, H, 3, 0, 1, w2)
-                kd, conv = 3 * H, (H, S, 1, 0)
-            if self.batch_norm:   # BatchNorm ResBlocks: per-token statistics when the tokens run separately
-                gk = {} if conv is None else dict(conv=conv)
-                cur, a0, _ = engine._bn_block_fwd(a0, cur, w1, w2, kd, gk, c1, c2, (blk.block[2], blk.block[5]),
-                                                  S if self.seperate else 1, self.training, p, engine._mix(seed, r),
-                                                  None, T)
-                continue
-            a1 = torch.empty(N, H, device=x.device, dtype=T)
-            K.gemm(a0, w1, N, H, kd, conv=conv, bias=c1.bias, C2=a1, c2_mode=1)
-            nxt = torch.empty(N, H, device=x.device)
-            an = torch.empty(N, H, device=x.device, dtype=T)
-            K.gemm(a1, w2, N, H, kd, conv=conv, bias=c2.bias, drop=(p, engine._mix(seed, r)), resid=cur, C=nxt, C2=an,
-                   c2_mode=1)
-            cur, a0 = nxt, an
-        return cur.view(B, S, H).permute(0, 2, 1)
-
-
-def _gelu_operand(x, T):
-    """GELU(x) in operand dtype T through the GEMM epilogue with an empty contraction (K = 0):
-    v = 0 + resid = x, C2 = gelu(v)."""
-    N, H = x.shape
-    out = torch.empty(N, H, device=x.device, dtype=T)
-    dummy = torch.zeros(8, 8, device=x.device, dtype=T)
-    K.gemm(dummy, dummy, N, H, 0, resid=x, C2=out, c2_mode=1)
-    return out
+        return modules.cnn_block(self, x)
 
 
 class VQVAEPatch(Autoencoder):
