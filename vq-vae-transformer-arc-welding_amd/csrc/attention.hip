@@ -174,31 +174,40 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_mfma_kernel(const bf16* __res
       for (int ks = 0; ks < 4; ++ks) s[st] = mfma32(row_frag(Ks, 32 * st + r, ks, hf), qf[ks], s[st]);
     }
     const bool edge = (k0 + TILE - 1 > qw) || (k0 + TILE > T_);
+    // causal / length mask as selects against one per-lane limit, only on the (wave-uniform) edge tiles: the empty
+    // asm keeps the branch -- if-converted, the 64 compares + selects ran on every tile (a third of the loop's VALU)
+    if (edge) {
+      asm volatile("" ::: "memory");
+      const int lim = min(q, T_ - 1) - (k0 + 4 * hf);
+#pragma unroll
+      for (int st = 0; st < 2; ++st)
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+          s[st][i] = (32 * st + 8 * (i >> 2) + (i & 3) > lim) ? -__builtin_huge_valf() : s[st][i];
+    }
     float mx = -__builtin_huge_valf();
-    // causal / length mask as selects against one per-lane limit (the per-element `if` compiled to 32 branches)
-    const int lim = min(q, T_ - 1) - (k0 + 4 * hf);
 #pragma unroll
     for (int st = 0; st < 2; ++st)
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        if (edge) s[st][i] = (32 * st + 8 * (i >> 2) + (i & 3) > lim) ? -__builtin_huge_valf() : s[st][i];
-        mx = fmaxf(mx, s[st][i]);
-      }
+      for (int i = 0; i < 16; ++i) mx = fmaxf(mx, s[st][i]);
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
     const float mn = fmaxf(m, mx);
     const float alpha = __builtin_amdgcn_exp2f((m - mn) * c2);   // v_exp_f32: arguments <= 0, -inf -> 0
     const float mc = mn * c2;
     m = mn;
-    float ls = 0.f;
+    // exponent arguments and the row sum as f32 pairs (v_pk_fma_f32 / v_pk_add_f32)
+    f32x2 ls2 = {0.f, 0.f};
 #pragma unroll
     for (int st = 0; st < 2; ++st)
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const float p = __builtin_amdgcn_exp2f(s[st][i] * c2 - mc);
-        s[st][i] = p;
-        ls += p;
+      for (int i = 0; i < 16; i += 2) {
+        const f32x2 a = __builtin_elementwise_fma((f32x2){s[st][i], s[st][i + 1]}, (f32x2){c2, c2}, (f32x2){-mc, -mc});
+        const f32x2 p = {__builtin_amdgcn_exp2f(a.x), __builtin_amdgcn_exp2f(a.y)};
+        s[st][i] = p.x;
+        s[st][i + 1] = p.y;
+        ls2 += p;
       }
-    l = l * alpha + ls;
+    l = l * alpha + (ls2.x + ls2.y);
 #pragma unroll
     for (int dt = 0; dt < 2; ++dt)
 #pragma unroll
@@ -289,13 +298,16 @@ __global__ __launch_bounds__(256, 2) void attn_dq_mfma_kernel(const bf16* __rest
         s = mfma32(row_frag(Ks, 32 * st + r, ks, hf), qf[ks], s);
         dp = mfma32(row_frag(Vs, 32 * st + r, ks, hf), gf[ks], dp);
       }
-      const int lim = min(q, T_ - 1) - (k0 + 32 * st + 4 * hf);
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        float p = __builtin_amdgcn_exp2f(s[i] * c2 - L2);
-        if (edge) p = (8 * (i >> 2) + (i & 3) > lim) ? 0.f : p;
-        s[i] = p * (dp[i] - Dl);
+      for (int i = 0; i < 16; ++i) s[i] = __builtin_amdgcn_exp2f(s[i] * c2 - L2);
+      if (edge) {   // kept a real (wave-uniform) branch, as in the forward
+        asm volatile("" ::: "memory");
+        const int lim = min(q, T_ - 1) - (k0 + 32 * st + 4 * hf);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) s[i] = (8 * (i >> 2) + (i & 3) > lim) ? 0.f : s[i];
       }
+#pragma unroll
+      for (int i = 0; i < 16; ++i) s[i] = s[i] * (dp[i] - Dl);
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) {
         const uint4 db = pack8(s, s2);
@@ -374,24 +386,30 @@ __global__ __launch_bounds__(256, 2) void attn_dkv_mfma_kernel(const bf16* __res
         dp = mfma32(row_frag(Gs, 32 * qs + r, ks, hf), vf[ks], dp);
       }
       f32x16 p;
+      float Dv[16];
 #pragma unroll
       for (int g4 = 0; g4 < 4; ++g4) {
         const int ql = 32 * qs + 8 * g4 + 4 * hf;  // first of this register group's 4 queries (tile-local)
         const float4 L4 = *reinterpret_cast<const float4*>(Ls + ql);
         const float4 D4 = *reinterpret_cast<const float4*>(Ds + ql);
-        const float Lv[4] = {L4.x, L4.y, L4.z, L4.w}, Dv[4] = {D4.x, D4.y, D4.z, D4.w};
+        const float Lv[4] = {L4.x, L4.y, L4.z, L4.w};
+        Dv[4 * g4] = D4.x;
+        Dv[4 * g4 + 1] = D4.y;
+        Dv[4 * g4 + 2] = D4.z;
+        Dv[4 * g4 + 3] = D4.w;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int i = 4 * g4 + e;
-          float pv = __builtin_amdgcn_exp2f(s[i] * c2 - Lv[e]);
-          if (edge) {
-            const int qq = q0 + ql + e;
-            pv = (qq < key || qq >= T_) ? 0.f : pv;
-          }
-          p[i] = pv;
-          s[i] = pv * (dp[i] - Dv[e]);
+        for (int e = 0; e < 4; ++e) p[4 * g4 + e] = __builtin_amdgcn_exp2f(s[4 * g4 + e] * c2 - Lv[e]);
+      }
+      if (edge) {   // kept a real (wave-uniform) branch, as in the forward
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int qq = q0 + 32 * qs + 8 * (i >> 2) + 4 * hf + (i & 3);
+          p[i] = (qq < key || qq >= T_) ? 0.f : p[i];
         }
       }
+#pragma unroll
+      for (int i = 0; i < 16; ++i) s[i] = p[i] * (dp[i] - Dv[i]);
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) {
         const uint4 pb = pack8(p, s2), db = pack8(s, s2);
