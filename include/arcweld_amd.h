@@ -185,10 +185,12 @@ int aw_patchify(const float* x, int64_t B, int L, int C, int P, void* patches, i
  * mode 4: conv (O,I,k)     -> [O][ldo] zero padded, col i*k+j  (patch embed, 1 input channel)
  * `ldo` is the output row length (ignored except for mode 4).  Batched form only:
  * mode 5: plain cast of O*I elements;
- * mode 6: conv (O,I,k) tap t -> [I/32][O][32] K-step-major (the fused encoder chain's weight stream; I % 32 == 0). */
+ * mode 6: conv (O,I,k) tap t -> [I/32][O][32] K-step-major (the fused encoder chain's weight stream; I % 32 == 0);
+ * mode 7: conv stored tap-major (O,3,I) -> [3*O][I], row j*O+o (decoder conv input-gradient when the optimizer keeps
+ *         the weight tap-major; the forward copy [O][3*I] of such a weight is mode 5 over O x 3I). */
 int aw_weight_relayout(const float* W, int O, int I, int k, int tap, int mode, void* out, int64_t ldo,
                        int dtype, void* stream);
-/* Batched form: up to AW_RELAYOUT_MAX_JOBS relayouts (modes 0-6 above; mode 5 casts e.g. the Linear weights of
+/* Batched form: up to AW_RELAYOUT_MAX_JOBS relayouts (modes 0-7 above; mode 5 casts e.g. the Linear weights of
  * model/transformer_block.py) into one output dtype, one launch per call. */
 #define AW_RELAYOUT_MAX_JOBS 40
 typedef struct {

@@ -72,6 +72,15 @@ def test_update_kernel_copies_equal_a_fresh_relayout(T, chain, monkeypatch):
         K.weight_relayout_batch([j.relayout_job() for j in fresh])
         for j, f in zip(st.jobs, fresh):
             assert torch.equal(j.out, f.out), (j.name, j.mode)
+        # the decoder convs are stored tap-major by the Trainer: check their copies against torch permutes of the
+        # parameter itself (independent of both the relayout and the update kernel's index maps)
+        dec = [j for j in st.jobs if j.name.startswith(("dec", "dgw"))]
+        assert dec and all(not j.param.is_contiguous() for j in dec)
+        for j in dec:
+            W = j.param.detach()
+            want = W.permute(0, 2, 1).reshape(j.O, 3 * j.I) if j.name.startswith("dec") else \
+                W.permute(2, 0, 1).reshape(3 * j.O, j.I)
+            assert torch.equal(j.out, want.to(j.out.dtype)), j.name
 
 
 def test_outside_weight_change_triggers_a_refresh():

@@ -298,6 +298,33 @@ def test_trainer_centre_tap_layout_matches_dense_layout(fp32_parity, monkeypatch
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("batch_norm", [False, True])
+def test_trainer_tap_major_decoder_layout_matches_dense_layout(fp32_parity, monkeypatch, batch_norm):
+    """The Trainer stores the decoder k = 3 conv weights tap-major ((O, 3, I) segments: contiguous weight-gradient
+    atomics, plain-cast forward operands); three steps with dropout give the same parameters as the reference's dense
+    (O, I, 3) layout, and the state_dict keeps the reference's shapes."""
+    from arcweld.optim import RAdam
+    from arcweld.trainer import Trainer
+    kw = dict(hidden_dim=64, num_embeddings=64, embedding_dim=16, n_resblocks=2, patch_size=25)
+    xs = [torch.tensor(gen.windows(730 + i, 16), device="cuda") for i in range(3)]
+    out = []
+    for declare in (True, False):
+        if not declare:
+            monkeypatch.setattr(RAdam, "declare_tap_major", lambda self, ps: None)
+        m = make_model(kw, 302, "cuda", batch_norm=batch_norm, dropout=0.1).train()
+        tr = Trainer(gradient_clip_val=0.7)
+        tr.setup_optimizer(m)
+        w = m.decoder[1].shared_conv[0].block[1].weight
+        assert (not w.is_contiguous()) == declare and w.shape == (64, 64, 3)
+        for x in xs:
+            tr.micro_step(m, x, 0, 1.0)
+            tr.optimizer_step(m)
+        out.append({k: v.detach().clone() for k, v in m.state_dict().items()})
+    for k in out[0]:
+        torch.testing.assert_close(out[0][k].float(), out[1][k].float(), rtol=1e-5, atol=1e-6, msg=k)
+
+
+@pytest.mark.gpu
 def test_batchnorm_model_tokenizes_and_trains_graphed(fp32_parity):
     """BatchNorm ResBlocks on the other entry points: the fused tokenization gives the train-step indices of the
     golden (batch statistics in train mode), the standalone encoder modules agree with it, and captured steps

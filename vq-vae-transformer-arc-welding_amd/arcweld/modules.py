@@ -171,7 +171,7 @@ def cnn_block(mod, x):
                 K.weight_relayout_batch([engine._centre_job(c1.weight, w1), engine._centre_job(c2.weight, w2)])
             else:
                 w1, w2 = e(H, 3 * H, dt=T), e(H, 3 * H, dt=T)
-                K.weight_relayout_batch([(c1.weight, H, H, 3, 0, 1, w1), (c2.weight, H, H, 3, 0, 1, w2)])
+                K.weight_relayout_batch([engine._conv3_job(c1.weight, 1, w1), engine._conv3_job(c2.weight, 1, w2)])
             sr = _mix(seed, r)
             if mod.batch_norm:   # per-token statistics when the tokens run separately, over all positions otherwise
                 gk = {} if conv is None else dict(conv=conv)
@@ -202,8 +202,9 @@ def cnn_block(mod, x):
                 Cw, cm = engine._centre_grad(slot(c.weight))
                 return (A, Bm, H, H, N, dict(a_trans=True, b_trans=True, C=Cw, accumulate=True, col_map=cm,
                                              a_rowsum=slot(c.bias)))
-            return (A, Bm, H, 3 * H, N, dict(a_trans=True, b_trans=True, conv=wconv, C=slot(c.weight).view(H, 3 * H),
-                                             accumulate=True, col_map=(H, 3, 0), a_rowsum=slot(c.bias)))
+            Cw, cm = engine._conv3_grad(slot(c.weight))
+            return (A, Bm, H, 3 * H, N, dict(a_trans=True, b_trans=True, conv=wconv, C=Cw, accumulate=True,
+                                             col_map=cm, a_rowsum=slot(c.bias)))
 
         gy = _tokens(g, F32)
         nb = len(blocks)
@@ -217,7 +218,7 @@ def cnn_block(mod, x):
                 W1d, W2d = w1, w2
             else:   # dgrad operands [3O][I]
                 W1d, W2d = e(3 * H, H, dt=T), e(3 * H, H, dt=T)
-                K.weight_relayout_batch([(c1.weight, H, H, 3, 0, 2, W1d), (c2.weight, H, H, 3, 0, 2, W2d)])
+                K.weight_relayout_batch([engine._conv3_job(c1.weight, 2, W1d), engine._conv3_job(c2.weight, 2, W2d)])
             if mod.batch_norm:
                 gk = {} if dconv is None else dict(conv=dconv)
                 gy, _ = engine._bn_block_bwd(gy, xr, a0, bs, W1d, W2d, kd, gk, wg, c1, c2, (blk.block[2], blk.block[5]),

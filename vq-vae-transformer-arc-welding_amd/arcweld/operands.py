@@ -29,7 +29,17 @@ class OperandJob:
         self.O, self.I, self.k, self.tap, self.mode, self.ldo, self.out = O, I, k, tap, mode, ldo, out
 
     def relayout_job(self):
-        return (self.src, self.O, self.I, self.k, self.tap, self.mode, self.out, self.ldo)
+        """(src, O, I, k, tap, mode, out, ldo) for the layout the source has NOW: a k = 3 conv weight the optimizer
+        stores tap-major (arcweld.optim.RAdam.declare_tap_major: (O, 3, I) storage) turns the forward copy [O][3I]
+        into a plain cast (mode 5 over O x 3I) and the input-gradient copy [3O][I] into mode 7."""
+        s = self.src
+        if self.mode in (1, 2) and self.k == 3 and s.dim() == 3 and not s.is_contiguous() \
+                and s.stride() == (3 * self.I, 1, self.I):
+            st = s.permute(0, 2, 1)       # the (O, 3, I) storage, contiguous
+            if self.mode == 1:
+                return (st, self.O, 3 * self.I, 1, 0, 5, self.out, self.ldo)
+            return (st, self.O, self.I, 3, 0, 7, self.out, self.ldo)
+        return (s, self.O, self.I, self.k, self.tap, self.mode, self.out, self.ldo)
 
 
 class OperandSet:

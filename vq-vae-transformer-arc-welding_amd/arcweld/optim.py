@@ -10,6 +10,9 @@ is re-bound to a view of it, so that
 * the gradient all-reduce of data parallelism is a few large RCCL calls over the flat gradient buffer,
 * conv weights declared centre-tap (declare_centre_tap) keep their provably-dead side taps out of the
   all-reduce, the norm and the update,
+* k = 3 conv weights declared tap-major (declare_tap_major) are stored (O, 3, I) in their segment, so that the
+  weight-gradient GEMM accumulates whole contiguous rows [O][3I] (the reference's (O, I, 3) order would scatter
+  every atomic over three times the cache lines) and the forward operand [O][3I] is a plain cast of the segment,
 * the clip coefficient (Lightning ``gradient_clip_val``) is computed on device and fed to the update kernel:
   no host synchronisation anywhere in the step.
 
@@ -42,6 +45,15 @@ class RAdam(torch.optim.Optimizer):
             raise RuntimeError("declare_centre_tap must precede flatten()")
         self._centre = [p for p in params]
 
+    def declare_tap_major(self, params):
+        """k = 3 conv weights (O, I, 3) to store tap-major: each keeps its own segment of 3*O*I elements, laid out
+        (O, 3, I); the parameter becomes the strided view .permute(0, 2, 1) of it (shape, values and state_dict
+        unchanged).  RAdam, clip norm and all-reduce are elementwise over the segment, so nothing else changes.  Call
+        before the first flatten()."""
+        if self._flat is not None:
+            raise RuntimeError("declare_tap_major must precede flatten()")
+        self._tap_major = [p for p in params]
+
     def _build(self):
         params = [p for g in self.param_groups for p in g["params"]]
         dev = params[0].device
@@ -56,6 +68,8 @@ class RAdam(torch.optim.Optimizer):
                            and float(self.param_groups[owner_of[id(centre[0])]]["weight_decay"]) == 0.0):
             centre = []          # the exactness argument needs one group, wd 0 and one (O, I, 3) shape
         cidx = {id(p): j for j, p in enumerate(centre)}
+        tmaj = set(id(p) for p in getattr(self, "_tap_major", []) if id(p) in owner_of and id(p) not in cidx
+                   and p.dim() == 3 and p.shape[2] == 3)
         al = lambda n: (n + 63) // 64 * 64      # 256-B aligned segments  # noqa: E731
         # segments: (param, offset, length, weight decay, group); a centre-tap param has ONE segment (its centre)
         segs, place, total, blk = [], {}, 0, None
@@ -80,6 +94,9 @@ class RAdam(torch.optim.Optimizer):
                 O, I, _ = p.shape
                 return buf[blk:blk + 3 * len(centre) * O * I].view(3, len(centre), O, I)[:, cidx[id(p)]].permute(1, 2, 0)
             o = place[id(p)]
+            if id(p) in tmaj:
+                O, I, _ = p.shape
+                return buf[o:o + p.numel()].view(O, 3, I).permute(0, 2, 1)
             return buf[o:o + p.numel()].view_as(p)
 
         for p in params:
@@ -205,8 +222,9 @@ class RAdam(torch.optim.Optimizer):
                 # centre-tap: the job's source is then that centre view, k = 1)
                 if j.src.numel() != F["segs"][i][2]:
                     return False
+                _, O, I, k_, tap, mode, _, ldo = j.relayout_job()     # the mode for the source's storage order
                 d.out = j.out.data_ptr()
-                d.O, d.I, d.k, d.tap, d.mode, d.ldo = j.O, j.I, j.k, j.tap, j.mode, j.ldo
+                d.O, d.I, d.k, d.tap, d.mode, d.ldo = O, I, k_, tap, mode, ldo
                 d.dtype = K.dtype_code(j.out.dtype)
         raw = torch.frombuffer(bytearray(bytes(table)), dtype=torch.uint8)
         F["ops_d"] = raw.to(F["p"].device)

@@ -16,6 +16,8 @@ find_unused_parameters=True behaviour: their grad stays None in the reference).
 """
 from __future__ import annotations
 
+import os
+
 import math
 import time
 
@@ -106,6 +108,9 @@ class Trainer:
             opt = opt[0]
         if hasattr(model, "centre_tap_parameters") and hasattr(opt, "declare_centre_tap"):
             opt.declare_centre_tap(model.centre_tap_parameters())
+        if hasattr(model, "tap_major_parameters") and hasattr(opt, "declare_tap_major") \
+                and os.environ.get("ARCWELD_TAP_MAJOR", "1") != "0":     # 0: the reference layout (A/B only)
+            opt.declare_tap_major(model.tap_major_parameters())
         opt.flatten()
         active = model.active_parameters() if hasattr(model, "active_parameters") else None
         opt.set_active(active)

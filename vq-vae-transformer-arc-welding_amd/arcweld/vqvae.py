@@ -164,6 +164,26 @@ def _centre_grad(g):
     return c, (0, 1, 0)
 
 
+def _conv3_job(w, mode, out):
+    """Relayout job of a decoder k = 3 conv weight (mode 1: [O][3I] forward, mode 2: [3O][I] input gradient) for
+    either storage order of the weight (contiguous (O, I, 3), or the optimizer's tap-major (O, 3, I))."""
+    from .operands import OperandJob
+    return OperandJob("", w, w, w.shape[0], w.shape[1], 3, 0, mode, out).relayout_job()
+
+
+def _conv3_grad(g):
+    """Where a decoder k = 3 conv weight-gradient GEMM (columns j*I + i) writes: (C [O][3I], col_map).  The
+    reference's contiguous (O, I, 3) layout takes the columns through the (I, 3) column map; the optimizer's tap-major
+    storage (arcweld.optim.RAdam.declare_tap_major, (O, 3, I)) is [O][3I] itself, written by contiguous atomics."""
+    O, I = g.shape[0], g.shape[1]
+    if g.is_contiguous():
+        return g.view(O, 3 * I), (I, 3, 0)
+    st = g.permute(0, 2, 1)
+    if not st.is_contiguous():
+        raise ValueError("decoder conv gradient: unsupported layout")
+    return st.reshape(O, 3 * I), (0, 1, 0)
+
+
 def _bn_stats(h, G, bn, training):
     """BatchNorm statistics [4][G][H] of h [N][H] (rows grouped by row % G); training moves the running stats."""
     N, H = h.shape
@@ -490,8 +510,9 @@ def backward(m, sv, g_emb, g_xhat, slot, mid_hook=None):
     wgrads = []
     dgw = [(sv.ops[f"dgw{r}_1"], sv.ops[f"dgw{r}_2"]) for r in range(R)]
     def wg_dec(c, A, B):
-        return (A, B, H, 3 * H, N, dict(a_trans=True, b_trans=True, conv=wconv, C=slot(c.weight).view(H, 3 * H),
-                                        accumulate=True, col_map=(H, 3, 0), a_rowsum=slot(c.bias)))
+        Cw, cm = _conv3_grad(slot(c.weight))
+        return (A, B, H, 3 * H, N, dict(a_trans=True, b_trans=True, conv=wconv, C=Cw, accumulate=True, col_map=cm,
+                                        a_rowsum=slot(c.bias)))
 
     for r in reversed(range(R)):
         c1, c2 = pr["dec"][r]
@@ -503,14 +524,12 @@ def backward(m, sv, g_emb, g_xhat, slot, mid_hook=None):
             continue
         gh = e(N, H, dt=T)
         K.gemm(go, W2d, N, H, 3 * H, b_trans=True, conv=dconv_in, pre=sv.dhs[r], C=gh)
-        wgrads.append((go, sv.da1s[r], H, 3 * H, N, dict(a_trans=True, b_trans=True, conv=wconv,
-                       C=slot(c2.weight).view(H, 3 * H), accumulate=True, col_map=(H, 3, 0), a_rowsum=slot(c2.bias))))
+        wgrads.append(wg_dec(c2, go, sv.da1s[r]))
         gyn, gon = e(N, H), e(N, H, dt=T)
         K.gemm(gh, W1d, N, H, 3 * H, b_trans=True, conv=dconv_in, pre=sv.ys[r], resid=gy, C=gyn, C2=gon,
                c2_mode=3 if r > 0 else 2, drop2=(p_drop, sv.dec_seed[r - 1] if r > 0 else 0),
                seed_ptr=sv.ctr)
-        wgrads.append((gh, sv.ya0s[r], H, 3 * H, N, dict(a_trans=True, b_trans=True, conv=wconv,
-                       C=slot(c1.weight).view(H, 3 * H), accumulate=True, col_map=(H, 3, 0), a_rowsum=slot(c1.bias))))
+        wgrads.append(wg_dec(c1, gh, sv.ya0s[r]))
         gy, go = gyn, gon
     K.gemm_grouped(wgrads)
 

@@ -139,6 +139,10 @@ __device__ __forceinline__ int64_t op_dst(const aw_operand_desc& d, uint32_t l) 
     }
     case 5:
       return (int64_t)l;
+    case 7: {   // tap-major storage (O, 3, I) -> [3 O][I], row j O + o
+      const uint32_t oj = l / I, i = l - oj * I, o = oj / 3u, j = oj - o * 3u;
+      return ((int64_t)j * O + o) * I + i;
+    }
     case 6: {   // (O, I, k) tap t -> K-step-major [I / 32][O][32]
       const uint32_t oi = l / k, j = l - oi * k;
       if (j != (uint32_t)d.tap) return -1;

@@ -75,6 +75,7 @@ __device__ __forceinline__ int64_t relayout_count(const aw_relayout_job& jb) {
     case 2: return (int64_t)3 * jb.O * jb.I;
     case 3: return (int64_t)jb.k * jb.O * jb.I;
     case 4: return (int64_t)jb.O * jb.ldo;
+    case 7: return (int64_t)3 * jb.O * jb.I;
     default: return (int64_t)jb.O * jb.I;   // 5 (copy), 6 (K-step-major tap)
   }
 }
@@ -109,6 +110,10 @@ __global__ __launch_bounds__(256) void relayout_batch_kernel(RelayoutJobs J) {
     } else if (mode == 4) {
       const uint32_t o = e / ldo, j = e - o * ldo;
       v = j < k ? W[o * k + j] : 0.f;
+    } else if (mode == 7) {    // tap-major storage (O, 3, I) -> [3O][I], row j O + o (declare_tap_major)
+      const uint32_t jo = e / I, i = e - jo * I;
+      const uint32_t j = jo / O, o = jo - j * O;
+      v = W[(o * 3 + j) * I + i];
     } else if (mode == 6) {    // K-step-major tap [I / 32][O][32] (the encoder chain's weight stream)
       const uint32_t s = e / (O * 32), r = e - s * O * 32;
       const uint32_t o = r >> 5, i = s * 32 + (r & 31);
@@ -721,14 +726,15 @@ extern "C" int aw_weight_relayout_batch(const aw_relayout_job* jobs, int n, int 
   int64_t most = 0;
   for (int i = 0; i < n; ++i) {
     const aw_relayout_job& jb = jobs[i];
-    AW_REQUIRE(jb.W && jb.out && jb.O > 0 && jb.I > 0 && jb.k > 0 && jb.mode >= 0 && jb.mode <= 6 && !(jb.mode == 6 && jb.I % 32),
+    AW_REQUIRE(jb.W && jb.out && jb.O > 0 && jb.I > 0 && jb.k > 0 && jb.mode >= 0 && jb.mode <= 7 && !(jb.mode == 6 && jb.I % 32),
                "aw_weight_relayout_batch: bad job %d", i);
     AW_REQUIRE(!(jb.mode == 4 && jb.ldo < jb.k), "aw_weight_relayout_batch: job %d ldo < k", i);
     AW_REQUIRE((int64_t)jb.O * jb.I * (jb.k > 3 ? jb.k : 3) < (1ll << 31) && (int64_t)jb.O * jb.ldo < (1ll << 31),
                "aw_weight_relayout_batch: job %d exceeds 2^31 elements", i);
     J.j[i] = jb;
     const int64_t c = jb.mode == 4 ? (int64_t)jb.O * jb.ldo
-                                    : (int64_t)jb.O * jb.I * (jb.mode == 0 || jb.mode >= 5 ? 1 : (jb.mode == 3 ? jb.k : 3));
+                                    : (int64_t)jb.O * jb.I * ((jb.mode == 0 || jb.mode == 5 || jb.mode == 6) ? 1
+                                                              : (jb.mode == 3 ? jb.k : 3));
     most = c > most ? c : most;
   }
   int gx = (int)((most + 255) / 256);

@@ -206,6 +206,11 @@ class VQVAEPatch(Autoencoder):
         an exactly-zero gradient.  The optimizer keeps those taps out of the all-reduce, clip norm and update."""
         return [blk.block[i].weight for blk in self.encoder[0].shared_conv for i in (1, 4)]
 
+    def tap_major_parameters(self):
+        """The decoder ResBlock k = 3 conv weights (vq_vae_patch_embedd.py:142-145 with :60-74): the optimizer stores
+        them (O, 3, I) so their weight-gradient GEMM writes contiguous rows (arcweld.optim.RAdam.declare_tap_major)."""
+        return [blk.block[i].weight for blk in self.decoder[1].shared_conv for i in (1, 4)]
+
     def backward_split_parameter(self):
         """First parameter (in registration order) whose gradient is final at fused_train_step's mid_hook (the
         residual VQ's codebooks are EMA buffers: the decoder's 1x1 conv comes first then)."""
