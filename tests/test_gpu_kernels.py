@@ -265,6 +265,46 @@ def test_gemm_grouped_weight_grads_match_single_launches(K, tile, dtype, conv):
         torch.testing.assert_close(bg.cpu(), bs.cpu(), rtol=1e-5, atol=1e-4)
 
 
+def _shift_taps(x, S):
+    """[tokens][cin] -> [tokens][3 cin]: tap j holds x[t + j - 1] inside each window of S tokens (zero across)."""
+    n, c = x.shape
+    w = x.view(n // S, S, c)
+    z = torch.zeros_like(w[:, :1])
+    prev = torch.cat([z, w[:, :-1]], 1)
+    nxt = torch.cat([w[:, 1:], z], 1)
+    return torch.cat([prev, w, nxt], 2).view(n, 3 * c)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("conv,G,Cout,Cin,Ntok", [(True, 4, 512, 512, 16 * 256), (False, 3, 320, 256, 16 * 300),
+                                                  (True, 2, 256, 128, 16 * 40)])
+def test_gemm_grouped_wgrad_tiles_vs_fp32_reference(dtype, conv, G, Cout, Cin, Ntok):
+    """aw_gemm_grouped at weight-gradient shapes against A^T B in fp32 on the same operands: contiguous rows (the
+    optimizer's tap-major decoder weights), the implicit k = 3 taps, ragged M, split token reductions meeting in the
+    accumulating atomics, bias row sums, accumulation into a non-zero C."""
+    from arcweld import kernels as K
+    S = 16
+    N = 3 * Cin if conv else Cin
+    probs, refs = [], []
+    for g in range(G):
+        A = _rand((Ntok, Cout), 60 + g, dtype)
+        x = _rand((Ntok, Cin), 70 + g, dtype)
+        C0 = _rand((Cout, N), 80 + g)
+        b0 = _rand((Cout,), 90 + g)
+        C, b = C0.clone(), b0.clone()
+        kw = dict(a_trans=True, b_trans=True, C=C, accumulate=True, a_rowsum=b)
+        if conv:
+            kw["conv"] = (Cin, S, 1, 1)
+        probs.append((A, x, Cout, N, Ntok, kw))
+        Bf = _shift_taps(x.float(), S) if conv else x.float()
+        refs.append((C, b, C0 + A.float().t() @ Bf, b0 + A.float().sum(0)))
+    K.gemm_grouped(probs)
+    rtol, atol = _tol(dtype, Ntok)
+    for C, b, Cr, br in refs:
+        torch.testing.assert_close(C, Cr, rtol=rtol, atol=atol * np.sqrt(Ntok) * 4)
+        torch.testing.assert_close(b, br, rtol=1e-5, atol=1e-3)
+
+
 @pytest.mark.parametrize("act", [0, 1])
 def test_gemm_bf16_pre_activation_operand(K, tile, act):
     """pre (the saved GELU pre-activation) may be bf16: identical to passing the same values as f32."""
