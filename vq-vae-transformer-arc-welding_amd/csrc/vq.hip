@@ -6,6 +6,8 @@
 // (torch's CPU sgemm on this shape is bit-identical to that chain -- measured), so the
 // argmin (lexicographic (d, k) minimum == torch.argmin first-index tie rule) is bit-exact.
 // No MFMA (the north-star design): fp32 VALU, whose rate equals the f32-input MFMA's on gfx950.
+#include <stdlib.h>
+
 #include "common.h"
 
 namespace {
@@ -23,46 +25,48 @@ namespace {
 // and the argmin the lexicographic (d, k) minimum (torch.argmin's first-index tie rule).  The register footprint
 // does not depend on D, so the stress codebook (K 8192 x D 256) runs at the same occupancy.
 constexpr int VQ_THREADS = 512;
-constexpr int VQ_ROWS = 64;
 constexpr int VQ_CODES = 512;
 constexpr int VQ_DC = 16;           // embedding floats per staged chunk
 
-template <int D> struct VqLds {
+template <int D, int ROWS> struct VqLds {
   static constexpr int ZP = D + 4;                                   // z image pitch (disjoint banks per row)
-  static constexpr int Z = VQ_ROWS * ZP;                             // floats
+  static constexpr int Z = ROWS * ZP;                                // floats
   static constexpr int E = VQ_DC * VQ_CODES;                         // floats per stage, [d][code]
-  static constexpr int TOTAL = Z + 2 * E + 2 * VQ_CODES + VQ_ROWS;   // + ee[2][512] + zz[64]
+  static constexpr int TOTAL = Z + 2 * E + 2 * VQ_CODES + ROWS;      // + ee[2][512] + zz[ROWS]
 };
 
 __device__ __forceinline__ bool lex_less(float d, int k, float bd, int bk) { return d < bd || (d == bd && k < bk); }
 
-template <int D>
+// RPL = rows per lane (ROWS = 8 RPL rows per workgroup): 8 for long row counts, 4 to put two workgroups on every CU
+// when N / 64 would leave the chip at one (the bench shape: N 16384 -> 512 workgroups of 32 rows)
+template <int D, int RPL>
 __global__ __launch_bounds__(VQ_THREADS, 2) void vq_fwd_kernel(const float* __restrict__ z,
                                                                const float* __restrict__ E, int64_t N, int K,
                                                                float* __restrict__ zq, int64_t* __restrict__ idx,
                                                                float* __restrict__ counts,
                                                                double* __restrict__ sqerr) {
-  using L = VqLds<D>;
+  constexpr int ROWS = 8 * RPL;
+  using L = VqLds<D, ROWS>;
   constexpr int ZP = L::ZP, ND = D / VQ_DC;
   __shared__ __attribute__((aligned(16))) float smem[L::TOTAL];
   float* zs = smem;
   float* es = smem + L::Z;                 // [2][VQ_DC][VQ_CODES]
   float* ees = es + 2 * L::E;              // [2][VQ_CODES]
-  float* zzs = ees + 2 * VQ_CODES;         // [VQ_ROWS]
+  float* zzs = ees + 2 * VQ_CODES;         // [ROWS]
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int lr = lane >> 3, lc = lane & 7;
-  const int64_t row0 = (int64_t)blockIdx.x * VQ_ROWS;
+  const int64_t row0 = (int64_t)blockIdx.x * ROWS;
 
   // ---- z tile -> LDS (rows beyond N are zero), |z|^2 per row
-  for (int i = tid; i < VQ_ROWS * (D / 4); i += VQ_THREADS) {
+  for (int i = tid; i < ROWS * (D / 4); i += VQ_THREADS) {
     const int r = i / (D / 4), q = i - r * (D / 4);
     const int64_t gr = row0 + r;
     const float4 v = gr < N ? reinterpret_cast<const float4*>(z + gr * D)[q] : make_float4(0.f, 0.f, 0.f, 0.f);
     *reinterpret_cast<float4*>(zs + r * ZP + 4 * q) = v;
   }
   __syncthreads();
-  if (tid < VQ_ROWS) {
+  if (tid < ROWS) {
     float s = 0.f;
     for (int d = 0; d < D; ++d) s = __fadd_rn(s, __fmul_rn(zs[tid * ZP + d], zs[tid * ZP + d]));
     zzs[tid] = s;
@@ -98,15 +102,15 @@ __global__ __launch_bounds__(VQ_THREADS, 2) void vq_fwd_kernel(const float* __re
     if (dc == ND - 1) ees[(ct & 1) * VQ_CODES + tid] = ee_acc;
   };
 
-  f32x2 acc[8][4];                 // [row i][code pair jp]: codes 8lc + 2jp, 8lc + 2jp + 1
+  f32x2 acc[RPL][4];               // [row i][code pair jp]: codes 8lc + 2jp, 8lc + 2jp + 1
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+  for (int i = 0; i < RPL; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x2{0.f, 0.f};
-  float best[8];
-  int bestk[8];
+  float best[RPL];
+  int bestk[RPL];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
+  for (int i = 0; i < RPL; ++i) {
     best[i] = __builtin_huge_valf();
     bestk[i] = 0x7fffffff;
   }
@@ -114,9 +118,9 @@ __global__ __launch_bounds__(VQ_THREADS, 2) void vq_fwd_kernel(const float* __re
   load(0);
   store(0);
   __syncthreads();
-  float zz[8];
+  float zz[RPL];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) zz[i] = zzs[lr + 8 * i];
+  for (int i = 0; i < RPL; ++i) zz[i] = zzs[lr + 8 * i];
 
   for (int st = 0; st < nsteps; ++st) {
     if (st + 1 < nsteps) load(st + 1);
@@ -125,16 +129,16 @@ __global__ __launch_bounds__(VQ_THREADS, 2) void vq_fwd_kernel(const float* __re
     const float* zb = zs + lr * ZP + dc * VQ_DC;
 #pragma unroll 1
     for (int q = 0; q < VQ_DC / 4; ++q) {   // not unrolled: hoisted operand reads of four steps would spill
-      float4 zv[8];
+      float4 zv[RPL];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) zv[i] = *reinterpret_cast<const float4*>(zb + 8 * i * ZP + 4 * q);
+      for (int i = 0; i < RPL; ++i) zv[i] = *reinterpret_cast<const float4*>(zb + 8 * i * ZP + 4 * q);
 #pragma unroll
       for (int dd = 0; dd < 4; ++dd) {
         const float4 e0 = *reinterpret_cast<const float4*>(eb + (4 * q + dd) * VQ_CODES);
         const float4 e1 = *reinterpret_cast<const float4*>(eb + (4 * q + dd) * VQ_CODES + 4);
         const f32x2 ep[4] = {f32x2{e0.x, e0.y}, f32x2{e0.z, e0.w}, f32x2{e1.x, e1.y}, f32x2{e1.z, e1.w}};
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
+        for (int i = 0; i < RPL; ++i) {
           const float zi = dd == 0 ? zv[i].x : dd == 1 ? zv[i].y : dd == 2 ? zv[i].z : zv[i].w;
           const f32x2 zp = f32x2{zi, zi};
 #pragma unroll
@@ -149,7 +153,7 @@ __global__ __launch_bounds__(VQ_THREADS, 2) void vq_fwd_kernel(const float* __re
         const int gk = ct * VQ_CODES + w * 64 + 8 * lc + j;
         const float e2 = eet[j];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
+        for (int i = 0; i < RPL; ++i) {
           const float dot = (j & 1) ? acc[i][j >> 1].y : acc[i][j >> 1].x;
           const float dist = __fsub_rn(__fadd_rn(zz[i], e2), __fmul_rn(2.f, dot));
           if (gk < K && lex_less(dist, gk, best[i], bestk[i])) {
@@ -159,7 +163,7 @@ __global__ __launch_bounds__(VQ_THREADS, 2) void vq_fwd_kernel(const float* __re
         }
       }
 #pragma unroll
-      for (int i = 0; i < 8; ++i)
+      for (int i = 0; i < RPL; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = f32x2{0.f, 0.f};
     }
@@ -169,7 +173,7 @@ __global__ __launch_bounds__(VQ_THREADS, 2) void vq_fwd_kernel(const float* __re
 
   // ---- argmin across the 8 code lanes of a row group, then across the 8 waves (LDS, the e stages are free)
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
+  for (int i = 0; i < RPL; ++i) {
 #pragma unroll
     for (int o = 1; o < 8; o <<= 1) {
       const float d = __shfl_xor(best[i], o, 64);
@@ -180,29 +184,30 @@ __global__ __launch_bounds__(VQ_THREADS, 2) void vq_fwd_kernel(const float* __re
       }
     }
   }
-  float* rd = es;                                        // [8 waves][64 rows]
-  int* rk = reinterpret_cast<int*>(es + 8 * VQ_ROWS);
+  float* rd = es;                                        // [8 waves][ROWS]
+  int* rk = reinterpret_cast<int*>(es + 8 * ROWS);
   if (lc == 0) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      rd[w * VQ_ROWS + lr + 8 * i] = best[i];
-      rk[w * VQ_ROWS + lr + 8 * i] = bestk[i];
+    for (int i = 0; i < RPL; ++i) {
+      rd[w * ROWS + lr + 8 * i] = best[i];
+      rk[w * ROWS + lr + 8 * i] = bestk[i];
     }
   }
   __syncthreads();
   if (w != 0) return;
   const int r = lane;
+  const bool live = r < ROWS;
   const int64_t row = row0 + r;
-  float bd = rd[r];
-  int bk = rk[r];
+  float bd = live ? rd[r] : 0.f;
+  int bk = live ? rk[r] : 0;
 #pragma unroll
   for (int v = 1; v < 8; ++v)
-    if (lex_less(rd[v * VQ_ROWS + r], rk[v * VQ_ROWS + r], bd, bk)) {
-      bd = rd[v * VQ_ROWS + r];
-      bk = rk[v * VQ_ROWS + r];
+    if (live && lex_less(rd[v * ROWS + r], rk[v * ROWS + r], bd, bk)) {
+      bd = rd[v * ROWS + r];
+      bk = rk[v * ROWS + r];
     }
   double se = 0.0;
-  if (row < N) {
+  if (live && row < N) {
     if (bk < 0 || bk >= K) bk = 0;  // all-NaN row guard (torch would return the NaN position)
     idx[row] = bk;
     atomicAdd(counts + bk, 1.0f);
@@ -290,15 +295,29 @@ extern "C" int aw_vq_forward(const float* z, const float* E, int64_t N, int K, i
              "aw_vq_forward: z/E/zq must be 16-B aligned");
   if (N == 0) return AW_OK;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  dim3 grid(aw_cdiv(N, VQ_ROWS));
+  // 64-row workgroups while they fill every CU twice; 32-row ones below that, where two of them fit one CU's LDS
+  // (D <= 64: 78 KB each) -- the bench shape N 16384 then runs 512 workgroups, two per CU
+  static int rows_env = -1;
+  if (rows_env < 0) {
+    const char* e = getenv("ARCWELD_VQ_ROWS");
+    rows_env = e ? atoi(e) : 0;
+  }
+  const bool half = rows_env ? rows_env == 32 : (N < 512 * 64 && D <= 64);
+  const dim3 grid(aw_cdiv(N, half ? 32 : 64));
+#define AW_VQ_CASE(DD)                                                                                               \
+  case DD:                                                                                                           \
+    if (half) hipLaunchKernelGGL((vq_fwd_kernel<DD, 4>), grid, dim3(VQ_THREADS), 0, s, z, E, N, K, zq, idx, counts, sqerr); \
+    else hipLaunchKernelGGL((vq_fwd_kernel<DD, 8>), grid, dim3(VQ_THREADS), 0, s, z, E, N, K, zq, idx, counts, sqerr);     \
+    break;
   switch (D) {
-    case 16: hipLaunchKernelGGL(vq_fwd_kernel<16>, grid, dim3(VQ_THREADS), 0, s, z, E, N, K, zq, idx, counts, sqerr); break;
-    case 32: hipLaunchKernelGGL(vq_fwd_kernel<32>, grid, dim3(VQ_THREADS), 0, s, z, E, N, K, zq, idx, counts, sqerr); break;
-    case 64: hipLaunchKernelGGL(vq_fwd_kernel<64>, grid, dim3(VQ_THREADS), 0, s, z, E, N, K, zq, idx, counts, sqerr); break;
-    case 128: hipLaunchKernelGGL(vq_fwd_kernel<128>, grid, dim3(VQ_THREADS), 0, s, z, E, N, K, zq, idx, counts, sqerr); break;
-    case 256: hipLaunchKernelGGL(vq_fwd_kernel<256>, grid, dim3(VQ_THREADS), 0, s, z, E, N, K, zq, idx, counts, sqerr); break;
+    AW_VQ_CASE(16)
+    AW_VQ_CASE(32)
+    AW_VQ_CASE(64)
+    AW_VQ_CASE(128)
+    AW_VQ_CASE(256)
     default: aw::set_error("aw_vq_forward: unsupported embedding dim %d (16/32/64/128/256)", D); return AW_ERR_ARG;
   }
+#undef AW_VQ_CASE
   return aw::check_launch("aw_vq_forward");
 }
 
