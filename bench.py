@@ -114,8 +114,7 @@ def transformer_workload(dev, rank, world, args, seqs, n_cycles, accumulate=1, l
     g.manual_seed(2000 + rank)
     wins = [torch.randn(seqs, 200 * nc, 2, device=dev, generator=g) for _ in range(2)]
     cond = torch.zeros(seqs, dtype=torch.long, device=dev)
-    use_graph = not args.no_graph and accumulate == 1
-    static_w = wins[0].clone()
+    use_graph = not args.no_graph
 
     def train(w):
         ids = tokenize.encode_ids(vq, w)
@@ -124,18 +123,22 @@ def transformer_workload(dev, rank, world, args, seqs, n_cycles, accumulate=1, l
 
     batches = [train(w) for w in wins] if pretokenized else None
 
+    def group(src, i):   # the micro-batches of optimizer step i (one, or an accumulation group)
+        g = [src[(i + j) % 2] for j in range(accumulate)]
+        return g if accumulate > 1 else g[0]
+
     def step(i):
         if pretokenized:
             if use_graph:
-                tr.graphed_step(dec, batches[i % 2], 1.0 / world)
+                tr.graphed_step(dec, group(batches, i), 1.0 / (accumulate * world))
             else:
                 for j in range(accumulate):
                     tr.micro_step(dec, batches[(i + j) % 2], j, 1.0 / (accumulate * world))
                 tr.optimizer_step(dec)
         elif use_graph:
-            # tokenization is captured with the step: the static window buffer feeds the encoder inside g1
-            static_w.copy_(wins[i % 2])
-            tr.graphed_step(dec, static_w, 1.0 / world)
+            # tokenization is captured with the step: the static window buffer feeds the encoder inside g1, once
+            # per micro-batch of the group
+            tr.graphed_step(dec, group(wins, i), 1.0 / (accumulate * world))
         else:
             for j in range(accumulate):
                 tr.micro_step(dec, train(wins[(i + j) % 2]), j, 1.0 / (accumulate * world))

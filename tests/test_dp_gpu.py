@@ -116,7 +116,9 @@ def _reference(name, make, batches):
 
 def test_data_parallel_world2_matches_gradient_mean_reference():
     port = _free_port()
-    out = mp.Manager().dict()
+    # the manager's server process is spawned, not forked: a fork of this process (which may already hold the GPU
+    # from earlier tests) can crash in the child's garbage collector
+    out = mp.get_context("spawn").Manager().dict()
     mp.spawn(_worker, args=(2, port, out), nprocs=2, join=True)
     for name, make, batches in (("vqvae", _vqvae, _vq_batches()), ("decoder", _decoder, _dec_batches())):
         ref = _reference(name, make, batches)

@@ -9,7 +9,8 @@ where its ``backward_late_parameters()`` are final (VQ-VAE: the decoder side; Tr
 the later half of the blocks): their all-reduce is launched (async, RCCL stream) between the two replays and
 overlaps the rest of the backward; the remaining gradients' all-reduce follows.  Replay needs no host values: dropout masks come from
 a device counter (aw_gemm_args.seed_ptr), the RAdam step number and clip coefficient live on the device.  Inputs
-are copied into static buffers before each replay.
+are copied into static buffers before each replay; with gradient accumulation the forward/backward graphs are
+replayed once per micro-batch before the update.
 
 The first `warmup` calls run eagerly on their own batches (lazy device state -- RNG counters, optimizer
 buffers -- is created there); the next call captures and replays, so every call is exactly one step on the
@@ -75,26 +76,36 @@ class StepGraphs:
             self.trainer._update(self.model)
 
     def run(self, batch):
+        """One optimizer step over `batch`, or over a list of micro-batches (accumulate_grad_batches > 1: the
+        forward/backward graph is replayed once per micro-batch, gradients accumulating in the flat buffer; the
+        all-reduce runs once, split around the last micro-batch's backward -- DDP's no_sync accumulation)."""
+        batches = batch if isinstance(batch, list) else [batch]
         self.calls += 1
         if self.calls <= self.warmup:
-            loss = self.trainer.micro_step(self.model, batch, 0, self.scale)
+            for j, b in enumerate(batches):
+                loss = self.trainer.micro_step(self.model, b, j, self.scale)
             for w in self.allreduce("all"):
                 w.wait()
             self.trainer._update(self.model)
             self.trainer.global_step += 1
             return loss
         if self.static is None:
-            self._capture(batch)
-        else:
-            _copy_into(self.static, batch)
-        if self.split:
-            self.g1a.replay()
-            works = self.allreduce("late")       # decoder side: overlaps the encoder-side backward below
-            self.g1b.replay()
-            works += self.allreduce("early")
-        else:
-            self.g1.replay()
-            works = self.allreduce("all")
+            self._capture(batches[0])
+        last = len(batches) - 1
+        works = []
+        for j, b in enumerate(batches):
+            _copy_into(self.static, b)        # ordered after the previous replay on this stream
+            if self.split:
+                self.g1a.replay()
+                if j == last:
+                    works = self.allreduce("late")       # decoder side: overlaps the encoder-side backward below
+                self.g1b.replay()
+                if j == last:
+                    works += self.allreduce("early")
+            else:
+                self.g1.replay()
+                if j == last:
+                    works = self.allreduce("all")
         for w in works:
             w.wait()
         self.g2.replay()

@@ -91,7 +91,7 @@ class Trainer:
         self.accumulate = max(1, int(accumulate_grad_batches))
         self.log_every = log_every_n_steps
         self.fused_grad_sink = fused_grad_sink
-        self.hip_graphs = hip_graphs   # capture the step (needs accumulate_grad_batches == 1, fixed batch shape)
+        self.hip_graphs = hip_graphs   # capture the step (fixed batch shape; accumulation groups replay per micro-batch)
         self.global_step = 0
         self.history = []
         self.optimizer = None
@@ -153,8 +153,9 @@ class Trainer:
         self.global_step += 1
 
     def graphed_step(self, model, batch, scale):
-        """One full optimizer step (accumulate_grad_batches == 1) replayed from captured HIP graphs; the first
-        call warms up eagerly and captures.  Returns the (static) loss tensor."""
+        """One full optimizer step replayed from captured HIP graphs: `batch` is one micro-batch, or the list of
+        micro-batches of one accumulation group (their forward/backward graph replayed once each, then one update).
+        The first calls warm up eagerly and capture.  Returns the (static) loss tensor."""
         from .graphs import StepGraphs
         if getattr(self, "_graphs", None) is None or self._graphs.model is not model:
             self._graphs = StepGraphs(self, model, scale, lambda region: self._allreduce_region(model, region))
@@ -199,12 +200,25 @@ class Trainer:
             if hasattr(loader, "set_epoch"):
                 loader.set_epoch(epoch)
             n = len(loader) if hasattr(loader, "__len__") else None
+            group = []          # micro-batches of the current accumulation group (captured path)
             for i, batch in enumerate(loader):
                 batch = _to_device(batch, dev)
                 # a residual-VQ model synchronises its codebooks with host-issued collectives in the forward
                 # (arcweld/residual_vq.py): eager steps when data parallel
                 graphable = not (getattr(model, "use_improved_vq", False) and self.world() > 1)
-                if self.hip_graphs and graphable and self.accumulate == 1 and _fixed_shape(self, batch):
+                graphed = self.hip_graphs and graphable and _fixed_shape(self, batch)
+                if not graphed and group:
+                    # a batch the captured step cannot take (e.g. a ragged last batch): the group so far runs
+                    # eagerly, accumulating into the same gradients, and the eager path below takes over
+                    for j, b in enumerate(group):
+                        self.micro_step(model, b, j, scale)
+                    group = []
+                if graphed:
+                    # Lightning steps on every accumulate-th batch and on the last batch of the epoch
+                    group.append(batch)
+                    if len(group) < self.accumulate and not (n is not None and i + 1 == n):
+                        continue
+                    batch, group = (group if self.accumulate > 1 else group[0]), []
                     loss = self.graphed_step(model, batch, scale)
                     if self.global_step % self.log_every == 0:
                         # the captured step's static loss tensor holds this replay's value
