@@ -134,8 +134,9 @@ __device__ __forceinline__ void store4_bf16(bf16* dst, const f32x16& a, int g4, 
 __global__ __launch_bounds__(256, 2) void attn_fwd_mfma_kernel(const bf16* __restrict__ qkv, int T_, int nh, int d,
                                                             bf16* __restrict__ y, float* __restrict__ lse,
                                                             float c2, float scale) {
-  __shared__ __attribute__((aligned(16))) char Ks[IMG];
-  __shared__ __attribute__((aligned(16))) char Vs[IMG];
+  // K/V images double-buffered (tile t in buffer t & 1): storing tile t cannot race the reads of tile t - 1, so one
+  // barrier per tile publishes it
+  __shared__ __attribute__((aligned(16))) char KV[4 * IMG];
   const int nqb = (T_ + BLK - 1) / BLK;
   const BlockId id(nqb, nh);
   const int qb = nqb - 1 - id.x;  // longest key ranges first
@@ -157,7 +158,8 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_mfma_kernel(const bf16* __res
   tile_load(vr, base, ld, 2 * d + h * HS, 0, T_, tid);
   for (int t = 0; t < nt; ++t) {
     const int k0 = t * TILE;
-    __syncthreads();
+    char* Ks = KV + (t & 1) * 2 * IMG;
+    char* Vs = Ks + IMG;
     tile_store(kr, Ks, tid);
     tile_store(vr, Vs, tid);
     __syncthreads();
@@ -239,8 +241,7 @@ __global__ __launch_bounds__(256, 2) void attn_dq_mfma_kernel(const bf16* __rest
                                                            const bf16* __restrict__ y, const float* __restrict__ lse,
                                                            float* __restrict__ delta, int T_, int nh, int d,
                                                            bf16* __restrict__ dqkv, float c2, float scale) {
-  __shared__ __attribute__((aligned(16))) char Ks[IMG];
-  __shared__ __attribute__((aligned(16))) char Vs[IMG];
+  __shared__ __attribute__((aligned(16))) char KV[4 * IMG];   // double-buffered K/V images, as in the forward
   const int nqb = (T_ + BLK - 1) / BLK;
   const BlockId id(nqb, nh);
   const int qb = nqb - 1 - id.x;
@@ -280,7 +281,8 @@ __global__ __launch_bounds__(256, 2) void attn_dq_mfma_kernel(const bf16* __rest
   tile_load(vr, base, ld, 2 * d + h * HS, 0, T_, tid);
   for (int t = 0; t < nt; ++t) {
     const int k0 = t * TILE;
-    __syncthreads();
+    char* Ks = KV + (t & 1) * 2 * IMG;
+    char* Vs = Ks + IMG;
     tile_store(kr, Ks, tid);
     tile_store(vr, Vs, tid);
     __syncthreads();
@@ -331,10 +333,9 @@ __global__ __launch_bounds__(256, 2) void attn_dkv_mfma_kernel(const bf16* __res
                                                             const float* __restrict__ lse,
                                                             const float* __restrict__ delta, int T_, int nh, int d,
                                                             bf16* __restrict__ dqkv, float c2, float scale) {
-  __shared__ __attribute__((aligned(16))) char Qs[IMG];
-  __shared__ __attribute__((aligned(16))) char Gs[IMG];
-  __shared__ __attribute__((aligned(16))) float Ls[TILE];
-  __shared__ __attribute__((aligned(16))) float Ds[TILE];
+  // double-buffered per query tile: Q image, dO image, lse and delta rows (one barrier per tile, as in the forward)
+  __shared__ __attribute__((aligned(16))) char QG[4 * IMG];
+  __shared__ __attribute__((aligned(16))) float LD[4 * TILE];
   const BlockId id((T_ + BLK - 1) / BLK, nh);
   const int kb = id.x;  // early key blocks see the most queries: launched first
   const int h = id.h, b = id.b;
@@ -366,7 +367,11 @@ __global__ __launch_bounds__(256, 2) void attn_dkv_mfma_kernel(const bf16* __res
   };
   load(qstart);
   for (int q0 = qstart; q0 < T_; q0 += TILE) {
-    __syncthreads();
+    const int bsel = ((q0 - qstart) / TILE) & 1;
+    char* Qs = QG + bsel * 2 * IMG;
+    char* Gs = Qs + IMG;
+    float* Ls = LD + bsel * 2 * TILE;
+    float* Ds = Ls + TILE;
     tile_store(qr, Qs, tid);
     tile_store(gr, Gs, tid);
     if (tid < TILE) {
