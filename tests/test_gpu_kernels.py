@@ -276,14 +276,15 @@ def _shift_taps(x, S):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("conv,G,Cout,Cin,Ntok", [(True, 4, 512, 512, 16 * 256), (False, 3, 320, 256, 16 * 300),
-                                                  (True, 2, 256, 128, 16 * 40)])
-def test_gemm_grouped_wgrad_tiles_vs_fp32_reference(dtype, conv, G, Cout, Cin, Ntok):
+@pytest.mark.parametrize("conv,G,Cout,Cin,Ntok,S", [(True, 4, 512, 512, 16 * 256, 16), (False, 3, 320, 256, 16 * 300, 16),
+                                                    (True, 2, 256, 128, 16 * 40, 16), (True, 3, 200, 192, 40 * 21, 40),
+                                                    (True, 2, 136, 64, 8 * 77, 8)])
+def test_gemm_grouped_wgrad_tiles_vs_fp32_reference(dtype, conv, G, Cout, Cin, Ntok, S):
     """aw_gemm_grouped at weight-gradient shapes against A^T B in fp32 on the same operands: contiguous rows (the
     optimizer's tap-major decoder weights), the implicit k = 3 taps, ragged M, split token reductions meeting in the
-    accumulating atomics, bias row sums, accumulation into a non-zero C."""
+    accumulating atomics, bias row sums, accumulation into a non-zero C; windows of 8, 16 and 40 tokens, ragged M
+    and token counts that are not whole 64-token steps (the bf16 conv forms run the three-tap tile)."""
     from arcweld import kernels as K
-    S = 16
     N = 3 * Cin if conv else Cin
     probs, refs = [], []
     for g in range(G):
