@@ -73,25 +73,52 @@ void dispatch(const GemmP& P, hipStream_t s, bool ragged) {
 }
 
 
-// sum of the split-K slabs -> C (accumulate mode: += through the column map; else alpha*sum + beta*C)
+// sum of the split-K slabs -> C (accumulate mode: += through the column map; else alpha*sum + beta*C).
+// Four consecutive elements per thread (N % 4 == 0: float4 slab loads) and four independent partial sums over the
+// splits, so a thread keeps its slab loads in flight instead of waiting on one add chain per split.
+__device__ __forceinline__ void reduce_store(const aw_gemm_args& p, float* C, int64_t r, int c, float acc) {
+  if (p.accumulate) {
+    const int64_t oc = p.col_mod > 0 ? (int64_t)(c % p.col_mod) * p.col_mul + c / p.col_mod + p.col_off
+                                     : (int64_t)c * (p.col_mul > 0 ? p.col_mul : 1) + p.col_off;
+    C[r * p.ldc + oc] += p.alpha * acc;
+  } else {
+    float v = p.alpha * acc;
+    if (p.beta != 0.f) v += p.beta * C[r * p.ldc + c];
+    C[r * p.ldc + c] = v;
+  }
+}
+
 __global__ __launch_bounds__(256) void gemm_reduce_kernel(const float* __restrict__ ws, int splits, int M, int N,
                                                           aw_gemm_args p) {
   const int64_t n = (int64_t)M * N;
   float* C = reinterpret_cast<float*>(p.C);
+  if ((N & 3) == 0) {
+    const int64_t n4 = n >> 2;
+    const f32x4* w4 = reinterpret_cast<const f32x4*>(ws);
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n4; q += (int64_t)gridDim.x * blockDim.x) {
+      f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0, a2 = a0, a3 = a0;
+      int s = 0;
+      for (; s + 4 <= splits; s += 4) {
+        a0 += w4[(s + 0) * n4 + q];
+        a1 += w4[(s + 1) * n4 + q];
+        a2 += w4[(s + 2) * n4 + q];
+        a3 += w4[(s + 3) * n4 + q];
+      }
+      for (; s < splits; ++s) a0 += w4[s * n4 + q];
+      const f32x4 acc = (a0 + a1) + (a2 + a3);
+      const int64_t e = q << 2;
+      const int64_t r = e / N;
+      const int c = (int)(e - r * N);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) reduce_store(p, C, r, c + k, acc[k]);
+    }
+    return;
+  }
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
     float acc = 0.f;
     for (int s = 0; s < splits; ++s) acc += ws[s * n + e];
     const int64_t r = e / N;
-    const int c = (int)(e - r * N);
-    if (p.accumulate) {
-      const int64_t oc = p.col_mod > 0 ? (int64_t)(c % p.col_mod) * p.col_mul + c / p.col_mod + p.col_off
-                                       : (int64_t)c * (p.col_mul > 0 ? p.col_mul : 1) + p.col_off;
-      C[r * p.ldc + oc] += p.alpha * acc;
-    } else {
-      float v = p.alpha * acc;
-      if (p.beta != 0.f) v += p.beta * C[r * p.ldc + c];
-      C[r * p.ldc + c] = v;
-    }
+    reduce_store(p, C, r, (int)(e - r * N), acc);
   }
 }
 
@@ -249,7 +276,7 @@ extern "C" int aw_gemm_ws(const aw_gemm_args* args, float* ws, int64_t ws_elems,
     dispatch<float>(P, s, ragged);
   if (P.ws) {
     const int64_t n = (int64_t)a.M * a.N;
-    int64_t g = (n + 255) / 256;
+    int64_t g = ((a.N & 3) == 0 ? n / 4 + 255 : n + 255) / 256;
     if (g > 2048) g = 2048;
     hipLaunchKernelGGL(gemm_reduce_kernel, dim3((int)g), dim3(256), 0, s, P.ws, P.splits, a.M, a.N, a);
   }
