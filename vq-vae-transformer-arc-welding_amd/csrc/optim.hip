@@ -57,6 +57,18 @@ __device__ __forceinline__ int next_seg(const int64_t* off, int nseg, int s, int
   return s;
 }
 
+// Segment table of the grad-norm pass in LDS (offsets and the end of the live part -- the segment's start when the
+// segment is inactive, so one compare decides): the per-element tests are LDS reads, so an iteration's gradient loads
+// no longer wait on global reads of the table (35.8 -> 23.8 us).  The update kernels keep only the offsets in LDS:
+// the larger table cost them more in occupancy than the lookups saved (123 -> 142 us, same-box A/B).
+__device__ __forceinline__ void load_segs(const int64_t* __restrict__ off, const int64_t* __restrict__ len,
+                                          const int* __restrict__ active, int nseg, int64_t* s_off, int64_t* s_end) {
+  for (int i = threadIdx.x; i < nseg; i += blockDim.x) {
+    s_off[i] = off[i];
+    s_end[i] = active[i] ? off[i] + len[i] : off[i];
+  }
+}
+
 __device__ __forceinline__ float radam_one(float gr, float& pv, float& mv, float& vv, float wd, float gs,
                                            const RAdamScalars& S) {
   gr = gs == 1.0f ? gr : gr * gs;
@@ -220,8 +232,8 @@ __global__ __launch_bounds__(256) void sumsq_kernel(const float* __restrict__ g,
                                                     const int64_t* __restrict__ seg_len,
                                                     const int* __restrict__ seg_active, int nseg, int64_t total,
                                                     double* ws) {
-  __shared__ int64_t s_off[MAXSEG_LDS];
-  for (int i = threadIdx.x; i < nseg; i += blockDim.x) s_off[i] = seg_off[i];
+  __shared__ int64_t s_off[MAXSEG_LDS], s_end[MAXSEG_LDS];
+  load_segs(seg_off, seg_len, seg_active, nseg, s_off, s_end);
   __syncthreads();
   float acc = 0.f;
   const int64_t n4 = total >> 2;
@@ -238,7 +250,7 @@ __global__ __launch_bounds__(256) void sumsq_kernel(const float* __restrict__ g,
       use[u] = false;
       if (q < n4) {
         s = next_seg(s_off, nseg, s, e);
-        use[u] = seg_active[s] && e < s_off[s] + seg_len[s];
+        use[u] = e < s_end[s];
       }
       v[u] = use[u] ? reinterpret_cast<const float4*>(g)[q] : make_float4(0.f, 0.f, 0.f, 0.f);
     }
