@@ -282,7 +282,7 @@ int aw_radam_step(float* param, float* grad, float* exp_avg, float* exp_avg_sq, 
  * produce from the new values), so the training step needs no relayout launch.  ops: device array of
  * AW_OPS_PER_SEG descriptors per segment (ops[AW_OPS_PER_SEG*s + j]; mode -1 = none): flat element l of segment s
  * (the parameter in its storage order: (O, I, k) contiguous; a declare_centre_tap segment is its [O][I] centre,
- * described as k = 1, tap = 0) goes to `out` at the index of relayout mode `mode` (0-6), cast to `dtype`. */
+ * described as k = 1, tap = 0) goes to `out` at the index of relayout mode `mode` (0-7), cast to `dtype`. */
 #define AW_OPS_PER_SEG 2
 typedef struct {
   void* out;

@@ -52,20 +52,31 @@ __device__ __forceinline__ int find_seg(const int64_t* off, int nseg, int64_t e)
 
 // Segment of element e for a thread whose elements only increase (grid-stride loops): advance from the last one
 // (amortised O(1); the binary search per element it replaces made both kernels ALU-bound).
-__device__ __forceinline__ int next_seg(const int64_t* off, int nseg, int s, int64_t e) {
+template <typename Off>
+__device__ __forceinline__ int next_seg(const Off* off, int nseg, int s, int64_t e) {
   while (s + 1 < nseg && off[s + 1] <= e) ++s;
   return s;
 }
 
 // Segment table of the grad-norm pass in LDS (offsets and the end of the live part -- the segment's start when the
 // segment is inactive, so one compare decides): the per-element tests are LDS reads, so an iteration's gradient loads
-// no longer wait on global reads of the table (35.8 -> 23.8 us).  The update kernels keep only the offsets in LDS:
-// the larger table cost them more in occupancy than the lookups saved (123 -> 142 us, same-box A/B).
+// no longer wait on global reads of the table (35.8 -> 23.8 us).  The operand-writing update kernel keeps the same
+// table as 32-bit offsets (load_segs32, 8 KB of LDS: 125 -> 120.5 us, same-box A/B; the 16 KB int64 table cost it
+// more in occupancy than the lookups saved, 123 -> 142 us).
 __device__ __forceinline__ void load_segs(const int64_t* __restrict__ off, const int64_t* __restrict__ len,
                                           const int* __restrict__ active, int nseg, int64_t* s_off, int64_t* s_end) {
   for (int i = threadIdx.x; i < nseg; i += blockDim.x) {
     s_off[i] = off[i];
     s_end[i] = active[i] ? off[i] + len[i] : off[i];
+  }
+}
+
+// The same table as 32-bit element offsets (total < 2^31): the update kernels' LDS stays 8 KB.
+__device__ __forceinline__ void load_segs32(const int64_t* __restrict__ off, const int64_t* __restrict__ len,
+                                            const int* __restrict__ active, int nseg, int* s_off, int* s_end) {
+  for (int i = threadIdx.x; i < nseg; i += blockDim.x) {
+    s_off[i] = (int)off[i];
+    s_end[i] = (int)(active[i] ? off[i] + len[i] : off[i]);
   }
 }
 
@@ -175,6 +186,28 @@ __device__ __forceinline__ void op_store(const aw_operand_desc& d, uint32_t l, f
     reinterpret_cast<float*>(d.out)[t] = v;
 }
 
+// The four elements l0..l0+3 of one float4 (l0 % 4 == 0, all inside the segment): one 8-B (bf16) or 16-B (f32)
+// store when their operand positions are consecutive -- plain casts (mode 5, a k = 1 matrix in mode 0) and the
+// tap-major input-gradient copy (mode 7, rows of I % 4 == 0) -- else four element stores.  The element stores
+// left the copies at under 1 TB/s (a 2-B store per lane).
+__device__ __forceinline__ void op_store4(const aw_operand_desc& d, uint32_t l0, const float (&pv)[4]) {
+  int64_t t0 = -1;
+  if (d.mode == 5 || (d.mode == 0 && d.k == 1 && d.tap == 0)) t0 = l0;
+  else if (d.mode == 7 && (d.I & 3) == 0) t0 = op_dst(d, l0);
+  if (t0 >= 0 && ((uintptr_t)d.out & 15) == 0) {
+    if (d.dtype == AW_BF16) {
+      typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+      bf16x4 h = {(bf16)pv[0], (bf16)pv[1], (bf16)pv[2], (bf16)pv[3]};
+      reinterpret_cast<bf16x4*>(d.out)[t0 >> 2] = h;
+    } else {
+      reinterpret_cast<float4*>(d.out)[t0 >> 2] = make_float4(pv[0], pv[1], pv[2], pv[3]);
+    }
+    return;
+  }
+#pragma unroll
+  for (int c = 0; c < 4; ++c) op_store(d, l0 + c, pv[c]);
+}
+
 // radam_kernel that also refreshes the operand copies of every updated element (up to AW_OPS_PER_SEG per segment,
 // ops[AW_OPS_PER_SEG * s + j], mode < 0 = unused): the per-step relayout launch of the forward disappears and the
 // updated weights are cast while still in registers.
@@ -187,20 +220,20 @@ __global__ __launch_bounds__(256) void radam_ops_kernel(float* __restrict__ p, f
                                                         RAdamScalars S, const float* __restrict__ gscale,
                                                         const int64_t* __restrict__ step_ptr,
                                                         const aw_operand_desc* __restrict__ ops, int zero_g) {
-  __shared__ int64_t s_off[MAXSEG_LDS];
+  __shared__ int s_off[MAXSEG_LDS], s_end[MAXSEG_LDS];
   __shared__ RAdamScalars s_S;
-  for (int i = threadIdx.x; i < nseg; i += blockDim.x) s_off[i] = seg_off[i];
+  load_segs32(seg_off, seg_len, seg_active, nseg, s_off, s_end);
   if (step_ptr && threadIdx.x == 0) s_S = radam_scalars(*step_ptr, S.lr, S.beta1, S.beta2, S.eps);
   __syncthreads();
   if (step_ptr) S = s_S;
   const float gs = gscale ? gscale[0] : 1.0f;
-  const int64_t n4 = total >> 2;
+  const int n4 = (int)(total >> 2);
   int s = 0;
-  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n4; q += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t e = q << 2;
+  for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < n4; q += gridDim.x * blockDim.x) {
+    const int e = q << 2;
     s = next_seg(s_off, nseg, s, e);
-    const int64_t len = seg_len[s];
-    if (e >= s_off[s] + len || !seg_active[s]) continue;
+    const int end = s_end[s];
+    if (e >= end) continue;   // past the segment's live part (or an inactive segment): no global read decides it
     const float wd = seg_wd[s];
     const float4 g4 = reinterpret_cast<const float4*>(g)[q];
     float4 p4 = reinterpret_cast<const float4*>(p)[q];
@@ -215,14 +248,19 @@ __global__ __launch_bounds__(256) void radam_ops_kernel(float* __restrict__ p, f
     reinterpret_cast<float4*>(v)[q] = v4;
     if (zero_g) reinterpret_cast<float4*>(g)[q] = make_float4(0.f, 0.f, 0.f, 0.f);   // zero_grad, fused
     const uint32_t l0 = (uint32_t)(e - s_off[s]);
+    const int64_t len = end - s_off[s];
     const float pv[4] = {p4.x, p4.y, p4.z, p4.w};
 #pragma unroll
     for (int j = 0; j < AW_OPS_PER_SEG; ++j) {
       const aw_operand_desc d = ops[AW_OPS_PER_SEG * s + j];
       if (d.mode < 0) continue;
+      if ((int64_t)l0 + 4 <= len) {
+        op_store4(d, l0, pv);
+      } else {
 #pragma unroll
-      for (int c = 0; c < 4; ++c)
-        if ((int64_t)l0 + c < len) op_store(d, l0 + c, pv[c]);   // past seg_len: alignment padding
+        for (int c = 0; c < 4; ++c)
+          if ((int64_t)l0 + c < len) op_store(d, l0 + c, pv[c]);   // past seg_len: alignment padding
+      }
     }
   }
 }
@@ -320,6 +358,7 @@ extern "C" int aw_radam_step_ops(float* param, float* grad, float* exp_avg, floa
              "aw_radam_step_ops: null pointer");
   AW_REQUIRE(nseg > 0 && nseg <= MAXSEG_LDS, "aw_radam_step_ops: nseg must be in [1, %d]", MAXSEG_LDS);
   AW_REQUIRE((step_ptr || step >= 1) && total >= 0, "aw_radam_step_ops: step counts from 1");
+  AW_REQUIRE(total < ((int64_t)1 << 31), "aw_radam_step_ops: total must be < 2^31 elements");
   AW_REQUIRE(total % 4 == 0 && ((uintptr_t)param & 15) == 0 && ((uintptr_t)grad & 15) == 0 &&
                  ((uintptr_t)exp_avg & 15) == 0 && ((uintptr_t)exp_avg_sq & 15) == 0,
              "aw_radam_step_ops: flat buffers must be 16-B aligned with total %% 4 == 0");
