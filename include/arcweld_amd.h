@@ -134,6 +134,10 @@ int aw_encoder_chain_fwd(const aw_encoder_chain_args* args, void* stream);
  */
 int aw_vq_forward(const float* z, const float* E, int64_t N, int K, int D,
                   float* zq, int64_t* idx, float* counts, double* sqerr, void* stream);
+/* aw_vq_forward that also writes z_q_ste into zq_copy (NULL = none; 16-B aligned, copy_dtype AW_BF16 or AW_F32):
+ * the GEMM operand of the decoder's first conv, without a separate cast launch. */
+int aw_vq_forward_ex(const float* z, const float* E, int64_t N, int K, int D, float* zq, int64_t* idx, float* counts,
+                     double* sqerr, void* zq_copy, int copy_dtype, void* stream);
 /* loss = m + beta*m with m = sqerr/(N*D) (vector_quantizer.py:107-108); perplexity = exp(-sum p log(p+1e-10)),
  * p = counts/N (:114-115).  Each output is one f32 device scalar. */
 int aw_vq_finalize(const float* counts, const double* sqerr, int64_t N, int K, int D, float beta,
@@ -142,6 +146,11 @@ int aw_vq_finalize(const float* counts, const double* sqerr, int64_t N, int K, i
  * g_zq may be NULL (treated as 0); g_loss is a device scalar.  dE is accumulated (not overwritten). */
 int aw_vq_backward(const float* z, const float* E, const int64_t* idx, const float* g_zq, const float* g_loss,
                    int64_t N, int K, int D, float beta, float* dz, float* dE, void* stream);
+/* aw_vq_backward that also writes dz into dz_copy (NULL = none; copy_dtype AW_BF16 or AW_F32): the operand of the
+ * SepCNN backward GEMMs. */
+int aw_vq_backward_ex(const float* z, const float* E, const int64_t* idx, const float* g_zq, const float* g_loss,
+                      int64_t N, int K, int D, float beta, float* dz, float* dE, void* dz_copy, int copy_dtype,
+                      void* stream);
 /* ------------------------------------------------------------------ residual VQ with EMA codebooks (csrc/rvq.hip)
  * ResidualVQLightning (model/vector_quantizer.py:9-56) wraps vector-quantize-pytorch's ResidualVQ (third-party, not
  * installed here: its published algorithm is restated, parity unpinned).  Per layer i: aw_vq_forward on residual r_i

@@ -203,6 +203,34 @@ def test_vq_small_forward_backward_vs_reference(K):
     assert oh.sum().item() == N
 
 
+@pytest.mark.parametrize("cdt", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("Kc,D,N", [(512, 64, 16384), (64, 16, 1000)])
+def test_vq_operand_copies_match_the_cast_outputs(K, cdt, Kc, D, N):
+    """aw_vq_forward_ex / aw_vq_backward_ex: the operand copies are exactly the cast of z_q and dz (the step's cast
+    launches they replace), and the primary outputs are unchanged by writing them."""
+    z = torch.tensor(gen.normal(301, (N, D), 0.08), device=DEV)
+    E = torch.tensor(gen.normal(302, (Kc, D), 0.08), device=DEV)
+    outs = []
+    for copy in (False, True):
+        zq, idx = torch.empty_like(z), torch.empty(N, dtype=torch.int64, device=DEV)
+        counts, sq = torch.zeros(Kc, device=DEV), torch.zeros(1, dtype=torch.float64, device=DEV)
+        zc = torch.full((N, D), float("nan"), device=DEV, dtype=cdt) if copy else None
+        K.vq_forward(z, E, zq, idx, counts, sq, zq_copy=zc)
+        g_zq = torch.tensor(gen.normal(303, (N, D), 1.0), device=DEV)
+        dz, dE = torch.empty_like(z), torch.zeros_like(E)
+        dc = torch.full((N, D), float("nan"), device=DEV, dtype=cdt) if copy else None
+        K.vq_backward(z, E, idx, g_zq, torch.tensor([1.5], device=DEV), 0.25, dz, dE, dz_copy=dc)
+        outs.append((zq, idx, counts, sq, dz, dE))
+        if copy:
+            assert torch.equal(zc, zq.to(cdt))
+            assert torch.equal(dc, dz.to(cdt))
+    for i, (a, b) in enumerate(zip(*outs)):
+        if i in (3, 5):   # sqerr (f64) and dE (f32): atomics, summation order differs run to run
+            torch.testing.assert_close(a, b, rtol=1e-6, atol=1e-9)
+        else:
+            assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("use_ws", [True, False])
 def test_gemm_split_k_accumulate_colmap(K, tile, dtype, use_ws):

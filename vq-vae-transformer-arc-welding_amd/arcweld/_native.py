@@ -90,8 +90,10 @@ SIGNATURES = {
     "aw_gemm_set_tile": [c_int],
     "aw_weight_relayout_batch": [ctypes.POINTER(RelayoutJob), c_int, c_int, c_p],
     "aw_vq_forward": [c_p, c_p, c_i64, c_int, c_int, c_p, c_p, c_p, c_p, c_p],
+    "aw_vq_forward_ex": [c_p, c_p, c_i64, c_int, c_int, c_p, c_p, c_p, c_p, c_p, c_int, c_p],
     "aw_vq_finalize": [c_p, c_p, c_i64, c_int, c_int, c_f, c_p, c_p, c_p],
     "aw_vq_backward": [c_p, c_p, c_p, c_p, c_p, c_i64, c_int, c_int, c_f, c_p, c_p, c_p],
+    "aw_vq_backward_ex": [c_p, c_p, c_p, c_p, c_p, c_i64, c_int, c_int, c_f, c_p, c_p, c_p, c_int, c_p],
     "aw_vq_onehot": [c_p, c_i64, c_int, c_p, c_p],
     "aw_vq_gather": [c_p, c_p, c_i64, c_int, c_p, c_p],
     "aw_patchify": [c_p, c_i64, c_int, c_int, c_int, c_p, c_i64, c_int, c_p],

@@ -148,10 +148,15 @@ def encoder_chain_fwd(x0, a0, W1, W2, b1, b2, drop=(0.0, ()), seed_ptr=None, h=N
 
 
 # ------------------------------------------------------------------------------------------------ VQ
-def vq_forward(z2d, E, zq, idx, counts, sqerr, stream=None):
+def vq_forward(z2d, E, zq, idx, counts, sqerr, stream=None, zq_copy=None):
+    """zq_copy: optional bf16/f32 tensor that also receives z_q (aw_vq_forward_ex)."""
     N, D = z2d.shape
-    call("aw_vq_forward", ptr(z2d), ptr(E), N, E.shape[0], D, ptr(zq), ptr(idx), ptr(counts), ptr(sqerr),
-         stream_ptr(stream))
+    if zq_copy is None:
+        call("aw_vq_forward", ptr(z2d), ptr(E), N, E.shape[0], D, ptr(zq), ptr(idx), ptr(counts), ptr(sqerr),
+             stream_ptr(stream))
+    else:
+        call("aw_vq_forward_ex", ptr(z2d), ptr(E), N, E.shape[0], D, ptr(zq), ptr(idx), ptr(counts), ptr(sqerr),
+             ptr(zq_copy), dtype_code(zq_copy.dtype), stream_ptr(stream))
 
 
 def vq_finalize(counts, sqerr, N, K, D, beta, loss, perplexity, stream=None):
@@ -159,10 +164,15 @@ def vq_finalize(counts, sqerr, N, K, D, beta, loss, perplexity, stream=None):
          stream_ptr(stream))
 
 
-def vq_backward(z2d, E, idx, g_zq, g_loss, beta, dz, dE, stream=None):
+def vq_backward(z2d, E, idx, g_zq, g_loss, beta, dz, dE, stream=None, dz_copy=None):
+    """dz_copy: optional bf16/f32 tensor that also receives dz (aw_vq_backward_ex)."""
     N, D = z2d.shape
-    call("aw_vq_backward", ptr(z2d), ptr(E), ptr(idx), ptr(g_zq), ptr(g_loss), N, E.shape[0], D, float(beta),
-         ptr(dz), ptr(dE), stream_ptr(stream))
+    if dz_copy is None:
+        call("aw_vq_backward", ptr(z2d), ptr(E), ptr(idx), ptr(g_zq), ptr(g_loss), N, E.shape[0], D, float(beta),
+             ptr(dz), ptr(dE), stream_ptr(stream))
+    else:
+        call("aw_vq_backward_ex", ptr(z2d), ptr(E), ptr(idx), ptr(g_zq), ptr(g_loss), N, E.shape[0], D, float(beta),
+             ptr(dz), ptr(dE), ptr(dz_copy), dtype_code(dz_copy.dtype), stream_ptr(stream))
 
 
 # ------------------------------------------------------------------------ residual VQ (EMA codebooks)

@@ -346,10 +346,12 @@ def forward(m, x, training: bool, need_backward: bool, dtype=None, seed: int = 0
         zq = e(N, D)
         idx = e(N, dt=torch.int64)
         counts, sq = acc["counts"], acc["vq_sq"]
-        K.vq_forward(z, pr["E"], zq, idx, counts, sq)
+        zq_T = None if T == F32 else e(N, D, dt=T)    # the operand copy comes out of the VQ kernel itself
+        K.vq_forward(z, pr["E"], zq, idx, counts, sq, zq_copy=zq_T)
         emb_loss, perplexity = e(()), e(())
         K.vq_finalize(counts, sq, N, Kc, D, m.vector_quantization.beta, emb_loss, perplexity)
-    zq_T = zq if T == F32 else _cast(zq, T)
+    if pr["E"] is None or T == F32:
+        zq_T = zq if T == F32 else _cast(zq, T)
 
     # ---- decoder: 1x1 conv + ResBlocks with k=3 convs along the window
     y0, ya0 = e(N, H), e(N, H, dt=T)
@@ -541,15 +543,19 @@ def backward(m, sv, g_emb, g_xhat, slot, mid_hook=None):
 
     # ---- vector quantizer (straight-through + codebook/commitment loss)
     dz = e(N, D)
+    dz_T = dz if T == F32 else None
     if pr["E"] is None:   # residual VQ: straight-through + commitment terms, codebooks are EMA buffers
         res, qs = sv.rvq
         nq = res.shape[0]
         K.rvq_backward(res, qs, gzq, g_emb if nq == 1 else g_emb.expand(nq).contiguous(), dz)
     else:
-        K.vq_backward(sv.z, pr["E"], sv.idx, gzq, g_emb, m.vector_quantization.beta, dz, slot(pr["E"]))
+        dz_T = dz if T == F32 else e(N, D, dt=T)    # operand copy written by the VQ backward kernel
+        K.vq_backward(sv.z, pr["E"], sv.idx, gzq, g_emb, m.vector_quantization.beta, dz, slot(pr["E"]),
+                      dz_copy=None if T == F32 else dz_T)
     if mid_hook is not None:
         mid_hook()
-    dz_T = dz if T == F32 else _cast(dz, T)
+    if dz_T is None:
+        dz_T = _cast(dz, T)
 
     # ---- SepCNNBlock
     K.gemm(dz_T, sv.xR_T, D, H, N, a_trans=True, b_trans=True, C=slot(pr["sep"].weight).view(D, H), accumulate=True,

@@ -44,7 +44,8 @@ __global__ __launch_bounds__(VQ_THREADS, 2) void vq_fwd_kernel(const float* __re
                                                                const float* __restrict__ E, int64_t N, int K,
                                                                float* __restrict__ zq, int64_t* __restrict__ idx,
                                                                float* __restrict__ counts,
-                                                               double* __restrict__ sqerr) {
+                                                               double* __restrict__ sqerr, void* __restrict__ zq2,
+                                                               int zq2_bf16) {
   constexpr int ROWS = 8 * RPL;
   using L = VqLds<D, ROWS>;
   constexpr int ZP = L::ZP, ND = D / VQ_DC;
@@ -226,6 +227,14 @@ __global__ __launch_bounds__(VQ_THREADS, 2) void vq_fwd_kernel(const float* __re
       o.z = __fadd_rn(zv.z, d2);
       o.w = __fadd_rn(zv.w, d3);
       op[q] = o;
+      if (zq2) {   // the GEMM operand copy of z_q (the decoder's first conv reads it): no separate cast launch
+        if (zq2_bf16) {
+          typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+          reinterpret_cast<bf16x4*>(zq2)[row * (D / 4) + q] = bf16x4{(bf16)o.x, (bf16)o.y, (bf16)o.z, (bf16)o.w};
+        } else {
+          reinterpret_cast<float4*>(zq2)[row * (D / 4) + q] = o;
+        }
+      }
       s += d0 * d0 + d1 * d1 + d2 * d2 + d3 * d3;
     }
     se = s;
@@ -258,7 +267,8 @@ __global__ void vq_finalize_kernel(const float* counts, const double* sqerr, int
 
 __global__ void vq_bwd_kernel(const float* __restrict__ z, const float* __restrict__ E, const int64_t* __restrict__ idx,
                               const float* __restrict__ g_zq, const float* __restrict__ g_loss, int64_t N, int D,
-                              float beta, float* __restrict__ dz, float* __restrict__ dE) {
+                              float beta, float* __restrict__ dz, float* __restrict__ dE,
+                              void* __restrict__ dz2, int dz2_bf16) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= N * D) return;
   const int64_t r = i / D;
@@ -267,7 +277,12 @@ __global__ void vq_bwd_kernel(const float* __restrict__ z, const float* __restri
   const float g = g_loss ? g_loss[0] : 0.f;
   const float scale = 2.0f / (float)((double)N * (double)D);
   const float diff = E[k * D + d] - z[i];  // z_q - z
-  dz[i] = (g_zq ? g_zq[i] : 0.f) - g * scale * diff;
+  const float v = (g_zq ? g_zq[i] : 0.f) - g * scale * diff;
+  dz[i] = v;
+  if (dz2) {   // operand copy for the SepCNN backward GEMMs
+    if (dz2_bf16) reinterpret_cast<bf16*>(dz2)[i] = (bf16)v;
+    else reinterpret_cast<float*>(dz2)[i] = v;
+  }
   if (g != 0.f) atomicAdd(dE + k * D + d, g * beta * scale * diff);
 }
 
@@ -287,9 +302,12 @@ __global__ void vq_gather_kernel(const float* E, const int64_t* idx, int64_t N, 
 
 }  // namespace
 
-extern "C" int aw_vq_forward(const float* z, const float* E, int64_t N, int K, int D, float* zq, int64_t* idx,
-                             float* counts, double* sqerr, void* stream) {
+extern "C" int aw_vq_forward_ex(const float* z, const float* E, int64_t N, int K, int D, float* zq, int64_t* idx,
+                                float* counts, double* sqerr, void* zq_copy, int copy_dtype, void* stream) {
   AW_REQUIRE(z && E && zq && idx && counts && sqerr, "aw_vq_forward: null pointer");
+  AW_REQUIRE(!zq_copy || ((copy_dtype == AW_BF16 || copy_dtype == AW_F32) && ((uintptr_t)zq_copy % 16) == 0),
+             "aw_vq_forward_ex: zq_copy must be 16-B aligned bf16 or f32");
+  const int cbf = copy_dtype == AW_BF16;
   AW_REQUIRE(N >= 0 && K > 0, "aw_vq_forward: bad N/K");
   AW_REQUIRE(((uintptr_t)z % 16) == 0 && ((uintptr_t)E % 16) == 0 && ((uintptr_t)zq % 16) == 0,
              "aw_vq_forward: z/E/zq must be 16-B aligned");
@@ -306,8 +324,10 @@ extern "C" int aw_vq_forward(const float* z, const float* E, int64_t N, int K, i
   const dim3 grid(aw_cdiv(N, half ? 32 : 64));
 #define AW_VQ_CASE(DD)                                                                                               \
   case DD:                                                                                                           \
-    if (half) hipLaunchKernelGGL((vq_fwd_kernel<DD, 4>), grid, dim3(VQ_THREADS), 0, s, z, E, N, K, zq, idx, counts, sqerr); \
-    else hipLaunchKernelGGL((vq_fwd_kernel<DD, 8>), grid, dim3(VQ_THREADS), 0, s, z, E, N, K, zq, idx, counts, sqerr);     \
+    if (half) hipLaunchKernelGGL((vq_fwd_kernel<DD, 4>), grid, dim3(VQ_THREADS), 0, s, z, E, N, K, zq, idx, counts, sqerr, \
+                                 zq_copy, cbf);                                                                      \
+    else hipLaunchKernelGGL((vq_fwd_kernel<DD, 8>), grid, dim3(VQ_THREADS), 0, s, z, E, N, K, zq, idx, counts, sqerr,     \
+                            zq_copy, cbf);                                                                           \
     break;
   switch (D) {
     AW_VQ_CASE(16)
@@ -321,6 +341,11 @@ extern "C" int aw_vq_forward(const float* z, const float* E, int64_t N, int K, i
   return aw::check_launch("aw_vq_forward");
 }
 
+extern "C" int aw_vq_forward(const float* z, const float* E, int64_t N, int K, int D, float* zq, int64_t* idx,
+                             float* counts, double* sqerr, void* stream) {
+  return aw_vq_forward_ex(z, E, N, K, D, zq, idx, counts, sqerr, nullptr, AW_F32, stream);
+}
+
 extern "C" int aw_vq_finalize(const float* counts, const double* sqerr, int64_t N, int K, int D, float beta,
                               float* loss, float* perplexity, void* stream) {
   AW_REQUIRE(counts && sqerr && loss && perplexity && N > 0 && K > 0 && D > 0, "aw_vq_finalize: bad args");
@@ -329,15 +354,22 @@ extern "C" int aw_vq_finalize(const float* counts, const double* sqerr, int64_t 
   return aw::check_launch("aw_vq_finalize");
 }
 
-extern "C" int aw_vq_backward(const float* z, const float* E, const int64_t* idx, const float* g_zq,
-                              const float* g_loss, int64_t N, int K, int D, float beta, float* dz, float* dE,
-                              void* stream) {
+extern "C" int aw_vq_backward_ex(const float* z, const float* E, const int64_t* idx, const float* g_zq,
+                                 const float* g_loss, int64_t N, int K, int D, float beta, float* dz, float* dE,
+                                 void* dz_copy, int copy_dtype, void* stream) {
   AW_REQUIRE(z && E && idx && dz && dE && N >= 0 && K > 0 && D > 0, "aw_vq_backward: bad args");
+  AW_REQUIRE(!dz_copy || copy_dtype == AW_BF16 || copy_dtype == AW_F32, "aw_vq_backward_ex: bad copy dtype");
   if (N == 0) return AW_OK;
   const int64_t n = N * D;
   hipLaunchKernelGGL(vq_bwd_kernel, dim3(aw_cdiv(n, 256)), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), z,
-                     E, idx, g_zq, g_loss, N, D, beta, dz, dE);
+                     E, idx, g_zq, g_loss, N, D, beta, dz, dE, dz_copy, copy_dtype == AW_BF16 ? 1 : 0);
   return aw::check_launch("aw_vq_backward");
+}
+
+extern "C" int aw_vq_backward(const float* z, const float* E, const int64_t* idx, const float* g_zq,
+                              const float* g_loss, int64_t N, int K, int D, float beta, float* dz, float* dE,
+                              void* stream) {
+  return aw_vq_backward_ex(z, E, idx, g_zq, g_loss, N, K, D, beta, dz, dE, nullptr, AW_F32, stream);
 }
 
 extern "C" int aw_vq_onehot(const int64_t* idx, int64_t N, int K, float* onehot, void* stream) {
