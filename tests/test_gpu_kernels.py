@@ -350,3 +350,14 @@ def test_gemm_bf16_pre_activation_operand(K, tile, act):
         K.gemm(A, W, M, N, Kd, b_trans=False, act=act_code, pre=p, resid=resid, C=C, C2=C2, c2_mode=2)
         outs.append((C.cpu(), C2.cpu()))
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+
+
+@pytest.mark.parametrize("n,off", [(409600, 0), (1001, 0), (4099, 1)])
+def test_mse_loss_vs_fp64(K, n, off):
+    """aw_mse_fwd / aw_mse_finalize: float4 path, scalar tail, and an unaligned view (scalar path throughout)."""
+    from arcweld.functional import mse_loss
+    a = torch.tensor(gen.normal(401, (n + off,), 1.0), device=DEV)[off:]
+    b = torch.tensor(gen.normal(402, (n + off,), 1.0), device=DEV)[off:]
+    got = mse_loss(a, b).item()
+    ref = ((a.double() - b.double()) ** 2).mean().item()
+    np.testing.assert_allclose(got, ref, rtol=2e-6)
