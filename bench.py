@@ -49,6 +49,8 @@ def parse():
                     help="skip the configs[4] line (codebook 8192x256, T 1025, 16-block Transformer)")
     ap.add_argument("--seqs", type=int, default=51, help="Transformer sequences per GPU per step (configs[2])")
     ap.add_argument("--n-cycles", type=int, default=20)
+    ap.add_argument("--only", default="all", choices=["all", "transformer_pretokenized"],
+                    help="profiling aid: run one sub-line alone (the PMC passes of tools/prof_transformer.sh)")
     ap.add_argument("--gemm-tile", type=int, default=0, choices=[0, 128, 256],
                     help="GEMM tile policy (aw_gemm_set_tile): 0 = automatic")
     return ap.parse_args()
@@ -150,10 +152,37 @@ def transformer_workload(dev, rank, world, args, seqs, n_cycles, accumulate=1, l
         orig, orig_fused = dec.training_step, dec.fused_train_step
         dec.training_step = lambda w, i: orig(train(w), i)
         dec.fused_train_step = lambda w, scale, mid_hook=None: orig_fused(train(w), scale, mid_hook=mid_hook)
-    el = _timed_steps(step, max(args.warmup, 1 if use_graph else 0), args.steps, world)
+    el = _timed_steps(step, max(args.warmup, 3 if use_graph else 0), args.steps, world)
     windows = world * seqs * accumulate * nc * args.steps
     flops = transformer_flops_per_seq(T, n_blocks, 512, V) * seqs * accumulate * world * args.steps
+    roof, attn = None, None
+    if not args.no_profile:
+        # per-launch HIP events cannot sit inside the captured graph: a profiled eager pass of the same step follows
+        from arcweld import kernels
+        n_prof = min(args.steps, 5)
+        kernels.PROFILE = []
+        t1 = time.perf_counter()
+        for i in range(n_prof):
+            for j in range(accumulate):
+                k = (i + j) % 2      # graphed runs patched training_step to tokenize its window batch itself
+                b = batches[k] if pretokenized else (wins[k] if use_graph else train(wins[k]))
+                tr.micro_step(dec, b, j, 1.0 / (accumulate * world))
+            tr.optimizer_step(dec)
+        torch.cuda.synchronize()
+        pel = (time.perf_counter() - t1) / n_prof
+        prof = (kernels.PROFILE, n_prof)
+        kernels.PROFILE = None
+        traffic, tsrc = transformer_traffic()
+        roof = gemm_roofline(prof, pel, el, args.steps, BF16_PEAK_TFLOPS, "bf16",
+                             traffic if pretokenized else None, tsrc if pretokenized else None)
+        roof["kernel"] = "gemm_kernel<bf16> (aw_gemm / aw_gemm_grouped): the decoder's Linear layers, fwd + dgrad + wgrad"
+        if not pretokenized and any(e[3] == "gemm_f32" for e in prof[0]):
+            roof["tokenize_gemm_f32"] = {k: v for k, v in gemm_roofline(prof, pel, el, args.steps, FP32_PEAK_TFLOPS,
+                                                                          "f32").items()
+                                         if k in ("achieved", "peak", "frac", "launches_per_step", "gemm_ms_per_step")}
+        attn = attn_roofline(prof)
     return {"value": round(windows / el, 2), "unit": "windows/s", "ms_per_step": round(el * 1e3 / args.steps, 3),
+            "steps": args.steps, "roofline": roof, "attention": attn,
             "config": {"workload": (f"Transformer train step on ids tokenized once at setup ({label})" if pretokenized
                                     else f"tokenize (frozen VQ-VAE encoder, fp32 exact) + Transformer train step ({label})"),
                        "seqs_per_gpu_per_micro_batch": seqs, "accumulate_grad_batches": accumulate,
@@ -198,6 +227,24 @@ def _cpu_model():
     return "unknown"
 
 
+def _cgroup_cpus():
+    """CPUs granted by the cgroup CPU quota (cgroup v2 cpu.max / v1 cfs quota), None when unlimited or unknown."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        return None if q == "max" else max(1, int(int(q) / int(per)))
+    except (OSError, ValueError):
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+            q = int(f.read())
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+            per = int(f.read())
+        return None if q <= 0 else max(1, q // per)
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_baseline(seconds):
     """Oracle port (oracle/vqvae.py, torch CPU fp32) on a bounded sample of the same workload: full-size model,
     B=32 windows per step, fwd+bwd+clip+RAdam; windows/s.  Threads: the CPUs this process may use -- on the GPU box
@@ -210,8 +257,11 @@ def cpu_baseline(seconds):
         avail = len(os.sched_getaffinity(0))
     except AttributeError:
         avail = nproc
+    quota = _cgroup_cpus()
     share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
-    threads = max(1, min(avail, share) if share > 0 else avail)
+    # all the CPUs this process may actually run on: the affinity set, capped by the cgroup CPU quota (the GPU box
+    # grants each GPU's job a share of a larger host; its affinity mask lists every host CPU) and OMP_NUM_THREADS
+    threads = max(1, min(x for x in (avail, quota or avail, share or avail)))
     torch.set_num_threads(threads)
     cfg = ov.VQVAEConfig(dropout_p=0.0)
     sd = ov.det_state_dict(cfg, 1)
@@ -235,10 +285,11 @@ def cpu_baseline(seconds):
             break
     el = time.time() - t0
     return {"value": round(B * steps / el, 2), "unit": "windows/s", "cores": threads, "kind": "port",
-            "nproc": nproc, "affinity_cpus": avail, "cpu_model": _cpu_model(),
+            "nproc": nproc, "affinity_cpus": avail, "cgroup_cpu_quota": quota, "omp_num_threads": share or None,
+            "cpu_model": _cpu_model(),
             "sample": f"oracle/vqvae.py full-size VQ-VAE (H512 R8 K512xD64) fp32 train step, B={B} windows, "
                       f"{steps} timed steps ({el:.1f} s) after 1 warm-up, torch CPU {threads} threads "
-                      f"(the process's CPU share of a {nproc}-CPU host)",
+                      f"(= min of the affinity set, the cgroup quota and OMP_NUM_THREADS on a {nproc}-CPU host)",
             "reference": REFERENCE_CPU}
 
 
@@ -269,7 +320,8 @@ def vqvae_workload(dev, rank, world, args, dtype, steps, warmup, profile=True, K
             else:
                 eager_step(i)
 
-        elapsed = _timed_steps(step, max(warmup, 1 if use_graph else 0), steps, world)
+        # graphed_step runs 2 eager warm-up calls and captures on the 3rd: >= 3 untimed calls keep the capture out
+        elapsed = _timed_steps(step, max(warmup, 3 if use_graph else 0), steps, world)
         # per-GEMM HIP events cannot sit inside a captured graph: the kernel durations for the roofline come from a
         # profiled eager pass over the same workload right after the timed region (GPU-side durations are the
         # same; rocprofv3 in profiles/ cross-checks them against the graph replays)
@@ -288,9 +340,11 @@ def vqvae_workload(dev, rank, world, args, dtype, steps, warmup, profile=True, K
 
 
 def gemm_roofline(prof, prof_el, elapsed, steps, peak, dtype_name, traffic=None, traffic_src=None):
+    """The GEMM family of one operand dtype over the profiled eager steps (HIP events per launch)."""
     lst, n_prof = prof
-    ms = sum(e0.elapsed_time(e1) for e0, e1, _ in lst)
-    flops = sum(f for _, _, f in lst)
+    lst = [e for e in lst if e[3] == f"gemm_{dtype_name}"]
+    ms = sum(e0.elapsed_time(e1) for e0, e1, _, _ in lst)
+    flops = sum(e[2] for e in lst)
     n = len(lst)
     achieved = flops / (ms * 1e-3) / 1e12
     return {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
@@ -303,6 +357,36 @@ def gemm_roofline(prof, prof_el, elapsed, steps, peak, dtype_name, traffic=None,
             "measured_over": f"{n_prof} eager steps after the timed region (HIP events per launch, on the launch "
                              "stream)",
             "eager_ms_per_step_with_events": round(prof_el * 1e3, 3)}
+
+
+def attn_roofline(prof):
+    """The flash-attention kernels of the profiled steps (HIP events per launch; algorithmic FLOPs: the causal QK^T
+    and PV of the forward, twice that for the backward) against the bf16 dense MFMA peak."""
+    lst, n_prof = prof
+    out = {}
+    for tag in ("attn_fwd", "attn_bwd"):
+        ev = [e for e in lst if e[3] == tag]
+        if not ev:
+            continue
+        us = sum(e0.elapsed_time(e1) for e0, e1, _, _ in ev) * 1e3 / len(ev)
+        tf = sum(e[2] for e in ev) / len(ev) / (us * 1e-6) / 1e12
+        out[tag] = {"avg_launch_us": round(us, 2), "achieved": round(tf, 2), "peak": BF16_PEAK_TFLOPS,
+                    "unit": "TFLOP/s", "frac": round(tf / BF16_PEAK_TFLOPS, 4),
+                    "gflop_per_launch": round(sum(e[2] for e in ev) / len(ev) / 1e9, 4),
+                    "launches_per_step": len(ev) // n_prof}
+    return out
+
+
+def transformer_traffic():
+    """HBM bytes per bf16 GEMM launch of the decoder train step from the committed PMC passes of the
+    transformer_pretokenized workload (tools/prof_transformer.sh; FETCH_SIZE doubled per the gfx950 note)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "r0*", "*", "pmc_transformer_gemm_traffic.json")))
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        d = json.load(f)
+    return round(d["avg_bytes_per_launch"]), os.path.relpath(files[-1], REPO)
 
 
 def vq_kernel_roofline(dev, N, K, D, iters=10):
@@ -339,9 +423,9 @@ def stress_workload(dev, rank, world, args):
     and the 16-block Transformer at T = 1025 (n_cycles 64, V 8194; 16 sequences = 1024 windows per GPU, tokenized
     by that VQ-VAE), each reported as windows/s with its roofline."""
     from arcweld.precision import operands
-    n = max(2, args.steps // 4)
-    el, prof, pel = vqvae_workload(dev, rank, world, args, torch.bfloat16, n, 2, profile=not args.no_profile,
-                                   K=8192, D=256)
+    n = max(20, args.steps)                 # steady state: >= 20 timed replays after the capture (warm-up >= 3)
+    el, prof, pel = vqvae_workload(dev, rank, world, args, torch.bfloat16, n, max(5, args.warmup),
+                                   profile=not args.no_profile, K=8192, D=256)
     out = {"vqvae": {"value": round(world * args.batch * n / el, 2), "unit": "windows/s",
                      "ms_per_step": round(el * 1e3 / n, 3), "steps": n,
                      "config": {"workload": "VQ-VAE-Patch train step, stress codebook (configs[4])",
@@ -350,6 +434,7 @@ def stress_workload(dev, rank, world, args):
                      "vq_kernel": vq_kernel_roofline(dev, args.batch * 16, 8192, 256)}}
     sargs = argparse.Namespace(**vars(args))
     sargs.steps = n
+    sargs.warmup = max(5, args.warmup)
     with operands(torch.bfloat16):
         out["transformer"] = transformer_workload(dev, rank, world, sargs, 16, 64, K=8192, D=256, n_blocks=16,
                                                   label="configs[4] stress: 16 blocks, T 1025, codebook 8192x256")
@@ -387,6 +472,17 @@ def main():
     from arcweld import _native
     _native.call("aw_gemm_set_tile", args.gemm_tile)
 
+    if args.only == "transformer_pretokenized":
+        from arcweld.precision import operands
+        with operands(torch.bfloat16):
+            line = transformer_workload(dev, rank, world, args, args.seqs, args.n_cycles, pretokenized=True,
+                                        label="configs[2], the reference's regime")
+        if rank == 0:
+            print(json.dumps({"only": args.only, **line}), flush=True)
+        if distributed:
+            dist.destroy_process_group()
+        return
+
     # headline: configs[1] in bf16 (BASELINE.json names bf16 for it; an explicit opt-in, arcweld.precision)
     elapsed, prof, prof_el = vqvae_workload(dev, rank, world, args, torch.bfloat16, args.steps, args.warmup,
                                             profile=not args.no_profile)
@@ -399,8 +495,9 @@ def main():
     if not args.no_fp32:
         # the same step with exact-fp32 operands (the default numerics, the reference's): priced against the
         # 157.3 TF fp32 MFMA roof
-        n32 = max(2, args.steps // 4)
-        el32, prof32, pel32 = vqvae_workload(dev, rank, world, args, torch.float32, n32, 2, profile=not args.no_profile)
+        n32 = max(20, args.steps)           # steady state: >= 20 timed replays after the capture (warm-up >= 3)
+        el32, prof32, pel32 = vqvae_workload(dev, rank, world, args, torch.float32, n32, max(5, args.warmup),
+                                             profile=not args.no_profile)
         extra["fp32"] = {"value": round(world * args.batch * n32 / el32, 2), "unit": "windows/s",
                          "ms_per_step": round(el32 * 1e3 / n32, 3), "steps": n32, "dtype": "f32",
                          "roofline": gemm_roofline(prof32, pel32, el32, n32, FP32_PEAK_TFLOPS, "f32") if prof32 else None}

@@ -67,8 +67,8 @@ def test_update_kernel_copies_equal_a_fresh_relayout(T, chain, monkeypatch):
         torch.cuda.synchronize()
         names = [j.name for j in st.jobs]
         assert any(n.startswith("chain") for n in names) == chain
-        fresh = [operands.OperandJob(j.name, j.param, j.src, j.O, j.I, j.k, j.tap, j.mode, torch.zeros_like(j.out),
-                                     j.ldo) for j in st.jobs]
+        fresh = [operands.OperandJob(j.name, j.param, j.O, j.I, j.k, j.tap, j.mode, torch.zeros_like(j.out),
+                                     j.ldo, derive=j.derive) for j in st.jobs]
         K.weight_relayout_batch([j.relayout_job() for j in fresh])
         for j, f in zip(st.jobs, fresh):
             assert torch.equal(j.out, f.out), (j.name, j.mode)
@@ -105,3 +105,38 @@ def test_outside_weight_change_triggers_a_refresh():
     assert n == [1]
     w = st.out["Wd0"]
     torch.testing.assert_close(w.float(), m.decoder[0].weight[:, :, 0].float().to(w.dtype).float())
+
+
+@pytest.mark.parametrize("T", [torch.bfloat16, torch.float32])
+def test_forward_before_optimizer_then_fit_then_load_state_dict(T):
+    """An operand set built by a forward BEFORE the optimizer re-stores the weights (flat buffer, centre-tap and
+    tap-major views) follows the parameters' new storage: forward -> Trainer steps -> forward equals a fresh model
+    with the trained weights, and a load_state_dict afterwards is picked up too (arcweld/operands.py derive)."""
+    from arcweld.precision import operands as prec
+    from arcweld.trainer import Trainer
+    with prec(T):
+        m = make_model(KW, 333, "cuda").train()
+        x = torch.tensor(gen.windows(370, 8), device="cuda")
+        with torch.no_grad():
+            m.eval()
+            m(x)                                     # builds the operand set on the reference layouts
+            m.train()
+        tr = Trainer(gradient_clip_val=0.7)
+        tr.setup_optimizer(m)
+        for i in range(2):
+            tr.micro_step(m, torch.tensor(gen.windows(371 + i, 8), device="cuda"), 0, 1.0)
+            tr.optimizer_step(m)
+
+        def eval_out(model):
+            with torch.no_grad():
+                model.eval()
+                out = model(x)[1]
+                model.train()
+            return out
+
+        ref = make_model(KW, 333, "cuda")
+        ref.load_state_dict(m.state_dict())
+        torch.testing.assert_close(eval_out(m), eval_out(ref), rtol=0, atol=0)
+        other = make_model(KW, 334, "cuda")
+        m.load_state_dict(other.state_dict())
+        torch.testing.assert_close(eval_out(m), eval_out(other), rtol=0, atol=0)

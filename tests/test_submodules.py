@@ -222,3 +222,73 @@ def test_cnn_block_trains_with_torch_optimizer(fp32_parity):
         opt.step()
         losses.append(float(loss))
     assert losses[-1] < losses[0]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("batch_norm", [False, True])
+@pytest.mark.parametrize("L", [16, 1, 7])
+def test_resblock_autograd(L, batch_norm, fp32_parity):
+    """ResBlock.forward on its own (vq_vae_patch_embedd.py:73-74): k = 3 / pad = 1 convs along L -- the decoder's
+    use at L = S, the per-token encoder's at L = 1 (centre tap only), and an odd length."""
+    m, cfg, sd = _model(batch_norm)
+    blk = m.decoder[1].shared_conv[0]
+    pre = "decoder.1.shared_conv.0."
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(B, cfg.H, L, generator=g)
+    gr = torch.randn(B, cfg.H, L, generator=g)
+    y, gx = _run(blk, x.cuda(), gr)
+    refp = _ref_params(sd, pre)
+    xr = x.clone().permute(0, 2, 1).contiguous().requires_grad_(True)
+    yr = ov._resblock(xr, sd, pre[:-1], None, cfg, True, token_axis_conv=True).permute(0, 2, 1)
+    (yr * gr).sum().backward()
+    _close(y, yr, "y")
+    _close(gx, xr.grad.permute(0, 2, 1), "x.grad")
+    _check_module(blk, pre, refp, sd, ["block.1.bias", "block.4.bias"] if batch_norm else [])
+
+
+@pytest.mark.gpu
+def test_causal_self_attention_autograd(fp32_parity):
+    """CausalSelfAttention.forward on its own (transformer_block.py:40-63)."""
+    blk, sd = _block()
+    g = torch.Generator().manual_seed(12)
+    x = torch.randn(3, 48, 64, generator=g)
+    gr = torch.randn(3, 48, 64, generator=g)
+    y, gx = _run(blk.attn, x.cuda(), gr)
+    refp = _ref_params(sd, "attn.")
+    refp.pop("attn.bias", None)
+    xr = x.clone().requires_grad_(True)
+    yr = od.attn_forward(sd, "attn.", xr, 4)
+    (yr * gr).sum().backward()
+    _close(y, yr, "y")
+    _close(gx, xr.grad, "x.grad")
+    _check_module(blk.attn, "attn.", refp, sd)
+
+
+@pytest.mark.gpu
+def test_block_mlpf_autograd(fp32_parity):
+    """Block.mlpf on its own (transformer_block.py:81-83), on a (B, T, d) input and a flat (R, d) one."""
+    blk, sd = _block()
+    g = torch.Generator().manual_seed(13)
+    for shape in ((3, 48, 64), (40, 64)):
+        for p in blk.mlp.parameters():
+            p.grad = None
+        x = torch.randn(*shape, generator=g)
+        gr = torch.randn(*shape, generator=g)
+        y, gx = _run(blk.mlpf, x.cuda(), gr)
+        refp = _ref_params({k: v.clone() for k, v in sd.items()}, "mlp.")
+        xr = x.clone().requires_grad_(True)
+        yr = od.mlp_forward({**sd, **refp}, "mlp.", xr)
+        (yr * gr).sum().backward()
+        _close(y, yr, "y")
+        _close(gx, xr.grad, "x.grad")
+        _check_module(blk.mlp, "mlp.", refp, sd)
+
+
+def test_submodule_forwards_exist():
+    """The reference's reachable sub-module forwards all exist on the mirror (no nn.Module NotImplementedError)."""
+    from model.transformer_block import Block, CausalSelfAttention
+    from model.vq_vae_patch_embedd import ResBlock
+    for cls in (ResBlock, CausalSelfAttention):
+        assert cls.forward is not torch.nn.Module.forward, cls
+    blk = Block(d_model=32, seq_len=8, n_head=2, res_dropout=0.0, att_dropout=0.0)
+    assert callable(blk.mlpf)

@@ -3,6 +3,7 @@ FETCH_SIZE and WRITE_SIZE come from separate passes (TCC slots); on gfx950 FETCH
 wide coalesced streaming reads, so it is doubled; both are in KiB.
 
 usage: python tools/pmc_traffic.py <fetch counter_collection.csv> <write counter_collection.csv> [kernel-substr]
+       [exclude-substr]   (e.g. "<float" leaves the exact-f32 instantiations out of a bf16 family)
 Prints per-kernel average bytes per launch (and the GEMM family aggregate) as JSON."""
 import csv
 import json
@@ -21,7 +22,7 @@ def load(path, counter):
     return per
 
 
-def main(fetch_csv, write_csv, sub="gemm_kernel"):
+def main(fetch_csv, write_csv, sub="gemm_kernel", exclude=None):
     fe = load(fetch_csv, "FETCH_SIZE")
     wr = load(write_csv, "WRITE_SIZE")
     out = {}
@@ -34,10 +35,10 @@ def main(fetch_csv, write_csv, sub="gemm_kernel"):
         fb = 2.0 * 1024.0 * sum(f) / len(f)
         wb = 1024.0 * sum(w) / len(w)
         out[name[:120]] = {"launches": len(f), "fetch_bytes": fb, "write_bytes": wb, "bytes_per_launch": fb + wb}
-        if sub in name:
+        if sub in name and not (exclude and exclude in name):
             tot_b += (fb + wb) * len(f)
             tot_n += len(f)
-    res = {"family": sub, "launches": tot_n, "avg_bytes_per_launch": tot_b / tot_n if tot_n else None,
+    res = {"family": sub, "excluded": exclude, "launches": tot_n, "avg_bytes_per_launch": tot_b / tot_n if tot_n else None,
            "kernels": out}
     print(json.dumps(res, indent=1))
 

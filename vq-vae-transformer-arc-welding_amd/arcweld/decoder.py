@@ -52,10 +52,10 @@ def _operand_jobs(m, T_):
         for nm, lin in (("qkv", blk.attn.c_attn), ("o", blk.attn.c_proj), ("fc", blk.mlp.c_fc), ("p", blk.mlp.c_proj)):
             w = lin.weight
             if w.dtype != T_:
-                jobs.append(J(f"b{i}_{nm}", w, w, w.shape[0], w.shape[1], 1, 0, 5,
+                jobs.append(J(f"b{i}_{nm}", w, w.shape[0], w.shape[1], 1, 0, 5,
                               torch.empty(w.shape, device=w.device, dtype=T_)))
     w = m.lm_head.weight
-    jobs.append(J("Wlm", w, w, w.shape[0], w.shape[1], 1, 0, 5,
+    jobs.append(J("Wlm", w, w.shape[0], w.shape[1], 1, 0, 5,
                   torch.zeros(_pad8(w.shape[0]), w.shape[1], device=w.device, dtype=T_)))
     return jobs
 

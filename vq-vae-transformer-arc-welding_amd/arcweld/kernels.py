@@ -82,12 +82,18 @@ def _gemm_args(A, B, M, N, K, *, a_trans=False, b_trans=False, conv=None, alpha=
     return a
 
 
-def _timed(s, fn, flops):
+def _timed(s, fn, flops, tag):
+    """Bench profiling (PROFILE is a list): HIP events around one launch on its stream, with the launch's
+    algorithmic FLOPs and a kernel-family tag ("gemm_bf16", "gemm_f32", "attn_fwd", "attn_bwd")."""
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(s)
     fn(s.cuda_stream)
     e1.record(s)
-    PROFILE.append((e0, e1, flops))
+    PROFILE.append((e0, e1, flops, tag))
+
+
+def _gemm_tag(A):
+    return "gemm_bf16" if A.dtype == torch.bfloat16 else "gemm_f32"
 
 
 def gemm(A, B, M, N, K, *, stream=None, flops=None, **kw):
@@ -103,7 +109,7 @@ def gemm(A, B, M, N, K, *, stream=None, flops=None, **kw):
         return kw.get("C")
     s = stream if stream is not None else torch.cuda.current_stream()
     _timed(s, lambda sp: call("aw_gemm_ws", ctypes.byref(a), ptr(ws), wsn, sp),
-           _algorithmic_flops(M, N, K, kw.get("conv"), flops))
+           _algorithmic_flops(M, N, K, kw.get("conv"), flops), _gemm_tag(A))
     return kw.get("C")
 
 
@@ -121,7 +127,7 @@ def gemm_grouped(problems, stream=None):
             continue
         s = stream if stream is not None else torch.cuda.current_stream()
         fl = sum(_algorithmic_flops(M, N, K, kw.get("conv"), None) for (_, _, M, N, K, kw) in chunk)
-        _timed(s, lambda sp: call("aw_gemm_grouped", arr, len(chunk), sp), fl)
+        _timed(s, lambda sp: call("aw_gemm_grouped", arr, len(chunk), sp), fl, _gemm_tag(chunk[0][0]))
 
 
 # ---------------------------------------------------------------------------------- fused encoder chain
@@ -371,22 +377,41 @@ def embed_bwd(ids, dx, dwtok, stream=None):
     call("aw_embed_bwd", ptr(ids), B, T, dwtok.shape[1], ptr(dx), ptr(dwtok), stream_ptr(stream))
 
 
+def attn_flops(B, T, n_head, d):
+    """Algorithmic FLOPs of the causal attention forward: QK^T and PV over the T(T+1)/2 causal pairs per head."""
+    return 4.0 * B * n_head * (T * (T + 1) / 2) * (d // n_head)
+
+
+def _maybe_timed(stream, tag, flops, fn):
+    if PROFILE is None:
+        fn(stream_ptr(stream))
+        return
+    s = stream if stream is not None else torch.cuda.current_stream()
+    _timed(s, fn, flops, tag)
+
+
 def attn_fwd(qkv, B, T, n_head, d, y, lse, drop=(0.0, 0), seed_ptr=None, stream=None):
     """drop = (p, seed): attention-probability dropout (aw_attn_fwd_dropout); p = 0 is plain aw_attn_fwd."""
     if drop[0] > 0:
-        call("aw_attn_fwd_dropout", ptr(qkv), B, T, n_head, d, dtype_code(qkv.dtype), ptr(y), ptr(lse), float(drop[0]),
-             int(drop[1]) & 0xFFFFFFFFFFFFFFFF, ptr(seed_ptr), stream_ptr(stream))
+        _maybe_timed(stream, "attn_fwd", attn_flops(B, T, n_head, d), lambda sp: call(
+            "aw_attn_fwd_dropout", ptr(qkv), B, T, n_head, d, dtype_code(qkv.dtype), ptr(y), ptr(lse),
+            float(drop[0]), int(drop[1]) & 0xFFFFFFFFFFFFFFFF, ptr(seed_ptr), sp))
         return
-    call("aw_attn_fwd", ptr(qkv), B, T, n_head, d, dtype_code(qkv.dtype), ptr(y), ptr(lse), stream_ptr(stream))
+    _maybe_timed(stream, "attn_fwd", attn_flops(B, T, n_head, d), lambda sp: call(
+        "aw_attn_fwd", ptr(qkv), B, T, n_head, d, dtype_code(qkv.dtype), ptr(y), ptr(lse), sp))
 
 
 def attn_bwd(qkv, y, dy, lse, B, T, n_head, d, dqkv, ws, drop=(0.0, 0), seed_ptr=None, stream=None):
+    """Algorithmic FLOPs: twice the forward (dQ, dK, dV, dP; the recomputed S is not counted)."""
+    fl = 2.0 * attn_flops(B, T, n_head, d)
     if drop[0] > 0:
-        call("aw_attn_bwd_dropout", ptr(qkv), ptr(y), ptr(dy), ptr(lse), B, T, n_head, d, dtype_code(qkv.dtype),
-             ptr(dqkv), ptr(ws), float(drop[0]), int(drop[1]) & 0xFFFFFFFFFFFFFFFF, ptr(seed_ptr), stream_ptr(stream))
+        _maybe_timed(stream, "attn_bwd", fl, lambda sp: call(
+            "aw_attn_bwd_dropout", ptr(qkv), ptr(y), ptr(dy), ptr(lse), B, T, n_head, d, dtype_code(qkv.dtype),
+            ptr(dqkv), ptr(ws), float(drop[0]), int(drop[1]) & 0xFFFFFFFFFFFFFFFF, ptr(seed_ptr), sp))
         return
-    call("aw_attn_bwd", ptr(qkv), ptr(y), ptr(dy), ptr(lse), B, T, n_head, d, dtype_code(qkv.dtype), ptr(dqkv),
-         ptr(ws), stream_ptr(stream))
+    _maybe_timed(stream, "attn_bwd", fl, lambda sp: call(
+        "aw_attn_bwd", ptr(qkv), ptr(y), ptr(dy), ptr(lse), B, T, n_head, d, dtype_code(qkv.dtype), ptr(dqkv),
+        ptr(ws), sp))
 
 
 # ------------------------------------------------------------------------------ ResBlock BatchNorm

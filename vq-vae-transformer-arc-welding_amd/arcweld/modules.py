@@ -147,16 +147,29 @@ def patch_embed(mod, x):
 def cnn_block(mod, x):
     """CNNBlock (vq_vae_patch_embedd.py:93-114): (B, H, S) -> (B, H, S).  seperate=True: every token on its own
     (centre taps), False: k=3 convolutions along the token axis; BatchNorm ResBlocks when batch_norm."""
+    return _resblock_stack(mod, list(mod.shared_conv), mod.seperate, mod.batch_norm, mod.dropout_p, x)
+
+
+def resblock(mod, x):
+    """ResBlock.forward (vq_vae_patch_embedd.py:73-74): x + block(x) on (B, C, L), both convs k = 3 / pad = 1 along
+    L (an L = 1 slice -- the per-token encoder -- leaves only the centre tap, as in the reference)."""
+    c1 = mod.block[1]
+    if tuple(c1.kernel_size) != (3,) or tuple(c1.stride) != (1,) or tuple(c1.padding) != (1,):
+        raise NotImplementedError("ResBlock on the HIP path: kernel_size 3, stride 1, padding 1 (the reference's use)")
+    bn = isinstance(mod.block[2], torch.nn.BatchNorm1d)
+    return _resblock_stack(mod, [mod], False, bn, float(mod.block[6].p), x)
+
+
+def _resblock_stack(mod, blocks, sep, batch_norm, dropout_p, x):
+    """A stack of ResBlocks (the module `mod` owns their parameters) as one autograd node."""
     T = operand_dtype()
-    sep = mod.seperate
-    blocks = list(mod.shared_conv)
 
     def fwd(x, save):
         B, H, S = x.shape
         N = B * S
         e = _empty(x.device)
         training = mod.training
-        p = mod.dropout_p if training else 0.0
+        p = dropout_p if training else 0.0
         seed = _seed(p)
         cur = _tokens(x, F32)
         a0 = _gelu_operand(cur, T)
@@ -173,7 +186,7 @@ def cnn_block(mod, x):
                 w1, w2 = e(H, 3 * H, dt=T), e(H, 3 * H, dt=T)
                 K.weight_relayout_batch([engine._conv3_job(c1.weight, 1, w1), engine._conv3_job(c2.weight, 1, w2)])
             sr = _mix(seed, r)
-            if mod.batch_norm:   # per-token statistics when the tokens run separately, over all positions otherwise
+            if batch_norm:   # per-token statistics when the tokens run separately, over all positions otherwise
                 gk = {} if conv is None else dict(conv=conv)
                 y, an, bs = engine._bn_block_fwd(a0, cur, w1, w2, kd, gk, c1, c2, (blk.block[2], blk.block[5]),
                                                  S if sep else 1, training, p, sr, None, T)
@@ -208,7 +221,7 @@ def cnn_block(mod, x):
 
         gy = _tokens(g, F32)
         nb = len(blocks)
-        go = _masked_copy(gy, T, p, sv.blocks[-1][5]) if (nb and not mod.batch_norm) else None
+        go = _masked_copy(gy, T, p, sv.blocks[-1][5]) if (nb and not batch_norm) else None
         wgrads = []
         for r in reversed(range(nb)):
             blk = blocks[r]
@@ -219,7 +232,7 @@ def cnn_block(mod, x):
             else:   # dgrad operands [3O][I]
                 W1d, W2d = e(3 * H, H, dt=T), e(3 * H, H, dt=T)
                 K.weight_relayout_batch([engine._conv3_job(c1.weight, 2, W1d), engine._conv3_job(c2.weight, 2, W2d)])
-            if mod.batch_norm:
+            if batch_norm:
                 gk = {} if dconv is None else dict(conv=dconv)
                 gy, _ = engine._bn_block_bwd(gy, xr, a0, bs, W1d, W2d, kd, gk, wg, c1, c2, (blk.block[2], blk.block[5]),
                                              S if sep else 1, sv.training, p, sr, None, T, slot, wgrads,
@@ -336,6 +349,109 @@ def patch_unembed(mod, x):
         gx = e(N, H)
         K.gemm(gY2, sv.W, N, H, k1 * H, b_trans=True, C=gx)
         return _channel_major(gx, B, S).contiguous()
+
+    return run(mod, fwd, bwd, x)
+
+
+# ------------------------------------------------------------------------------------------- transformer pieces
+def causal_self_attention(mod, x):
+    """CausalSelfAttention.forward (transformer_block.py:40-63): resid_drop(c_proj(softmax(mask(q k^T / sqrt(hs)))
+    v)) on (B, T, d) -- QKV GEMM, flash attention (probability dropout inside the kernel), c_proj GEMM with the
+    residual dropout in its epilogue."""
+    Td = operand_dtype()
+    nh = mod.n_head
+
+    def fwd(x, save):
+        B, T, d = x.shape
+        R = B * T
+        e = _empty(x.device)
+        training = mod.training
+        p = float(mod.resid_dropout.p) if training else 0.0
+        pa = float(mod.attn_pdrop) if training else 0.0
+        s_res, s_probs = _seed(p), _seed(pa)
+        xa = _cast(x.reshape(R, d), Td)
+        Wqkv, Wo = _cast(mod.c_attn.weight, Td), _cast(mod.c_proj.weight, Td)
+        qkv = e(R, 3 * d, dt=Td)
+        K.gemm(xa, Wqkv, R, 3 * d, d, bias=mod.c_attn.bias, C=qkv)
+        y, lse = e(R, d, dt=Td), e(B * nh * T)
+        K.attn_fwd(qkv, B, T, nh, d, y, lse, drop=(pa, s_probs))
+        out = e(R, d)
+        K.gemm(y, Wo, R, d, d, bias=mod.c_proj.bias, drop=(p, s_res), C=out)
+        sv = _Saved()
+        sv.shape, sv.p, sv.pa, sv.seeds = (B, T, d), p, pa, (s_res, s_probs)
+        if save:
+            sv.c = dict(xa=xa, qkv=qkv, y=y, lse=lse, Wqkv=Wqkv, Wo=Wo)
+        return out.view(B, T, d), sv
+
+    def bwd(sv, g, slot, need_x):
+        B, T, d = sv.shape
+        R = B * T
+        e = _empty(g.device)
+        c = sv.c
+        s_res, s_probs = sv.seeds
+        go = _masked_copy(g.reshape(R, d).float().contiguous(), Td, sv.p, s_res)
+        gy = e(R, d, dt=Td)
+        K.gemm(go, c["Wo"], R, d, d, b_trans=True, C=gy)
+        K.gemm(go, c["y"], d, d, R, a_trans=True, b_trans=True, C=slot(mod.c_proj.weight), accumulate=True,
+               a_rowsum=slot(mod.c_proj.bias))
+        dqkv = e(R, 3 * d, dt=Td)
+        ws = e(B * nh * T)
+        K.attn_bwd(c["qkv"], c["y"], gy, c["lse"], B, T, nh, d, dqkv, ws, drop=(sv.pa, s_probs))
+        K.gemm(dqkv, c["xa"], 3 * d, d, R, a_trans=True, b_trans=True, C=slot(mod.c_attn.weight), accumulate=True,
+               a_rowsum=slot(mod.c_attn.bias))
+        if not need_x:
+            return None
+        gx = e(R, d)
+        K.gemm(dqkv, c["Wqkv"], R, d, 3 * d, b_trans=True, C=gx)
+        return gx.view(B, T, d)
+
+    return run(mod, fwd, bwd, x)
+
+
+def mlp(mod, x):
+    """Block.mlpf (transformer_block.py:81-83): dropout(c_proj(NewGELU(c_fc(x)))) on (..., d); `mod` is the block's
+    ``mlp`` ModuleDict.  The tanh-GELU and the dropout run in the GEMM epilogues."""
+    Td = operand_dtype()
+
+    def fwd(x, save):
+        shape = x.shape
+        d = shape[-1]
+        R = x.numel() // d
+        e = _empty(x.device)
+        training = mod.training
+        p = float(mod["dropout"].p) if training else 0.0
+        s = _seed(p)
+        xa = _cast(x.reshape(R, d), Td)
+        Wfc, Wp = _cast(mod["c_fc"].weight, Td), _cast(mod["c_proj"].weight, Td)
+        dh = Wfc.shape[0]
+        h, gl = e(R, dh, dt=Td), e(R, dh, dt=Td)
+        K.gemm(xa, Wfc, R, dh, d, bias=mod["c_fc"].bias, act=K.AW_ACT_GELU_TANH, C=h, C2=gl, c2_mode=1)
+        out = e(R, d)
+        K.gemm(gl, Wp, R, d, dh, bias=mod["c_proj"].bias, drop=(p, s), C=out)
+        sv = _Saved()
+        sv.shape, sv.p, sv.seed = shape, p, s
+        if save:
+            sv.c = dict(xa=xa, h=h, g=gl, Wfc=Wfc, Wp=Wp)
+        return out.view(shape), sv
+
+    def bwd(sv, g, slot, need_x):
+        d = sv.shape[-1]
+        R = g.numel() // d
+        e = _empty(g.device)
+        c = sv.c
+        dh = c["Wfc"].shape[0]
+        go = _masked_copy(g.reshape(R, d).float().contiguous(), Td, sv.p, sv.seed)
+        gh = e(R, dh, dt=Td)
+        K.gemm(go, c["Wp"], R, dh, d, b_trans=True, act=K.AW_ACT_GELU_TANH, pre=c["h"], C=gh)
+        K.gemm(go, c["g"], d, dh, R, a_trans=True, b_trans=True, C=slot(mod["c_proj"].weight), accumulate=True,
+               a_rowsum=slot(mod["c_proj"].bias))
+        K.gemm(gh, c["xa"], dh, d, R, a_trans=True, b_trans=True, C=slot(mod["c_fc"].weight), accumulate=True,
+               a_rowsum=slot(mod["c_fc"].bias))
+        if not need_x:
+            return None
+        gx = e(R, d)
+        K.gemm(gh, c["Wfc"], R, d, dh, b_trans=True, C=gx)
+        return gx.view(sv.shape)
 
     return run(mod, fwd, bwd, x)
 

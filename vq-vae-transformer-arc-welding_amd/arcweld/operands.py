@@ -20,26 +20,38 @@ from . import kernels as K
 
 
 class OperandJob:
-    """One operand copy: `param` (the nn.Parameter whose flat segment feeds it), `src` (the tensor the relayout reads:
-    the parameter or its contiguous centre-tap view), relayout (O, I, k, tap, mode, ldo) and the output tensor."""
-    __slots__ = ("name", "param", "src", "O", "I", "k", "tap", "mode", "ldo", "out")
+    """One operand copy: `param` (the nn.Parameter whose flat segment feeds it), its relayout source and geometry
+    (O, I, k, tap, mode, ldo) and the output tensor.  The source is derived from `param` at every use
+    (``derive(param) -> (src, O, I, k, tap, mode)``; default: the parameter itself with the geometry given here), so a
+    job built before the optimizer re-stores the parameter (flat buffer, tap-major or centre-tap views) reads the
+    storage the parameter has now, never a view of a buffer it no longer uses."""
+    __slots__ = ("name", "param", "derive", "O", "I", "k", "tap", "mode", "ldo", "out")
 
-    def __init__(self, name, param, src, O, I, k, tap, mode, out, ldo=0):
-        self.name, self.param, self.src = name, param, src
+    def __init__(self, name, param, O, I, k, tap, mode, out, ldo=0, derive=None):
+        self.name, self.param, self.derive = name, param, derive
         self.O, self.I, self.k, self.tap, self.mode, self.ldo, self.out = O, I, k, tap, mode, ldo, out
+
+    def geometry(self):
+        """(src, O, I, k, tap, mode) for the parameter's current storage."""
+        if self.derive is not None:
+            return self.derive(self.param)
+        return (self.param, self.O, self.I, self.k, self.tap, self.mode)
+
+    @property
+    def src(self):
+        return self.geometry()[0]
 
     def relayout_job(self):
         """(src, O, I, k, tap, mode, out, ldo) for the layout the source has NOW: a k = 3 conv weight the optimizer
         stores tap-major (arcweld.optim.RAdam.declare_tap_major: (O, 3, I) storage) turns the forward copy [O][3I]
         into a plain cast (mode 5 over O x 3I) and the input-gradient copy [3O][I] into mode 7."""
-        s = self.src
-        if self.mode in (1, 2) and self.k == 3 and s.dim() == 3 and not s.is_contiguous() \
-                and s.stride() == (3 * self.I, 1, self.I):
+        s, O, I, k, tap, mode = self.geometry()
+        if mode in (1, 2) and k == 3 and s.dim() == 3 and not s.is_contiguous() and s.stride() == (3 * I, 1, I):
             st = s.permute(0, 2, 1)       # the (O, 3, I) storage, contiguous
-            if self.mode == 1:
-                return (st, self.O, 3 * self.I, 1, 0, 5, self.out, self.ldo)
-            return (st, self.O, self.I, 3, 0, 7, self.out, self.ldo)
-        return (s, self.O, self.I, self.k, self.tap, self.mode, self.out, self.ldo)
+            if mode == 1:
+                return (st, O, 3 * I, 1, 0, 5, self.out, self.ldo)
+            return (st, O, I, 3, 0, 7, self.out, self.ldo)
+        return (s, O, I, k, tap, mode, self.out, self.ldo)
 
 
 class OperandSet:

@@ -28,7 +28,11 @@ from . import kernels as K
 F32 = torch.float32
 
 
-def _world():
+def _world(sync=None):
+    """Ranks the codebooks synchronise over: the process group's size, or 1 when ``sync`` is False (a Trainer that
+    runs each rank as an independent replica, ``devices=1``, sets ``ResidualVQ.sync_codebooks = False``)."""
+    if sync is False:
+        return 1
     d = torch.distributed
     return d.get_world_size() if d.is_available() and d.is_initialized() else 1
 
@@ -54,6 +58,7 @@ class EuclideanCodebook(nn.Module):
         self.register_buffer("embed", embed)
         self._initted_host = None      # host mirror of `initted` (read once, then kept in step with it)
         self._ws = None
+        self.sync_codebooks = None     # None: follow the process group; False: this rank's codebook only
         self.init_rows = None          # fixed k-means init rows (tests); None draws them like the library
 
     def _load_from_state_dict(self, *args, **kwargs):
@@ -77,7 +82,7 @@ class EuclideanCodebook(nn.Module):
         if rows is None:
             rows = torch.randperm(N, device=dev)[:Kc] if N >= Kc else torch.randint(0, N, (Kc,), device=dev)
         rows = rows.to(dev, torch.int64)
-        ws = _world()
+        ws = _world(self.sync_codebooks)
         if ws > 1:
             torch.distributed.broadcast(rows, 0)        # one set of initial means (rank 0's rows ...)
         means = torch.empty(Kc, D, device=dev)
@@ -121,7 +126,7 @@ class EuclideanCodebook(nn.Module):
             K.vq_finalize(counts, sq, N, Kc, D, 0.0, loss, perp)     # mse(q, r): commitment_weight 1
             sums = torch.zeros(Kc, D, device=dev)
             K.vq_cluster_sums(r, idx, Kc, sums)
-            ws = _world()
+            ws = _world(self.sync_codebooks)
             if ws > 1:
                 torch.distributed.all_reduce(counts)
                 torch.distributed.all_reduce(sums)
@@ -162,6 +167,17 @@ class ResidualVQ(nn.Module):
         self.layers = nn.ModuleList([VectorQuantize(dim, codebook_size, kmeans_init, kmeans_iters,
                                                     threshold_ema_dead_code, **kw) for _ in range(num_quantizers)])
         self._rng_counter = None
+
+    @property
+    def sync_codebooks(self):
+        """Whether the codebooks all-reduce their EMA statistics across ranks (None: whenever torch.distributed is
+        initialised).  Set by arcweld.trainer.Trainer from its data-parallel mode."""
+        return self.layers[0]._codebook.sync_codebooks if len(self.layers) else None
+
+    @sync_codebooks.setter
+    def sync_codebooks(self, value):
+        for layer in self.layers:
+            layer._codebook.sync_codebooks = value
 
     def seed_counter(self, dev):
         """Device counter mixed into the dead-code sampling seed; advanced once per training forward, so captured

@@ -91,6 +91,7 @@ class Trainer:
         self.accumulate = max(1, int(accumulate_grad_batches))
         self.log_every = log_every_n_steps
         self.fused_grad_sink = fused_grad_sink
+        self.bucket_elems = BUCKET_ELEMS   # all-reduce bucket (fp32 elements)
         self.hip_graphs = hip_graphs   # capture the step (fixed batch shape; accumulation groups replay per micro-batch)
         self.global_step = 0
         self.history = []
@@ -121,9 +122,14 @@ class Trainer:
             broadcast_params(model, opt)
         if hasattr(model, "operand_set") and hasattr(opt, "attach_operands"):
             opt.attach_operands(model.operand_set())     # the update kernel keeps the GEMM operand copies current
+        for mod in model.modules():
+            if hasattr(mod, "sync_codebooks"):
+                # residual-VQ codebooks synchronise across ranks only when the ranks train one model together
+                mod.sync_codebooks = bool(self.data_parallel)
         self.optimizer = opt
         self._graphs = None          # a captured step belongs to one optimizer
         self._graph_shape = None
+        self._late_key = None        # the late/early all-reduce spans follow this optimizer's flat offsets
         return opt
 
     def micro_step(self, model, batch, batch_idx, scale):
@@ -146,7 +152,8 @@ class Trainer:
         return world() if self.data_parallel else 1
 
     def optimizer_step(self, model):
-        works = allreduce_spans(self.optimizer.flat_grad, _spans(self.optimizer)) if self.data_parallel else []
+        works = allreduce_spans(self.optimizer.flat_grad, _spans(self.optimizer), self.bucket_elems) \
+            if self.data_parallel else []
         for w in works:
             w.wait()
         self._update(model)
@@ -170,12 +177,12 @@ class Trainer:
         if not self.data_parallel:
             return []
         if region == "all" or not hasattr(model, "backward_late_parameters"):
-            return allreduce_spans(flat, _spans(opt)) if region in ("all", "late") else []
+            return allreduce_spans(flat, _spans(opt), self.bucket_elems) if region in ("all", "late") else []
         key = (id(model), getattr(model, "task", None))      # the late set of the decoder follows its task
         if getattr(self, "_late_key", None) != key:
             late = opt.param_spans(model.backward_late_parameters())
             self._late_spans, self._early_spans, self._late_key = late, opt.live_spans_excluding(late), key
-        return allreduce_spans(flat, self._late_spans if region == "late" else self._early_spans)
+        return allreduce_spans(flat, self._late_spans if region == "late" else self._early_spans, self.bucket_elems)
 
     def fit(self, model, datamodule=None, train_dataloaders=None, val_dataloaders=None):
         if datamodule is not None:

@@ -19,6 +19,8 @@ weight-gradient GEMMs with the bias gradient fused as an A-row-sum).  Operands a
 """
 from __future__ import annotations
 
+import weakref
+
 import torch
 
 from . import kernels as K
@@ -127,21 +129,22 @@ def _operand_jobs(m, T, chain):
     pr = _params(m)
     dev = pr["pe"].weight.device
     e = lambda *s: torch.empty(*s, device=dev, dtype=T)  # noqa: E731
-    jobs = [J("Wp", pr["pe"].weight, pr["pe"].weight, H, 1, P, 0, 4, torch.zeros(H, sh.ldp, device=dev, dtype=T),
+    jobs = [J("Wp", pr["pe"].weight, H, 1, P, 0, 4, torch.zeros(H, sh.ldp, device=dev, dtype=T),
               sh.ldp)]
+    centre = lambda w: _centre_job(w, None)[:6]  # noqa: E731  (the centre tap of the CURRENT storage)
+    chain_src = lambda w: _centre_job(w, None)[:5] + (6,)  # noqa: E731
     for r, (c1, c2) in enumerate(pr["enc"]):
         for nm, c in (("1", c1), ("2", c2)):
-            src, O, I, k, tap, mode, _ = _centre_job(c.weight, None)
-            jobs.append(J(f"enc{r}_{nm}", c.weight, src, O, I, k, tap, mode, e(H, H)))
+            jobs.append(J(f"enc{r}_{nm}", c.weight, H, H, 1, 0, 0, e(H, H), derive=centre))
             if chain:   # K-step-major copies for the fused chain's weight stream (the backward reads enc_w)
-                jobs.append(J(f"chain{r}_{nm}", c.weight, src, O, I, k, tap, 6, e(H, H)))
-    jobs.append(J("Ws", pr["sep"].weight, pr["sep"].weight, D, H, 1, 0, 0, e(D, H)))
-    jobs.append(J("Wd0", pr["dec0"].weight, pr["dec0"].weight, H, D, 1, 0, 0, e(H, D)))
+                jobs.append(J(f"chain{r}_{nm}", c.weight, H, H, 1, 0, 6, e(H, H), derive=chain_src))
+    jobs.append(J("Ws", pr["sep"].weight, D, H, 1, 0, 0, e(D, H)))
+    jobs.append(J("Wd0", pr["dec0"].weight, H, D, 1, 0, 0, e(H, D)))
     for r, (c1, c2) in enumerate(pr["dec"]):
         for nm, c in (("1", c1), ("2", c2)):
-            jobs.append(J(f"dec{r}_{nm}", c.weight, c.weight, H, H, 3, 0, 1, e(H, 3 * H)))     # forward [O][3I]
-            jobs.append(J(f"dgw{r}_{nm}", c.weight, c.weight, H, H, 3, 0, 2, e(3 * H, H)))     # dgrad [3O][I]
-    jobs.append(J("Wt1", pr["t1"].weight, pr["t1"].weight, H, H, k1, 0, 3, e(k1 * H, H)))
+            jobs.append(J(f"dec{r}_{nm}", c.weight, H, H, 3, 0, 1, e(H, 3 * H)))     # forward [O][3I]
+            jobs.append(J(f"dgw{r}_{nm}", c.weight, H, H, 3, 0, 2, e(3 * H, H)))     # dgrad [3O][I]
+    jobs.append(J("Wt1", pr["t1"].weight, H, H, k1, 0, 3, e(k1 * H, H)))
     return jobs
 
 
@@ -168,7 +171,7 @@ def _conv3_job(w, mode, out):
     """Relayout job of a decoder k = 3 conv weight (mode 1: [O][3I] forward, mode 2: [3O][I] input gradient) for
     either storage order of the weight (contiguous (O, I, 3), or the optimizer's tap-major (O, 3, I))."""
     from .operands import OperandJob
-    return OperandJob("", w, w, w.shape[0], w.shape[1], 3, 0, mode, out).relayout_job()
+    return OperandJob("", w, w.shape[0], w.shape[1], 3, 0, mode, out).relayout_job()
 
 
 def _conv3_grad(g):
@@ -270,11 +273,13 @@ def forward(m, x, training: bool, need_backward: bool, dtype=None, seed: int = 0
     sv.ctr = rng_snapshot(m, dev, p_drop)
     acc = accumulators(m, dev, sh.K, H)
     sv.acc = acc
-    # the head-backward sums of the block are this forward's only while no other forward awaits its backward
-    pending = m.__dict__.get("_acc_pending", 0)
-    sv.head_gsums = acc["head_gsums"] if pending == 0 else torch.zeros(2 * H, device=dev, dtype=torch.float64)
-    if need_backward:
-        m.__dict__["_acc_pending"] = pending + 1
+    # the head-backward sums of the block belong to one saved forward at a time: the owner is held by a weak
+    # reference, released by its backward -- or by its collection when it is never backpropagated
+    owner = m.__dict__.get("_acc_owner")
+    owned = owner is not None and owner() is not None
+    sv.head_gsums = acc["head_gsums"] if not owned else torch.zeros(2 * H, device=dev, dtype=torch.float64)
+    if need_backward and not owned:
+        m.__dict__["_acc_owner"] = weakref.ref(sv)
 
     # ---- operand copies of the weights (relayout + cast): persistent, refreshed by one batched relayout only when
     #      a weight changed outside the optimizer (the flat RAdam rewrites them in its update kernel)
@@ -487,7 +492,9 @@ def backward(m, sv, g_emb, g_xhat, slot, mid_hook=None):
 
     # ---- head + BN backward
     gsums = sv.head_gsums
-    m.__dict__["_acc_pending"] = max(0, m.__dict__.get("_acc_pending", 1) - 1)
+    owner = m.__dict__.get("_acc_owner")
+    if owner is not None and owner() is sv:
+        m.__dict__["_acc_owner"] = None
     K.unpatch_head_bwd1(sv.Y2, sh.Q, sv.stats, pr["t2"].weight.view(H, 5), g_xhat, gsums,
                         slot(pr["t2"].weight).view(H, 5), slot(pr["t2"].bias), slot(bn.weight), slot(bn.bias))
     gY = e(N * k1, H, dt=T)

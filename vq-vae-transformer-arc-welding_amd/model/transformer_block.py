@@ -31,6 +31,10 @@ class CausalSelfAttention(nn.Module):
         # mask per (b, h, i, j) the backward regenerates; p > 0 takes the runtime-size VALU kernels
         self.attn_pdrop = float(attn_pdrop)
 
+    def forward(self, x):
+        """(B, T, d) -> resid_dropout(c_proj(attention)) (reference :40-63), an autograd node of its own."""
+        return modules.causal_self_attention(self, x)
+
 
 class Block(nn.Module):
     """x + attn(ln_1(x)); x + mlp(ln_2(x)) (reference :66-88)."""
@@ -47,6 +51,8 @@ class Block(nn.Module):
             dropout=nn.Dropout(res_dropout),
         ))
         self.res_dropout = res_dropout
+        m = self.mlp
+        self.mlpf = lambda x: modules.mlp(m, x)   # MLP forward (reference :81-83), an autograd node of its own
 
     def forward(self, x):
         """(B, T, d) -> (B, T, d); dropout active in training mode.  An autograd node of its own when anything

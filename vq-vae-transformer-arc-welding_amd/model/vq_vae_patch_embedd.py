@@ -71,6 +71,10 @@ class ResBlock(nn.Module):
             nn.Dropout(p=dropout_p),
         )
 
+    def forward(self, x):
+        """(B, C, L) -> x + block(x): an autograd node of its own on the per-block kernels (arcweld.modules)."""
+        return modules.resblock(self, x)
+
 
 class SepCNNBlock(nn.Module):
     """Per-token Conv1d(H -> D, k=1) then permute to (B, S, D) (reference :77-91)."""
