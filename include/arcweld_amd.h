@@ -93,6 +93,10 @@ int aw_gemm_grouped(const aw_gemm_args* args, int n, void* stream);
 /* Tile policy knob: 0 = automatic (256x128 tiles for bf16 launches that fill the chip, else 128x128), 128 or 256 =
  * force that tile for every eligible launch (bf16, non-ragged) -- used by the tests to cover both pipelines. */
 int aw_gemm_set_tile(int bm);
+/* Weight-gradient kernel policy for the grouped decoder k = 3 launches (model/vq_vae_patch_embedd.py:60-74 grads):
+ * 0 = automatic (the 8-wave ping-pong kernel when the shape qualifies and fills the chip), 1 = force it whenever the
+ * shape qualifies, -1 = always the generic grouped GEMM (tests, A/B). */
+int aw_gemm_set_wgrad_policy(int mode);
 
 /* ------------------------------------------------------------------------ fused encoder ResBlock chain
  * The per-token encoder stack in bf16 operands (model/vq_vae_patch_embedd.py:60-74, applied by
@@ -238,6 +242,17 @@ int aw_unpatch_head_bwd1(const float* y, int64_t R, int H, int Q, const float* s
 int aw_unpatch_head_bwd2(const float* y, int64_t R, int H, int Q, const float* stats, const float* w2,
                          const float* g_xhat, const double* gsums, int training, void* g_y, int gy_dtype, float* db_y,
                          void* stream);
+/* The same three passes with y in y_dtype (AW_F32, or AW_BF16 when H is a power of two in 64..2048): the bf16
+ * operand mode stores the ConvT output in bf16, halving the head's three HBM passes over it; the BN statistics
+ * still come from the f32 values in the ConvT epilogue. */
+int aw_unpatch_head_fwd_ex(const void* y, int y_dtype, int64_t R, int H, int Q, const float* stats, const float* w2,
+                           const float* b2, float* x_hat, void* stream);
+int aw_unpatch_head_bwd1_ex(const void* y, int y_dtype, int64_t R, int H, int Q, const float* stats, const float* w2,
+                            const float* g_xhat, double* gsums, float* gw2, float* gb2, float* ggamma, float* gbeta,
+                            void* stream);
+int aw_unpatch_head_bwd2_ex(const void* y, int y_dtype, int64_t R, int H, int Q, const float* stats, const float* w2,
+                            const float* g_xhat, const double* gsums, int training, void* g_y, int gy_dtype,
+                            float* db_y, void* stream);
 /* BatchNorm1d of the `--batchnorm 1` ResBlocks (model/vq_vae_patch_embedd.py:60-74).  Activations h are
  * [N rows][H channels] f32; statistics are per (group, channel), group = row % G (decoder G = 1; encoder G = S
  * token positions, each its own batch of B rows: CNNBlock(seperate=True) runs the blocks per token slice).

@@ -361,3 +361,83 @@ def test_mse_loss_vs_fp64(K, n, off):
     got = mse_loss(a, b).item()
     ref = ((a.double() - b.double()) ** 2).mean().item()
     np.testing.assert_allclose(got, ref, rtol=2e-6)
+
+
+@pytest.mark.parametrize("policy,G,Cout,Cin,Ntok,S,ref_layout,alpha", [
+    (0, 16, 512, 512, 16 * 1024, 16, False, 1.0),     # the decoder's grouped launch at full size (auto policy)
+    (1, 3, 256, 128, 1024, 8, True, 1.0),             # forced at a small shape: windows of 8, (O, I, 3) column map
+    (1, 2, 512, 64, 2048, 32, False, 0.5),            # windows of 32, one channel block, alpha
+    (-1, 4, 512, 512, 4096, 16, False, 1.0)])         # the generic grouped GEMM on the same form
+def test_wgrad_conv3_kernel_vs_fp32_reference(policy, G, Cout, Cin, Ntok, S, ref_layout, alpha):
+    """The 8-wave ping-pong decoder weight-gradient kernel (csrc/wgrad.hip, model/vq_vae_patch_embedd.py:60-74 grads)
+    against a torch fp32 reference on the same bf16 operands: dW[o][j, i] += alpha sum_t dy[t][o] x[t+j-1][i] inside
+    each window, the bias row sums, accumulation into a non-zero gradient, the tap-major [O][3I] layout and the
+    reference's (O, I, 3) column map."""
+    from arcweld import _native
+    from arcweld import kernels as K
+    g = torch.Generator(device=DEV).manual_seed(1234 + G)
+    probs, refs = [], []
+    for k in range(G):
+        A = torch.randn(Ntok, Cout, device=DEV, generator=g).to(torch.bfloat16)
+        x = torch.randn(Ntok, Cin, device=DEV, generator=g).to(torch.bfloat16)
+        C0 = torch.randn(Cout, Cin, 3, device=DEV, generator=g)
+        b0 = torch.randn(Cout, device=DEV, generator=g)
+        full = A.float().t() @ _shift_taps(x.float(), S)          # [O][3I], column j*I + i
+        if ref_layout:       # the reference's contiguous (O, I, 3) weight: column j*I + i -> i*3 + j
+            C = C0.clone()
+            kw = dict(C=C.view(Cout, 3 * Cin), col_map=(Cin, 3, 0))
+            want = C0 + alpha * full.view(Cout, 3, Cin).permute(0, 2, 1)
+        else:                # the optimizer's tap-major (O, 3, I) storage: contiguous rows
+            C = C0.view(Cout, 3 * Cin).clone()
+            kw = dict(C=C)
+            want = C0.view(Cout, 3 * Cin) + alpha * full
+        b = b0.clone()
+        probs.append((A, x, Cout, 3 * Cin, Ntok, dict(a_trans=True, b_trans=True, conv=(Cin, S, 1, 1), accumulate=True,
+                                                      a_rowsum=b, alpha=alpha, **kw)))
+        refs.append((C, b, want, b0 + alpha * A.float().sum(0)))
+    _native.call("aw_gemm_set_wgrad_policy", policy)
+    try:
+        K.gemm_grouped(probs)
+        torch.cuda.synchronize()
+    finally:
+        _native.call("aw_gemm_set_wgrad_policy", 0)
+    for C, b, want, bw in refs:
+        scale = float(want.abs().max())
+        torch.testing.assert_close(C, want, rtol=1e-4, atol=2e-5 * scale)
+        torch.testing.assert_close(b, bw, rtol=1e-4, atol=2e-5 * float(bw.abs().max()))
+
+
+@pytest.mark.parametrize("training", [True, False])
+def test_unpatch_head_bf16_y_equals_f32_y(training):
+    """aw_unpatch_head_*_ex with the ConvT output in bf16 (the bf16 operand mode, model/vq_vae_patch_embedd.py:24-31)
+    computes exactly what the f32 passes compute on the same (bf16-representable) values: x_hat, the ConvT2 / BN
+    gradients, the per-channel sums and g_y are bit-identical."""
+    from arcweld import kernels as K
+    B, Q, H = 64, 80, 512
+    R = B * Q
+    y16 = (torch.randn(R, H, device=DEV, generator=torch.Generator(device=DEV).manual_seed(3)) * 1.3 + 0.2).to(
+        torch.bfloat16)
+    stats = torch.cat([torch.randn(H, device=DEV) * 0.1, torch.rand(H, device=DEV) + 0.5,
+                       torch.randn(H, device=DEV) * 0.2 + 1.0, torch.randn(H, device=DEV) * 0.1])
+    w2 = torch.randn(H, 5, device=DEV) * 0.05
+    b2 = torch.randn(1, device=DEV)
+    g = torch.randn(B, Q * 5 // 2, 2, device=DEV)
+    outs = []
+    for y in (y16.float(), y16):
+        x_hat = torch.empty(B, Q * 5 // 2, 2, device=DEV)
+        K.unpatch_head_fwd(y, Q, stats, w2, b2, x_hat)
+        gsums = torch.zeros(2 * H, device=DEV, dtype=torch.float64)
+        gw2, gb2 = torch.zeros(H, 5, device=DEV), torch.zeros(1, device=DEV)
+        gga, gbe = torch.zeros(H, device=DEV), torch.zeros(H, device=DEV)
+        K.unpatch_head_bwd1(y, Q, stats, w2, g, gsums, gw2, gb2, gga, gbe)
+        gy, dby = torch.empty(R, H, device=DEV, dtype=torch.bfloat16), torch.zeros(H, device=DEV)
+        K.unpatch_head_bwd2(y, Q, stats, w2, g, gsums, training, gy, dby)
+        torch.cuda.synchronize()
+        outs.append((x_hat, gsums, gw2, gb2, gga, gbe, gy, dby))
+    # the per-channel reductions end in atomics (order varies run to run): close, not bitwise; the per-row
+    # quantities (x_hat, g_y) use the same inputs in the same order
+    torch.testing.assert_close(outs[1][0], outs[0][0], rtol=0, atol=0)
+    for a, b in zip(outs[1][1:6], outs[0][1:6]):
+        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6 * float(b.abs().max()))
+    torch.testing.assert_close(outs[1][6].float(), outs[0][6].float(), rtol=1e-2, atol=1e-3)
+    torch.testing.assert_close(outs[1][7], outs[0][7], rtol=1e-4, atol=1e-5 * float(outs[0][7].abs().max()))

@@ -88,6 +88,7 @@ SIGNATURES = {
     "aw_gemm_workspace": [ctypes.POINTER(GemmArgs)],
     "aw_gemm_grouped": [ctypes.POINTER(GemmArgs), c_int, c_p],
     "aw_gemm_set_tile": [c_int],
+    "aw_gemm_set_wgrad_policy": [c_int],
     "aw_weight_relayout_batch": [ctypes.POINTER(RelayoutJob), c_int, c_int, c_p],
     "aw_vq_forward": [c_p, c_p, c_i64, c_int, c_int, c_p, c_p, c_p, c_p, c_p],
     "aw_vq_forward_ex": [c_p, c_p, c_i64, c_int, c_int, c_p, c_p, c_p, c_p, c_p, c_int, c_p],
@@ -104,6 +105,9 @@ SIGNATURES = {
     "aw_bn_finalize": [c_p, c_i64, c_int, c_p, c_p, c_p, c_p, c_p, c_f, c_f, c_int, c_p, c_p],
     "aw_unpatch_head_bwd1": [c_p, c_i64, c_int, c_int, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p],
     "aw_unpatch_head_bwd2": [c_p, c_i64, c_int, c_int, c_p, c_p, c_p, c_p, c_int, c_p, c_int, c_p, c_p],
+    "aw_unpatch_head_fwd_ex": [c_p, c_int, c_i64, c_int, c_int, c_p, c_p, c_p, c_p, c_p],
+    "aw_unpatch_head_bwd1_ex": [c_p, c_int, c_i64, c_int, c_int, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p],
+    "aw_unpatch_head_bwd2_ex": [c_p, c_int, c_i64, c_int, c_int, c_p, c_p, c_p, c_p, c_int, c_p, c_int, c_p, c_p],
     "aw_bn_group_stats": [c_p, c_i64, c_int, c_int, c_p, c_p],
     "aw_bn_group_finalize": [c_p, c_i64, c_int, c_int, c_p, c_p, c_p, c_p, c_p, c_f, c_f, c_int, c_p, c_p],
     "aw_bn_apply": [c_p, c_i64, c_int, c_int, c_p, c_int, c_p, c_f, ctypes.c_uint64, c_p, c_p, c_p, c_int, c_p],

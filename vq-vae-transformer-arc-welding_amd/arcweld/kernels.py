@@ -272,20 +272,27 @@ def bn_finalize(colstats, n, H, gamma, beta, rm, rv, nbt, eps, momentum, trainin
 
 
 def unpatch_head_fwd(y, Q, stats, w2, b2, x_hat, stream=None):
+    """y (R, H) f32 or bf16 (the ConvT output in the bf16 operand mode)."""
     R, H = y.shape
-    call("aw_unpatch_head_fwd", ptr(y), R, H, Q, ptr(stats), ptr(w2), ptr(b2), ptr(x_hat), stream_ptr(stream))
+    call("aw_unpatch_head_fwd_ex", ptr(y), dtype_code(y.dtype), R, H, Q, ptr(stats), ptr(w2), ptr(b2), ptr(x_hat),
+         stream_ptr(stream))
 
 
 def unpatch_head_bwd1(y, Q, stats, w2, g_xhat, gsums, gw2, gb2, ggamma, gbeta, stream=None):
     R, H = y.shape
-    call("aw_unpatch_head_bwd1", ptr(y), R, H, Q, ptr(stats), ptr(w2), ptr(g_xhat), ptr(gsums), ptr(gw2), ptr(gb2),
-         ptr(ggamma), ptr(gbeta), stream_ptr(stream))
+    call("aw_unpatch_head_bwd1_ex", ptr(y), dtype_code(y.dtype), R, H, Q, ptr(stats), ptr(w2), ptr(g_xhat), ptr(gsums),
+         ptr(gw2), ptr(gb2), ptr(ggamma), ptr(gbeta), stream_ptr(stream))
 
 
 def unpatch_head_bwd2(y, Q, stats, w2, g_xhat, gsums, training, g_y, db_y, stream=None):
     R, H = y.shape
-    call("aw_unpatch_head_bwd2", ptr(y), R, H, Q, ptr(stats), ptr(w2), ptr(g_xhat), ptr(gsums), int(training),
-         ptr(g_y), dtype_code(g_y.dtype), ptr(db_y), stream_ptr(stream))
+    call("aw_unpatch_head_bwd2_ex", ptr(y), dtype_code(y.dtype), R, H, Q, ptr(stats), ptr(w2), ptr(g_xhat),
+         ptr(gsums), int(training), ptr(g_y), dtype_code(g_y.dtype), ptr(db_y), stream_ptr(stream))
+
+
+def head_bf16_ok(H):
+    """The head passes take a bf16 ConvT output when H is a power of two in 64..2048 (aw_unpatch_head_*_ex)."""
+    return 64 <= H <= 2048 and H & (H - 1) == 0
 
 
 def mse_fwd(a, b, sqerr, stream=None):

@@ -392,7 +392,9 @@ def forward(m, x, training: bool, need_backward: bool, dtype=None, seed: int = 0
 
     # ---- un-patch: ConvT(H->H, k1) with BN statistics in the epilogue, then the fused head
     bn = pr["bn"]
-    Y = e(N, k1 * H)
+    # bf16 operand mode: the ConvT output is stored in bf16 (the head's three passes read it; the BN statistics come
+    # from the f32 values inside the epilogue); exact-f32 mode keeps it f32
+    Y = e(N, k1 * H, dt=T if (T != F32 and K.head_bf16_ok(H)) else F32)
     colstats = acc["colstats"] if training else None
     K.gemm(yR_T, Wt1, N, k1 * H, H, bias=pr["t1"].bias, bias_mod=H, C=Y, colstats=colstats, stats_mod=H)
     stats = e(4 * H)

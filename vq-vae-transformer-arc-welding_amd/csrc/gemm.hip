@@ -301,6 +301,7 @@ extern "C" int aw_gemm_grouped(const aw_gemm_args* args, int n, void* stream) {
   }
   AW_REQUIRE(a.accumulate && !a.C2 && !a.bias && !a.colstats, "aw_gemm_grouped: accumulate-mode problems only");
   if (a.M == 0 || a.N == 0) return AW_OK;
+  if (wgrad_conv3_try(args, n, reinterpret_cast<hipStream_t>(stream))) return aw::check_launch("aw_gemm_grouped");
   GemmP P;
   plan(a, n, true, P);
   for (int g = 0; g < n; ++g) {

@@ -831,6 +831,9 @@ inline void launch_tiled(const GemmP& P, hipStream_t s) {
 // code) has no compiled specialisation, so the caller falls back to the EP_GENERIC kernel.
 bool launch_fast_fwd(const GemmP& P, hipStream_t s, bool is_bf16, Layout ly, uint32_t code);
 bool launch_fast_bwd(const GemmP& P, hipStream_t s, bool is_bf16, Layout ly, uint32_t code);
+// The grouped decoder k = 3 weight gradient on the 8-wave ping-pong kernel (wgrad.hip); false when the shape or
+// the policy (aw_gemm_set_wgrad_policy) rules it out (the caller then runs the generic grouped GEMM).
+bool wgrad_conv3_try(const aw_gemm_args* args, int n, hipStream_t s);
 
 #define AW_FAST_CASE(T, LY, CODE) \
   case (CODE): launch_tiled<T, LY, (CODE)>(P, s); return true;

@@ -20,6 +20,8 @@ namespace awg {
   X(T, LY, EP_BIAS | EP_C)                                                  \
   X(T, LY, EP_BIAS | EP_BIASMOD | EP_C | EP_STATS)                          \
   X(T, LY, EP_BIAS | EP_BIASMOD | EP_C)                                     \
+  X(T, LY, EP_BIAS | EP_BIASMOD | EP_C | EP_CBF | EP_STATS)                 \
+  X(T, LY, EP_BIAS | EP_BIASMOD | EP_C | EP_CBF)                            \
   X(T, LY, EP_BIAS | EP_C | EP_CBF)                                         \
   X(T, LY, EP_BIAS | EP_DROP | EP_RESID | EP_C)                             \
   X(T, LY, EP_BIAS | EP_RESID | EP_C)                                       \

@@ -237,8 +237,21 @@ __device__ __forceinline__ float wave_sum_to_last(float v) {
   return v;
 }
 
-template <int NS>
-__global__ __launch_bounds__(256) void head_fwd_kernel(const float* __restrict__ y, int64_t R, int H, int Q,
+// 4 consecutive channels of y as f32 (y f32, or bf16: the ConvT output stored in the operand dtype)
+__device__ __forceinline__ float4 head_load4(const float* y, int64_t e) { return *reinterpret_cast<const float4*>(y + e); }
+__device__ __forceinline__ float4 head_load4(const bf16* y, int64_t e) {
+  const uint2 h = *reinterpret_cast<const uint2*>(y + e);
+  return make_float4(__uint_as_float(h.x << 16), __uint_as_float(h.x & 0xFFFF0000u), __uint_as_float(h.y << 16),
+                     __uint_as_float(h.y & 0xFFFF0000u));
+}
+__device__ __forceinline__ float2 head_load2(const float* y, int64_t e) { return *reinterpret_cast<const float2*>(y + e); }
+__device__ __forceinline__ float2 head_load2(const bf16* y, int64_t e) {
+  const uint32_t h = *reinterpret_cast<const uint32_t*>(y + e);
+  return make_float2(__uint_as_float(h << 16), __uint_as_float(h & 0xFFFF0000u));
+}
+
+template <int NS, typename TY = float>
+__global__ __launch_bounds__(256) void head_fwd_kernel(const TY* __restrict__ y, int64_t R, int H, int Q,
                                                        const float* __restrict__ st, const float* __restrict__ w2,
                                                        const float* __restrict__ b2, float* __restrict__ x_hat) {
   const int lane = threadIdx.x & 63;
@@ -264,8 +277,7 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(const float* __restrict__
   auto load_row = [&](int d, int64_t r) {
 #pragma unroll
     for (int s = 0; s < NS; ++s)
-      nv[d][s] = (hp.on[s] && r < R) ? *reinterpret_cast<const float4*>(y + r * H + lane * 4 + 256 * s)
-                                     : make_float4(0.f, 0.f, 0.f, 0.f);
+      nv[d][s] = (hp.on[s] && r < R) ? head_load4(y, r * H + lane * 4 + 256 * s) : make_float4(0.f, 0.f, 0.f, 0.f);
   };
 #pragma unroll
   for (int d = 0; d < FD; ++d) load_row(d, wave + d * nw);
@@ -501,7 +513,8 @@ struct Head2 {   // the two channels c0, c0+1 of a thread as register pairs
 // of look-ahead kept ~8 KB per CU in flight (1.9-3.3 TB/s); HEAD_CS_DEPTH rows are loaded ahead instead.
 constexpr int HEAD_CS_DEPTH = 2;
 
-__global__ __launch_bounds__(1024) void head_bwd1_cs_kernel(const float* __restrict__ y, int64_t R, int H, int Q,
+template <typename TY>
+__global__ __launch_bounds__(1024) void head_bwd1_cs_kernel(const TY* __restrict__ y, int64_t R, int H, int Q,
                                                            const float* __restrict__ st, const float* __restrict__ w2,
                                                            const float* __restrict__ gx, double* __restrict__ gsums,
                                                            float* __restrict__ gw2, float* __restrict__ gb2,
@@ -527,7 +540,7 @@ __global__ __launch_bounds__(1024) void head_bwd1_cs_kernel(const float* __restr
     const float* gp = gx + rr * 5;          // row r = b*Q + q -> g_xhat[b][5q + j]
 #pragma unroll
     for (int j = 0; j < 5; ++j) ngo[d][j] = in ? gp[j] : 0.f;
-    nv[d] = in ? *reinterpret_cast<const float2*>(y + rr * H + c0) : make_float2(0.f, 0.f);
+    nv[d] = in ? head_load2(y, rr * H + c0) : make_float2(0.f, 0.f);
   };
   const int64_t r0 = (int64_t)blockIdx.x * rpb + rg;
 #pragma unroll
@@ -577,8 +590,8 @@ __global__ __launch_bounds__(1024) void head_bwd1_cs_kernel(const float* __restr
   }
 }
 
-template <typename T>
-__global__ __launch_bounds__(1024) void head_bwd2_cs_kernel(const float* __restrict__ y, int64_t R, int H, int Q,
+template <typename T, typename TY>
+__global__ __launch_bounds__(1024) void head_bwd2_cs_kernel(const TY* __restrict__ y, int64_t R, int H, int Q,
                                                            const float* __restrict__ st, const float* __restrict__ w2,
                                                            const float* __restrict__ gx,
                                                            const double* __restrict__ gsums, int training,
@@ -607,7 +620,7 @@ __global__ __launch_bounds__(1024) void head_bwd2_cs_kernel(const float* __restr
     const float* gp = gx + rr * 5;          // row r = b*Q + q -> g_xhat[b][5q + j]
 #pragma unroll
     for (int j = 0; j < 5; ++j) ngo[d][j] = in ? gp[j] : 0.f;
-    nv[d] = in ? *reinterpret_cast<const float2*>(y + rr * H + c0) : make_float2(0.f, 0.f);
+    nv[d] = in ? head_load2(y, rr * H + c0) : make_float2(0.f, 0.f);
   };
   const int64_t r0 = (int64_t)blockIdx.x * rpb + rg;
 #pragma unroll
@@ -801,11 +814,12 @@ extern "C" int aw_bn_finalize(const double* colstats, int64_t n, int H, const fl
   return aw::check_launch("aw_bn_finalize");
 }
 
-extern "C" int aw_unpatch_head_fwd(const float* y, int64_t R, int H, int Q, const float* stats, const float* w2,
-                                   const float* b2, float* x_hat, void* stream) {
-  AW_REQUIRE(y && stats && w2 && b2 && x_hat && R >= 0 && Q > 0 && H > 0, "aw_unpatch_head_fwd: bad args");
+extern "C" int aw_unpatch_head_fwd_ex(const void* yv, int y_dtype, int64_t R, int H, int Q, const float* stats,
+                                      const float* w2, const float* b2, float* x_hat, void* stream) {
+  AW_REQUIRE(yv && stats && w2 && b2 && x_hat && R >= 0 && Q > 0 && H > 0, "aw_unpatch_head_fwd: bad args");
   AW_REQUIRE(H % 4 == 0 && H <= 256 * HEAD_MAXV, "aw_unpatch_head_fwd: H must be a multiple of 4 and <= 1024");
   AW_REQUIRE(R % Q == 0, "aw_unpatch_head_fwd: rows must be whole windows");
+  AW_REQUIRE(y_dtype == AW_F32 || y_dtype == AW_BF16, "aw_unpatch_head_fwd: bad y_dtype %d", y_dtype);
   if (R == 0) return AW_OK;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   // one resident round of workgroups: a grid larger than what fits at the kernel's occupancy runs a second, partly
@@ -821,29 +835,44 @@ extern "C" int aw_unpatch_head_fwd(const float* y, int64_t R, int H, int Q, cons
     return per > 0 && cus > 0 ? per * cus : 2048;
   }();
   dim3 grid(grid_for(R * 64, 256, fwd_wgs));
-  switch ((H + 255) / 256) {
-    case 1: hipLaunchKernelGGL(head_fwd_kernel<1>, grid, dim3(256), 0, s, y, R, H, Q, stats, w2, b2, x_hat); break;
-    case 2: hipLaunchKernelGGL(head_fwd_kernel<2>, grid, dim3(256), 0, s, y, R, H, Q, stats, w2, b2, x_hat); break;
-    case 3: hipLaunchKernelGGL(head_fwd_kernel<3>, grid, dim3(256), 0, s, y, R, H, Q, stats, w2, b2, x_hat); break;
-    default: hipLaunchKernelGGL(head_fwd_kernel<4>, grid, dim3(256), 0, s, y, R, H, Q, stats, w2, b2, x_hat); break;
+#define AW_HF(NSV, TY) \
+  hipLaunchKernelGGL((head_fwd_kernel<NSV, TY>), grid, dim3(256), 0, s, (const TY*)yv, R, H, Q, stats, w2, b2, x_hat)
+  const int ns = (H + 255) / 256;
+  if (y_dtype == AW_BF16) {
+    if (ns == 1) AW_HF(1, bf16); else if (ns == 2) AW_HF(2, bf16); else if (ns == 3) AW_HF(3, bf16); else AW_HF(4, bf16);
+  } else {
+    if (ns == 1) AW_HF(1, float); else if (ns == 2) AW_HF(2, float); else if (ns == 3) AW_HF(3, float); else AW_HF(4, float);
   }
+#undef AW_HF
   return aw::check_launch("aw_unpatch_head_fwd");
 }
 
-extern "C" int aw_unpatch_head_bwd1(const float* y, int64_t R, int H, int Q, const float* stats, const float* w2,
-                                    const float* g_xhat, double* gsums, float* gw2, float* gb2, float* ggamma,
-                                    float* gbeta, void* stream) {
-  AW_REQUIRE(y && stats && w2 && g_xhat && gsums && gw2 && gb2, "aw_unpatch_head_bwd1: null pointer");
+extern "C" int aw_unpatch_head_fwd(const float* y, int64_t R, int H, int Q, const float* stats, const float* w2,
+                                   const float* b2, float* x_hat, void* stream) {
+  return aw_unpatch_head_fwd_ex(y, AW_F32, R, H, Q, stats, w2, b2, x_hat, stream);
+}
+
+extern "C" int aw_unpatch_head_bwd1_ex(const void* yv, int y_dtype, int64_t R, int H, int Q, const float* stats,
+                                       const float* w2, const float* g_xhat, double* gsums, float* gw2, float* gb2,
+                                       float* ggamma, float* gbeta, void* stream) {
+  AW_REQUIRE(yv && stats && w2 && g_xhat && gsums && gw2 && gb2, "aw_unpatch_head_bwd1: null pointer");
   AW_REQUIRE(H % 4 == 0 && H <= 256 * HEAD_MAXV && R % Q == 0, "aw_unpatch_head_bwd1: bad shape");
+  AW_REQUIRE(y_dtype == AW_F32 || (y_dtype == AW_BF16 && head_cs_ok(H)),
+             "aw_unpatch_head_bwd1: y_dtype %d (bf16 y needs H a power of two in 64..2048)", y_dtype);
   if (R == 0) return AW_OK;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const size_t sh = 7 * H * sizeof(float);
   if (head_cs_ok(H)) {
     const dim3 g1(grid_for(R * (H / 2), 1024, head_wgs()));
-    hipLaunchKernelGGL(head_bwd1_cs_kernel, g1, dim3(1024), sh, s, y, R, H, Q, stats, w2, g_xhat, gsums, gw2, gb2,
-                       ggamma, gbeta);
+    if (y_dtype == AW_BF16)
+      hipLaunchKernelGGL(head_bwd1_cs_kernel<bf16>, g1, dim3(1024), sh, s, (const bf16*)yv, R, H, Q, stats, w2, g_xhat,
+                         gsums, gw2, gb2, ggamma, gbeta);
+    else
+      hipLaunchKernelGGL(head_bwd1_cs_kernel<float>, g1, dim3(1024), sh, s, (const float*)yv, R, H, Q, stats, w2,
+                         g_xhat, gsums, gw2, gb2, ggamma, gbeta);
     return aw::check_launch("aw_unpatch_head_bwd1");
   }
+  const float* y = (const float*)yv;
   dim3 grid(grid_for(R * 64, 256, 512));
 #define AW_H1(NSV) \
   hipLaunchKernelGGL(head_bwd1_kernel<NSV>, grid, dim3(256), sh, s, y, R, H, Q, stats, w2, g_xhat, gsums, gw2, gb2, \
@@ -858,24 +887,36 @@ extern "C" int aw_unpatch_head_bwd1(const float* y, int64_t R, int H, int Q, con
   return aw::check_launch("aw_unpatch_head_bwd1");
 }
 
-extern "C" int aw_unpatch_head_bwd2(const float* y, int64_t R, int H, int Q, const float* stats, const float* w2,
-                                    const float* g_xhat, const double* gsums, int training, void* g_y, int gy_dtype,
-                                    float* db_y, void* stream) {
-  AW_REQUIRE(y && stats && w2 && g_xhat && gsums && g_y && db_y, "aw_unpatch_head_bwd2: null pointer");
+extern "C" int aw_unpatch_head_bwd1(const float* y, int64_t R, int H, int Q, const float* stats, const float* w2,
+                                    const float* g_xhat, double* gsums, float* gw2, float* gb2, float* ggamma,
+                                    float* gbeta, void* stream) {
+  return aw_unpatch_head_bwd1_ex(y, AW_F32, R, H, Q, stats, w2, g_xhat, gsums, gw2, gb2, ggamma, gbeta, stream);
+}
+
+extern "C" int aw_unpatch_head_bwd2_ex(const void* yv, int y_dtype, int64_t R, int H, int Q, const float* stats,
+                                       const float* w2, const float* g_xhat, const double* gsums, int training,
+                                       void* g_y, int gy_dtype, float* db_y, void* stream) {
+  AW_REQUIRE(yv && stats && w2 && g_xhat && gsums && g_y && db_y, "aw_unpatch_head_bwd2: null pointer");
   AW_REQUIRE(H % 4 == 0 && H <= 256 * HEAD_MAXV && R % Q == 0, "aw_unpatch_head_bwd2: bad shape");
+  AW_REQUIRE(y_dtype == AW_F32 || (y_dtype == AW_BF16 && head_cs_ok(H)),
+             "aw_unpatch_head_bwd2: y_dtype %d (bf16 y needs H a power of two in 64..2048)", y_dtype);
   if (R == 0) return AW_OK;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const size_t sh = H * sizeof(float);
   if (head_cs_ok(H)) {
     dim3 g2(grid_for(R * (H / 2), 1024, head_wgs()));
-    if (gy_dtype == AW_BF16)
-      hipLaunchKernelGGL(head_bwd2_cs_kernel<bf16>, g2, dim3(1024), sh, s, y, R, H, Q, stats, w2, g_xhat, gsums,
-                         training, (bf16*)g_y, db_y);
-    else
-      hipLaunchKernelGGL(head_bwd2_cs_kernel<float>, g2, dim3(1024), sh, s, y, R, H, Q, stats, w2, g_xhat, gsums,
-                         training, (float*)g_y, db_y);
+#define AW_H2C(T, TY) \
+  hipLaunchKernelGGL((head_bwd2_cs_kernel<T, TY>), g2, dim3(1024), sh, s, (const TY*)yv, R, H, Q, stats, w2, g_xhat, \
+                     gsums, training, (T*)g_y, db_y)
+    if (gy_dtype == AW_BF16) {
+      if (y_dtype == AW_BF16) AW_H2C(bf16, bf16); else AW_H2C(bf16, float);
+    } else {
+      if (y_dtype == AW_BF16) AW_H2C(float, bf16); else AW_H2C(float, float);
+    }
+#undef AW_H2C
     return aw::check_launch("aw_unpatch_head_bwd2");
   }
+  const float* y = (const float*)yv;
   dim3 grid(grid_for(R * 64, 256, 1024));
 #define AW_H2(TY, NSV) \
   hipLaunchKernelGGL((head_bwd2_kernel<TY, NSV>), grid, dim3(256), sh, s, y, R, H, Q, stats, w2, g_xhat, gsums, \
@@ -888,6 +929,13 @@ extern "C" int aw_unpatch_head_bwd2(const float* y, int64_t R, int H, int Q, con
   }
 #undef AW_H2
   return aw::check_launch("aw_unpatch_head_bwd2");
+}
+
+extern "C" int aw_unpatch_head_bwd2(const float* y, int64_t R, int H, int Q, const float* stats, const float* w2,
+                                    const float* g_xhat, const double* gsums, int training, void* g_y, int gy_dtype,
+                                    float* db_y, void* stream) {
+  return aw_unpatch_head_bwd2_ex(y, AW_F32, R, H, Q, stats, w2, g_xhat, gsums, training, g_y, gy_dtype, db_y,
+                                 stream);
 }
 
 extern "C" int aw_mse_fwd(const float* a, const float* b, int64_t n, double* sqerr, void* stream) {

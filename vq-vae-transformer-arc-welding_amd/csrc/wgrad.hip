@@ -1,0 +1,355 @@
+// Weight gradients of the decoder's k = 3 / pad = 1 ResBlock convs (model/vq_vae_patch_embedd.py:60-74 via
+// :142-145; the reference's autograd computes them through cuDNN's wgrad):
+//   dW[o][j*I + i] += sum_t dy[t][o] * x[t + j - 1][i]   (x zero outside the token's window of `seg` tokens)
+// as one launch over all (up to 16) convs of the ResBlock stack, bf16 operands, fp32 accumulation.
+//
+// gfx950 design (one workgroup per CU, 512 threads = 8 waves, 160 KB LDS):
+//  * Tile = 256 output channels x (3 taps x 64 input channels).  Both operands are token-major ([K][rows]), so each
+//    K-tile of 64 tokens stages dy[64][256] (32 KB) and ONE x[64][64] image (8 KB) that serves all three taps: tap j
+//    reads the x rows shifted by j - 1 (the shift never leaves a window, and windows never straddle a 64-token
+//    K-tile since seg | 64).  The taps' window masks are one AND per B fragment (element 0 for j = 0, element 7
+//    for j = 2, on the lanes whose token sits at a window edge).  Decoder shape (16 convs, O = I = 512):
+//    2 x 8 tiles per conv = 256 tiles = one per CU, every tile owns its output block -> no split-K, no atomics:
+//    the epilogue adds into the gradient with plain read-modify-write.
+//  * Four LDS buffers of 40 KB: LDS-DMA (buffer_load ... lds) of K-tile t + 3 is issued while t is consumed, each
+//    wave retires its own DMA with a counted vmcnt (never 0 in the loop) and a barrier publishes it.
+//  * Two wave groups ping-pong (the guide's 8-wave schedule): group 1 runs one barrier behind group 0, so while one
+//    group issues its 44 ds_read_b64_tr_b16 + 5 DMA instructions the other runs its 48 MFMAs
+//    (v_mfma_f32_16x16x32_bf16, 128 x 48 outputs per wave).
+//  * LDS images are [16-row block][64 k][16 rows] with the k field XOR-swizzled (k ^ (bit3(k) << 2)): every
+//    transposed read of a 32-lane half hits 8 distinct 32-B slots (conflict-free for all three tap shifts), and the
+//    A-fragment addresses are one lane base + immediate offsets.  The swizzle is applied to the DMA source address
+//    (the image is lane-linear per DMA instruction).
+#include "gemm_core.h"
+
+#pragma clang diagnostic ignored "-Winline-asm"
+
+namespace {
+
+constexpr int W3_BM = 256;                 // output rows (o) per tile
+constexpr int W3_CB = 64;                  // input channels per tile (x 3 taps = 192 output columns)
+constexpr int W3_BK = 64;                  // tokens per K-tile
+constexpr int W3_NTH = 512;
+constexpr int W3_A = W3_BK * W3_BM * 2;    // 32768 B: dy image
+constexpr int W3_B = W3_BK * W3_CB * 2;    // 8192 B: x image
+constexpr int W3_BUF = W3_A + W3_B;        // 40960 B
+constexpr int W3_NBUF = 4;                 // 163840 B = the whole LDS of a CU
+constexpr int W3_DMA = 5;                  // DMA instructions per thread per K-tile (4 dy + 1 x)
+
+struct W3Params {
+  int M, cin, K, seg, ngroups, tiles_m, tiles_i, nblocks;
+  int lda, ldb, ldc;
+  int col_mod, col_mul, col_off;
+  float alpha;
+  const void* A[AW_GEMM_MAX_GROUPS];       // dy [K][lda] bf16
+  const void* B[AW_GEMM_MAX_GROUPS];       // x  [K][ldb] bf16
+  float* C[AW_GEMM_MAX_GROUPS];            // dW [M][ldc] f32 (columns through the col map)
+  float* rowsum[AW_GEMM_MAX_GROUPS];       // bias gradient (NULL: none)
+};
+
+typedef int v4i32 __attribute__((ext_vector_type(4)));
+typedef short v4i16 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
+
+// byte of the swizzled k field: the k row lives at 32 * (k ^ (bit3(k) << 2)) inside its 16-row block
+__device__ __forceinline__ int w3_kfield(int k) { return 32 * (k ^ (((k >> 3) & 1) << 2)); }
+
+__device__ __forceinline__ v4i32 w3_desc(const void* base) {
+  const uint64_t b = (uint64_t)(uintptr_t)base;
+  return v4i32{(int)__builtin_amdgcn_readfirstlane((uint32_t)b),
+               (int)__builtin_amdgcn_readfirstlane((uint32_t)(b >> 32) & 0xFFFFu), 0x7FFFFFFF, 0x00020000};
+}
+
+__device__ __forceinline__ void w3_dma(uint32_t m0, int off, v4i32 desc) {
+  asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" ::"s"(m0), "v"(off), "s"(desc)
+               : "memory", "m0");
+}
+
+__device__ __forceinline__ uint4 w3_tr(const char* p_lo, const char* p_hi) {
+  const v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(uintptr_t)p_lo);
+  const v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(uintptr_t)p_hi);
+  uint4 out;
+  memcpy(&out, &lo, 8);
+  memcpy(reinterpret_cast<char*>(&out) + 8, &hi, 8);
+  return out;
+}
+
+template <int N> __device__ __forceinline__ void w3_vmcnt() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+
+__device__ __forceinline__ void w3_barrier() {
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+__global__ __launch_bounds__(W3_NTH, 1) void wgrad_conv3_kernel(W3Params P) {
+  __shared__ __attribute__((aligned(16))) char smem[W3_NBUF * W3_BUF];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 2, wc = wid & 3;           // wave group (M half) and N quarter
+  const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
+
+  int unit = awg::xcd_remap(blockIdx.x, P.nblocks);
+  const int per_group = P.tiles_m * P.tiles_i;
+  const int grp = unit / per_group;
+  unit -= grp * per_group;
+  const int tm = unit / P.tiles_i, ti = unit % P.tiles_i;
+  const int m0 = tm * W3_BM, ci0 = ti * W3_CB;
+  const char* Ag = reinterpret_cast<const char*>(P.A[grp]) + (int64_t)m0 * 2;
+  const char* Bg = reinterpret_cast<const char*>(P.B[grp]) + (int64_t)ci0 * 2;
+
+  // ---- DMA source offsets (bytes, K-tile 0) of this thread's chunks; the image is lane-linear: chunk c of a
+  //      K-tile lands at byte 16 c of the image
+  int offA[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int c = tid + W3_NTH * i;
+    const int mb = c >> 7, w = c & 127;
+    const int kf = w >> 1, half = w & 1;
+    const int k = kf ^ (((kf >> 3) & 1) << 2);
+    offA[i] = (k * P.lda + mb * 16 + half * 8) * 2;
+  }
+  int offB;
+  {
+    const int c = tid;
+    const int cb = c >> 7, w = c & 127;
+    const int kf = w >> 1, half = w & 1;
+    const int k = kf ^ (((kf >> 3) & 1) << 2);
+    offB = (k * P.ldb + cb * 16 + half * 8) * 2;
+  }
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
+  const uint32_t wave_dst = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(tid & ~63)) * 16u;
+  const int64_t a_step = (int64_t)W3_BK * P.lda * 2, b_step = (int64_t)W3_BK * P.ldb * 2;
+
+  auto dma = [&](int t) {
+#ifdef W3_SKIP_DMA
+    if (t >= 3) return;       // probe: the loop's DMA left out (operands stale), prologue kept
+#endif
+    const uint32_t buf = lds0 + (uint32_t)((t & (W3_NBUF - 1)) * W3_BUF);
+    const v4i32 da = w3_desc(Ag + t * a_step);
+    const v4i32 db = w3_desc(Bg + t * b_step);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) w3_dma(buf + wave_dst + (uint32_t)(i * W3_NTH * 16), offA[i], da);
+    w3_dma(buf + W3_A + wave_dst, offB, db);
+  };
+
+  // ---- fragment addresses (bytes within a buffer)
+  // A fragment (i, u, h): block mb = wr*8 + i, k = 32u + 8g + 4h + q, rows 4p..4p+3 of the block
+  const int a_lo = w3_kfield(8 * g + q) + 8 * p;           // h = 0  (+ 1024 u + 2048 mb, no carry: see kfield)
+  const int a_hi = w3_kfield(8 * g + 4 + q) + 8 * p;       // h = 1
+  // B fragment f of this wave: output column c = wc*48 + 16 f -> tap j = c / 64, channel block cb = (c % 64) / 16;
+  // rows shifted by j - 1 (wrapped into the image: only masked elements read a wrapped row)
+  int b_addr[3][2][2];
+  int tap[3];
+#pragma unroll
+  for (int f = 0; f < 3; ++f) {
+    const int c = wc * 48 + 16 * f;
+    const int j = c >> 6, cb = (c & 63) >> 4;
+    tap[f] = j;
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int r = (32 * u + 8 * g + 4 * h + q + j - 1) & 63;
+        b_addr[f][u][h] = W3_A + cb * 2048 + w3_kfield(r) + 8 * p;
+      }
+  }
+  // window masks: element 0 of the fragment (token 32u + 8g) for tap 0, element 7 (token 32u + 8g + 7) for tap 2;
+  // branch-free per fragment (all-ones for the other taps)
+  const uint32_t mask_e0 = ((8 * g) % P.seg == 0) ? 0xFFFF0000u : 0xFFFFFFFFu;
+  const uint32_t mask_e7 = ((8 * g + 8) % P.seg == 0) ? 0x0000FFFFu : 0xFFFFFFFFu;
+  uint32_t mlo[3], mhi[3];
+#pragma unroll
+  for (int f = 0; f < 3; ++f) {
+    mlo[f] = tap[f] == 0 ? mask_e0 : 0xFFFFFFFFu;
+    mhi[f] = tap[f] == 2 ? mask_e7 : 0xFFFFFFFFu;
+  }
+
+  float* rowptr = P.rowsum[grp];
+  const bool wave_rowsum = rowptr != nullptr && ti == 0 && wc == 0;
+  float rowacc[8] = {};
+
+  f32x4 acc[8][3];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int f = 0; f < 3; ++f) acc[i][f] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = P.K / W3_BK;
+  // ---- prologue: K-tiles 0..2 in flight, tile 0 retired and published
+  dma(0);
+  if (nk > 1) dma(1);
+  if (nk > 2) dma(2);
+  if (nk > 2) w3_vmcnt<2 * W3_DMA>();
+  else if (nk > 1) w3_vmcnt<W3_DMA>();
+  else w3_vmcnt<0>();
+  w3_barrier();
+#ifndef W3_NO_STAGGER
+  if (wr == 1) w3_barrier();                         // group 1 runs one barrier behind group 0
+#endif
+
+  uint4 af[2][8], bfr[2][3];
+  for (int t = 0; t < nk; ++t) {
+    // ---- read segment: this group's fragments of K-tile t, the DMA of t + 3, retire t + 1
+    const char* buf = smem + (t & (W3_NBUF - 1)) * W3_BUF;
+#ifndef W3_SKIP_READS
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int o = (wr * 8 + i) * 2048 + 1024 * u;
+        af[u][i] = w3_tr(buf + o + a_lo, buf + o + a_hi);
+      }
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int f = 0; f < 3; ++f) bfr[u][f] = w3_tr(buf + b_addr[f][u][0], buf + b_addr[f][u][1]);
+#else
+    if (t == 0) {             // probe: fragments read once, the loop's LDS reads left out
+      for (int u = 0; u < 2; ++u)
+        for (int i = 0; i < 8; ++i) af[u][i] = w3_tr(buf + (wr * 8 + i) * 2048 + 1024 * u + a_lo, buf + a_hi);
+      for (int u = 0; u < 2; ++u)
+        for (int f = 0; f < 3; ++f) bfr[u][f] = w3_tr(buf + b_addr[f][u][0], buf + b_addr[f][u][1]);
+    }
+#endif
+    if (t + 3 < nk) dma(t + 3);
+    const int newer = min(nk - 1, t + 3) - (t + 1);   // tiles issued after t + 1 (still allowed in flight)
+    if (newer >= 2) w3_vmcnt<2 * W3_DMA>();
+    else if (newer == 1) w3_vmcnt<W3_DMA>();
+    else w3_vmcnt<0>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this buffer's reads retire before the barrier (WAR)
+    w3_barrier();
+    // ---- MFMA segment
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int f = 0; f < 3; ++f) {
+        bfr[u][f].x &= mlo[f];
+        bfr[u][f].w &= mhi[f];
+      }
+    __builtin_amdgcn_s_setprio(1);
+#ifndef W3_SKIP_MFMA
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int f = 0; f < 3; ++f)
+          acc[i][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, af[u][i]),
+                                                             __builtin_bit_cast(bf16x8, bfr[u][f]), acc[i][f], 0, 0, 0);
+#else
+#pragma unroll
+    for (int u = 0; u < 2; ++u)     // probe: MFMAs left out, the fragments kept live
+#pragma unroll
+      for (int i = 0; i < 8; ++i) asm volatile("" ::"v"(af[u][i].x), "v"(af[u][i].w));
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int f = 0; f < 3; ++f) asm volatile("" ::"v"(bfr[u][f].x), "v"(bfr[u][f].w));
+#endif
+    __builtin_amdgcn_s_setprio(0);
+    if (wave_rowsum) {
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) rowacc[i] += awg::frag_sum<bf16>(af[u][i]);
+    }
+    w3_barrier();
+  }
+#ifndef W3_NO_STAGGER
+  if (wr == 0) w3_barrier();                         // both groups end on the same barrier count
+#endif
+
+  // ---- epilogue: this tile owns its output block -> plain read-modify-write of the f32 gradient
+  const float alpha = P.alpha;
+  float* C = P.C[grp];
+#pragma unroll
+  for (int f = 0; f < 3; ++f) {
+    const int c = wc * 48 + 16 * f + li;
+    const int n = (c >> 6) * P.cin + ci0 + (c & 63);
+    const int64_t oc = P.col_mod > 0 ? (int64_t)(n % P.col_mod) * P.col_mul + n / P.col_mod + P.col_off
+                                     : (int64_t)n * (P.col_mul > 0 ? P.col_mul : 1) + P.col_off;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int row = m0 + wr * 128 + 16 * i + 4 * g;
+      float* d = C + (int64_t)row * P.ldc + oc;
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = d[(int64_t)r * P.ldc];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) d[(int64_t)r * P.ldc] = v[r] + alpha * acc[i][f][r];
+    }
+  }
+  if (wave_rowsum) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      float v = rowacc[i];
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      if (lane < 16) atomicAdd(rowptr + m0 + wr * 128 + 16 * i + lane, alpha * v);
+    }
+  }
+}
+
+int g_policy = 0;   // aw_gemm_set_wgrad_policy: 0 automatic, 1 force, -1 off
+
+}  // namespace
+
+namespace awg {
+
+// The grouped decoder k = 3 weight gradient on the ping-pong kernel when the shape allows it; false -> the caller
+// runs the generic grouped GEMM.
+bool wgrad_conv3_try(const aw_gemm_args* args, int n, hipStream_t s) {
+  const aw_gemm_args& a = args[0];
+  if (g_policy < 0) return false;
+  const int cin = a.conv_cin;
+  const bool shape = a.a_dtype == AW_BF16 && a.a_trans && a.b_trans && cin > 0 && a.conv_operand == 1 &&
+                     a.N == 3 * cin && a.M % W3_BM == 0 && cin % W3_CB == 0 && a.K % W3_BK == 0 && a.K > 0 &&
+                     (a.conv_seg == 8 || a.conv_seg == 16 || a.conv_seg == 32) && a.accumulate && a.beta == 0.f &&
+                     a.c_dtype == AW_F32 && a.lda % 8 == 0 && a.ldb % 8 == 0;
+  if (!shape) return false;
+  const int tiles = (a.M / W3_BM) * (cin / W3_CB);
+  if (g_policy == 0 && tiles * n < 128) return false;   // too few tiles to fill the chip without split-K
+  const int64_t ea = ((int64_t)a.K - 1) * a.lda + a.M, eb = ((int64_t)a.K - 1) * a.ldb + cin;
+  if (ea * 2 >= 0x7FFFFFF0 || eb * 2 >= 0x7FFFFFF0) return false;
+  W3Params P;
+  memset(&P, 0, sizeof(P));
+  P.M = a.M;
+  P.cin = cin;
+  P.K = a.K;
+  P.seg = a.conv_seg;
+  P.ngroups = n;
+  P.tiles_m = a.M / W3_BM;
+  P.tiles_i = cin / W3_CB;
+  P.nblocks = tiles * n;
+  P.lda = (int)a.lda;
+  P.ldb = (int)a.ldb;
+  P.ldc = (int)a.ldc;
+  P.col_mod = a.col_mod;
+  P.col_mul = a.col_mul;
+  P.col_off = a.col_off;
+  P.alpha = a.alpha;
+  for (int g = 0; g < n; ++g) {
+    P.A[g] = args[g].A;
+    P.B[g] = args[g].B;
+    P.C[g] = reinterpret_cast<float*>(args[g].C);
+    P.rowsum[g] = args[g].a_rowsum;
+  }
+  hipLaunchKernelGGL(wgrad_conv3_kernel, dim3(P.nblocks), dim3(W3_NTH), 0, s, P);
+  return true;
+}
+
+}  // namespace awg
+
+extern "C" int aw_gemm_set_wgrad_policy(int mode) {
+  AW_REQUIRE(mode >= -1 && mode <= 1, "aw_gemm_set_wgrad_policy: mode must be -1, 0 or 1");
+  g_policy = mode;
+  return AW_OK;
+}
+
+#ifdef W3_PROBE
+// tools/probe/wgrad3_probe.py: the kernel alone (variants built with the W3_SKIP_* / W3_NO_STAGGER knobs above)
+extern "C" int w3_probe_grouped(const aw_gemm_args* args, int n, void* stream) {
+  g_policy = 1;
+  return awg::wgrad_conv3_try(args, n, reinterpret_cast<hipStream_t>(stream)) ? aw::check_launch("w3") : -1;
+}
+#endif
