@@ -13,14 +13,15 @@ REPO = os.path.dirname(os.path.dirname(HERE))
 SRC = os.path.join(REPO, "vq-vae-transformer-arc-welding_amd", "csrc")
 VARIANTS = {"base": [], "skip_dma": ["-DW3_SKIP_DMA"], "skip_reads": ["-DW3_SKIP_READS"],
             "skip_mfma": ["-DW3_SKIP_MFMA"], "no_stagger": ["-DW3_NO_STAGGER"],
-            "skip_dma_reads": ["-DW3_SKIP_DMA", "-DW3_SKIP_READS"]}
+            "skip_dma_reads": ["-DW3_SKIP_DMA", "-DW3_SKIP_READS"], "sched0_dma_in_m": ["-DW3_SCHED=0"], "sched2_dma_r_t2": ["-DW3_SCHED=2"], "stamps": ["-DW3_STAMPS"], "stamps_s2": ["-DW3_STAMPS", "-DW3_SCHED=2"]}
 
 
 def build():
     procs = []
     for name, flags in VARIANTS.items():
         out = os.path.join(HERE, "build", f"w3_{name}.so")
-        cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-fPIC", "-shared", "-std=c++17",
+        # -Bsymbolic: each probe library calls its OWN launcher (not the arcweld library's, loaded earlier)
+        cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-fPIC", "-shared", "-std=c++17", "-Wl,-Bsymbolic",
                "-munsafe-fp-atomics", "-DW3_PROBE", *flags, "-I" + os.path.join(REPO, "include"),
                os.path.join(SRC, "wgrad.hip"), os.path.join(SRC, "runtime.hip"), "-o", out]
         procs.append(subprocess.Popen(cmd))
@@ -69,6 +70,24 @@ def main(iters=10):
         def run(lib=lib):
             assert lib.w3_probe_grouped(arr, G, ctypes.c_void_p(s)) == 0
         rows.append((f"probe {name}", timeit(run)))
+    for sname in ("stamps", "stamps_s2"):
+      lib = ctypes.CDLL(os.path.join(HERE, "build", f"w3_{sname}.so"))
+      buf = (ctypes.c_uint64 * 384)()
+      print(sname)
+      if lib.w3_probe_stamps(buf, 384) == 384:
+        # per (workgroup, group, K-tile): R issue, barrier wait, M, rowsum, barrier wait (cycles of s_memtime)
+        segs = ("R", "bar1", "M", "post", "bar2")
+        tot = {k: [] for k in segs}
+        for wg in range(8):
+            for grp in range(2):
+                for t in range(4):
+                    b = ((wg * 2 + grp) * 4 + t) * 6
+                    v = [buf[b + k] for k in range(6)]
+                    for k, name in enumerate(segs):
+                        tot[name].append(v[k + 1] - v[k])
+                    if wg < 1:
+                        print(f"wg {wg} grp {grp} t {t}: " + " ".join(f"{n}={v[k + 1] - v[k]}" for k, n in enumerate(segs)))
+        print("median cycles: " + " ".join(f"{n}={sorted(x)[len(x) // 2]}" for n, x in tot.items()), flush=True)
     for name, us in rows:
         print(f"{name:34s} {us:8.1f} us  {fl / us / 1e6:7.1f} TFLOP/s  frac {fl / us / 1e6 / 2500:.3f}", flush=True)
 

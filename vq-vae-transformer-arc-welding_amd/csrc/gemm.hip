@@ -48,7 +48,6 @@ template <typename T>
 void dispatch(const GemmP& P, hipStream_t s, bool ragged) {
   const Layout ly = layout_of(P.a);
   uint32_t code = epi_code(P.a, P, ragged);
-  if (P.bm == 256 && code != EP_ACCUM) code = EP_GENERIC;   // specialised epilogues are compiled for 128-row tiles
   constexpr bool BF = sizeof(T) == 2;
   if (code == EP_ACCUM) {
     switch (ly) {
@@ -193,7 +192,8 @@ static bool plain_output(const aw_gemm_args& a) {
 //    shape of the path: forward / input-gradient M = 16384, K = 512 .. 2048 and the grouped weight gradients);
 //    plain f32 outputs that cannot fill the chip twice are split over K (slab workspace when the caller provides
 //    one, f32 atomics in grouped launches, <= 2 adders);
-//  * aw_gemm_set_tile(256) forces the 256x128 tile (generic / accumulate epilogues) for eligible bf16 launches.
+//  * 256x128 ping-pong tiles, one workgroup per CU, for bf16 launches whose 256-row tiles fill the chip
+//    (aw_gemm_set_tile(256) forces them for every eligible bf16 launch, (128) disables them).
 static void plan(const aw_gemm_args& a, int ngroups, bool grouped, GemmP& P) {
   P.a = a;
   P.ngroups = ngroups;
@@ -216,7 +216,13 @@ static void plan(const aw_gemm_args& a, int ngroups, bool grouped, GemmP& P) {
   P.tiles_n = aw_cdiv(a.N, BN);
   const int t256 = aw_cdiv(a.M, 256) * P.tiles_n * ngroups;
   int bm = 128, splits = 1;
-  if (a.a_dtype == AW_BF16 && !is_ragged(a) && g_tile_override == 256) {
+  // 256-row ping-pong tiles (one workgroup per CU) for the bf16 forward layouts (both operands K-contiguous) whose
+  // 256-row tiles alone fill the chip and that run at least 16 K steps: the decoder convs (K = 1536; same-box A/B
+  // 35.6 / 44.9 vs 38.4 / 46.0 us).  The input-gradient layouts (transposed weight reads) and the K = 512 encoder
+  // convs measured slower on the 256-row tile (e.g. 54.1 vs 51.0 us, 33.3 vs 31.5 us) and keep the 128-row form.
+  // aw_gemm_set_tile(128) keeps every launch on the 128-row form, (256) forces the 256-row tile where eligible.
+  const bool auto256 = t256 >= 256 && !grouped && !a.accumulate && !a.a_trans && !a.b_trans && a.K >= 16 * BK;
+  if (a.a_dtype == AW_BF16 && !is_ragged(a) && (g_tile_override == 256 || (g_tile_override == 0 && auto256))) {
     bm = 256;
     if (a.accumulate && t256 < 240 && a.K >= 24 * BK) splits = 2;
   }

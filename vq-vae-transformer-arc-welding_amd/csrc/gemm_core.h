@@ -2,9 +2,8 @@
 //
 // Two tile configurations (template BMT):
 //   BMT = 128: 128x128 tile, 256 threads (4 waves as 2x2), two LDS stages, two workgroups per CU;
-//   BMT = 256: 256x128 tile, 512 threads (8 waves as 4x2), three LDS stages (two K steps of loads in flight),
-//              one workgroup per CU (aw_gemm_set_tile; measured slower than two 128-row workgroups per CU on every
-//              shape of this path, so the automatic policy does not pick it).
+//   BMT = 256: 256x128 tile, 512 threads (8 waves as 4x2), three LDS stages, one workgroup per CU, the two wave
+//              groups ping-ponging between fragment reads + DMA issue and MFMAs (see the main loop).
 // Every wave owns a 64x64 output block = 4x4 fragments of 16x16.  K is staged 128 bytes per operand row per step
 // (64 bf16 / 32 f32).  Operands reach LDS by LDS-DMA (gfx950 `buffer_load ... lds`): the image swizzle is applied
 // to the source address, out-of-range offsets implement every mask (M/N/K tails, implicit-conv window edges).
@@ -541,40 +540,70 @@ __global__ __launch_bounds__(Cfg<BMT>::NTH, RAGGED ? 1 : Cfg<BMT>::MINB) void ge
       __syncthreads();
     }
   } else if constexpr (use_dma) {
-    // three-stage ring: steps t+1 and t+2 are in flight while step t computes.  Each wave retires its own DMA of
-    // step t+1 with a counted vmcnt (leaving step t+2 in flight) and the raw barrier publishes it to every wave;
-    // the barrier also orders every wave's reads of stage t before the DMA of step t+3 overwrites it.
+    // 256-row tile, one workgroup per CU: two wave groups ping-pong (the 8-wave schedule of the guide, as in
+    // wgrad.hip).  Group g = waves 4g..4g+3 (rows 128g..128g+127, one wave per SIMD); group 1 runs one barrier
+    // behind group 0, so on every SIMD one wave issues its fragment reads (16 ds_read_b128 / tr pairs) and the DMA
+    // of step t + 2 while its partner runs 32 MFMAs.  Three LDS stages: the DMA of step t + 2 overwrites the stage
+    // of step t - 1, whose reads both groups retired before the last barrier (lgkmcnt(0) ending each read segment);
+    // each wave retires its own DMA of step t + 1 with a counted vmcnt, the barrier publishes it.
     constexpr int PER_STEP = SA::NCH + SB::NCH;
-    uint32_t S0 = 0u, S1 = (uint32_t)STAGE, S2 = 2u * (uint32_t)STAGE;
-    sa.dma(kbeg, S0);
-    sb.dma(kbeg, S0);
+    const int grp = wid >> 2;
+    auto stage_of = [](int t) { return (uint32_t)((t % 3) * STAGE); };
+    sa.dma(kbeg, 0u);
+    sb.dma(kbeg, 0u);
     if (nk > 1) {
-      sa.dma(kbeg + BK, S1);
-      sb.dma(kbeg + BK, S1);
+      sa.dma(kbeg + BK, stage_of(1));
+      sb.dma(kbeg + BK, stage_of(1));
       wait_vmcnt<PER_STEP>();
     } else {
       wait_vmcnt<0>();
     }
+    __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    if (grp == 1) __builtin_amdgcn_s_barrier();
     AW_STAMP(1);
+    uint4 af[2][FM], bfr[2][4];
     for (int kt = 0; kt < nk; ++kt) {
-      // stages rotate S0 -> S1 -> S2: step kt computes from S0 and step kt+2 loads into S2
-      if (kt + 2 < nk) {
-        sa.dma(kbeg + (kt + 2) * BK, S2);
-        sb.dma(kbeg + (kt + 2) * BK, S2);
+      const char* a_l = smem + stage_of(kt);
+      const char* b_l = a_l + A_IMG;
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+#pragma unroll
+        for (int f = 0; f < FM; ++f) af[u][f] = frag<T, ATR, BMT * (int)sizeof(T)>(a_l, wm * WR + f * 16, lane, u);
+#pragma unroll
+        for (int f = 0; f < 4; ++f) bfr[u][f] = frag<T, BTR, BN * (int)sizeof(T)>(b_l, wn * 64 + f * 16, lane, u);
       }
-      compute(smem + S0);
-      if (kt + 2 < nk) wait_vmcnt<PER_STEP>();
-      else wait_vmcnt<0>();
+      if (kt + 2 < nk) {
+        sa.dma(kbeg + (kt + 2) * BK, stage_of(kt + 2));
+        sb.dma(kbeg + (kt + 2) * BK, stage_of(kt + 2));
+        wait_vmcnt<PER_STEP>();            // step kt + 1 retired, kt + 2 in flight
+      } else {
+        wait_vmcnt<0>();
+      }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
       __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-      const uint32_t t0 = S0;
-      S0 = S1;
-      S1 = S2;
-      S2 = t0;
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) Mfma<T>::run(acc[i][j], af[u][i], bfr[u][j]);
+      __builtin_amdgcn_s_setprio(0);
+      if (wave_rowsum) {
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+          for (int f = 0; f < FM; ++f) rowacc[f] += frag_sum<T>(af[u][f]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
     }
+    if (grp == 0) __builtin_amdgcn_s_barrier();   // both groups end on the same barrier count
   } else {
     // register staging (ragged shapes): LDS stage s holds K step t (t % 2 == s) while the registers of the other
     // set carry the loads of step t+1; the loads of step t+2 are issued at the top of step t
@@ -831,11 +860,10 @@ inline void launch_tiled(const GemmP& P, hipStream_t s) {
 // code) has no compiled specialisation, so the caller falls back to the EP_GENERIC kernel.
 bool launch_fast_fwd(const GemmP& P, hipStream_t s, bool is_bf16, Layout ly, uint32_t code);
 bool launch_fast_bwd(const GemmP& P, hipStream_t s, bool is_bf16, Layout ly, uint32_t code);
+bool launch_fast_256(const GemmP& P, hipStream_t s, Layout ly, uint32_t code);   // bf16, P.bm == 256
 // The grouped decoder k = 3 weight gradient on the 8-wave ping-pong kernel (wgrad.hip); false when the shape or
 // the policy (aw_gemm_set_wgrad_policy) rules it out (the caller then runs the generic grouped GEMM).
 bool wgrad_conv3_try(const aw_gemm_args* args, int n, hipStream_t s);
 
-#define AW_FAST_CASE(T, LY, CODE) \
-  case (CODE): launch_tiled<T, LY, (CODE)>(P, s); return true;
 
 }  // namespace awg

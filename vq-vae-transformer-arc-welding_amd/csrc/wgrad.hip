@@ -11,11 +11,12 @@
 //    for j = 2, on the lanes whose token sits at a window edge).  Decoder shape (16 convs, O = I = 512):
 //    2 x 8 tiles per conv = 256 tiles = one per CU, every tile owns its output block -> no split-K, no atomics:
 //    the epilogue adds into the gradient with plain read-modify-write.
-//  * Four LDS buffers of 40 KB: LDS-DMA (buffer_load ... lds) of K-tile t + 3 is issued while t is consumed, each
-//    wave retires its own DMA with a counted vmcnt (never 0 in the loop) and a barrier publishes it.
+//  * Four LDS buffers of 40 KB: LDS-DMA (buffer_load ... lds) of K-tile t + 3 is issued inside the MFMA segment of
+//    tile t (hidden among the MFMAs), each wave retires its own DMA with a counted vmcnt (never 0 in the loop) two
+//    tiles later and a barrier publishes it.
 //  * Two wave groups ping-pong (the guide's 8-wave schedule): group 1 runs one barrier behind group 0, so while one
-//    group issues its 44 ds_read_b64_tr_b16 + 5 DMA instructions the other runs its 48 MFMAs
-//    (v_mfma_f32_16x16x32_bf16, 128 x 48 outputs per wave).
+//    group issues its 44 ds_read_b64_tr_b16 (one lane base per operand, immediate offsets) the other runs its 48
+//    MFMAs (v_mfma_f32_16x16x32_bf16, 128 x 48 outputs per wave); the reads are waited for at their first use.
 //  * LDS images are [16-row block][64 k][16 rows] with the k field XOR-swizzled (k ^ (bit3(k) << 2)): every
 //    transposed read of a 32-lane half hits 8 distinct 32-B slots (conflict-free for all three tap shifts), and the
 //    A-fragment addresses are one lane base + immediate offsets.  The swizzle is applied to the DMA source address
@@ -35,6 +36,11 @@ constexpr int W3_B = W3_BK * W3_CB * 2;    // 8192 B: x image
 constexpr int W3_BUF = W3_A + W3_B;        // 40960 B
 constexpr int W3_NBUF = 4;                 // 163840 B = the whole LDS of a CU
 constexpr int W3_DMA = 5;                  // DMA instructions per thread per K-tile (4 dy + 1 x)
+// where the DMA is issued (probe knob; 1 measured fastest): 0 = K-tile t + 3 inside the MFMA segment, 1 = t + 3 in the
+// read segment (which then retires its reads before the barrier), 2 = t + 2 in the read segment
+#ifndef W3_SCHED
+#define W3_SCHED 1
+#endif
 
 struct W3Params {
   int M, cin, K, seg, ngroups, tiles_m, tiles_i, nblocks;
@@ -81,6 +87,19 @@ __device__ __forceinline__ void w3_barrier() {
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_sched_barrier(0);
 }
+
+#ifdef W3_STAMPS
+// probe: s_memtime at the segment boundaries of K-tiles [W3_T0, W3_T0 + 4) for waves 0 and 4 of workgroups 0..7
+#define W3_T0 96
+__device__ uint64_t g_w3_stamps[8 * 2 * 4 * 6];
+#define W3_STAMP(k)                                                                                             \
+  do {                                                                                                          \
+    if (blockIdx.x < 8 && (wid & 3) == 0 && lane == 0 && t >= W3_T0 && t < W3_T0 + 4)                           \
+      g_w3_stamps[((blockIdx.x * 2 + (wid >> 2)) * 4 + (t - W3_T0)) * 6 + (k)] = __builtin_amdgcn_s_memtime();   \
+  } while (0)
+#else
+#define W3_STAMP(k) do { } while (0)
+#endif
 
 __global__ __launch_bounds__(W3_NTH, 1) void wgrad_conv3_kernel(W3Params P) {
   __shared__ __attribute__((aligned(16))) char smem[W3_NBUF * W3_BUF];
@@ -138,7 +157,11 @@ __global__ __launch_bounds__(W3_NTH, 1) void wgrad_conv3_kernel(W3Params P) {
   const int a_hi = w3_kfield(8 * g + 4 + q) + 8 * p;       // h = 1
   // B fragment f of this wave: output column c = wc*48 + 16 f -> tap j = c / 64, channel block cb = (c % 64) / 16;
   // rows shifted by j - 1 (wrapped into the image: only masked elements read a wrapped row)
-  int b_addr[3][2][2];
+  // u = 1 adds 32 rows = 1024 bytes to the swizzled address for every row r < 32 (kfield leaves bit 5 alone); the
+  // rows that leave the image (r = -1 or 64: tap 0 / tap 2 at a window edge) only feed masked elements, and their
+  // addresses stay inside this buffer
+  int b_base[3][2];
+  int b_addr[3][2][2];   // (W3_SKIP_READS probe only)
   int tap[3];
 #pragma unroll
   for (int f = 0; f < 3; ++f) {
@@ -146,12 +169,11 @@ __global__ __launch_bounds__(W3_NTH, 1) void wgrad_conv3_kernel(W3Params P) {
     const int j = c >> 6, cb = (c & 63) >> 4;
     tap[f] = j;
 #pragma unroll
+    for (int h = 0; h < 2; ++h) b_base[f][h] = W3_A + cb * 2048 + w3_kfield((8 * g + 4 * h + q + j - 1) & 63) + 8 * p;
+#pragma unroll
     for (int u = 0; u < 2; ++u)
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int r = (32 * u + 8 * g + 4 * h + q + j - 1) & 63;
-        b_addr[f][u][h] = W3_A + cb * 2048 + w3_kfield(r) + 8 * p;
-      }
+      for (int h = 0; h < 2; ++h) b_addr[f][u][h] = b_base[f][h] + 1024 * u;
   }
   // window masks: element 0 of the fragment (token 32u + 8g) for tap 0, element 7 (token 32u + 8g + 7) for tap 2;
   // branch-free per fragment (all-ones for the other taps)
@@ -165,8 +187,15 @@ __global__ __launch_bounds__(W3_NTH, 1) void wgrad_conv3_kernel(W3Params P) {
   }
 
   float* rowptr = P.rowsum[grp];
-  const bool wave_rowsum = rowptr != nullptr && ti == 0 && wc == 0;
-  float rowacc[8] = {};
+  // bias gradient (row sums of dy over the tokens): every tile of a row block takes every tiles_i-th K-tile, and within a
+  // tile the group's 4 waves share the work: wave wc sums A fragments 2wc and 2wc + 1 with an MFMA against an all-ones
+  // B fragment (4 extra MFMAs on those K-tiles; a VALU sum of all 16 fragments in one wave of the ti == 0 tiles
+  // cost ~1000 cycles per K-tile on the critical path)
+  const bool tile_rowsum = rowptr != nullptr;
+  int rs_count = ti;        // this tile sums K-tiles t == ti (mod tiles_i): the work is spread over the row's tiles
+  const int wcu = __builtin_amdgcn_readfirstlane(wc);
+  const uint4 ones = make_uint4(0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u);
+  f32x4 rs[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
 
   f32x4 acc[8][3];
 #pragma unroll
@@ -178,10 +207,15 @@ __global__ __launch_bounds__(W3_NTH, 1) void wgrad_conv3_kernel(W3Params P) {
   // ---- prologue: K-tiles 0..2 in flight, tile 0 retired and published
   dma(0);
   if (nk > 1) dma(1);
+#if W3_SCHED == 2
+  if (nk > 1) w3_vmcnt<W3_DMA>();
+  else w3_vmcnt<0>();
+#else
   if (nk > 2) dma(2);
   if (nk > 2) w3_vmcnt<2 * W3_DMA>();
   else if (nk > 1) w3_vmcnt<W3_DMA>();
   else w3_vmcnt<0>();
+#endif
   w3_barrier();
 #ifndef W3_NO_STAGGER
   if (wr == 1) w3_barrier();                         // group 1 runs one barrier behind group 0
@@ -190,19 +224,25 @@ __global__ __launch_bounds__(W3_NTH, 1) void wgrad_conv3_kernel(W3Params P) {
   uint4 af[2][8], bfr[2][3];
   for (int t = 0; t < nk; ++t) {
     // ---- read segment: this group's fragments of K-tile t, the DMA of t + 3, retire t + 1
+    W3_STAMP(0);
     const char* buf = smem + (t & (W3_NBUF - 1)) * W3_BUF;
 #ifndef W3_SKIP_READS
+    {
+      // one lane base per read kind, the rest as immediate offsets of the ds_read instructions
+      const char* pa_lo = buf + wr * 8 * 2048 + a_lo;
+      const char* pa_hi = buf + wr * 8 * 2048 + a_hi;
 #pragma unroll
-    for (int u = 0; u < 2; ++u)
+      for (int u = 0; u < 2; ++u)
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int o = (wr * 8 + i) * 2048 + 1024 * u;
-        af[u][i] = w3_tr(buf + o + a_lo, buf + o + a_hi);
+        for (int i = 0; i < 8; ++i) af[u][i] = w3_tr(pa_lo + (i * 2048 + 1024 * u), pa_hi + (i * 2048 + 1024 * u));
+#pragma unroll
+      for (int f = 0; f < 3; ++f) {
+        const char* pb_lo = buf + b_base[f][0];
+        const char* pb_hi = buf + b_base[f][1];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) bfr[u][f] = w3_tr(pb_lo + 1024 * u, pb_hi + 1024 * u);
       }
-#pragma unroll
-    for (int u = 0; u < 2; ++u)
-#pragma unroll
-      for (int f = 0; f < 3; ++f) bfr[u][f] = w3_tr(buf + b_addr[f][u][0], buf + b_addr[f][u][1]);
+    }
 #else
     if (t == 0) {             // probe: fragments read once, the loop's LDS reads left out
       for (int u = 0; u < 2; ++u)
@@ -211,13 +251,30 @@ __global__ __launch_bounds__(W3_NTH, 1) void wgrad_conv3_kernel(W3Params P) {
         for (int f = 0; f < 3; ++f) bfr[u][f] = w3_tr(buf + b_addr[f][u][0], buf + b_addr[f][u][1]);
     }
 #endif
+#if W3_SCHED == 1
+    // DMA of K-tile t + 3 into buffer (t - 1) % 4: the other group read tile t - 1 in the previous segment and retired
+    // those reads before the barrier (the lgkmcnt(0) below), so the buffer is free
     if (t + 3 < nk) dma(t + 3);
     const int newer = min(nk - 1, t + 3) - (t + 1);   // tiles issued after t + 1 (still allowed in flight)
+#elif W3_SCHED == 2
+    // DMA of K-tile t + 2 into buffer (t - 2) % 4, consumed by both groups' MFMAs before the last barrier
+    if (t + 2 < nk) dma(t + 2);
+    const int newer = min(nk - 1, t + 2) - (t + 1);
+#else
+    // the DMA of K-tile t + 3 goes out in this tile's MFMA segment (see there); tiles t + 1 and t + 2 are in flight
+    const int newer = min(nk - 1, t + 2) - (t + 1);
+#endif
     if (newer >= 2) w3_vmcnt<2 * W3_DMA>();
     else if (newer == 1) w3_vmcnt<W3_DMA>();
     else w3_vmcnt<0>();
+#if W3_SCHED == 1
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this buffer's reads retire before the barrier (WAR)
+#endif
+    // the reads' own lgkmcnt waits come at their first use in the MFMA segment: their latency overlaps the barrier
+    // and the other group's MFMAs
+    W3_STAMP(1);
     w3_barrier();
+    W3_STAMP(2);
     // ---- MFMA segment
 #pragma unroll
     for (int u = 0; u < 2; ++u)
@@ -229,13 +286,20 @@ __global__ __launch_bounds__(W3_NTH, 1) void wgrad_conv3_kernel(W3Params P) {
     __builtin_amdgcn_s_setprio(1);
 #ifndef W3_SKIP_MFMA
 #pragma unroll
-    for (int u = 0; u < 2; ++u)
+    for (int u = 0; u < 2; ++u) {
 #pragma unroll
       for (int i = 0; i < 8; ++i)
 #pragma unroll
         for (int f = 0; f < 3; ++f)
           acc[i][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, af[u][i]),
                                                              __builtin_bit_cast(bf16x8, bfr[u][f]), acc[i][f], 0, 0, 0);
+#if W3_SCHED == 0
+      // K-tile t + 3 -> buffer (t - 1) % 4, issued behind the first 24 MFMAs: both groups finished reading tile
+      // t - 1 before the barrier that opened this segment (the other group's MFMAs of t - 1 consumed them), so the
+      // DMA cannot overwrite data still being read (WAR); its issue cost hides among the MFMAs
+      if (u == 0 && t + 3 < nk) dma(t + 3);
+#endif
+    }
 #else
 #pragma unroll
     for (int u = 0; u < 2; ++u)     // probe: MFMAs left out, the fragments kept live
@@ -246,14 +310,29 @@ __global__ __launch_bounds__(W3_NTH, 1) void wgrad_conv3_kernel(W3Params P) {
 #pragma unroll
       for (int f = 0; f < 3; ++f) asm volatile("" ::"v"(bfr[u][f].x), "v"(bfr[u][f].w));
 #endif
-    __builtin_amdgcn_s_setprio(0);
-    if (wave_rowsum) {
-#pragma unroll
-      for (int u = 0; u < 2; ++u)
-#pragma unroll
-        for (int i = 0; i < 8; ++i) rowacc[i] += awg::frag_sum<bf16>(af[u][i]);
+    const bool rs_now = tile_rowsum && rs_count == 0;
+    rs_count = rs_count == 0 ? P.tiles_i - 1 : rs_count - 1;
+    if (rs_now) {
+#define W3_RS(a, b)                                                                                                \
+  for (int u = 0; u < 2; ++u) {                                                                                   \
+    rs[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, af[u][a]),                          \
+                                                    __builtin_bit_cast(bf16x8, ones), rs[0], 0, 0, 0);             \
+    rs[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, af[u][b]),                          \
+                                                    __builtin_bit_cast(bf16x8, ones), rs[1], 0, 0, 0);             \
+  }
+      switch (wcu) {            // wave-uniform: static fragment indices (no dynamic register indexing)
+        case 0: W3_RS(0, 1) break;
+        case 1: W3_RS(2, 3) break;
+        case 2: W3_RS(4, 5) break;
+        default: W3_RS(6, 7) break;
+      }
+#undef W3_RS
     }
+    __builtin_amdgcn_s_setprio(0);
+    W3_STAMP(3);
+    W3_STAMP(4);
     w3_barrier();
+    W3_STAMP(5);
   }
 #ifndef W3_NO_STAGGER
   if (wr == 0) w3_barrier();                         // both groups end on the same barrier count
@@ -279,14 +358,11 @@ __global__ __launch_bounds__(W3_NTH, 1) void wgrad_conv3_kernel(W3Params P) {
       for (int r = 0; r < 4; ++r) d[(int64_t)r * P.ldc] = v[r] + alpha * acc[i][f][r];
     }
   }
-  if (wave_rowsum) {
+  if (tile_rowsum && li == 0) {   // column 0 of D = A . ones: lane 16g holds rows 4g..4g+3 of the fragment
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      float v = rowacc[i];
-      v += __shfl_xor(v, 16, 64);
-      v += __shfl_xor(v, 32, 64);
-      if (lane < 16) atomicAdd(rowptr + m0 + wr * 128 + 16 * i + lane, alpha * v);
-    }
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) atomicAdd(rowptr + m0 + wr * 128 + 16 * (2 * wcu + j) + 4 * g + r, alpha * rs[j][r]);
   }
 }
 
@@ -351,5 +427,12 @@ extern "C" int aw_gemm_set_wgrad_policy(int mode) {
 extern "C" int w3_probe_grouped(const aw_gemm_args* args, int n, void* stream) {
   g_policy = 1;
   return awg::wgrad_conv3_try(args, n, reinterpret_cast<hipStream_t>(stream)) ? aw::check_launch("w3") : -1;
+}
+extern "C" int w3_probe_stamps(uint64_t* host, int n) {
+#ifdef W3_STAMPS
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_w3_stamps), n * sizeof(uint64_t)) == hipSuccess ? n : -1;
+#else
+  return 0;
+#endif
 }
 #endif
