@@ -194,19 +194,21 @@ def transformer_workload(dev, rank, world, args, seqs, n_cycles, accumulate=1, l
 
 
 def gemm_traffic():
-    """HBM bytes per launch of the GEMM family from the committed rocprofv3 PMC passes (FETCH_SIZE and WRITE_SIZE in
+    """HBM bytes of the GEMM family from the newest committed rocprofv3 PMC passes (FETCH_SIZE and WRITE_SIZE in
     separate runs, FETCH_SIZE doubled on gfx950; tools/pmc_traffic.py) of this same workload: counters cannot be
-    read from inside the timed run."""
+    read from inside the timed run.  Since round 3 the family is every kernel an aw_gemm / aw_gemm_grouped call
+    launches (gemm_kernel, wgrad_conv3_kernel, gemm_reduce_kernel) and the file carries its bytes per traced step,
+    which gemm_roofline divides by the calls per step (older files: the per-kernel-launch average)."""
     import glob
-    newest = os.path.join(REPO, "profiles", "r02", "session6_pmc", "pmc_gemm_traffic.json")   # the newest passes
-    files = [newest] if os.path.exists(newest) else sorted(
-        glob.glob(os.path.join(REPO, "profiles", "*", "*", "pmc_gemm_traffic.json")) +
-        glob.glob(os.path.join(REPO, "profiles", "*", "pmc_gemm_traffic.json")))
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "r0*", "*", "pmc_gemm_traffic.json")))
     if not files:
         return None, None
     with open(files[-1]) as f:
         d = json.load(f)
-    return round(d["avg_bytes_per_launch"]), os.path.relpath(files[-1], REPO)
+    src = os.path.relpath(files[-1], REPO)
+    if d.get("bytes_per_step"):
+        return {"bytes_per_step": d["bytes_per_step"]}, src
+    return round(d["avg_bytes_per_launch"]), src
 
 
 REFERENCE_CPU = {"value": 85.0, "unit": "windows/s", "cores": 8, "kind": "reference",
@@ -347,6 +349,8 @@ def gemm_roofline(prof, prof_el, elapsed, steps, peak, dtype_name, traffic=None,
     flops = sum(e[2] for e in lst)
     n = len(lst)
     achieved = flops / (ms * 1e-3) / 1e12
+    if isinstance(traffic, dict):     # family bytes per traced step -> per aw_gemm call
+        traffic = round(traffic["bytes_per_step"] / max(1, n // n_prof))
     return {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
             "frac": round(achieved / peak, 4), "traffic": traffic, "traffic_unit": "bytes/launch",
             "traffic_source": traffic_src, "kernel": f"gemm_kernel<{dtype_name}> (aw_gemm)",
@@ -386,7 +390,10 @@ def transformer_traffic():
         return None, None
     with open(files[-1]) as f:
         d = json.load(f)
-    return round(d["avg_bytes_per_launch"]), os.path.relpath(files[-1], REPO)
+    src = os.path.relpath(files[-1], REPO)
+    if d.get("bytes_per_step"):
+        return {"bytes_per_step": d["bytes_per_step"]}, src
+    return round(d["avg_bytes_per_launch"]), src
 
 
 def vq_kernel_roofline(dev, N, K, D, iters=10):

@@ -12,8 +12,9 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(os.path.dirname(HERE))
 SRC = os.path.join(REPO, "vq-vae-transformer-arc-welding_amd", "csrc")
 VARIANTS = {"base": [], "skip_dma": ["-DW3_SKIP_DMA"], "skip_reads": ["-DW3_SKIP_READS"],
-            "skip_mfma": ["-DW3_SKIP_MFMA"], "no_stagger": ["-DW3_NO_STAGGER"],
-            "skip_dma_reads": ["-DW3_SKIP_DMA", "-DW3_SKIP_READS"], "sched0_dma_in_m": ["-DW3_SCHED=0"], "sched2_dma_r_t2": ["-DW3_SCHED=2"], "stamps": ["-DW3_STAMPS"], "stamps_s2": ["-DW3_STAMPS", "-DW3_SCHED=2"]}
+            "skip_mfma": ["-DW3_SKIP_MFMA"], "skip_dma_reads": ["-DW3_SKIP_DMA", "-DW3_SKIP_READS"],
+            "mask_in_m": ["-DW3_MASK_IN_M"], "no_prio": ["-DW3_NO_PRIO"], "sched2": ["-DW3_SCHED=2"],
+            "sched0": ["-DW3_SCHED=0"], "stamps": ["-DW3_STAMPS"], "stamps_s2": ["-DW3_STAMPS", "-DW3_SCHED=2"]}
 
 
 def build():

@@ -270,12 +270,8 @@ __global__ __launch_bounds__(W3_NTH, 1) void wgrad_conv3_kernel(W3Params P) {
 #if W3_SCHED == 1
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this buffer's reads retire before the barrier (WAR)
 #endif
-    // the reads' own lgkmcnt waits come at their first use in the MFMA segment: their latency overlaps the barrier
-    // and the other group's MFMAs
-    W3_STAMP(1);
-    w3_barrier();
-    W3_STAMP(2);
-    // ---- MFMA segment
+#if W3_SCHED == 1 && !defined(W3_MASK_IN_M)
+    // the window masks while the reads are retired anyway: the MFMA segment opens with MFMAs (no VALU head)
 #pragma unroll
     for (int u = 0; u < 2; ++u)
 #pragma unroll
@@ -283,7 +279,25 @@ __global__ __launch_bounds__(W3_NTH, 1) void wgrad_conv3_kernel(W3Params P) {
         bfr[u][f].x &= mlo[f];
         bfr[u][f].w &= mhi[f];
       }
+#endif
+    // otherwise the reads' own lgkmcnt waits come at their first use in the MFMA segment: their latency overlaps the
+    // barrier and the other group's MFMAs
+    W3_STAMP(1);
+    w3_barrier();
+    W3_STAMP(2);
+    // ---- MFMA segment
+#if W3_SCHED != 1 || defined(W3_MASK_IN_M)
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int f = 0; f < 3; ++f) {
+        bfr[u][f].x &= mlo[f];
+        bfr[u][f].w &= mhi[f];
+      }
+#endif
+#ifndef W3_NO_PRIO
     __builtin_amdgcn_s_setprio(1);
+#endif
 #ifndef W3_SKIP_MFMA
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
@@ -328,7 +342,9 @@ __global__ __launch_bounds__(W3_NTH, 1) void wgrad_conv3_kernel(W3Params P) {
       }
 #undef W3_RS
     }
+#ifndef W3_NO_PRIO
     __builtin_amdgcn_s_setprio(0);
+#endif
     W3_STAMP(3);
     W3_STAMP(4);
     w3_barrier();
