@@ -98,38 +98,6 @@ int aw_gemm_set_tile(int bm);
  * shape qualifies, -1 = always the generic grouped GEMM (tests, A/B). */
 int aw_gemm_set_wgrad_policy(int mode);
 
-/* ------------------------------------------------------------------------ fused encoder ResBlock chain
- * The per-token encoder stack in bf16 operands (model/vq_vae_patch_embedd.py:60-74, applied by
- * CNNBlock(seperate=True) to every token slice on its own, :103-110: k = 3 / pad = 1 convs on length-1 inputs, so
- * only the centre taps act and every token is independent).  One launch runs all R ResBlocks for 64-token tiles
- * with the activations resident on chip: per block
- *   h = a . W1^T + b1 (-> h, bf16);  a1 = gelu(h) (-> a1, bf16);
- *   x = x + dropout(a1 . W2^T + b2) (-> x, f32);  a = gelu(x) (-> aout, bf16; the last block stores x itself).
- * Dropout masks are the GEMM epilogue's (element r*H + c, seed mix(drop_seed[r], *seed_ptr)), so a backward made
- * of aw_gemm launches regenerates them.  H = 512; R <= AW_CHAIN_MAX_BLOCKS; any output pointer may be NULL.
- * The saved tensors are written with non-temporal stores while the weights stream (they are read back only by the
- * backward, and allocating them in L2 would evict the weight rows every CU of an XCD is reading). */
-#define AW_CHAIN_MAX_BLOCKS 16
-typedef struct {
-  int64_t N;
-  int H, R;
-  const float* x0;                                  /* [N][H] f32, block-0 input */
-  const void* a0;                                   /* [N][H] bf16, gelu(x0) */
-  const void* W1[AW_CHAIN_MAX_BLOCKS];              /* bf16 centre taps K-step-major [H/32][H out][32 in]
-                                                       (aw_weight_relayout_batch mode 6) */
-  const void* W2[AW_CHAIN_MAX_BLOCKS];
-  const float* b1[AW_CHAIN_MAX_BLOCKS];
-  const float* b2[AW_CHAIN_MAX_BLOCKS];
-  float drop_p;
-  uint64_t drop_seed[AW_CHAIN_MAX_BLOCKS];
-  const uint64_t* seed_ptr;
-  void* h[AW_CHAIN_MAX_BLOCKS];                     /* out bf16 [N][H] */
-  void* a1[AW_CHAIN_MAX_BLOCKS];                    /* out bf16 [N][H] */
-  float* x[AW_CHAIN_MAX_BLOCKS];                    /* out f32 [N][H] */
-  void* aout[AW_CHAIN_MAX_BLOCKS];                  /* out bf16 [N][H] */
-} aw_encoder_chain_args;
-int aw_encoder_chain_fwd(const aw_encoder_chain_args* args, void* stream);
-
 /* -------------------------------------------------------------------------------- vector quantizer
  * VectorQuantizer.forward (model/vector_quantizer.py:76-119), fp32, codebook staged in LDS, no MFMA:
  *   dist = fl(fl(|z|^2 + |e_k|^2) - 2 * (k-ordered fmaf chain z.e_k)), argmin with first-index ties,
@@ -198,7 +166,7 @@ int aw_patchify(const float* x, int64_t B, int L, int C, int P, void* patches, i
  * mode 4: conv (O,I,k)     -> [O][ldo] zero padded, col i*k+j  (patch embed, 1 input channel)
  * `ldo` is the output row length (ignored except for mode 4).  Batched form only:
  * mode 5: plain cast of O*I elements;
- * mode 6: conv (O,I,k) tap t -> [I/32][O][32] K-step-major (the fused encoder chain's weight stream; I % 32 == 0);
+ * (mode 6 is retired: it fed the round-2 fused encoder chain, deleted in round 3);
  * mode 7: conv stored tap-major (O,3,I) -> [3*O][I], row j*O+o (decoder conv input-gradient when the optimizer keeps
  *         the weight tap-major; the forward copy [O][3*I] of such a weight is mode 5 over O x 3I). */
 int aw_weight_relayout(const float* W, int O, int I, int k, int tap, int mode, void* out, int64_t ldo,

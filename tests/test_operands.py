@@ -1,6 +1,6 @@
 """Persistent weight operands kept current by the optimizer (arcweld/operands.py, aw_radam_step_ops): the update
 kernel's cast copies equal a fresh aw_weight_relayout_batch of the updated weights (every relayout mode the step
-uses, bf16 and fp32 operands, the fused chain's K-step-major copies), training with them follows the per-forward
+uses, bf16 and fp32 operands, H = 64 and the configs[1] width H = 512), training with them follows the per-forward
 relayout trajectory (to the run-to-run noise of the weight-gradient atomics), and a maintained step issues no relayout launch."""
 import pytest
 import torch
@@ -12,7 +12,7 @@ pytestmark = pytest.mark.gpu
 KW = dict(hidden_dim=64, num_embeddings=64, embedding_dim=16, n_resblocks=2, patch_size=25)
 
 
-def _train(attach, T, steps=3, chain=False, monkeypatch=None):
+def _train(attach, T, steps=3, monkeypatch=None):
     from arcweld import kernels as K
     from arcweld.precision import operands as prec
     from arcweld.trainer import Trainer
@@ -45,15 +45,14 @@ def test_maintained_operands_follow_the_relayout_trajectory(T, monkeypatch):
     assert len(calls1) == 1            # maintained: only the first forward (flatten moved the weights)
 
 
-@pytest.mark.parametrize("T,chain", [(torch.bfloat16, False), (torch.float32, False), (torch.bfloat16, True)])
-def test_update_kernel_copies_equal_a_fresh_relayout(T, chain, monkeypatch):
+@pytest.mark.parametrize("T,H", [(torch.bfloat16, 64), (torch.float32, 64), (torch.bfloat16, 512)])
+def test_update_kernel_copies_equal_a_fresh_relayout(T, H):
     from arcweld import kernels as K
     from arcweld import operands
-    monkeypatch.setenv("ARCWELD_ENCODER_CHAIN", "1" if chain else "0")
     from arcweld.precision import operands as prec
     from arcweld.trainer import Trainer
     from model.vq_vae_patch_embedd import VQVAEPatch
-    kw = dict(KW, hidden_dim=512) if chain else KW      # the chain serves H = 512
+    kw = dict(KW, hidden_dim=H)
     m = VQVAEPatch(input_dim=2, learning_rate=1e-3, dropout_p=0.0, batch_norm=False, **kw).cuda().train()
     with prec(T):
         tr = Trainer(gradient_clip_val=0.7)
@@ -66,7 +65,7 @@ def test_update_kernel_copies_equal_a_fresh_relayout(T, chain, monkeypatch):
             tr.optimizer_step(m)
         torch.cuda.synchronize()
         names = [j.name for j in st.jobs]
-        assert any(n.startswith("chain") for n in names) == chain
+        assert sum(n.startswith("enc") for n in names) == 2 * KW["n_resblocks"]
         fresh = [operands.OperandJob(j.name, j.param, j.O, j.I, j.k, j.tap, j.mode, torch.zeros_like(j.out),
                                      j.ldo, derive=j.derive) for j in st.jobs]
         K.weight_relayout_batch([j.relayout_job() for j in fresh])

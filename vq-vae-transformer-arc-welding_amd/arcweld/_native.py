@@ -25,22 +25,6 @@ c_f = ctypes.c_float
 c_p = ctypes.c_void_p
 
 
-AW_CHAIN_MAX_BLOCKS = 16
-
-
-class EncoderChainArgs(ctypes.Structure):
-    """aw_encoder_chain_args (include/arcweld_amd.h)."""
-    _fields_ = [
-        ("N", c_i64), ("H", c_int), ("R", c_int),
-        ("x0", c_p), ("a0", c_p),
-        ("W1", c_p * AW_CHAIN_MAX_BLOCKS), ("W2", c_p * AW_CHAIN_MAX_BLOCKS),
-        ("b1", c_p * AW_CHAIN_MAX_BLOCKS), ("b2", c_p * AW_CHAIN_MAX_BLOCKS),
-        ("drop_p", c_f), ("drop_seed", ctypes.c_uint64 * AW_CHAIN_MAX_BLOCKS), ("seed_ptr", c_p),
-        ("h", c_p * AW_CHAIN_MAX_BLOCKS), ("a1", c_p * AW_CHAIN_MAX_BLOCKS),
-        ("x", c_p * AW_CHAIN_MAX_BLOCKS), ("aout", c_p * AW_CHAIN_MAX_BLOCKS),
-    ]
-
-
 class GemmArgs(ctypes.Structure):
     _fields_ = [
         ("M", c_int), ("N", c_int), ("K", c_int),
@@ -135,7 +119,6 @@ SIGNATURES = {
     "aw_embed_bwd": [c_p, c_i64, c_int, c_int, c_p, c_p, c_p],
     "aw_attn_fwd": [c_p, c_i64, c_int, c_int, c_int, c_int, c_p, c_p, c_p],
     "aw_attn_bwd": [c_p, c_p, c_p, c_p, c_i64, c_int, c_int, c_int, c_int, c_p, c_p, c_p],
-    "aw_encoder_chain_fwd": [c_p, c_p],
     "aw_attn_fwd_dropout": [c_p, c_i64, c_int, c_int, c_int, c_int, c_p, c_p, c_f, ctypes.c_uint64, c_p, c_p],
     "aw_attn_bwd_dropout": [c_p, c_p, c_p, c_p, c_i64, c_int, c_int, c_int, c_int, c_p, c_p, c_f, ctypes.c_uint64,
                             c_p, c_p],

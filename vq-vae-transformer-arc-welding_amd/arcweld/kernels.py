@@ -130,29 +130,6 @@ def gemm_grouped(problems, stream=None):
         _timed(s, lambda sp: call("aw_gemm_grouped", arr, len(chunk), sp), fl, _gemm_tag(chunk[0][0]))
 
 
-# ---------------------------------------------------------------------------------- fused encoder chain
-def encoder_chain_fwd(x0, a0, W1, W2, b1, b2, drop=(0.0, ()), seed_ptr=None, h=None, a1=None, x=None, aout=None,
-                      stream=None):
-    """aw_encoder_chain_fwd: all R per-token ResBlocks of the encoder in one launch (bf16 operands).  W1/W2: lists
-    of R bf16 centre taps in the K-step-major layout [H/32][H][32] (weight_relayout_batch mode 6); h/a1/x/aout: lists
-    of R output tensors (entries may be None)."""
-    N, H = x0.shape
-    R = len(W1)
-    a = nat.EncoderChainArgs()
-    a.N, a.H, a.R = int(N), int(H), int(R)
-    a.x0, a.a0 = ptr(x0), ptr(a0)
-    a.drop_p = float(drop[0])
-    for r in range(R):
-        a.W1[r], a.W2[r], a.b1[r], a.b2[r] = ptr(W1[r]), ptr(W2[r]), ptr(b1[r]), ptr(b2[r])
-        a.drop_seed[r] = int(drop[1][r]) & 0xFFFFFFFFFFFFFFFF if drop[0] > 0 else 0
-        a.h[r] = ptr(h[r]) if h else None
-        a.a1[r] = ptr(a1[r]) if a1 else None
-        a.x[r] = ptr(x[r]) if x else None
-        a.aout[r] = ptr(aout[r]) if aout else None
-    a.seed_ptr = ptr(seed_ptr)
-    call("aw_encoder_chain_fwd", ctypes.byref(a), stream_ptr(stream))
-
-
 # ------------------------------------------------------------------------------------------------ VQ
 def vq_forward(z2d, E, zq, idx, counts, sqerr, stream=None, zq_copy=None):
     """zq_copy: optional bf16/f32 tensor that also receives z_q (aw_vq_forward_ex)."""

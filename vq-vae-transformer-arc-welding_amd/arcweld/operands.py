@@ -2,7 +2,7 @@
 
 A forward needs each weight in the layout (and dtype) its GEMMs read: the centre tap of an encoder conv as [O][I],
 a decoder conv as [O][3I] (forward) and [3O][I] (input gradient), the ConvT as [kO][I], the patch embed zero-padded
-(aw_weight_relayout modes 0-6).  An OperandSet allocates those copies once per (model, key) and
+(aw_weight_relayout modes 0-5, 7).  An OperandSet allocates those copies once per (model, key) and
 
 * refreshes them with ONE aw_weight_relayout_batch launch when a weight changed outside the optimizer (signature:
   data_ptr and version counter of every source parameter -- load_state_dict, .to(), manual edits), and

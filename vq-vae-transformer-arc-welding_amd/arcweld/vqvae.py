@@ -81,16 +81,6 @@ class VQVAEShapes:
         self.ldp = (self.P + 7) // 8 * 8
 
 
-def use_encoder_chain(m, T, H, R):
-    """The fused encoder chain (csrc/encoder_chain.hip) serves bf16 operands, H = 512, Identity-norm ResBlocks
-    (--batchnorm 0) and 1 <= R <= 16.  Opt-in (ARCWELD_ENCODER_CHAIN=1): at the configs[1] shape it ties the 16
-    per-block GEMM launches it replaces (388 vs 398 us, whole step 3.77 vs 3.73 ms), because each
-    64-token tile streams all 8 MB of weights through one CU's LDS-DMA port."""
-    import os
-    return (T == torch.bfloat16 and H == 512 and 1 <= R <= 16 and not m.batch_norm
-            and os.environ.get("ARCWELD_ENCODER_CHAIN", "0") == "1")
-
-
 def _params(m):
     """Reference-layout parameter tensors of a VQVAEPatch, by role."""
     enc = [(blk.block[1], blk.block[4]) for blk in m.encoder[0].shared_conv]
@@ -122,7 +112,7 @@ def _centre_job(w, out):
     return (c, O, I, 1, 0, 0, out)
 
 
-def _operand_jobs(m, T, chain):
+def _operand_jobs(m, T):
     """Every weight operand of the training step (forward and backward): arcweld.operands.OperandJob list."""
     from .operands import OperandJob as J
     sh = VQVAEShapes(m, 1)
@@ -133,12 +123,9 @@ def _operand_jobs(m, T, chain):
     jobs = [J("Wp", pr["pe"].weight, H, 1, P, 0, 4, torch.zeros(H, sh.ldp, device=dev, dtype=T),
               sh.ldp)]
     centre = lambda w: _centre_job(w, None)[:6]  # noqa: E731  (the centre tap of the CURRENT storage)
-    chain_src = lambda w: _centre_job(w, None)[:5] + (6,)  # noqa: E731
     for r, (c1, c2) in enumerate(pr["enc"]):
         for nm, c in (("1", c1), ("2", c2)):
             jobs.append(J(f"enc{r}_{nm}", c.weight, H, H, 1, 0, 0, e(H, H), derive=centre))
-            if chain:   # K-step-major copies for the fused chain's weight stream (the backward reads enc_w)
-                jobs.append(J(f"chain{r}_{nm}", c.weight, H, H, 1, 0, 6, e(H, H), derive=chain_src))
     jobs.append(J("Ws", pr["sep"].weight, D, H, 1, 0, 0, e(D, H)))
     jobs.append(J("Wd0", pr["dec0"].weight, H, D, 1, 0, 0, e(H, D)))
     for r, (c1, c2) in enumerate(pr["dec"]):
@@ -152,9 +139,7 @@ def _operand_jobs(m, T, chain):
 def operand_set(m, T=None):
     """The OperandSet the training step of `m` reads (for arcweld.optim.RAdam.attach_operands)."""
     T = operand_dtype(T)
-    sh = VQVAEShapes(m, 1)
-    chain = use_encoder_chain(m, T, sh.H, sh.R)
-    return operands.peek(m, ("vqvae", T, chain), lambda: _operand_jobs(m, T, chain))
+    return operands.peek(m, ("vqvae", T), lambda: _operand_jobs(m, T))
 
 
 def _centre_grad(g):
@@ -284,11 +269,9 @@ def forward(m, x, training: bool, need_backward: bool, dtype=None, seed: int = 0
 
     # ---- operand copies of the weights (relayout + cast): persistent, refreshed by one batched relayout only when
     #      a weight changed outside the optimizer (the flat RAdam rewrites them in its update kernel)
-    chain = use_encoder_chain(m, T, H, R)
-    ops = operands.get(m, ("vqvae", T, chain), lambda: _operand_jobs(m, T, chain))
+    ops = operands.get(m, ("vqvae", T), lambda: _operand_jobs(m, T))
     Wp, Ws, Wd0, Wt1 = ops["Wp"], ops["Ws"], ops["Wd0"], ops["Wt1"]
     enc_w = [(ops[f"enc{r}_1"], ops[f"enc{r}_2"]) for r in range(R)]
-    chain_w = [(ops[f"chain{r}_1"], ops[f"chain{r}_2"]) for r in range(R)] if chain else []
     dec_w = [(ops[f"dec{r}_1"], ops[f"dec{r}_2"]) for r in range(R)]
     sv.ops = ops
 
@@ -301,16 +284,7 @@ def forward(m, x, training: bool, need_backward: bool, dtype=None, seed: int = 0
     # ---- encoder ResBlocks (per-token: centre taps)
     xs, a0s, hs, a1s = [x0], [a0], [], []
     sv.enc_bs, sv.dec_bs = [], []
-    if chain:
-        # one fused launch for the whole stack (csrc/encoder_chain.hip); same saved tensors as the loop below
-        hs = [e(N, H, dt=T) for _ in range(R)]
-        a1s = [e(N, H, dt=T) for _ in range(R)]
-        xs += [e(N, H) for _ in range(R - 1)] + [None]
-        a0s += [e(N, H, dt=T) for _ in range(R)]
-        K.encoder_chain_fwd(x0, a0, [w[0] for w in chain_w], [w[1] for w in chain_w], [c1.bias for c1, _ in pr["enc"]],
-                            [c2.bias for _, c2 in pr["enc"]], drop=(p_drop, sv.enc_seed), seed_ptr=sv.ctr,
-                            h=hs, a1=a1s, x=xs[1:], aout=a0s[1:])
-    for r, (c1, c2) in enumerate(pr["enc"] if not hs else []):
+    for r, (c1, c2) in enumerate(pr["enc"]):
         if pr["enc_bn"][r] is not None:   # BatchNorm ResBlocks: per-token statistics (G = S)
             xn, an, bs = _bn_block_fwd(a0s[r], xs[r], enc_w[r][0], enc_w[r][1], H, {}, c1, c2, pr["enc_bn"][r], S,
                                        training, p_drop, sv.enc_seed[r], sv.ctr, T, last=r == R - 1)

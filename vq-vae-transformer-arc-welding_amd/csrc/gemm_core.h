@@ -392,7 +392,7 @@ template <> struct Mfma<float> {
 // 4 consecutive elements (16-B aligned for f32, 8-B for bf16)
 // Epilogue outputs are stored non-temporally: they are read back by a later launch (often the backward), never by
 // this one, and allocating them in the XCD's L2 evicts the operand tiles the other workgroups are re-reading
-// (A/B over the bench: VQ-VAE step -0.4 %, transformer step -2 %; the fused encoder chain -26 %).
+// (A/B over the bench: VQ-VAE step -0.4 %, transformer step -2 %).
 #ifndef AW_GEMM_NT
 #define AW_GEMM_NT 1
 #endif

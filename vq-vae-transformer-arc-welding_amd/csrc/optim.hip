@@ -166,12 +166,6 @@ __device__ __forceinline__ int64_t op_dst(const aw_operand_desc& d, uint32_t l) 
       const uint32_t oj = l / I, i = l - oj * I, o = oj / 3u, j = oj - o * 3u;
       return ((int64_t)j * O + o) * I + i;
     }
-    case 6: {   // (O, I, k) tap t -> K-step-major [I / 32][O][32]
-      const uint32_t oi = l / k, j = l - oi * k;
-      if (j != (uint32_t)d.tap) return -1;
-      const uint32_t o = oi / I, i = oi - o * I;
-      return ((int64_t)(i >> 5) * O + o) * 32 + (i & 31);
-    }
     default:
       return -1;
   }

@@ -114,10 +114,6 @@ __global__ __launch_bounds__(256) void relayout_batch_kernel(RelayoutJobs J) {
       const uint32_t jo = e / I, i = e - jo * I;
       const uint32_t j = jo / O, o = jo - j * O;
       v = W[(o * 3 + j) * I + i];
-    } else if (mode == 6) {    // K-step-major tap [I / 32][O][32] (the encoder chain's weight stream)
-      const uint32_t s = e / (O * 32), r = e - s * O * 32;
-      const uint32_t o = r >> 5, i = s * 32 + (r & 31);
-      v = W[(o * I + i) * k + tap];
     } else {
       v = W[e];
     }
@@ -760,14 +756,14 @@ extern "C" int aw_weight_relayout_batch(const aw_relayout_job* jobs, int n, int 
   int64_t most = 0;
   for (int i = 0; i < n; ++i) {
     const aw_relayout_job& jb = jobs[i];
-    AW_REQUIRE(jb.W && jb.out && jb.O > 0 && jb.I > 0 && jb.k > 0 && jb.mode >= 0 && jb.mode <= 7 && !(jb.mode == 6 && jb.I % 32),
+    AW_REQUIRE(jb.W && jb.out && jb.O > 0 && jb.I > 0 && jb.k > 0 && jb.mode >= 0 && jb.mode <= 7 && jb.mode != 6,
                "aw_weight_relayout_batch: bad job %d", i);
     AW_REQUIRE(!(jb.mode == 4 && jb.ldo < jb.k), "aw_weight_relayout_batch: job %d ldo < k", i);
     AW_REQUIRE((int64_t)jb.O * jb.I * (jb.k > 3 ? jb.k : 3) < (1ll << 31) && (int64_t)jb.O * jb.ldo < (1ll << 31),
                "aw_weight_relayout_batch: job %d exceeds 2^31 elements", i);
     J.j[i] = jb;
     const int64_t c = jb.mode == 4 ? (int64_t)jb.O * jb.ldo
-                                    : (int64_t)jb.O * jb.I * ((jb.mode == 0 || jb.mode == 5 || jb.mode == 6) ? 1
+                                    : (int64_t)jb.O * jb.I * ((jb.mode == 0 || jb.mode == 5) ? 1
                                                               : (jb.mode == 3 ? jb.k : 3));
     most = c > most ? c : most;
   }
