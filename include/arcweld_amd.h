@@ -76,7 +76,13 @@ typedef struct {
   const uint64_t* seed_ptr;
   /* dtype of `pre` (AW_F32 or AW_BF16): bf16-mode forwards keep the GELU pre-activations in the operand dtype */
   int pre_dtype;
+  /* epilogue store policy for C / C2: AW_STORE_NT (0, non-temporal; the lines stay in the XCD's L2 until the
+   * end-of-kernel release writes them back) or AW_STORE_WT (1, write-through: the lines leave L2 at once, so the
+   * next dependent launch does not wait for that write-back; the VQ-VAE step's GEMM chain, +3 % per step). */
+  int store_policy;
 } aw_gemm_args;
+#define AW_STORE_NT 0
+#define AW_STORE_WT 1
 
 int aw_gemm(const aw_gemm_args* args, void* stream);
 /* Same, with a caller-provided f32 workspace: when the shape is split over K (small M*N, long K: the weight

@@ -18,6 +18,7 @@ HEADER = os.path.join(os.path.dirname(PKG_DIR), "include", "arcweld_amd.h")
 
 AW_F32, AW_BF16 = 0, 1
 AW_ACT_GELU_ERF, AW_ACT_GELU_TANH = 0, 1
+AW_STORE_NT, AW_STORE_WT = 0, 1   # aw_gemm_args.store_policy
 
 c_i64 = ctypes.c_int64
 c_int = ctypes.c_int
@@ -47,6 +48,7 @@ class GemmArgs(ctypes.Structure):
         ("accumulate", c_int), ("col_mod", c_int), ("col_mul", c_int), ("col_off", c_int),
         ("seed_ptr", c_p),
         ("pre_dtype", c_int),
+        ("store_policy", c_int),
     ]
 
 

@@ -25,6 +25,35 @@ def _ld(t):
     return t.stride(0)
 
 
+# Epilogue store policy of the GEMMs issued inside a `store_policy(...)` block (aw_gemm_args.store_policy):
+# nat.AW_STORE_NT (default) or nat.AW_STORE_WT (write-through: the VQ-VAE step, see arcweld/vqvae.py).
+_STORE_POLICY = [0]
+
+
+class store_policy:
+    """Context manager / decorator: GEMM launches issued inside use `policy` for their epilogue stores."""
+
+    def __init__(self, policy):
+        self.policy = int(policy)
+
+    def __enter__(self):
+        self._prev = _STORE_POLICY[0]
+        _STORE_POLICY[0] = self.policy
+
+    def __exit__(self, *exc):
+        _STORE_POLICY[0] = self._prev
+        return False
+
+    def __call__(self, fn):
+        import functools
+
+        @functools.wraps(fn)
+        def wrapped(*a, **k):
+            with store_policy(self.policy):
+                return fn(*a, **k)
+        return wrapped
+
+
 # Optional live profiler: when set to a list, every gemm() appends (start_event, end_event, algorithmic_flops)
 # recorded on the launch stream (bench.py uses it for the roofline of the GEMM kernel over the timed region).
 PROFILE = None
@@ -57,6 +86,7 @@ def _gemm_args(A, B, M, N, K, *, a_trans=False, b_trans=False, conv=None, alpha=
     a.alpha, a.beta = float(alpha), float(beta)
     a.bias = ptr(bias)
     a.act = int(act)
+    a.store_policy = _STORE_POLICY[0]
     a.pre, a.ld_pre = ptr(pre), _ld(pre)
     if pre is not None:
         if pre.dtype not in (torch.float32, torch.bfloat16):

@@ -24,6 +24,7 @@ import weakref
 
 import torch
 
+from . import _native as nat
 from . import kernels as K
 from . import operands
 from .precision import operand_dtype  # noqa: F401  (re-exported: model/ and arcweld.decoder import it from here)
@@ -238,6 +239,10 @@ def _bn_block_bwd(gy, x, a0, bs, w1d, w2d, Kd, dgemm_kw, wg, c1, c2, bns, G, tra
     return gx, gxo
 
 
+# The step's GEMM chain stores its epilogue outputs write-through (aw_gemm_args.store_policy): with 64 dependent
+# class-A launches per step, each launch otherwise waits for the previous one's end-of-kernel L2 write-back of up to
+# 32 MB of dirty output lines (same-box A/B: +3 % windows/s)
+@K.store_policy(nat.AW_STORE_WT)
 def forward(m, x, training: bool, need_backward: bool, dtype=None, seed: int = 0):
     """Returns (emb_loss (), x_hat (B, L, C), perplexity (), indices (N,), saved-or-None)."""
     T = operand_dtype(dtype)
@@ -457,6 +462,7 @@ def _cast(t, T):
     return out
 
 
+@K.store_policy(nat.AW_STORE_WT)
 def backward(m, sv, g_emb, g_xhat, slot, mid_hook=None):
     """Accumulate parameter gradients into ``slot(param)`` (f32 tensors shaped like the parameter).
 

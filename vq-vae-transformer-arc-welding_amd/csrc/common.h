@@ -10,6 +10,24 @@
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
 typedef __attribute__((ext_vector_type(2))) float f32x2;
+typedef __attribute__((ext_vector_type(2))) unsigned int u32x2;
+
+// Write-through (sc1) global stores for large streamed outputs: the written lines leave the XCD's L2 at once instead
+// of staying dirty until the end-of-kernel release writes them back (which the next launch waits for).  Vector
+// stores only (MI355X_MICROARCH.md: a 16-B sc1 store costs about a plain one).  AW_WT_MISC selects them in the
+// non-GEMM kernels that stream out tens of MB (RAdam, un-patch head backward; same-box A/B: neutral to +0.3 %).
+#ifndef AW_WT_MISC
+#define AW_WT_MISC 1
+#endif
+__device__ __forceinline__ void aw_st_wt(void* p, f32x4 v) {
+  asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
+}
+__device__ __forceinline__ void aw_st_wt(void* p, u32x2 v) {
+  asm volatile("global_store_dwordx2 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+}
+__device__ __forceinline__ void aw_st_wt(void* p, uint32_t v) {
+  asm volatile("global_store_dword %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+}
 typedef __bf16 bf16;
 
 // ---------------------------------------------------------------- error plumbing (host side)

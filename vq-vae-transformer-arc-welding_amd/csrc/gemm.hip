@@ -149,6 +149,8 @@ static int validate(const aw_gemm_args& a) {
   AW_REQUIRE(!(a.c2_mode && !a.C2), "aw_gemm: c2_mode without C2");
   AW_REQUIRE(!(a.colstats && a.stats_mod <= 0), "aw_gemm: colstats needs stats_mod > 0");
   AW_REQUIRE(a.pre_dtype == AW_F32 || a.pre_dtype == AW_BF16, "aw_gemm: bad pre_dtype %d", a.pre_dtype);
+  AW_REQUIRE(a.store_policy == AW_STORE_NT || a.store_policy == AW_STORE_WT, "aw_gemm: bad store_policy %d",
+             a.store_policy);
   const bool plain = !a.bias && !a.pre && !a.resid && a.drop_p <= 0.f && !a.C2 && !a.colstats && a.C &&
                      a.c_dtype == AW_F32 && (a.beta == 0.f || a.beta == 1.f || a.accumulate);
   AW_REQUIRE(!a.accumulate || plain, "aw_gemm: accumulate mode allows no other epilogue field (f32 C only)");
@@ -173,6 +175,13 @@ static bool is_ragged(const aw_gemm_args& a) {
   const bool rb = !a.b_trans ? (a.K % epc) != 0 : (a.N % epc != 0 && !padded(a.N, a.ldb));
   return ra || rb;
 }
+
+// most split-K slices of one grouped weight-gradient tile (their partials meet in the epilogue's f32 atomics)
+// (8: the transformer's four 512 x 512 projections, 64 tiles, take 63 instead of 103 us; the wider kinds already fill
+// the chip with two slices)
+#ifndef AW_GROUPED_MAXSPLIT
+#define AW_GROUPED_MAXSPLIT 8
+#endif
 
 static int g_tile_override = 0;   // aw_gemm_set_tile: 0 = automatic, 128 / 256 = force (tests, tuning)
 
@@ -224,7 +233,12 @@ static void plan(const aw_gemm_args& a, int ngroups, bool grouped, GemmP& P) {
   const bool auto256 = t256 >= 256 && !grouped && !a.accumulate && !a.a_trans && !a.b_trans && a.K >= 16 * BK;
   if (a.a_dtype == AW_BF16 && !is_ragged(a) && (g_tile_override == 256 || (g_tile_override == 0 && auto256))) {
     bm = 256;
-    if (a.accumulate && t256 < 240 && a.K >= 24 * BK) splits = 2;
+    if (a.accumulate && t256 < 240 && a.K >= 24 * BK) {
+      splits = 256 / t256;
+      if (splits > a.K / (12 * BK)) splits = a.K / (12 * BK);
+      if (grouped && splits > AW_GROUPED_MAXSPLIT) splits = AW_GROUPED_MAXSPLIT;
+      if (splits < 1) splits = 1;
+    }
   }
   if (bm == 128) {
     const int nb = aw_cdiv(a.M, 128) * P.tiles_n * ngroups;
@@ -233,7 +247,7 @@ static void plan(const aw_gemm_args& a, int ngroups, bool grouped, GemmP& P) {
       splits = 512 / nb;
       const int max_splits = a.K / (12 * BK);
       if (splits > max_splits) splits = max_splits;
-      if (grouped && splits > 2) splits = 2;
+      if (grouped && splits > AW_GROUPED_MAXSPLIT) splits = AW_GROUPED_MAXSPLIT;
       if (splits < 1) splits = 1;
     }
     if (grouped && a.accumulate && nb > 512 && nb < 1024 && a.K >= 48 * BK) {

@@ -99,11 +99,19 @@ enum EpiBits : uint32_t {
 
 // Diagnostic phase stamps (tools/probe only: defined there before this file is included; never in the library).
 #ifdef AW_GEMM_STAMPS
-__device__ uint64_t g_gemm_stamps[8192 * 8];
+static __device__ uint64_t g_gemm_stamps[8192 * 8];   // one copy per translation unit (each has its own kernels)
 #define AW_STAMP(i) do { if (threadIdx.x == 0 && blockIdx.y == 0 && blockIdx.x < 8192) \
     g_gemm_stamps[blockIdx.x * 8 + (i)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+// extern "C" reader of this translation unit's stamps (copies n words out, then zeroes them)
+#define AW_STAMP_EXPORT(name)                                                                                   \
+  extern "C" int name(uint64_t* out, int n) {                                                                  \
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(awg::g_gemm_stamps), (size_t)n * 8) != hipSuccess) return -1;     \
+    static uint64_t zeros[8192 * 8];                                                                            \
+    return hipMemcpyToSymbol(HIP_SYMBOL(awg::g_gemm_stamps), zeros, sizeof(zeros)) == hipSuccess ? n : -1;    \
+  }
 #else
 #define AW_STAMP(i) do { } while (0)
+#define AW_STAMP_EXPORT(name)
 #endif
 
 // ---------------------------------------------------------------- operand staging
@@ -396,18 +404,24 @@ template <> struct Mfma<float> {
 #ifndef AW_GEMM_NT
 #define AW_GEMM_NT 1
 #endif
-__device__ __forceinline__ void store4(void* base, bool is_bf16, int64_t e, const float (&v)[4]) {
-  typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+// wt (aw_gemm_args.store_policy == AW_STORE_WT): write-through (sc1) stores instead -- the lines leave the XCD's L2
+// at once, so the end-of-kernel release has no dirty output lines to write back before the next launch may start
+// (the VQ-VAE step's chain of 64 class-A launches: +3 %, same-box A/B)
+__device__ __forceinline__ void store4(void* base, bool is_bf16, int64_t e, const float (&v)[4], bool wt) {
   if (is_bf16) {
     bf16 h[4] = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
     u32x2 u;
     memcpy(&u, h, 8);
     u32x2* d = reinterpret_cast<u32x2*>(reinterpret_cast<bf16*>(base) + e);
-    if (AW_GEMM_NT) __builtin_nontemporal_store(u, d); else *d = u;
+    if (wt) aw_st_wt(d, u);
+    else if (AW_GEMM_NT) __builtin_nontemporal_store(u, d);
+    else *d = u;
   } else {
     f32x4 u = {v[0], v[1], v[2], v[3]};
     f32x4* d = reinterpret_cast<f32x4*>(reinterpret_cast<float*>(base) + e);
-    if (AW_GEMM_NT) __builtin_nontemporal_store(u, d); else *d = u;
+    if (wt) aw_st_wt(d, u);
+    else if (AW_GEMM_NT) __builtin_nontemporal_store(u, d);
+    else *d = u;
   }
 }
 
@@ -704,6 +718,7 @@ __global__ __launch_bounds__(Cfg<BMT>::NTH, RAGGED ? 1 : Cfg<BMT>::MINB) void ge
   const bool f_c2bf = EPF(EP_C2BF, p.c2_dtype == AW_BF16);
   const bool f_stats = EPF(EP_STATS, p.colstats != nullptr);
   const float alpha = GEN ? p.alpha : 1.f;       // specialised codes are issued for alpha == 1 only
+  const bool wt = p.store_policy == AW_STORE_WT;
   constexpr bool FASTGELU = sizeof(T) == 2;      // bf16 operands: branch-free erf (exact-f32 mode keeps erff)
   const uint64_t dseed = f_drop ? aw_seed_mix(p.drop_seed, p.seed_ptr) : 0ull;
   const uint64_t dseed2 = c2m == 3 ? aw_seed_mix(p.drop2_seed, p.seed_ptr) : 0ull;
@@ -785,8 +800,8 @@ __global__ __launch_bounds__(Cfg<BMT>::NTH, RAGGED ? 1 : Cfg<BMT>::MINB) void ge
           }
         }
         if (vec) {
-          if (f_c) store4(Cptr, f_cbf, row * p.ldc + col, v);
-          if (c2m) store4(p.C2, f_c2bf, row * p.ldc2 + col, w);
+          if (f_c) store4(Cptr, f_cbf, row * p.ldc + col, v, wt);
+          if (c2m) store4(p.C2, f_c2bf, row * p.ldc2 + col, w, wt);
         } else if constexpr (GEN) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) {

@@ -38,3 +38,5 @@ bool launch_fast_256(const GemmP& P, hipStream_t s, Layout ly, uint32_t code) {
 }
 
 }  // namespace awg
+
+AW_STAMP_EXPORT(aw_probe_stamps_256)   // probe builds only (AW_GEMM_STAMPS)

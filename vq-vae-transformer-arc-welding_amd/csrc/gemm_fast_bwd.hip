@@ -26,3 +26,5 @@ bool launch_fast_bwd(const GemmP& P, hipStream_t s, bool is_bf16, Layout ly, uin
 }
 
 }  // namespace awg
+
+AW_STAMP_EXPORT(aw_probe_stamps_bwd)   // probe builds only (AW_GEMM_STAMPS)

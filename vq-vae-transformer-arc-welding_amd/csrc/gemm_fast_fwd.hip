@@ -32,3 +32,5 @@ bool launch_fast_fwd(const GemmP& P, hipStream_t s, bool is_bf16, Layout ly, uin
 }
 
 }  // namespace awg
+
+AW_STAMP_EXPORT(aw_probe_stamps_fwd)   // probe builds only (AW_GEMM_STAMPS)

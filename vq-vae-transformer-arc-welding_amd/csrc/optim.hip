@@ -128,10 +128,17 @@ __global__ __launch_bounds__(256) void radam_kernel(float* __restrict__ p, float
     radam_one(g4.y, p4.y, m4.y, v4.y, wd, gs, S);
     radam_one(g4.z, p4.z, m4.z, v4.z, wd, gs, S);
     radam_one(g4.w, p4.w, m4.w, v4.w, wd, gs, S);
-    reinterpret_cast<float4*>(p)[q] = p4;
-    reinterpret_cast<float4*>(m)[q] = m4;
-    reinterpret_cast<float4*>(v)[q] = v4;
-    if (zero_g) reinterpret_cast<float4*>(g)[q] = make_float4(0.f, 0.f, 0.f, 0.f);   // zero_grad, fused
+    if (AW_WT_MISC) {
+      aw_st_wt(reinterpret_cast<float4*>(p) + q, (f32x4){p4.x, p4.y, p4.z, p4.w});
+      aw_st_wt(reinterpret_cast<float4*>(m) + q, (f32x4){m4.x, m4.y, m4.z, m4.w});
+      aw_st_wt(reinterpret_cast<float4*>(v) + q, (f32x4){v4.x, v4.y, v4.z, v4.w});
+      if (zero_g) aw_st_wt(reinterpret_cast<float4*>(g) + q, (f32x4){0.f, 0.f, 0.f, 0.f});
+    } else {
+      reinterpret_cast<float4*>(p)[q] = p4;
+      reinterpret_cast<float4*>(m)[q] = m4;
+      reinterpret_cast<float4*>(v)[q] = v4;
+      if (zero_g) reinterpret_cast<float4*>(g)[q] = make_float4(0.f, 0.f, 0.f, 0.f);   // zero_grad, fused
+    }
   }
 }
 
@@ -192,7 +199,15 @@ __device__ __forceinline__ void op_store4(const aw_operand_desc& d, uint32_t l0,
     if (d.dtype == AW_BF16) {
       typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
       bf16x4 h = {(bf16)pv[0], (bf16)pv[1], (bf16)pv[2], (bf16)pv[3]};
-      reinterpret_cast<bf16x4*>(d.out)[t0 >> 2] = h;
+      if (AW_WT_MISC) {
+        u32x2 u;
+        memcpy(&u, &h, 8);
+        aw_st_wt(reinterpret_cast<bf16x4*>(d.out) + (t0 >> 2), u);
+      } else {
+        reinterpret_cast<bf16x4*>(d.out)[t0 >> 2] = h;
+      }
+    } else if (AW_WT_MISC) {
+      aw_st_wt(reinterpret_cast<float4*>(d.out) + (t0 >> 2), (f32x4){pv[0], pv[1], pv[2], pv[3]});
     } else {
       reinterpret_cast<float4*>(d.out)[t0 >> 2] = make_float4(pv[0], pv[1], pv[2], pv[3]);
     }
@@ -237,10 +252,17 @@ __global__ __launch_bounds__(256) void radam_ops_kernel(float* __restrict__ p, f
     radam_one(g4.y, p4.y, m4.y, v4.y, wd, gs, S);
     radam_one(g4.z, p4.z, m4.z, v4.z, wd, gs, S);
     radam_one(g4.w, p4.w, m4.w, v4.w, wd, gs, S);
-    reinterpret_cast<float4*>(p)[q] = p4;
-    reinterpret_cast<float4*>(m)[q] = m4;
-    reinterpret_cast<float4*>(v)[q] = v4;
-    if (zero_g) reinterpret_cast<float4*>(g)[q] = make_float4(0.f, 0.f, 0.f, 0.f);   // zero_grad, fused
+    if (AW_WT_MISC) {
+      aw_st_wt(reinterpret_cast<float4*>(p) + q, (f32x4){p4.x, p4.y, p4.z, p4.w});
+      aw_st_wt(reinterpret_cast<float4*>(m) + q, (f32x4){m4.x, m4.y, m4.z, m4.w});
+      aw_st_wt(reinterpret_cast<float4*>(v) + q, (f32x4){v4.x, v4.y, v4.z, v4.w});
+      if (zero_g) aw_st_wt(reinterpret_cast<float4*>(g) + q, (f32x4){0.f, 0.f, 0.f, 0.f});
+    } else {
+      reinterpret_cast<float4*>(p)[q] = p4;
+      reinterpret_cast<float4*>(m)[q] = m4;
+      reinterpret_cast<float4*>(v)[q] = v4;
+      if (zero_g) reinterpret_cast<float4*>(g)[q] = make_float4(0.f, 0.f, 0.f, 0.f);   // zero_grad, fused
+    }
     const uint32_t l0 = (uint32_t)(e - s_off[s]);
     const int64_t len = end - s_off[s];
     const float pv[4] = {p4.x, p4.y, p4.z, p4.w};

@@ -644,7 +644,11 @@ __global__ __launch_bounds__(1024) void head_bwd2_cs_kernel(const TY* __restrict
       bf16 h[2] = {(bf16)g.x, (bf16)g.y};
       uint32_t u;
       memcpy(&u, h, 4);
-      *reinterpret_cast<uint32_t*>(gy + r * H + c0) = u;
+      if (AW_WT_MISC) aw_st_wt(gy + r * H + c0, u);
+      else *reinterpret_cast<uint32_t*>(gy + r * H + c0) = u;
+    } else if (AW_WT_MISC) {
+      u32x2 u = {__float_as_uint(g.x), __float_as_uint(g.y)};
+      aw_st_wt(gy + r * H + c0, u);
     } else {
       *reinterpret_cast<float2*>(gy + r * H + c0) = make_float2(g.x, g.y);
     }
