@@ -35,17 +35,17 @@ constexpr int WROWS = 32;    // rows (queries or keys) per wave
 constexpr int BLK = 128;     // rows per workgroup (4 waves)
 constexpr int IMG = TILE * ROWB;
 
-// One-dimensional grid of nqb * nh * B workgroups; the nqb row blocks of one (b, h) get consecutive logical ids and
-// the logical ids of one XCD are contiguous (hardware blocks i, i+8, i+16, ... run on one XCD), so the blocks that
-// re-read the same K/V (or Q/dO) tiles share that XCD's L2 and run at the same time.
+// One-dimensional grid of nqb * nh * B workgroups in row-block-major order: every (b, h)'s block x = 0 (the longest
+// causal range: the last query block in the forward and dQ, the first key block in dK/dV) is dispatched before any
+// x = 1, so the longest workgroups start first and the short ones fill the tail.  Same-box A/B at 51 x 321 against
+// the (b, h)-major order with the row blocks of one head on one XCD (their K/V re-reads shared in L2): forward
+// 24.9 -> 23.2 us, backward 81.7 -> 80.1 us (tools/attn_ab.sh).
 struct BlockId {
   int x, h, b;
   __device__ __forceinline__ BlockId(int nqb, int nh) {
-    const int n = (int)gridDim.x, bid = (int)blockIdx.x;
-    const int q = n / 8, r = n % 8, xcd = bid % 8, slot = bid / 8;
-    const int L = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + slot;
-    x = L % nqb;
-    const int bh = L / nqb;
+    const int nbh = (int)gridDim.x / nqb, bid = (int)blockIdx.x;
+    x = bid / nbh;
+    const int bh = bid % nbh;
     h = bh % nh;
     b = bh / nh;
   }
@@ -235,62 +235,134 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_mfma_kernel(const bf16* __res
   }
 }
 
-// ---------------------------------------------------------------- dQ (query-stationary)
-// Also computes delta_i = dO_i . O_i (rows it owns, from dy and y) and writes it for the dK/dV launch that follows.
-__global__ __launch_bounds__(256, 2) void attn_dq_mfma_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ dy,
+// ---------------------------------------------------------------- backward: LDS-DMA tile ring
+// The two backward kernels take every tile by LDS-DMA (buffer_load_dwordx4 ... lds: lane l of a wave-instruction
+// writes the 16 bytes at M0 + 16 l) into a ring NB tiles deep, so a workgroup keeps NB - 1 tiles of reads in flight
+// under its MFMA / softmax work; no staging VGPRs, no ds_write.  A piece is 1 KiB = 8 rows of a 64-row image; the
+// swizzle is applied on the SOURCE address (LDS slot c of row r holds chunk c ^ swz(r)), and rows past the end of
+// the sequence come back as zeros from the buffer range check.  Same-box A/B at 51 x 321 against the register-staged
+// double buffer: dQ + dK/dV 80.1 -> 76.5 us.  (The forward measured slower on the ring, 26.0 vs 23.2 us: at 80 KB of
+// LDS it runs two workgroups per CU instead of three, and with its loads alone -- no MFMA, no softmax -- the
+// register-staged forward already takes 19.7 us, so it is bound by the load pipeline, not by its depth.)
+typedef int v4i32 __attribute__((ext_vector_type(4)));
+constexpr int NB = 3;          // ring depth (tiles)
+constexpr int SLOT = 2 * IMG;  // one ring slot: two 64-row images
+
+__device__ __forceinline__ v4i32 rdesc(const char* base, uint32_t nbytes) {
+  const uint64_t p = (uint64_t)(uintptr_t)base;
+  return v4i32{(int)__builtin_amdgcn_readfirstlane((uint32_t)p),
+               (int)__builtin_amdgcn_readfirstlane((uint32_t)(p >> 32) & 0xFFFFu),
+               (int)__builtin_amdgcn_readfirstlane(nbytes), 0x00020000};
+}
+__device__ __forceinline__ void dma(uint32_t m0, int off, v4i32 desc) {
+  asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" ::"s"(m0), "v"(off), "s"(desc)
+               : "memory", "m0");
+}
+template <int N> __device__ __forceinline__ void vm_wait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+__device__ __forceinline__ void raw_barrier() {
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+}
+// source byte offset of lane `lane` in piece jj of a 64-row image whose rows are ldb bytes apart
+__device__ __forceinline__ int piece_off(int jj, int lane, int ldb) {
+  const int row = 8 * jj + (lane >> 3);
+  return row * ldb + (((lane & 7) ^ swz(row)) << 4);
+}
+__device__ __forceinline__ uint32_t lds_addr(const char* p) {
+  return (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const char*)p;
+}
+
+__device__ __forceinline__ void dma_dword(uint32_t m0, int off, v4i32 desc) {
+  asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dword %1, %2, 0 offen lds" ::"s"(m0), "v"(off), "s"(desc)
+               : "memory", "m0");
+}
+__device__ __forceinline__ void lgkm_wait0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+// dQ on the ring.  Wave w fills bytes [4 KiB w, 4 KiB w + 4 KiB) of every slot: K rows 32w.. (w < 2) or V
+// rows 32(w - 2).. (w >= 2).  The stationary operands of a wave are its own 32 rows only, so they are staged where
+// nothing but that wave's own later DMA lands: Q in bytes [4 KiB w, +4 KiB) of slot NB - 1 (a 128-row image over
+// the slot; the wave's first DMA into it follows its reads), dO and O in two 128-row images of their own.  It also
+// computes delta_i = dO_i . O_i for its rows and writes it (after its loop) for the dK/dV launch that follows.
+__global__ __launch_bounds__(256, 2) void attn_dq_ring_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ dy,
                                                            const bf16* __restrict__ y, const float* __restrict__ lse,
                                                            float* __restrict__ delta, int T_, int nh, int d,
                                                            bf16* __restrict__ dqkv, float c2, float scale) {
-  __shared__ __attribute__((aligned(16))) char KV[4 * IMG];   // double-buffered K/V images, as in the forward
+  __shared__ __attribute__((aligned(16))) char L[NB * SLOT + 4 * IMG];   // ring, dO image, O image
   const int nqb = (T_ + BLK - 1) / BLK;
   const BlockId id(nqb, nh);
   const int qb = nqb - 1 - id.x;
   const int h = id.h, b = id.b;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = lane & 31, hf = lane >> 5;
-  const int64_t ld = 3 * (int64_t)d;
-  const bf16* base = qkv + (int64_t)b * T_ * ld;
-  const bf16* gbase = dy + (int64_t)b * T_ * d;
-  const int qw = qb * BLK + w * WROWS, q = qw + r;
-  const int qc = min(q, T_ - 1);
-  uint4 qf[4], gf[4];
+  const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, hf = lane >> 5;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int ldb = 6 * d, ldg = 2 * d;   // bytes per qkv / dy / y row
+  const char* bbase = reinterpret_cast<const char*>(qkv) + (int64_t)b * T_ * ldb;
+  const uint32_t lring = lds_addr(L), lg = lring + NB * SLOT, ly = lg + 2 * IMG;
+  const int q0 = qb * BLK, qw = q0 + w * WROWS, q = qw + r;
+  const int kend = min(T_, q0 + BLK);
+  const int nt = (kend + TILE - 1) / TILE;
+  const int sel = w >> 1;   // 0: K image, 1: V image
+  int off[4];
 #pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    qf[s] = *reinterpret_cast<const uint4*>(base + (int64_t)qc * ld + h * HS + 16 * s + 8 * hf);
-    gf[s] = *reinterpret_cast<const uint4*>(gbase + (int64_t)qc * d + h * HS + 16 * s + 8 * hf);
+  for (int u = 0; u < 4; ++u) off[u] = piece_off(4 * (w & 1) + u, lane, ldb);
+  {   // own rows of Q, dO, O
+    const v4i32 dq = rdesc(bbase + (int64_t)q0 * ldb + h * HS * 2, (uint32_t)(T_ - q0) * ldb);
+    const int64_t gro = ((int64_t)b * T_ + q0) * ldg + h * HS * 2;
+    const v4i32 dg = rdesc(reinterpret_cast<const char*>(dy) + gro, (uint32_t)(T_ - q0) * ldg);
+    const v4i32 dyv = rdesc(reinterpret_cast<const char*>(y) + gro, (uint32_t)(T_ - q0) * ldg);
+    const uint32_t sq = lring + (NB - 1) * SLOT;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const uint32_t o = (4 * w + u) * 1024;
+      dma(sq + o, piece_off(4 * w + u, lane, ldb), dq);
+      dma(lg + o, piece_off(4 * w + u, lane, ldg), dg);
+      dma(ly + o, piece_off(4 * w + u, lane, ldg), dyv);
+    }
   }
-  const int64_t st_i = ((int64_t)b * nh + h) * T_ + qc;
+  auto issue = [&](int t) {
+    const int k0 = t * TILE;
+    const uint32_t nrec = t < nt ? (uint32_t)(T_ - k0) * ldb : 0u;
+    const v4i32 ds = rdesc(bbase + (int64_t)k0 * ldb + ((1 + sel) * d + h * HS) * 2, nrec);
+    const uint32_t s = lring + (t % NB) * SLOT + 4096 * w;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) dma(s + 1024 * u, off[u], ds);
+  };
+#pragma unroll
+  for (int t = 0; t < NB - 1; ++t) issue(t);
+  vm_wait<4 * (NB - 2)>();
+  raw_barrier();
+  uint4 qf[4], gf[4];
   float Dl = 0.f;
   {
-    const bf16* yb = y + (int64_t)b * T_ * d + (int64_t)qc * d + h * HS + 8 * hf;
+    const char* Qs = L + (NB - 1) * SLOT;
+    const char* Gs = L + NB * SLOT;
+    const char* Ys = Gs + 2 * IMG;
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-      const bf16x8 yv = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(yb + 16 * s));
+      qf[s] = row_frag(Qs, 32 * w + r, s, hf);
+      gf[s] = row_frag(Gs, 32 * w + r, s, hf);
+      const bf16x8 yv = __builtin_bit_cast(bf16x8, row_frag(Ys, 32 * w + r, s, hf));
       const bf16x8 gv = __builtin_bit_cast(bf16x8, gf[s]);
 #pragma unroll
       for (int e = 0; e < 8; ++e) Dl = fmaf((float)gv[e], (float)yv[e], Dl);
     }
     Dl += __shfl_xor(Dl, 32, 64);
-    if (hf == 0 && q < T_) delta[st_i] = Dl;
+    lgkm_wait0();   // the Q reads retire before this wave's DMA of tile NB - 1 overwrites them
   }
+  const int64_t st_i = ((int64_t)b * nh + h) * T_ + min(q, T_ - 1);
   const float L2 = lse[st_i] * 1.4426950408889634f;
   f32x16 acc[2] = {zero16(), zero16()};
-  const int kend = min(T_, qb * BLK + BLK);
-  const int nt = (kend + TILE - 1) / TILE;
-  TileRegs kr, vr;
-  tile_load(kr, base, ld, d + h * HS, 0, T_, tid);
-  tile_load(vr, base, ld, 2 * d + h * HS, 0, T_, tid);
+  const bool active = qw < T_;
   for (int t = 0; t < nt; ++t) {
-    const int k0 = t * TILE;
-    char* Ks = KV + (t & 1) * 2 * IMG;
-    char* Vs = Ks + IMG;
-    tile_store(kr, Ks, tid);
-    tile_store(vr, Vs, tid);
-    __syncthreads();
-    if (t + 1 < nt) {
-      tile_load(kr, base, ld, d + h * HS, k0 + TILE, T_, tid);
-      tile_load(vr, base, ld, 2 * d + h * HS, k0 + TILE, T_, tid);
+    if (t > 0) {
+      vm_wait<4 * (NB - 2)>();
+      raw_barrier();
     }
-    if (k0 > qw + WROWS - 1) continue;
+    issue(t + NB - 1);
+    const int k0 = t * TILE;
+    if (!active || k0 > qw + WROWS - 1) continue;
+    const char* Ks = L + (t % NB) * SLOT;
+    const char* Vs = Ks + IMG;
     const bool edge = (k0 + TILE - 1 > qw) || (k0 + TILE > T_);
 #pragma unroll
     for (int st = 0; st < 2; ++st) {
@@ -301,8 +373,8 @@ __global__ __launch_bounds__(256, 2) void attn_dq_mfma_kernel(const bf16* __rest
         dp = mfma32(row_frag(Vs, 32 * st + r, ks, hf), gf[ks], dp);
       }
 #pragma unroll
-      for (int i = 0; i < 16; ++i) s[i] = __builtin_amdgcn_exp2f(s[i] * c2 - L2);
-      if (edge) {   // kept a real (wave-uniform) branch, as in the forward
+      for (int i = 0; i < 16; ++i) s[i] = __builtin_amdgcn_exp2f(fmaf(s[i], c2, -L2));
+      if (edge) {
         asm volatile("" ::: "memory");
         const int lim = min(q, T_ - 1) - (k0 + 32 * st + 4 * hf);
 #pragma unroll
@@ -318,8 +390,10 @@ __global__ __launch_bounds__(256, 2) void attn_dq_mfma_kernel(const bf16* __rest
       }
     }
   }
+  vm_wait<0>();
   if (q < T_) {
-    bf16* out = dqkv + ((int64_t)b * T_ + q) * ld + h * HS;
+    if (hf == 0) delta[st_i] = Dl;
+    bf16* out = dqkv + ((int64_t)b * T_ + q) * (3 * (int64_t)d) + h * HS;
 #pragma unroll
     for (int dt = 0; dt < 2; ++dt)
 #pragma unroll
@@ -327,60 +401,87 @@ __global__ __launch_bounds__(256, 2) void attn_dq_mfma_kernel(const bf16* __rest
   }
 }
 
-// ---------------------------------------------------------------- dK, dV (key-stationary)
-// grid (ceil(T/128), n_head, B); wave w owns keys kb*128 + 32w .. +31; query tiles from the block's first key on.
-__global__ __launch_bounds__(256, 2) void attn_dkv_mfma_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ dy,
+// dK, dV on the ring, key-stationary.  A slot holds the query tile's Q image, dO image, lse row and
+// delta row; wave w fills bytes [4 KiB w, +4 KiB) of the two images (Q rows 32w.. for w < 2, dO rows 32(w - 2)..
+// for w >= 2) and one 256-byte row (lse for even w, delta for odd w: two waves load each row, the same bytes), so
+// every wave issues five pieces per tile.  The wave's own K rows are staged in slot NB - 1 (as Q in the dQ kernel),
+// its V rows in an image of their own.
+constexpr int DSLOT = 2 * IMG + 2 * TILE * 4;
+__global__ __launch_bounds__(256, 2) void attn_dkv_ring_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ dy,
                                                             const float* __restrict__ lse,
                                                             const float* __restrict__ delta, int T_, int nh, int d,
                                                             bf16* __restrict__ dqkv, float c2, float scale) {
-  // double-buffered per query tile: Q image, dO image, lse and delta rows (one barrier per tile, as in the forward)
-  __shared__ __attribute__((aligned(16))) char QG[4 * IMG];
-  __shared__ __attribute__((aligned(16))) float LD[4 * TILE];
+  __shared__ __attribute__((aligned(16))) char L[NB * DSLOT + 2 * IMG];
   const BlockId id((T_ + BLK - 1) / BLK, nh);
-  const int kb = id.x;  // early key blocks see the most queries: launched first
+  const int kb = id.x;
   const int h = id.h, b = id.b;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = lane & 31, hf = lane >> 5;
-  const int64_t ld = 3 * (int64_t)d;
-  const bf16* base = qkv + (int64_t)b * T_ * ld;
-  const bf16* gbase = dy + (int64_t)b * T_ * d;
-  const int kw = kb * BLK + w * WROWS, key = kw + r;
-  const int kc = min(key, T_ - 1);
-  uint4 kf[4], vf[4];
+  const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, hf = lane >> 5;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int ldb = 6 * d, ldg = 2 * d;
+  const char* bbase = reinterpret_cast<const char*>(qkv) + (int64_t)b * T_ * ldb;
+  const char* gbase = reinterpret_cast<const char*>(dy) + (int64_t)b * T_ * ldg;
+  const uint32_t lring = lds_addr(L), lv = lring + NB * DSLOT;
+  const int k0b = kb * BLK, kw = k0b + w * WROWS, key = kw + r;
+  const int qstart = k0b;   // BLK is a multiple of TILE
+  const int nqt = (T_ - qstart + TILE - 1) / TILE;
+  const int sel = w >> 1;   // 0: Q image, 1: dO image
+  const int lds_src = sel ? ldg : ldb;
+  int off[4];
 #pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    kf[s] = *reinterpret_cast<const uint4*>(base + (int64_t)kc * ld + d + h * HS + 16 * s + 8 * hf);
-    vf[s] = *reinterpret_cast<const uint4*>(base + (int64_t)kc * ld + 2 * d + h * HS + 16 * s + 8 * hf);
+  for (int u = 0; u < 4; ++u) off[u] = piece_off(4 * (w & 1) + u, lane, lds_src);
+  const int64_t sbase = ((int64_t)b * nh + h) * T_;
+  const float* vec = (w & 1) ? delta : lse;
+  {   // own rows of K (into slot NB - 1) and V
+    const v4i32 dk = rdesc(bbase + (int64_t)k0b * ldb + (d + h * HS) * 2, (uint32_t)(T_ - k0b) * ldb);
+    const v4i32 dv = rdesc(bbase + (int64_t)k0b * ldb + (2 * d + h * HS) * 2, (uint32_t)(T_ - k0b) * ldb);
+    const uint32_t sk = lring + (NB - 1) * DSLOT;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const uint32_t o = (4 * w + u) * 1024;
+      dma(sk + o, piece_off(4 * w + u, lane, ldb), dk);
+      dma(lv + o, piece_off(4 * w + u, lane, ldb), dv);
+    }
+  }
+  auto issue = [&](int i) {
+    const int q0 = qstart + TILE * i;
+    const bool valid = i < nqt;
+    const char* src = sel ? gbase + (int64_t)q0 * ldg + h * HS * 2 : bbase + (int64_t)q0 * ldb + h * HS * 2;
+    const v4i32 ds = rdesc(src, valid ? (uint32_t)(T_ - q0) * lds_src : 0u);
+    const v4i32 dvv = rdesc(reinterpret_cast<const char*>(vec + sbase + q0), valid ? (uint32_t)(T_ - q0) * 4 : 0u);
+    const uint32_t s = lring + (i % NB) * DSLOT;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) dma(s + 4096 * w + 1024 * u, off[u], ds);
+    dma_dword(s + 2 * IMG + (w & 1) * (TILE * 4), lane * 4, dvv);
+  };
+#pragma unroll
+  for (int i = 0; i < NB - 1; ++i) issue(i);
+  vm_wait<5 * (NB - 2)>();
+  raw_barrier();
+  uint4 kf[4], vf[4];
+  {
+    const char* Ksg = L + (NB - 1) * DSLOT;
+    const char* Vsg = L + NB * DSLOT;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      kf[s] = row_frag(Ksg, 32 * w + r, s, hf);
+      vf[s] = row_frag(Vsg, 32 * w + r, s, hf);
+    }
+    lgkm_wait0();
   }
   f32x16 dk[2] = {zero16(), zero16()}, dv[2] = {zero16(), zero16()};
-  const int64_t sbase = ((int64_t)b * nh + h) * T_;
-  const int qstart = (kb * BLK / TILE) * TILE;
-  TileRegs qr, gr;
-  float lsv = 0.f, dsv = 0.f;
-  auto load = [&](int q0) {
-    tile_load(qr, base, ld, h * HS, q0, T_, tid);
-    tile_load(gr, gbase, d, h * HS, q0, T_, tid);
-    if (tid < TILE) {
-      const int qq = q0 + tid;
-      lsv = qq < T_ ? lse[sbase + qq] * 1.4426950408889634f : 0.f;
-      dsv = qq < T_ ? delta[sbase + qq] : 0.f;
+  const bool active = kw < T_;
+  for (int i = 0; i < nqt; ++i) {
+    if (i > 0) {
+      vm_wait<5 * (NB - 2)>();
+      raw_barrier();
     }
-  };
-  load(qstart);
-  for (int q0 = qstart; q0 < T_; q0 += TILE) {
-    const int bsel = ((q0 - qstart) / TILE) & 1;
-    char* Qs = QG + bsel * 2 * IMG;
-    char* Gs = Qs + IMG;
-    float* Ls = LD + bsel * 2 * TILE;
-    float* Ds = Ls + TILE;
-    tile_store(qr, Qs, tid);
-    tile_store(gr, Gs, tid);
-    if (tid < TILE) {
-      Ls[tid] = lsv;
-      Ds[tid] = dsv;
-    }
-    __syncthreads();
-    if (q0 + TILE < T_) load(q0 + TILE);
-    if (q0 + TILE - 1 < kw) continue;  // every query of the tile precedes this wave's keys
+    issue(i + NB - 1);
+    const int q0 = qstart + TILE * i;
+    if (!active || q0 + TILE - 1 < kw) continue;
+    const char* Qs = L + (i % NB) * DSLOT;
+    const char* Gs = Qs + IMG;
+    const float* Ls = reinterpret_cast<const float*>(Qs + 2 * IMG);
+    const float* Ds = Ls + TILE;
     const bool edge = (q0 < kw + WROWS - 1) || (q0 + TILE > T_);
 #pragma unroll
     for (int qs = 0; qs < 2; ++qs) {
@@ -394,7 +495,7 @@ __global__ __launch_bounds__(256, 2) void attn_dkv_mfma_kernel(const bf16* __res
       float Dv[16];
 #pragma unroll
       for (int g4 = 0; g4 < 4; ++g4) {
-        const int ql = 32 * qs + 8 * g4 + 4 * hf;  // first of this register group's 4 queries (tile-local)
+        const int ql = 32 * qs + 8 * g4 + 4 * hf;
         const float4 L4 = *reinterpret_cast<const float4*>(Ls + ql);
         const float4 D4 = *reinterpret_cast<const float4*>(Ds + ql);
         const float Lv[4] = {L4.x, L4.y, L4.z, L4.w};
@@ -403,18 +504,19 @@ __global__ __launch_bounds__(256, 2) void attn_dkv_mfma_kernel(const bf16* __res
         Dv[4 * g4 + 2] = D4.z;
         Dv[4 * g4 + 3] = D4.w;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) p[4 * g4 + e] = __builtin_amdgcn_exp2f(s[4 * g4 + e] * c2 - Lv[e]);
+        for (int e = 0; e < 4; ++e)
+          p[4 * g4 + e] = __builtin_amdgcn_exp2f(fmaf(s[4 * g4 + e], c2, -Lv[e] * 1.4426950408889634f));
       }
-      if (edge) {   // kept a real (wave-uniform) branch, as in the forward
+      if (edge) {
         asm volatile("" ::: "memory");
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int qq = q0 + 32 * qs + 8 * (i >> 2) + 4 * hf + (i & 3);
-          p[i] = (qq < key || qq >= T_) ? 0.f : p[i];
+        for (int e = 0; e < 16; ++e) {
+          const int qq = q0 + 32 * qs + 8 * (e >> 2) + 4 * hf + (e & 3);
+          p[e] = (qq < key || qq >= T_) ? 0.f : p[e];
         }
       }
 #pragma unroll
-      for (int i = 0; i < 16; ++i) s[i] = p[i] * (dp[i] - Dv[i]);
+      for (int e = 0; e < 16; ++e) s[e] = p[e] * (dp[e] - Dv[e]);
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) {
         const uint4 pb = pack8(p, s2), db = pack8(s, s2);
@@ -427,8 +529,9 @@ __global__ __launch_bounds__(256, 2) void attn_dkv_mfma_kernel(const bf16* __res
       }
     }
   }
+  vm_wait<0>();
   if (key < T_) {
-    bf16* out = dqkv + ((int64_t)b * T_ + key) * ld + h * HS;
+    bf16* out = dqkv + ((int64_t)b * T_ + key) * (3 * (int64_t)d) + h * HS;
 #pragma unroll
     for (int dt = 0; dt < 2; ++dt)
 #pragma unroll
@@ -443,8 +546,9 @@ __global__ __launch_bounds__(256, 2) void attn_dkv_mfma_kernel(const bf16* __res
 
 namespace aw {
 
-bool attn_mfma_supported(int dtype, int hs, int d) {
-  return dtype == AW_BF16 && hs == HS && d % 8 == 0;
+// The backward's LDS-DMA buffer offsets are 32-bit: one sequence of qkv rows must stay under 2 GiB.
+bool attn_mfma_supported(int dtype, int hs, int d, int64_t T) {
+  return dtype == AW_BF16 && hs == HS && d % 8 == 0 && T * 6 * (int64_t)d < (1ll << 31);
 }
 
 void attn_fwd_mfma(const void* qkv, int64_t B, int T, int nh, int d, void* y, float* lse, hipStream_t s) {
@@ -458,9 +562,9 @@ void attn_bwd_mfma(const void* qkv, const void* y, const void* dy, const float* 
                    int nh, int d, void* dqkv, hipStream_t s) {
   const float scale = 1.0f / sqrtf((float)HS);
   dim3 grid((unsigned)(((T + BLK - 1) / BLK) * (int64_t)nh * B));
-  hipLaunchKernelGGL(attn_dq_mfma_kernel, grid, dim3(256), 0, s, (const bf16*)qkv, (const bf16*)dy, (const bf16*)y,
+  hipLaunchKernelGGL(attn_dq_ring_kernel, grid, dim3(256), 0, s, (const bf16*)qkv, (const bf16*)dy, (const bf16*)y,
                      lse, delta, T, nh, d, (bf16*)dqkv, scale * 1.4426950408889634f, scale);
-  hipLaunchKernelGGL(attn_dkv_mfma_kernel, grid, dim3(256), 0, s, (const bf16*)qkv, (const bf16*)dy, lse, delta, T,
+  hipLaunchKernelGGL(attn_dkv_ring_kernel, grid, dim3(256), 0, s, (const bf16*)qkv, (const bf16*)dy, lse, delta, T,
                      nh, d, (bf16*)dqkv, scale * 1.4426950408889634f, scale);
 }
 

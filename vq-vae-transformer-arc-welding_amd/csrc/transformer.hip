@@ -7,7 +7,7 @@
 #include "common.h"
 
 namespace aw {  // attention.hip: MFMA path for bf16, head size 64
-bool attn_mfma_supported(int dtype, int hs, int d);
+bool attn_mfma_supported(int dtype, int hs, int d, int64_t T);
 void attn_fwd_mfma(const void* qkv, int64_t B, int T, int nh, int d, void* y, float* lse, hipStream_t s);
 void attn_bwd_mfma(const void* qkv, const void* y, const void* dy, const float* lse, float* delta, int64_t B, int T,
                    int nh, int d, void* dqkv, hipStream_t s);   // delta computed by its dQ launch
@@ -883,7 +883,7 @@ extern "C" int aw_attn_fwd_dropout(const void* qkv, int64_t B, int T, int n_head
   AW_REQUIRE(hs >= 1 && hs <= 128, "aw_attn_fwd: head size %d unsupported (1..128)", hs);
   if (B == 0) return AW_OK;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  if (drop_p == 0.f && aw::attn_mfma_supported(dtype, hs, d)) {
+  if (drop_p == 0.f && aw::attn_mfma_supported(dtype, hs, d, T)) {
     aw::attn_fwd_mfma(qkv, B, T, n_head, d, y, lse, s);
     return aw::check_launch("aw_attn_fwd");
   }
@@ -932,7 +932,7 @@ extern "C" int aw_attn_bwd_dropout(const void* qkv, const void* y, const void* d
   dim3 grid(aw_cdiv(T, ATT_ROWS), n_head, (unsigned)B);
   const float scale = 1.0f / sqrtf((float)hs);
   const int64_t nrows = B * n_head * T;
-  if (drop_p == 0.f && aw::attn_mfma_supported(dtype, hs, d)) {
+  if (drop_p == 0.f && aw::attn_mfma_supported(dtype, hs, d, T)) {
     aw::attn_bwd_mfma(qkv, y, dy, lse, ws, B, T, n_head, d, dqkv, s);
     return aw::check_launch("aw_attn_bwd");
   }
