@@ -1,0 +1,46 @@
+"""Un-patch head passes at the VQ-VAE bench shape (B = 1024: R = 81920 rows of H = 512, Q = 80 rows per window):
+time per call of head_fwd, head_bwd1 and head_bwd2, f32 and bf16 y.
+usage: python tools/probe/head_probe.py [iters]"""
+import sys
+
+import torch
+
+sys.path.insert(0, "vq-vae-transformer-arc-welding_amd")
+from arcweld import kernels as K  # noqa: E402
+
+R, H, Q = 81920, 512, 80
+
+
+def main(iters=20):
+    dev = "cuda"
+    g = torch.Generator(device=dev).manual_seed(0)
+    stats = torch.cat([torch.randn(H, device=dev, generator=g) * 0.1, torch.rand(H, device=dev, generator=g) + 0.5,
+                       torch.rand(H, device=dev, generator=g) + 0.5, torch.randn(H, device=dev, generator=g) * 0.1])
+    w2 = torch.randn(H * 5, device=dev, generator=g) * 0.05
+    b2 = torch.zeros(1, device=dev)
+    x_hat = torch.empty(R * 5, device=dev)
+    gx = torch.randn(R * 5, device=dev, generator=g)
+    gsums = torch.zeros(2 * H, device=dev, dtype=torch.float64)
+    gw2, gb2, ggam, gbet = (torch.zeros(5 * H, device=dev), torch.zeros(1, device=dev), torch.zeros(H, device=dev),
+                            torch.zeros(H, device=dev))
+    gy = torch.empty(R, H, device=dev, dtype=torch.bfloat16)
+    dby = torch.zeros(H, device=dev)
+    for ydt in (torch.float32, torch.bfloat16):
+        y = torch.randn(R, H, device=dev, generator=g).to(ydt)
+        for name, fn in (("fwd", lambda: K.unpatch_head_fwd(y, Q, stats, w2, b2, x_hat)),
+                         ("bwd1", lambda: K.unpatch_head_bwd1(y, Q, stats, w2, gx, gsums, gw2, gb2, ggam, gbet)),
+                         ("bwd2", lambda: K.unpatch_head_bwd2(y, Q, stats, w2, gx, gsums, 1, gy, dby))):
+            for _ in range(3):
+                fn()
+            torch.cuda.synchronize()
+            t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            t0.record()
+            for _ in range(iters):
+                fn()
+            t1.record()
+            torch.cuda.synchronize()
+            print(f"{name} y={str(ydt)[6:]}: {t0.elapsed_time(t1) / iters * 1e3:.1f} us", flush=True)
+
+
+if __name__ == "__main__":
+    main(int(sys.argv[1]) if len(sys.argv) > 1 else 20)

@@ -54,63 +54,69 @@ __device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + e
 __device__ __forceinline__ float gelu_erf_grad(float x) {
   return 0.5f * (1.0f + erff(x * AW_INV_SQRT2)) + x * AW_INV_SQRT2PI * __expf(-0.5f * x * x);
 }
-// Branch-free GELU(erf) for the bf16-operand paths and the un-patch head: erfc by the Chebyshev fit of Numerical
-// Recipes 6.2 (fractional error < 1.2e-7 everywhere), Phi(x) = erfc(-x/sqrt 2)/2 evaluated without cancellation
-// for x < 0; ~16 VALU ops against ~50 (with divergence) for erff.  The exact-f32 (parity / tokenization) GEMMs keep
-// erff so that the codebook indices stay bit-exact.
-__device__ __forceinline__ float aw_erfc_nr(float z) {   // z >= 0
-  const float t = __builtin_amdgcn_rcpf(1.0f + 0.5f * z);      // v_rcp_f32 (1 ulp), not the IEEE division
-  float p = 0.17087277f;
-  p = fmaf(p, t, -0.82215223f);
-  p = fmaf(p, t, 1.48851587f);
-  p = fmaf(p, t, -1.13520398f);
-  p = fmaf(p, t, 0.27886807f);
-  p = fmaf(p, t, -0.18628806f);
-  p = fmaf(p, t, 0.09678418f);
-  p = fmaf(p, t, 0.37409196f);
-  p = fmaf(p, t, 1.00002368f);
-  p = fmaf(p, t, -1.26551223f);
-  return t * __expf(fmaf(-z, z, p));
+// Branch-free GELU(erf) for the bf16-operand paths and the un-patch head.  Phi(x) = 1 - erfc(x / sqrt 2) / 2 by
+// Abramowitz & Stegun 7.1.26: erfc(z) = t (a1 + t (a2 + t (a3 + t (a4 + t a5)))) exp(-z^2), t = 1 / (1 + p z), z >= 0,
+// absolute error <= 1.5e-7 (so |Phi error| <= 7.5e-8).  One exponential serves both GELU and its derivative:
+// exp(-z^2) = exp(-x^2 / 2) = sqrt(2 pi) phi(x), so GELU'(x) = Phi(x) + x phi(x) costs one FMA more.  About 7 VALU
+// operations + rcp + exp per element, against 15 + rcp + 2 exp for the Numerical Recipes erfc (whose polynomial sat
+// inside its exponential, leaving a second exp for phi).  Phi = 1/2 + copysign(1/2 - erfc/2, x): one v_bfi_b32 in place
+// of a compare + select.  The exact-f32 (parity / tokenization) GEMMs keep erff so that the codebook indices stay
+// bit-exact.
+#define AW_AS_P 0.23164189758f          /* p / sqrt 2, p = 0.3275911 */
+#define AW_AS_B1 0.127414796f           /* a_i / 2 */
+#define AW_AS_B2 -0.142248368f
+#define AW_AS_B3 0.7107068705f
+#define AW_AS_B4 -0.7265760135f
+#define AW_AS_B5 0.5307027145f
+#define AW_NHALF_LOG2E -0.72134752044f  /* -log2(e) / 2 */
+__device__ __forceinline__ float aw_phi_e(float x, float& e) {   // Phi(x); e = exp(-x^2 / 2)
+  const float t = __builtin_amdgcn_rcpf(fmaf(fabsf(x), AW_AS_P, 1.0f));   // v_rcp_f32 (1 ulp)
+  float q = fmaf(t, AW_AS_B5, AW_AS_B4);
+  q = fmaf(q, t, AW_AS_B3);
+  q = fmaf(q, t, AW_AS_B2);
+  q = fmaf(q, t, AW_AS_B1);
+  e = __builtin_amdgcn_exp2f(x * (x * AW_NHALF_LOG2E));
+  const float r = (q * t) * e;   // erfc(|x| / sqrt 2) / 2
+  return 0.5f + copysignf(0.5f - r, x);
 }
 __device__ __forceinline__ float aw_phi_cdf(float x) {    // P(N(0,1) <= x) = 0.5 * (1 + erf(x / sqrt 2))
-  const float r = 0.5f * aw_erfc_nr(fabsf(x) * AW_INV_SQRT2);
-  return x >= 0.f ? 1.0f - r : r;
+  float e;
+  return aw_phi_e(x, e);
 }
 __device__ __forceinline__ float gelu_erf_fast(float x) { return x * aw_phi_cdf(x); }
 __device__ __forceinline__ float gelu_erf_grad_fast(float x) {
-  return aw_phi_cdf(x) + x * AW_INV_SQRT2PI * __expf(-0.5f * x * x);
+  float e;
+  const float phi = aw_phi_e(x, e);
+  return fmaf(x * AW_INV_SQRT2PI, e, phi);
 }
 
 // The same functions on a pair of values (the two channels a thread owns): the polynomial and the products run as
-// v_pk_fma_f32 / v_pk_mul_f32 (two values per instruction), only rcp / exp / the sign select stay scalar.  Same
+// v_pk_fma_f32 / v_pk_mul_f32 (two values per instruction), only rcp / exp / the sign insert stay scalar.  Same
 // operations in the same order per element as the scalar forms above (up to FMA contraction).
 __device__ __forceinline__ f32x2 aw_splat2(float c) { return (f32x2){c, c}; }
+__device__ __forceinline__ f32x2 aw_phi_e2(f32x2 x, f32x2& e) {
+  const f32x2 t = {__builtin_amdgcn_rcpf(fmaf(fabsf(x.x), AW_AS_P, 1.0f)),
+                   __builtin_amdgcn_rcpf(fmaf(fabsf(x.y), AW_AS_P, 1.0f))};
+  f32x2 q = __builtin_elementwise_fma(t, aw_splat2(AW_AS_B5), aw_splat2(AW_AS_B4));
+  q = __builtin_elementwise_fma(q, t, aw_splat2(AW_AS_B3));
+  q = __builtin_elementwise_fma(q, t, aw_splat2(AW_AS_B2));
+  q = __builtin_elementwise_fma(q, t, aw_splat2(AW_AS_B1));
+  const f32x2 a = x * (x * aw_splat2(AW_NHALF_LOG2E));
+  e = (f32x2){__builtin_amdgcn_exp2f(a.x), __builtin_amdgcn_exp2f(a.y)};
+  const f32x2 h = aw_splat2(0.5f) - (q * t) * e;
+  return aw_splat2(0.5f) + (f32x2){copysignf(h.x, x.x), copysignf(h.y, x.y)};
+}
 __device__ __forceinline__ f32x2 aw_phi_cdf2(f32x2 x) {
-  const f32x2 z = (f32x2){fabsf(x.x), fabsf(x.y)} * aw_splat2(AW_INV_SQRT2);
-  const f32x2 d = __builtin_elementwise_fma(aw_splat2(0.5f), z, aw_splat2(1.0f));
-  const f32x2 t = {__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
-  f32x2 p = aw_splat2(0.17087277f);
-  p = __builtin_elementwise_fma(p, t, aw_splat2(-0.82215223f));
-  p = __builtin_elementwise_fma(p, t, aw_splat2(1.48851587f));
-  p = __builtin_elementwise_fma(p, t, aw_splat2(-1.13520398f));
-  p = __builtin_elementwise_fma(p, t, aw_splat2(0.27886807f));
-  p = __builtin_elementwise_fma(p, t, aw_splat2(-0.18628806f));
-  p = __builtin_elementwise_fma(p, t, aw_splat2(0.09678418f));
-  p = __builtin_elementwise_fma(p, t, aw_splat2(0.37409196f));
-  p = __builtin_elementwise_fma(p, t, aw_splat2(1.00002368f));
-  p = __builtin_elementwise_fma(p, t, aw_splat2(-1.26551223f));
-  const f32x2 e = __builtin_elementwise_fma(-z, z, p);
-  const f32x2 r = aw_splat2(0.5f) * (t * (f32x2){__expf(e.x), __expf(e.y)});
-  const f32x2 q = aw_splat2(1.0f) - r;
-  return (f32x2){x.x >= 0.f ? q.x : r.x, x.y >= 0.f ? q.y : r.y};
+  f32x2 e;
+  return aw_phi_e2(x, e);
 }
 __device__ __forceinline__ f32x2 gelu_erf_fast2(f32x2 x) { return x * aw_phi_cdf2(x); }
-// GELU and its derivative from one Phi evaluation
+// GELU and its derivative from one Phi evaluation (one exponential per element)
 __device__ __forceinline__ void gelu_erf_fast2_and_grad(f32x2 x, f32x2& g, f32x2& dg) {
-  const f32x2 phi = aw_phi_cdf2(x);
-  const f32x2 h = aw_splat2(-0.5f) * x * x;
+  f32x2 e;
+  const f32x2 phi = aw_phi_e2(x, e);
   g = x * phi;
-  dg = __builtin_elementwise_fma(x * aw_splat2(AW_INV_SQRT2PI), (f32x2){__expf(h.x), __expf(h.y)}, phi);
+  dg = __builtin_elementwise_fma(x * aw_splat2(AW_INV_SQRT2PI), e, phi);
 }
 __device__ __forceinline__ f32x2 gelu_erf_grad_fast2(f32x2 x) {
   f32x2 g, dg;

@@ -509,7 +509,7 @@ struct Head2 {   // the two channels c0, c0+1 of a thread as register pairs
 // of look-ahead kept ~8 KB per CU in flight (1.9-3.3 TB/s); HEAD_CS_DEPTH rows are loaded ahead instead.
 constexpr int HEAD_CS_DEPTH = 2;
 
-template <typename TY>
+template <typename TY, bool UNI>
 __global__ __launch_bounds__(1024) void head_bwd1_cs_kernel(const TY* __restrict__ y, int64_t R, int H, int Q,
                                                            const float* __restrict__ st, const float* __restrict__ w2,
                                                            const float* __restrict__ gx, double* __restrict__ gsums,
@@ -519,7 +519,10 @@ __global__ __launch_bounds__(1024) void head_bwd1_cs_kernel(const TY* __restrict
   for (int i = threadIdx.x; i < 7 * H; i += blockDim.x) red[i] = 0.f;
   __syncthreads();
   const int tpr = H >> 1, rpb = blockDim.x / tpr;
-  const int c0 = (threadIdx.x % tpr) * 2, rg = threadIdx.x / tpr;
+  const int c0 = (threadIdx.x % tpr) * 2;
+  // UNI (H >= 128: a row spans whole waves): the row index is wave-uniform, so the row's five g_xhat values come
+  // by scalar loads instead of five broadcast vector loads per row and wave
+  const int rg = UNI ? __builtin_amdgcn_readfirstlane((int)(threadIdx.x / tpr)) : (int)(threadIdx.x / tpr);
   Head2 hp;
   hp.load(st, w2, H, c0);
   f32x2 accw[5], accg = aw_splat2(0.f), accgx = aw_splat2(0.f);
@@ -586,7 +589,7 @@ __global__ __launch_bounds__(1024) void head_bwd1_cs_kernel(const TY* __restrict
   }
 }
 
-template <typename T, typename TY>
+template <typename T, typename TY, bool UNI>
 __global__ __launch_bounds__(1024) void head_bwd2_cs_kernel(const TY* __restrict__ y, int64_t R, int H, int Q,
                                                            const float* __restrict__ st, const float* __restrict__ w2,
                                                            const float* __restrict__ gx,
@@ -596,7 +599,10 @@ __global__ __launch_bounds__(1024) void head_bwd2_cs_kernel(const TY* __restrict
   for (int i = threadIdx.x; i < H; i += blockDim.x) red[i] = 0.f;
   __syncthreads();
   const int tpr = H >> 1, rpb = blockDim.x / tpr;
-  const int c0 = (threadIdx.x % tpr) * 2, rg = threadIdx.x / tpr;
+  const int c0 = (threadIdx.x % tpr) * 2;
+  // UNI (H >= 128: a row spans whole waves): the row index is wave-uniform, so the row's five g_xhat values come
+  // by scalar loads instead of five broadcast vector loads per row and wave
+  const int rg = UNI ? __builtin_amdgcn_readfirstlane((int)(threadIdx.x / tpr)) : (int)(threadIdx.x / tpr);
   Head2 hp;
   hp.load(st, w2, H, c0);
   const float invn = 1.0f / (float)R;
@@ -864,12 +870,16 @@ extern "C" int aw_unpatch_head_bwd1_ex(const void* yv, int y_dtype, int64_t R, i
   const size_t sh = 7 * H * sizeof(float);
   if (head_cs_ok(H)) {
     const dim3 g1(grid_for(R * (H / 2), 1024, head_wgs()));
-    if (y_dtype == AW_BF16)
-      hipLaunchKernelGGL(head_bwd1_cs_kernel<bf16>, g1, dim3(1024), sh, s, (const bf16*)yv, R, H, Q, stats, w2, g_xhat,
-                         gsums, gw2, gb2, ggamma, gbeta);
-    else
-      hipLaunchKernelGGL(head_bwd1_cs_kernel<float>, g1, dim3(1024), sh, s, (const float*)yv, R, H, Q, stats, w2,
-                         g_xhat, gsums, gw2, gb2, ggamma, gbeta);
+#define AW_H1C(TY, UNI)                                                                                            \
+  hipLaunchKernelGGL((head_bwd1_cs_kernel<TY, UNI>), g1, dim3(1024), sh, s, (const TY*)yv, R, H, Q, stats, w2, g_xhat, \
+                     gsums, gw2, gb2, ggamma, gbeta)
+    const bool uni = H >= 128;
+    if (y_dtype == AW_BF16) {
+      if (uni) AW_H1C(bf16, true); else AW_H1C(bf16, false);
+    } else {
+      if (uni) AW_H1C(float, true); else AW_H1C(float, false);
+    }
+#undef AW_H1C
     return aw::check_launch("aw_unpatch_head_bwd1");
   }
   const float* y = (const float*)yv;
@@ -905,9 +915,15 @@ extern "C" int aw_unpatch_head_bwd2_ex(const void* yv, int y_dtype, int64_t R, i
   const size_t sh = H * sizeof(float);
   if (head_cs_ok(H)) {
     dim3 g2(grid_for(R * (H / 2), 1024, head_wgs()));
-#define AW_H2C(T, TY) \
-  hipLaunchKernelGGL((head_bwd2_cs_kernel<T, TY>), g2, dim3(1024), sh, s, (const TY*)yv, R, H, Q, stats, w2, g_xhat, \
-                     gsums, training, (T*)g_y, db_y)
+#define AW_H2C(T, TY)                                                                                               \
+  do {                                                                                                              \
+    if (H >= 128)                                                                                                   \
+      hipLaunchKernelGGL((head_bwd2_cs_kernel<T, TY, true>), g2, dim3(1024), sh, s, (const TY*)yv, R, H, Q, stats,  \
+                         w2, g_xhat, gsums, training, (T*)g_y, db_y);                                               \
+    else                                                                                                            \
+      hipLaunchKernelGGL((head_bwd2_cs_kernel<T, TY, false>), g2, dim3(1024), sh, s, (const TY*)yv, R, H, Q, stats, \
+                         w2, g_xhat, gsums, training, (T*)g_y, db_y);                                               \
+  } while (0)
     if (gy_dtype == AW_BF16) {
       if (y_dtype == AW_BF16) AW_H2C(bf16, bf16); else AW_H2C(bf16, float);
     } else {
