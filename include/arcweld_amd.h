@@ -227,6 +227,15 @@ int aw_unpatch_head_bwd1_ex(const void* y, int y_dtype, int64_t R, int H, int Q,
 int aw_unpatch_head_bwd2_ex(const void* y, int y_dtype, int64_t R, int H, int Q, const float* stats, const float* w2,
                             const float* g_xhat, const double* gsums, int training, void* g_y, int gy_dtype,
                             float* db_y, void* stream);
+/* Fused training-step form of the head forward and pass 1 (train_reconstruction_embedding.py's step: loss =
+ * mse(x_hat, x) + embedding loss, autencoder_lightning_base.py:80-97; vq_vae_patch_embedd.py:27-30,52-57), H == 512:
+ * one read of y computes x_hat (as aw_unpatch_head_fwd_ex), g_xhat = (2 / (R*5)) * gscale[0] * (x_hat - x) (as
+ * aw_mse_bwd), sqerr (f64, +=) = sum (x_hat - x)^2 (as aw_mse_fwd), and pass 1 of the backward from that g_xhat
+ * (as aw_unpatch_head_bwd1_ex: gsums, gw2, gb2, ggamma, gbeta).  x: the input windows, same layout as x_hat. */
+int aw_unpatch_head_fwd_bwd1(const void* y, int y_dtype, int64_t R, int H, int Q, const float* stats, const float* w2,
+                             const float* b2, const float* x, const float* gscale, float* x_hat, float* g_xhat,
+                             double* sqerr, double* gsums, float* gw2, float* gb2, float* ggamma, float* gbeta,
+                             void* stream);
 /* BatchNorm1d of the `--batchnorm 1` ResBlocks (model/vq_vae_patch_embedd.py:60-74).  Activations h are
  * [N rows][H channels] f32; statistics are per (group, channel), group = row % G (decoder G = 1; encoder G = S
  * token positions, each its own batch of B rows: CNNBlock(seperate=True) runs the blocks per token slice).

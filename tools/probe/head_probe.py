@@ -25,11 +25,17 @@ def main(iters=20):
                             torch.zeros(H, device=dev))
     gy = torch.empty(R, H, device=dev, dtype=torch.bfloat16)
     dby = torch.zeros(H, device=dev)
+    xin = torch.randn(R * 5, device=dev, generator=g)
+    gscale = torch.ones(1, device=dev)
+    sq = torch.zeros(1, device=dev, dtype=torch.float64)
     for ydt in (torch.float32, torch.bfloat16):
         y = torch.randn(R, H, device=dev, generator=g).to(ydt)
         for name, fn in (("fwd", lambda: K.unpatch_head_fwd(y, Q, stats, w2, b2, x_hat)),
                          ("bwd1", lambda: K.unpatch_head_bwd1(y, Q, stats, w2, gx, gsums, gw2, gb2, ggam, gbet)),
-                         ("bwd2", lambda: K.unpatch_head_bwd2(y, Q, stats, w2, gx, gsums, 1, gy, dby))):
+                         ("bwd2", lambda: K.unpatch_head_bwd2(y, Q, stats, w2, gx, gsums, 1, gy, dby)),
+                         ("fwd+bwd1 fused", lambda: K.unpatch_head_fwd_bwd1(y, Q, stats, w2.view(H, 5), b2, xin, gscale,
+                                                                            x_hat, gx, sq, gsums, gw2, gb2, ggam,
+                                                                            gbet))):
             for _ in range(3):
                 fn()
             torch.cuda.synchronize()

@@ -93,6 +93,8 @@ SIGNATURES = {
     "aw_unpatch_head_bwd2": [c_p, c_i64, c_int, c_int, c_p, c_p, c_p, c_p, c_int, c_p, c_int, c_p, c_p],
     "aw_unpatch_head_fwd_ex": [c_p, c_int, c_i64, c_int, c_int, c_p, c_p, c_p, c_p, c_p],
     "aw_unpatch_head_bwd1_ex": [c_p, c_int, c_i64, c_int, c_int, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p],
+    "aw_unpatch_head_fwd_bwd1": [c_p, c_int, c_i64, c_int, c_int, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p,
+                                 c_p, c_p, c_p, c_p],
     "aw_unpatch_head_bwd2_ex": [c_p, c_int, c_i64, c_int, c_int, c_p, c_p, c_p, c_p, c_int, c_p, c_int, c_p, c_p],
     "aw_bn_group_stats": [c_p, c_i64, c_int, c_int, c_p, c_p],
     "aw_bn_group_finalize": [c_p, c_i64, c_int, c_int, c_p, c_p, c_p, c_p, c_p, c_f, c_f, c_int, c_p, c_p],

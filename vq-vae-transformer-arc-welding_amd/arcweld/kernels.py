@@ -297,6 +297,15 @@ def unpatch_head_bwd2(y, Q, stats, w2, g_xhat, gsums, training, g_y, db_y, strea
          ptr(gsums), int(training), ptr(g_y), dtype_code(g_y.dtype), ptr(db_y), stream_ptr(stream))
 
 
+def unpatch_head_fwd_bwd1(y, Q, stats, w2, b2, x, gscale, x_hat, g_xhat, sqerr, gsums, gw2, gb2, ggamma, gbeta,
+                          stream=None):
+    """Fused training-step head: forward + MSE value / gradient + backward pass 1 in one read of y (H == 512)."""
+    R, H = y.shape
+    call("aw_unpatch_head_fwd_bwd1", ptr(y), dtype_code(y.dtype), R, H, Q, ptr(stats), ptr(w2), ptr(b2), ptr(x),
+         ptr(gscale), ptr(x_hat), ptr(g_xhat), ptr(sqerr), ptr(gsums), ptr(gw2), ptr(gb2), ptr(ggamma), ptr(gbeta),
+         stream_ptr(stream))
+
+
 def head_bf16_ok(H):
     """The head passes take a bf16 ConvT output when H is a power of two in 64..2048 (aw_unpatch_head_*_ex)."""
     return 64 <= H <= 2048 and H & (H - 1) == 0

@@ -243,8 +243,12 @@ def _bn_block_bwd(gy, x, a0, bs, w1d, w2d, Kd, dgemm_kw, wg, c1, c2, bns, G, tra
 # class-A launches per step, each launch otherwise waits for the previous one's end-of-kernel L2 write-back of up to
 # 32 MB of dirty output lines (same-box A/B: +3 % windows/s)
 @K.store_policy(nat.AW_STORE_WT)
-def forward(m, x, training: bool, need_backward: bool, dtype=None, seed: int = 0):
-    """Returns (emb_loss (), x_hat (B, L, C), perplexity (), indices (N,), saved-or-None)."""
+def forward(m, x, training: bool, need_backward: bool, dtype=None, seed: int = 0, head=True):
+    """Returns (emb_loss (), x_hat (B, L, C), perplexity (), indices (N,), saved-or-None).
+
+    ``head=False`` (the fused training step, need_backward only) stops after the BN statistics of the ConvT output:
+    x_hat is returned unwritten, and the caller runs the head forward fused with the loss gradient and the first
+    head-backward pass (``head_train``)."""
     T = operand_dtype(dtype)
     if x.dtype != F32 or x.dim() != 3:
         raise ValueError("VQVAEPatch expects float32 windows of shape (B, seq_len, input_dim)")
@@ -386,7 +390,9 @@ def forward(m, x, training: bool, need_backward: bool, dtype=None, seed: int = 0
                   bn.momentum if bn.momentum is not None else 0.1, training, stats)
     x_hat = e(sh.B, sh.L, sh.C)
     Y2 = Y.view(N * k1, H)
-    K.unpatch_head_fwd(Y2, sh.Q, stats, pr["t2"].weight.view(H, 5), pr["t2"].bias, x_hat)
+    sv.head_fused = not head and need_backward and fused_head_ok(H)
+    if not sv.head_fused:
+        K.unpatch_head_fwd(Y2, sh.Q, stats, pr["t2"].weight.view(H, 5), pr["t2"].bias, x_hat)
 
     if not need_backward:
         return emb_loss, x_hat, perplexity, idx, None
@@ -396,6 +402,25 @@ def forward(m, x, training: bool, need_backward: bool, dtype=None, seed: int = 0
     sv.Y2, sv.stats = Y2, stats
     sv.enc_w, sv.Ws, sv.Wd0, sv.Wt1 = enc_w, Ws, Wd0, Wt1
     return emb_loss, x_hat, perplexity, idx, sv
+
+
+def fused_head_ok(H):
+    """aw_unpatch_head_fwd_bwd1 serves H == 512 (the reference's hidden size)."""
+    return H == 512
+
+
+def head_train(m, sv, x, gscale, x_hat, sqerr, slot):
+    """Head forward + MSE value and gradient + head-backward pass 1 in one read of the ConvT output (the fused
+    training step; ``forward(..., head=False)`` left x_hat for it).  Returns g_xhat; ``backward`` then skips pass 1."""
+    sh, H = sv.sh, sv.sh.H
+    pr = _params(m)
+    bn = pr["bn"]
+    g_xhat = torch.empty_like(x_hat)
+    K.unpatch_head_fwd_bwd1(sv.Y2, sh.Q, sv.stats, pr["t2"].weight.view(H, 5), pr["t2"].bias, x, gscale, x_hat,
+                            g_xhat, sqerr, sv.head_gsums, slot(pr["t2"].weight).view(H, 5), slot(pr["t2"].bias),
+                            slot(bn.weight), slot(bn.bias))
+    sv.head_pass1_done = True
+    return g_xhat
 
 
 @torch.no_grad()
@@ -481,8 +506,9 @@ def backward(m, sv, g_emb, g_xhat, slot, mid_hook=None):
     owner = m.__dict__.get("_acc_owner")
     if owner is not None and owner() is sv:
         m.__dict__["_acc_owner"] = None
-    K.unpatch_head_bwd1(sv.Y2, sh.Q, sv.stats, pr["t2"].weight.view(H, 5), g_xhat, gsums,
-                        slot(pr["t2"].weight).view(H, 5), slot(pr["t2"].bias), slot(bn.weight), slot(bn.bias))
+    if not getattr(sv, "head_pass1_done", False):
+        K.unpatch_head_bwd1(sv.Y2, sh.Q, sv.stats, pr["t2"].weight.view(H, 5), g_xhat, gsums,
+                            slot(pr["t2"].weight).view(H, 5), slot(pr["t2"].bias), slot(bn.weight), slot(bn.bias))
     gY = e(N * k1, H, dt=T)
     K.unpatch_head_bwd2(sv.Y2, sh.Q, sv.stats, pr["t2"].weight.view(H, 5), g_xhat, gsums, sv.training, gY,
                         slot(pr["t1"].bias))

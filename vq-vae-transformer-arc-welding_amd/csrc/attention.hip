@@ -244,21 +244,9 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_mfma_kernel(const bf16* __res
 // double buffer: dQ + dK/dV 80.1 -> 76.5 us.  (The forward measured slower on the ring, 26.0 vs 23.2 us: at 80 KB of
 // LDS it runs two workgroups per CU instead of three, and with its loads alone -- no MFMA, no softmax -- the
 // register-staged forward already takes 19.7 us, so it is bound by the load pipeline, not by its depth.)
-typedef int v4i32 __attribute__((ext_vector_type(4)));
 constexpr int NB = 3;          // ring depth (tiles)
 constexpr int SLOT = 2 * IMG;  // one ring slot: two 64-row images
 
-__device__ __forceinline__ v4i32 rdesc(const char* base, uint32_t nbytes) {
-  const uint64_t p = (uint64_t)(uintptr_t)base;
-  return v4i32{(int)__builtin_amdgcn_readfirstlane((uint32_t)p),
-               (int)__builtin_amdgcn_readfirstlane((uint32_t)(p >> 32) & 0xFFFFu),
-               (int)__builtin_amdgcn_readfirstlane(nbytes), 0x00020000};
-}
-__device__ __forceinline__ void dma(uint32_t m0, int off, v4i32 desc) {
-  asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" ::"s"(m0), "v"(off), "s"(desc)
-               : "memory", "m0");
-}
-template <int N> __device__ __forceinline__ void vm_wait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
 __device__ __forceinline__ void raw_barrier() {
   __builtin_amdgcn_sched_barrier(0);
   __builtin_amdgcn_s_barrier();
@@ -268,14 +256,6 @@ __device__ __forceinline__ void raw_barrier() {
 __device__ __forceinline__ int piece_off(int jj, int lane, int ldb) {
   const int row = 8 * jj + (lane >> 3);
   return row * ldb + (((lane & 7) ^ swz(row)) << 4);
-}
-__device__ __forceinline__ uint32_t lds_addr(const char* p) {
-  return (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const char*)p;
-}
-
-__device__ __forceinline__ void dma_dword(uint32_t m0, int off, v4i32 desc) {
-  asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dword %1, %2, 0 offen lds" ::"s"(m0), "v"(off), "s"(desc)
-               : "memory", "m0");
 }
 __device__ __forceinline__ void lgkm_wait0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
@@ -297,7 +277,7 @@ __global__ __launch_bounds__(256, 2) void attn_dq_ring_kernel(const bf16* __rest
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int ldb = 6 * d, ldg = 2 * d;   // bytes per qkv / dy / y row
   const char* bbase = reinterpret_cast<const char*>(qkv) + (int64_t)b * T_ * ldb;
-  const uint32_t lring = lds_addr(L), lg = lring + NB * SLOT, ly = lg + 2 * IMG;
+  const uint32_t lring = aw_lds_addr(L), lg = lring + NB * SLOT, ly = lg + 2 * IMG;
   const int q0 = qb * BLK, qw = q0 + w * WROWS, q = qw + r;
   const int kend = min(T_, q0 + BLK);
   const int nt = (kend + TILE - 1) / TILE;
@@ -306,30 +286,30 @@ __global__ __launch_bounds__(256, 2) void attn_dq_ring_kernel(const bf16* __rest
 #pragma unroll
   for (int u = 0; u < 4; ++u) off[u] = piece_off(4 * (w & 1) + u, lane, ldb);
   {   // own rows of Q, dO, O
-    const v4i32 dq = rdesc(bbase + (int64_t)q0 * ldb + h * HS * 2, (uint32_t)(T_ - q0) * ldb);
+    const aw_v4i32 dq = aw_rdesc(bbase + (int64_t)q0 * ldb + h * HS * 2, (uint32_t)(T_ - q0) * ldb);
     const int64_t gro = ((int64_t)b * T_ + q0) * ldg + h * HS * 2;
-    const v4i32 dg = rdesc(reinterpret_cast<const char*>(dy) + gro, (uint32_t)(T_ - q0) * ldg);
-    const v4i32 dyv = rdesc(reinterpret_cast<const char*>(y) + gro, (uint32_t)(T_ - q0) * ldg);
+    const aw_v4i32 dg = aw_rdesc(reinterpret_cast<const char*>(dy) + gro, (uint32_t)(T_ - q0) * ldg);
+    const aw_v4i32 dyv = aw_rdesc(reinterpret_cast<const char*>(y) + gro, (uint32_t)(T_ - q0) * ldg);
     const uint32_t sq = lring + (NB - 1) * SLOT;
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const uint32_t o = (4 * w + u) * 1024;
-      dma(sq + o, piece_off(4 * w + u, lane, ldb), dq);
-      dma(lg + o, piece_off(4 * w + u, lane, ldg), dg);
-      dma(ly + o, piece_off(4 * w + u, lane, ldg), dyv);
+      aw_dma16(sq + o, piece_off(4 * w + u, lane, ldb), dq);
+      aw_dma16(lg + o, piece_off(4 * w + u, lane, ldg), dg);
+      aw_dma16(ly + o, piece_off(4 * w + u, lane, ldg), dyv);
     }
   }
   auto issue = [&](int t) {
     const int k0 = t * TILE;
     const uint32_t nrec = t < nt ? (uint32_t)(T_ - k0) * ldb : 0u;
-    const v4i32 ds = rdesc(bbase + (int64_t)k0 * ldb + ((1 + sel) * d + h * HS) * 2, nrec);
+    const aw_v4i32 ds = aw_rdesc(bbase + (int64_t)k0 * ldb + ((1 + sel) * d + h * HS) * 2, nrec);
     const uint32_t s = lring + (t % NB) * SLOT + 4096 * w;
 #pragma unroll
-    for (int u = 0; u < 4; ++u) dma(s + 1024 * u, off[u], ds);
+    for (int u = 0; u < 4; ++u) aw_dma16(s + 1024 * u, off[u], ds);
   };
 #pragma unroll
   for (int t = 0; t < NB - 1; ++t) issue(t);
-  vm_wait<4 * (NB - 2)>();
+  aw_vm_wait<4 * (NB - 2)>();
   raw_barrier();
   uint4 qf[4], gf[4];
   float Dl = 0.f;
@@ -355,7 +335,7 @@ __global__ __launch_bounds__(256, 2) void attn_dq_ring_kernel(const bf16* __rest
   const bool active = qw < T_;
   for (int t = 0; t < nt; ++t) {
     if (t > 0) {
-      vm_wait<4 * (NB - 2)>();
+      aw_vm_wait<4 * (NB - 2)>();
       raw_barrier();
     }
     issue(t + NB - 1);
@@ -390,7 +370,7 @@ __global__ __launch_bounds__(256, 2) void attn_dq_ring_kernel(const bf16* __rest
       }
     }
   }
-  vm_wait<0>();
+  aw_vm_wait<0>();
   if (q < T_) {
     if (hf == 0) delta[st_i] = Dl;
     bf16* out = dqkv + ((int64_t)b * T_ + q) * (3 * (int64_t)d) + h * HS;
@@ -420,7 +400,7 @@ __global__ __launch_bounds__(256, 2) void attn_dkv_ring_kernel(const bf16* __res
   const int ldb = 6 * d, ldg = 2 * d;
   const char* bbase = reinterpret_cast<const char*>(qkv) + (int64_t)b * T_ * ldb;
   const char* gbase = reinterpret_cast<const char*>(dy) + (int64_t)b * T_ * ldg;
-  const uint32_t lring = lds_addr(L), lv = lring + NB * DSLOT;
+  const uint32_t lring = aw_lds_addr(L), lv = lring + NB * DSLOT;
   const int k0b = kb * BLK, kw = k0b + w * WROWS, key = kw + r;
   const int qstart = k0b;   // BLK is a multiple of TILE
   const int nqt = (T_ - qstart + TILE - 1) / TILE;
@@ -432,30 +412,30 @@ __global__ __launch_bounds__(256, 2) void attn_dkv_ring_kernel(const bf16* __res
   const int64_t sbase = ((int64_t)b * nh + h) * T_;
   const float* vec = (w & 1) ? delta : lse;
   {   // own rows of K (into slot NB - 1) and V
-    const v4i32 dk = rdesc(bbase + (int64_t)k0b * ldb + (d + h * HS) * 2, (uint32_t)(T_ - k0b) * ldb);
-    const v4i32 dv = rdesc(bbase + (int64_t)k0b * ldb + (2 * d + h * HS) * 2, (uint32_t)(T_ - k0b) * ldb);
+    const aw_v4i32 dk = aw_rdesc(bbase + (int64_t)k0b * ldb + (d + h * HS) * 2, (uint32_t)(T_ - k0b) * ldb);
+    const aw_v4i32 dv = aw_rdesc(bbase + (int64_t)k0b * ldb + (2 * d + h * HS) * 2, (uint32_t)(T_ - k0b) * ldb);
     const uint32_t sk = lring + (NB - 1) * DSLOT;
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const uint32_t o = (4 * w + u) * 1024;
-      dma(sk + o, piece_off(4 * w + u, lane, ldb), dk);
-      dma(lv + o, piece_off(4 * w + u, lane, ldb), dv);
+      aw_dma16(sk + o, piece_off(4 * w + u, lane, ldb), dk);
+      aw_dma16(lv + o, piece_off(4 * w + u, lane, ldb), dv);
     }
   }
   auto issue = [&](int i) {
     const int q0 = qstart + TILE * i;
     const bool valid = i < nqt;
     const char* src = sel ? gbase + (int64_t)q0 * ldg + h * HS * 2 : bbase + (int64_t)q0 * ldb + h * HS * 2;
-    const v4i32 ds = rdesc(src, valid ? (uint32_t)(T_ - q0) * lds_src : 0u);
-    const v4i32 dvv = rdesc(reinterpret_cast<const char*>(vec + sbase + q0), valid ? (uint32_t)(T_ - q0) * 4 : 0u);
+    const aw_v4i32 ds = aw_rdesc(src, valid ? (uint32_t)(T_ - q0) * lds_src : 0u);
+    const aw_v4i32 dvv = aw_rdesc(reinterpret_cast<const char*>(vec + sbase + q0), valid ? (uint32_t)(T_ - q0) * 4 : 0u);
     const uint32_t s = lring + (i % NB) * DSLOT;
 #pragma unroll
-    for (int u = 0; u < 4; ++u) dma(s + 4096 * w + 1024 * u, off[u], ds);
-    dma_dword(s + 2 * IMG + (w & 1) * (TILE * 4), lane * 4, dvv);
+    for (int u = 0; u < 4; ++u) aw_dma16(s + 4096 * w + 1024 * u, off[u], ds);
+    aw_dma4(s + 2 * IMG + (w & 1) * (TILE * 4), lane * 4, dvv);
   };
 #pragma unroll
   for (int i = 0; i < NB - 1; ++i) issue(i);
-  vm_wait<5 * (NB - 2)>();
+  aw_vm_wait<5 * (NB - 2)>();
   raw_barrier();
   uint4 kf[4], vf[4];
   {
@@ -472,7 +452,7 @@ __global__ __launch_bounds__(256, 2) void attn_dkv_ring_kernel(const bf16* __res
   const bool active = kw < T_;
   for (int i = 0; i < nqt; ++i) {
     if (i > 0) {
-      vm_wait<5 * (NB - 2)>();
+      aw_vm_wait<5 * (NB - 2)>();
       raw_barrier();
     }
     issue(i + NB - 1);
@@ -529,7 +509,7 @@ __global__ __launch_bounds__(256, 2) void attn_dkv_ring_kernel(const bf16* __res
       }
     }
   }
-  vm_wait<0>();
+  aw_vm_wait<0>();
   if (key < T_) {
     bf16* out = dqkv + ((int64_t)b * T_ + key) * (3 * (int64_t)d) + h * HS;
 #pragma unroll

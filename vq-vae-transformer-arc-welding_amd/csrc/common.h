@@ -30,6 +30,33 @@ __device__ __forceinline__ void aw_st_wt(void* p, uint32_t v) {
 }
 typedef __bf16 bf16;
 
+// ---------------------------------------------------------------- LDS-DMA (gfx950 buffer_load ... lds)
+// Lane l of one wave-instruction writes its 16 (dwordx4) or 4 (dword) bytes at M0 + 16 l / M0 + 4 l; the source is a
+// raw buffer whose range check returns zeros past nbytes (every mask and tail).  The inline asm is invisible to the
+// compiler's wait-count tracking: callers retire the loads with aw_vm_wait (a counted or a full vmcnt).
+// (The asm writes M0, declared clobbered; no compiler-generated code in these kernels uses M0, so the "reserved
+// register" warning is silenced.)
+#pragma clang diagnostic ignored "-Winline-asm"
+typedef int aw_v4i32 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ aw_v4i32 aw_rdesc(const void* base, uint32_t nbytes) {
+  const uint64_t p = (uint64_t)(uintptr_t)base;
+  return aw_v4i32{(int)__builtin_amdgcn_readfirstlane((uint32_t)p),
+                  (int)__builtin_amdgcn_readfirstlane((uint32_t)(p >> 32) & 0xFFFFu),
+                  (int)__builtin_amdgcn_readfirstlane(nbytes), 0x00020000};
+}
+__device__ __forceinline__ void aw_dma16(uint32_t m0, int off, aw_v4i32 desc) {
+  asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" ::"s"(m0), "v"(off), "s"(desc)
+               : "memory", "m0");
+}
+__device__ __forceinline__ void aw_dma4(uint32_t m0, int off, aw_v4i32 desc) {
+  asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dword %1, %2, 0 offen lds" ::"s"(m0), "v"(off), "s"(desc)
+               : "memory", "m0");
+}
+template <int N> __device__ __forceinline__ void aw_vm_wait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+__device__ __forceinline__ uint32_t aw_lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const char*)p;
+}
+
 // ---------------------------------------------------------------- error plumbing (host side)
 namespace aw {
 void set_error(const char* fmt, ...);

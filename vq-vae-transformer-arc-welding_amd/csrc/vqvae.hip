@@ -2,6 +2,7 @@
 // VQ-VAE-Patch layout and un-patch head kernels (model/vq_vae_patch_embedd.py) for gfx950.
 // HBM-bound byte/elementwise work: coalesced float4 traffic, one wave per row where a row reduction is needed.
 #include "common.h"
+#include <algorithm>
 
 namespace {
 
@@ -665,6 +666,386 @@ __global__ __launch_bounds__(1024) void head_bwd2_cs_kernel(const TY* __restrict
   for (int o = threadIdx.x; o < H; o += blockDim.x) atomicAdd(dby + o, red[o]);
 }
 
+// ---------------------------------------------------------------- fused head forward + pass 1 (training step)
+// The training step's loss is mse(x_hat, x) + the embedding loss (autencoder_lightning_base.py:80-97), so a row's
+// gradient g_xhat = c (x_hat - x) (c = 2 / numel * loss scale: aw_mse_bwd's formula) is known the moment its x_hat
+// is: one pass over y computes the forward (BN -> GELU -> ConvT2), the MSE sum and gradient, and pass 1's sums and
+// gradients (aw_unpatch_head_bwd1), from one Phi / exp per element -- y is read once instead of twice.
+// H = 512.  One wave per row; lane l owns 8 channels: f32 y -> 4l..4l+3 and 256+4l..+3 (the two 1-KiB halves of a
+// 2-KiB row), bf16 y -> 8l..8l+7 (one 1-KiB row).  Rows reach the wave's OWN slice of LDS by LDS-DMA in batches of
+// HB rows through a ring of three batches (two in flight while one computes), without VGPRs held by loads and
+// without barriers (nothing is shared between waves until the final per-channel reduction).  The x row (5 floats)
+// comes the same way.
+constexpr int HB = 4;          // rows per wave below which the grid shrinks
+constexpr int HFW = 8;         // waves per workgroup (one workgroup per CU: its per-channel atomics end the launch)
+template <typename TY> struct HeadRows {
+  static constexpr int ROWB = 512 * (int)sizeof(TY);   // bytes per y row
+  static constexpr int NP = ROWB / 1024;                // 1-KiB DMA pieces per row
+  static constexpr int XB = 32;                         // bytes per x slot (5 floats used)
+  static constexpr int HB = sizeof(TY) == 4 ? 2 : 4;    // rows per batch (even: the fused pass takes them in pairs)
+  static constexpr int PB = HB * (NP + 1);              // DMA instructions per batch and wave
+  static constexpr int NBUF = 3;                        // batches in the wave's ring (two in flight)
+  static constexpr int BATCH = HB * (ROWB + XB);
+  static constexpr int WAVE = NBUF * BATCH;
+  static constexpr int NG = sizeof(TY) == 4 ? 4 : 8;   // channels of a lane that are contiguous in a row
+  __device__ static int chan(int lane, int k) {
+    return sizeof(TY) == 4 ? (k < 4 ? 4 * lane + k : 256 + 4 * lane + k - 4) : 8 * lane + k;
+  }
+  __device__ static void row(const char* p, int lane, float (&v)[8]) {   // this lane's 8 channels of an LDS row
+    if constexpr (sizeof(TY) == 4) {
+      const float4 a = *reinterpret_cast<const float4*>(p + 16 * lane);
+      const float4 b = *reinterpret_cast<const float4*>(p + 1024 + 16 * lane);
+      v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+    } else {
+      const uint4 u = *reinterpret_cast<const uint4*>(p + 16 * lane);
+      const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        v[2 * i] = __uint_as_float(w[i] << 16);
+        v[2 * i + 1] = __uint_as_float(w[i] & 0xFFFF0000u);
+      }
+    }
+  }
+};
+
+template <typename TY>
+__global__ __launch_bounds__(64 * HFW, 1) void head_fwd_bwd1_kernel(
+    const TY* __restrict__ y, int64_t R, const float* __restrict__ st, const float* __restrict__ w2,
+    const float* __restrict__ b2, const float* __restrict__ x, const float* __restrict__ gscale, float gmul,
+    float* __restrict__ x_hat, float* __restrict__ g_xhat, double* __restrict__ sqerr, double* __restrict__ gsums,
+    float* __restrict__ gw2, float* __restrict__ gb2, float* __restrict__ ggamma, float* __restrict__ gbeta) {
+  using HR = HeadRows<TY>;
+  constexpr int H = 512;
+  // the waves' row buffers; after the row loop, their per-channel partial sums [wave][7H] (gw2 5H, sum g, sum g*xhat)
+  constexpr int LB = HFW * HR::WAVE > HFW * 7 * H * 4 ? HFW * HR::WAVE : HFW * 7 * H * 4;
+  __shared__ __attribute__((aligned(16))) char L[LB];
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int64_t wave = (int64_t)blockIdx.x * HFW + wv, nw = (int64_t)gridDim.x * HFW;
+  const char* Lw = L + wv * HR::WAVE;
+  const uint32_t lw = aw_lds_addr(Lw);
+  const aw_v4i32 dy = aw_rdesc(y, (uint32_t)(R * HR::ROWB));
+  const aw_v4i32 dx = aw_rdesc(x, (uint32_t)(R * 20));
+  auto issue = [&](int64_t bt) {   // batch bt of this wave's rows into buffer bt % NBUF; rows past R load zeros
+    const uint32_t base = lw + (uint32_t)((bt % HR::NBUF) * HR::BATCH);
+#pragma unroll
+    for (int k = 0; k < HR::HB; ++k) {
+      const int64_t r0 = wave + (bt * HR::HB + k) * nw;
+      const int r = (int)(r0 < R ? r0 : R);
+#pragma unroll
+      for (int pc = 0; pc < HR::NP; ++pc) aw_dma16(base + k * HR::ROWB + pc * 1024, r * HR::ROWB + pc * 1024 + 16 * lane, dy);
+      if (lane < 5) aw_dma4(base + HR::HB * HR::ROWB + k * HR::XB, r * 20 + 4 * lane, dx);
+    }
+  };
+  // per-channel state as pairs (channels chan(2p), chan(2p+1)): xn = v * inv + c, bn = xn * gam + bet
+  f32x2 inv[4], cc[4], gam[4], bet[4], w[4][5];
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const int o0 = HR::chan(lane, 2 * p), o1 = HR::chan(lane, 2 * p + 1);
+    inv[p] = (f32x2){st[H + o0], st[H + o1]};
+    cc[p] = -(f32x2){st[o0], st[o1]} * inv[p];
+    gam[p] = (f32x2){st[2 * H + o0], st[2 * H + o1]};
+    bet[p] = (f32x2){st[3 * H + o0], st[3 * H + o1]};
+#pragma unroll
+    for (int j = 0; j < 5; ++j) w[p][j] = (f32x2){w2[o0 * 5 + j], w2[o1 * 5 + j]};
+  }
+  f32x2 accw[4][5], accg[4], accgx[4];
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    accg[p] = accgx[p] = aw_splat2(0.f);
+#pragma unroll
+    for (int j = 0; j < 5; ++j) accw[p][j] = aw_splat2(0.f);
+  }
+  const float c = gmul * gscale[0];
+  const float bias = b2[0];
+  double sq = 0.0;
+  float gbs = 0.f;
+  const int64_t nrows = wave < R ? (R - 1 - wave) / nw + 1 : 0;
+  const int64_t nb = (nrows + HR::HB - 1) / HR::HB;
+  // a batch's x_hat / g_xhat values are stored right after the NEXT batch's wait: the wait covers stores too (vmcnt),
+  // and stored at once they would expose their write latency at every batch
+  float hx[HR::HB], hg[HR::HB];
+  int64_t hb = -1;   // batch whose values are held
+  auto flush = [&]() {
+    if (hb < 0) return;
+#pragma unroll
+    for (int k = 0; k < HR::HB; ++k) {
+      const int64_t r = wave + (hb * HR::HB + k) * nw;
+      if (r < R && lane < 5) {   // row r = b*Q + q -> x_hat[b][5q + j]
+        x_hat[r * 5 + lane] = hx[k];
+        g_xhat[r * 5 + lane] = hg[k];
+      }
+    }
+    hb = -1;
+  };
+  // counted waits: loads retire in order, so vmcnt <= PB (the newest batch) means batch bt has landed; the few stores
+  // between them only make the wait longer, never shorter
+  if (nb > 0) issue(0);
+  if (nb > 1) issue(1);
+  for (int64_t bt = 0; bt < nb; ++bt) {
+    if (bt + 1 < nb)
+      aw_vm_wait<HR::PB>();
+    else
+      aw_vm_wait<0>();
+    flush();
+    if (bt + 2 < nb) issue(bt + 2);
+    hb = bt;
+    const char* Lb = Lw + (bt % HR::NBUF) * HR::BATCH;
+    // two rows at a time: their forward halves, their 10 wave reductions and their backward halves interleave
+    // (at two waves per SIMD one row alone left the VALU waiting on its own dependency chains)
+#pragma unroll
+    for (int k0 = 0; k0 < HR::HB; k0 += 2) {
+      const int64_t r0 = wave + (bt * HR::HB + k0) * nw;
+      if (r0 >= R) break;   // wave-uniform
+      const bool two = r0 + nw < R;
+      f32x2 a[2][4], dg[2][4], xn[2][4];
+      float part[2][5];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        float v[8];
+        HR::row(Lb + (k0 + u) * HR::ROWB, lane, v);
+        f32x2 pj[5];
+#pragma unroll
+        for (int j = 0; j < 5; ++j) pj[j] = aw_splat2(0.f);
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+          xn[u][p] = __builtin_elementwise_fma((f32x2){v[2 * p], v[2 * p + 1]}, inv[p], cc[p]);
+          const f32x2 bn = __builtin_elementwise_fma(xn[u][p], gam[p], bet[p]);
+          f32x2 e;
+          const f32x2 phi = aw_phi_e2(bn, e);
+          a[u][p] = bn * phi;
+          dg[u][p] = __builtin_elementwise_fma(bn * aw_splat2(AW_INV_SQRT2PI), e, phi);
+#pragma unroll
+          for (int j = 0; j < 5; ++j) pj[j] = __builtin_elementwise_fma(a[u][p], w[p][j], pj[j]);
+        }
+#pragma unroll
+        for (int j = 0; j < 5; ++j) part[u][j] = pj[j].x + pj[j].y;
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int j = 0; j < 5; ++j) part[u][j] = wave_sum_to_last(part[u][j]);
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        if (u == 1 && !two) break;   // wave-uniform
+        const float* xs = reinterpret_cast<const float*>(Lb + HR::HB * HR::ROWB + (k0 + u) * HR::XB);
+        float go[5], xo = 0.f, gsel = 0.f, d2 = 0.f, gsum = 0.f;
+#pragma unroll
+        for (int j = 0; j < 5; ++j) {
+          const float xh = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(part[u][j]), 63)) + bias;
+          const float d = xh - xs[j];
+          go[j] = c * d;
+          d2 = fmaf(d, d, d2);
+          gsum += go[j];
+          if (lane == j) {
+            xo = xh;
+            gsel = go[j];
+          }
+        }
+        hx[k0 + u] = xo;
+        hg[k0 + u] = gsel;
+        sq += (double)d2;
+        gbs += gsum;
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+          f32x2 ga = aw_splat2(0.f);
+#pragma unroll
+          for (int j = 0; j < 5; ++j) {
+            ga = __builtin_elementwise_fma(aw_splat2(go[j]), w[p][j], ga);
+            accw[p][j] = __builtin_elementwise_fma(a[u][p], aw_splat2(go[j]), accw[p][j]);
+          }
+          const f32x2 gbn = ga * dg[u][p];
+          accg[p] += gbn;
+          accgx[p] = __builtin_elementwise_fma(gbn, xn[u][p], accgx[p]);
+        }
+      }
+    }
+  }
+  flush();
+  aw_vm_wait<0>();   // every DMA of this wave has landed before its buffer is reused (or the LDS released)
+  __syncthreads();
+  // per-channel sums: each wave writes its partials, then every entry is summed over the waves in fixed order and
+  // added to the gradients with one global atomic per workgroup (LDS atomics from 8 waves on the same channels
+  // measured 22 us of the 106 us launch)
+  float* part = reinterpret_cast<float*>(L);
+  float* mine = part + wv * 7 * H;
+#pragma unroll
+  for (int p = 0; p < 4; ++p)
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int o = HR::chan(lane, 2 * p + e);
+#pragma unroll
+      for (int j = 0; j < 5; ++j) mine[o * 5 + j] = accw[p][j][e];
+      mine[5 * H + o] = accg[p][e];
+      mine[6 * H + o] = accgx[p][e];
+    }
+  if (lane == 0) {
+    atomicAdd(gb2, gbs);
+    atomicAdd(sqerr, sq);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 7 * H; i += 64 * HFW) {
+    float t = 0.f;
+#pragma unroll
+    for (int q = 0; q < HFW; ++q) t += part[q * 7 * H + i];
+    if (i < 5 * H) {
+      atomicAdd(gw2 + i, t);
+    } else if (i < 6 * H) {
+      atomicAdd(gsums + (i - 5 * H), (double)t);
+      if (gbeta) atomicAdd(gbeta + (i - 5 * H), t);
+    } else {
+      atomicAdd(gsums + (i - 5 * H), (double)t);
+      if (ggamma) atomicAdd(ggamma + (i - 6 * H), t);
+    }
+  }
+}
+
+// Pass 2 on the same row stream (H = 512): g_y = BN backward of g * gelu'(bn) per row, its channel sums db_y.  The
+// row's five g_xhat values come by LDS-DMA beside its y row.
+template <typename T, typename TY>
+__global__ __launch_bounds__(64 * HFW, 1) void head_bwd2_rows_kernel(const TY* __restrict__ y, int64_t R,
+                                                                    const float* __restrict__ st,
+                                                                    const float* __restrict__ w2,
+                                                                    const float* __restrict__ gx,
+                                                                    const double* __restrict__ gsums, int training,
+                                                                    T* __restrict__ gy, float* __restrict__ dby) {
+  using HR = HeadRows<TY>;
+  constexpr int H = 512;
+  __shared__ __attribute__((aligned(16))) char L[HFW * HR::WAVE];   // row buffers, then the partial sums [wave][H]
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int64_t wave = (int64_t)blockIdx.x * HFW + wv, nw = (int64_t)gridDim.x * HFW;
+  const char* Lw = L + wv * HR::WAVE;
+  const uint32_t lw = aw_lds_addr(Lw);
+  const aw_v4i32 dy = aw_rdesc(y, (uint32_t)(R * HR::ROWB));
+  const aw_v4i32 dg = aw_rdesc(gx, (uint32_t)(R * 20));
+  auto issue = [&](int64_t bt) {
+    const uint32_t base = lw + (uint32_t)((bt % HR::NBUF) * HR::BATCH);
+#pragma unroll
+    for (int k = 0; k < HR::HB; ++k) {
+      const int64_t r0 = wave + (bt * HR::HB + k) * nw;
+      const int r = (int)(r0 < R ? r0 : R);
+#pragma unroll
+      for (int pc = 0; pc < HR::NP; ++pc) aw_dma16(base + k * HR::ROWB + pc * 1024, r * HR::ROWB + pc * 1024 + 16 * lane, dy);
+      if (lane < 5) aw_dma4(base + HR::HB * HR::ROWB + k * HR::XB, r * 20 + 4 * lane, dg);
+    }
+  };
+  const float invn = 1.0f / (float)R;
+  f32x2 inv[4], cc[4], gam[4], bet[4], P[4], sg[4], sgx[4], w[4][5], accd[4];
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const int o0 = HR::chan(lane, 2 * p), o1 = HR::chan(lane, 2 * p + 1);
+    inv[p] = (f32x2){st[H + o0], st[H + o1]};
+    cc[p] = -(f32x2){st[o0], st[o1]} * inv[p];
+    gam[p] = (f32x2){st[2 * H + o0], st[2 * H + o1]};
+    bet[p] = (f32x2){st[3 * H + o0], st[3 * H + o1]};
+    P[p] = gam[p] * inv[p];
+    sg[p] = training ? (f32x2){(float)gsums[o0], (float)gsums[o1]} * aw_splat2(invn) : aw_splat2(0.f);
+    sgx[p] = training ? (f32x2){(float)gsums[H + o0], (float)gsums[H + o1]} * aw_splat2(invn) : aw_splat2(0.f);
+    accd[p] = aw_splat2(0.f);
+#pragma unroll
+    for (int j = 0; j < 5; ++j) w[p][j] = (f32x2){w2[o0 * 5 + j], w2[o1 * 5 + j]};
+  }
+  const int64_t nrows = wave < R ? (R - 1 - wave) / nw + 1 : 0;
+  const int64_t nb = (nrows + HR::HB - 1) / HR::HB;
+  // a batch's g_y rows are stored right after the NEXT batch's wait (the wait covers stores too)
+  float hold[HR::HB][8];
+  int64_t hb = -1;
+  auto flush = [&]() {
+    if (hb < 0) return;
+#pragma unroll
+    for (int k = 0; k < HR::HB; ++k) {
+      const int64_t r = wave + (hb * HR::HB + k) * nw;
+      if (r >= R) break;
+      const float* out = hold[k];
+      // this lane's channels: f32 y -> 4l.. and 256+4l.. (two groups of 4), bf16 y -> 8l.. (one group of 8)
+      T* dst = gy + r * H;
+#pragma unroll
+      for (int q = 0; q < 8 / HR::NG; ++q) {
+        const int o = HR::chan(lane, q * HR::NG);
+        if constexpr (sizeof(T) == 2) {
+          if constexpr (HR::NG == 4) {
+            bf16 h[4] = {(bf16)out[4 * q], (bf16)out[4 * q + 1], (bf16)out[4 * q + 2], (bf16)out[4 * q + 3]};
+            u32x2 u;
+            memcpy(&u, h, 8);
+            aw_st_wt(dst + o, u);
+          } else {
+            bf16 h[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) h[i] = (bf16)out[i];
+            f32x4 u;
+            memcpy(&u, h, 16);
+            aw_st_wt(dst + o, u);
+          }
+        } else {
+#pragma unroll
+          for (int i = 0; i < HR::NG; i += 4)
+            aw_st_wt(dst + o + i, (f32x4){out[q * HR::NG + i], out[q * HR::NG + i + 1], out[q * HR::NG + i + 2],
+                                          out[q * HR::NG + i + 3]});
+        }
+      }
+    }
+    hb = -1;
+  };
+  // counted waits: loads retire in order, so vmcnt <= PB (the newest batch) means batch bt has landed; the few stores
+  // between them only make the wait longer, never shorter
+  if (nb > 0) issue(0);
+  if (nb > 1) issue(1);
+  for (int64_t bt = 0; bt < nb; ++bt) {
+    if (bt + 1 < nb)
+      aw_vm_wait<HR::PB>();
+    else
+      aw_vm_wait<0>();
+    flush();
+    if (bt + 2 < nb) issue(bt + 2);
+    hb = bt;
+    const char* Lb = Lw + (bt % HR::NBUF) * HR::BATCH;
+#pragma unroll
+    for (int k = 0; k < HR::HB; ++k) {
+      const int64_t r = wave + (bt * HR::HB + k) * nw;
+      if (r >= R) break;   // wave-uniform
+      float v[8];
+      HR::row(Lb + k * HR::ROWB, lane, v);
+      const float* gs = reinterpret_cast<const float*>(Lb + HR::HB * HR::ROWB + k * HR::XB);
+      float go[5];
+#pragma unroll
+      for (int j = 0; j < 5; ++j) go[j] = gs[j];
+      float* out = hold[k];
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        const f32x2 xn = __builtin_elementwise_fma((f32x2){v[2 * p], v[2 * p + 1]}, inv[p], cc[p]);
+        const f32x2 bn = __builtin_elementwise_fma(xn, gam[p], bet[p]);
+        f32x2 e;
+        const f32x2 phi = aw_phi_e2(bn, e);
+        const f32x2 d = __builtin_elementwise_fma(bn * aw_splat2(AW_INV_SQRT2PI), e, phi);
+        f32x2 ga = aw_splat2(0.f);
+#pragma unroll
+        for (int j = 0; j < 5; ++j) ga = __builtin_elementwise_fma(aw_splat2(go[j]), w[p][j], ga);
+        const f32x2 g = P[p] * (ga * d - __builtin_elementwise_fma(xn, sgx[p], sg[p]));
+        accd[p] += g;
+        out[2 * p] = g.x;
+        out[2 * p + 1] = g.y;
+      }
+    }
+  }
+  flush();
+  aw_vm_wait<0>();
+  __syncthreads();
+  float* part = reinterpret_cast<float*>(L);
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    part[wv * H + HR::chan(lane, 2 * p)] = accd[p].x;
+    part[wv * H + HR::chan(lane, 2 * p + 1)] = accd[p].y;
+  }
+  __syncthreads();
+  for (int o = threadIdx.x; o < H; o += 64 * HFW) {
+    float t = 0.f;
+#pragma unroll
+    for (int q = 0; q < HFW; ++q) t += part[q * H + o];
+    atomicAdd(dby + o, t);
+  }
+}
+
 // n4 float4 groups (0 when a or b is not 16-B aligned) then the scalar tail.  Four float4 loads of each input in
 // flight per thread: the one-element loop waited on a load per element (13.6 us at the bench's 409,600 elements).
 // Each thread sums a group of four float4 products in f32, the groups and waves in f64.
@@ -711,6 +1092,16 @@ __global__ void scalar_add_kernel(const float* a, const float* b, float* out) { 
 __global__ void mse_finalize_kernel(const double* s, int64_t n, float* out) { out[0] = (float)(s[0] / (double)n); }
 
 // channel-split head backward: H / 2 threads per row must divide the 1024-thread workgroup
+int head_cus() {   // the row-stream head passes run one workgroup per CU
+  static const int n = [] {
+    int dev = 0, c = 0;
+    return hipGetDevice(&dev) == hipSuccess &&
+                   hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && c > 0
+               ? c : 256;
+  }();
+  return n;
+}
+
 int head_wgs() {   // workgroups of the channel-split head passes (AW_HEAD_WGS: tuning override)
   // 256 measured best at H 512, B 1024: fewer starve the CUs of rows in flight, more serialise on the per-channel
   // global atomics every workgroup ends with
@@ -913,6 +1304,19 @@ extern "C" int aw_unpatch_head_bwd2_ex(const void* yv, int y_dtype, int64_t R, i
   if (R == 0) return AW_OK;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const size_t sh = H * sizeof(float);
+  if (H == 512 && R * 512 * (y_dtype == AW_F32 ? 4 : 2) < (1ll << 31)) {
+    const dim3 g2((unsigned)std::max<int64_t>(1, std::min<int64_t>(head_cus(), (R + HB * HFW - 1) / (HB * HFW))));
+#define AW_H2R(T, TY)                                                                                              \
+  hipLaunchKernelGGL((head_bwd2_rows_kernel<T, TY>), g2, dim3(64 * HFW), 0, s, (const TY*)yv, R, stats, w2, g_xhat, \
+                     gsums, training, (T*)g_y, db_y)
+    if (gy_dtype == AW_BF16) {
+      if (y_dtype == AW_BF16) AW_H2R(bf16, bf16); else AW_H2R(bf16, float);
+    } else {
+      if (y_dtype == AW_BF16) AW_H2R(float, bf16); else AW_H2R(float, float);
+    }
+#undef AW_H2R
+    return aw::check_launch("aw_unpatch_head_bwd2");
+  }
   if (head_cs_ok(H)) {
     dim3 g2(grid_for(R * (H / 2), 1024, head_wgs()));
 #define AW_H2C(T, TY)                                                                                               \
@@ -945,6 +1349,28 @@ extern "C" int aw_unpatch_head_bwd2_ex(const void* yv, int y_dtype, int64_t R, i
   }
 #undef AW_H2
   return aw::check_launch("aw_unpatch_head_bwd2");
+}
+
+extern "C" int aw_unpatch_head_fwd_bwd1(const void* yv, int y_dtype, int64_t R, int H, int Q, const float* stats,
+                                        const float* w2, const float* b2, const float* x, const float* gscale,
+                                        float* x_hat, float* g_xhat, double* sqerr, double* gsums, float* gw2,
+                                        float* gb2, float* ggamma, float* gbeta, void* stream) {
+  AW_REQUIRE(yv && stats && w2 && b2 && x && gscale && x_hat && g_xhat && sqerr && gsums && gw2 && gb2,
+             "aw_unpatch_head_fwd_bwd1: null pointer");
+  AW_REQUIRE(H == 512 && Q > 0 && R % Q == 0, "aw_unpatch_head_fwd_bwd1: needs H == 512 and whole windows");
+  AW_REQUIRE(y_dtype == AW_F32 || y_dtype == AW_BF16, "aw_unpatch_head_fwd_bwd1: bad y_dtype %d", y_dtype);
+  AW_REQUIRE(R * 512 * (y_dtype == AW_F32 ? 4 : 2) < (1ll << 31), "aw_unpatch_head_fwd_bwd1: y exceeds 2 GiB");
+  if (R == 0) return AW_OK;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const dim3 grid((unsigned)std::max<int64_t>(1, std::min<int64_t>(head_cus(), (R + HB * HFW - 1) / (HB * HFW))));
+  const float gmul = 2.0f / (float)(R * 5);   // aw_mse_bwd: 2 / numel
+  if (y_dtype == AW_BF16)
+    hipLaunchKernelGGL(head_fwd_bwd1_kernel<bf16>, grid, dim3(64 * HFW), 0, s, (const bf16*)yv, R, stats, w2, b2, x,
+                       gscale, gmul, x_hat, g_xhat, sqerr, gsums, gw2, gb2, ggamma, gbeta);
+  else
+    hipLaunchKernelGGL(head_fwd_bwd1_kernel<float>, grid, dim3(64 * HFW), 0, s, (const float*)yv, R, stats, w2, b2, x,
+                       gscale, gmul, x_hat, g_xhat, sqerr, gsums, gw2, gb2, ggamma, gbeta);
+  return aw::check_launch("aw_unpatch_head_fwd_bwd1");
 }
 
 extern "C" int aw_unpatch_head_bwd2(const float* y, int64_t R, int H, int Q, const float* stats, const float* w2,

@@ -165,17 +165,6 @@ class VQVAEPatch(Autoencoder):
         ``_grad_sink``).  ``mid_hook`` is called between the decoder-side and the encoder-side backward (see
         arcweld.vqvae.backward): the data-parallel step starts the decoder-side all-reduce there.  Returns the loss."""
         x = x.contiguous()
-        emb, x_hat, perp, idx, sv = engine.forward(self, x, self.training, need_backward=True, seed=self._next_seed())
-        self._last_indices = idx
-        sq = sv.acc["mse_sq"]            # zeroed with the forward's other accumulators (one fill launch)
-        K.mse_fwd(x_hat, x, sq)
-        recon = torch.empty((), device=x.device)
-        K.mse_finalize(sq, x.numel(), recon)
-        loss = torch.empty((), device=x.device)
-        K.scalar_add(recon.reshape(1), emb.reshape(1), loss)
-        g = self._loss_scale_tensor(float(scale), x.device)
-        g_xhat = torch.empty_like(x_hat)
-        K.mse_bwd(x_hat, x, g, g_xhat)
         sink = getattr(self, "_grad_sink", None)
 
         def slot(p):
@@ -184,6 +173,23 @@ class VQVAEPatch(Autoencoder):
             if p.grad is None:
                 p.grad = torch.zeros_like(p)
             return p.grad
+
+        # the head forward runs fused with the MSE gradient and the first head-backward pass (engine.head_train)
+        emb, x_hat, perp, idx, sv = engine.forward(self, x, self.training, need_backward=True, seed=self._next_seed(),
+                                                   head=False)
+        self._last_indices = idx
+        sq = sv.acc["mse_sq"]            # zeroed with the forward's other accumulators (one fill launch)
+        g = self._loss_scale_tensor(float(scale), x.device)
+        if sv.head_fused:
+            g_xhat = engine.head_train(self, sv, x, g, x_hat, sq, slot)
+        else:
+            K.mse_fwd(x_hat, x, sq)
+            g_xhat = torch.empty_like(x_hat)
+            K.mse_bwd(x_hat, x, g, g_xhat)
+        recon = torch.empty((), device=x.device)
+        K.mse_finalize(sq, x.numel(), recon)
+        loss = torch.empty((), device=x.device)
+        K.scalar_add(recon.reshape(1), emb.reshape(1), loss)
 
         engine.backward(self, sv, g, g_xhat, slot, mid_hook=mid_hook)
         self.log('train/loss', loss, prog_bar=True)
