@@ -346,6 +346,8 @@ __global__ __launch_bounds__(256, 2) void attn_dq_ring_kernel(const bf16* __rest
     const bool edge = (k0 + TILE - 1 > qw) || (k0 + TILE > T_);
 #pragma unroll
     for (int st = 0; st < 2; ++st) {
+      // keys k0+32.. lie after every query of the wave (or past T) on its diagonal tile: nothing to add
+      if (st == 1 && (k0 + 32 > qw + WROWS - 1 || k0 + 32 >= T_)) break;   // wave-uniform
       f32x16 s = zero16(), dp = zero16();
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
@@ -465,6 +467,8 @@ __global__ __launch_bounds__(256, 2) void attn_dkv_ring_kernel(const bf16* __res
     const bool edge = (q0 < kw + WROWS - 1) || (q0 + TILE > T_);
 #pragma unroll
     for (int qs = 0; qs < 2; ++qs) {
+      // queries q0+32qs.. all precede the wave's first key (or lie past T): every P of the sub-tile is masked
+      if (q0 + 32 * qs + 31 < kw || q0 + 32 * qs >= T_) continue;   // wave-uniform
       f32x16 s = zero16(), dp = zero16();
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
