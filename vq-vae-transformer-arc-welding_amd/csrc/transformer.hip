@@ -5,6 +5,7 @@
 #include <stdlib.h>
 
 #include "common.h"
+#include <algorithm>
 
 namespace aw {  // attention.hip: MFMA path for bf16, head size 64
 bool attn_mfma_supported(int dtype, int hs, int d, int64_t T);
@@ -549,6 +550,66 @@ __global__ __launch_bounds__(128) void attn_bwd_dkv_kernel(const T* __restrict__
 }
 
 // ---------------------------------------------------------------- cross entropy (one wave per row)
+// Rows of up to 64 * NC logits: one wave per row with all of the row's loads issued at once and the next row's in
+// flight while this one reduces (ce_fwd_kernel below, kept for V > 1024, walks a row twice -- max, then sum -- and waits
+// on its loads each time: 45 vs 16.5 us at 16371 x 514); 16-wave workgroups, one pair of f64 atomics per workgroup.
+template <int NC>
+__global__ __launch_bounds__(1024) void ce_fwd_rows_kernel(const float* __restrict__ logits, int64_t R, int V,
+                                                           int64_t ldl, const int64_t* __restrict__ y, int ignore,
+                                                           double* loss_sum, double* count, float* __restrict__ lse) {
+  __shared__ double part[16][2];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t nw = (int64_t)gridDim.x * 16;
+  double ls = 0.0, cnt = 0.0;
+  float nv[NC];
+  auto load = [&](int64_t r) {
+#pragma unroll
+    for (int k = 0; k < NC; ++k) {
+      const int i = lane + 64 * k;
+      nv[k] = (r < R && i < V) ? logits[r * ldl + i] : -__builtin_huge_valf();
+    }
+  };
+  int64_t r = (int64_t)blockIdx.x * 16 + wv;
+  load(r);
+  for (; r < R; r += nw) {
+    float v[NC];
+#pragma unroll
+    for (int k = 0; k < NC; ++k) v[k] = nv[k];
+    load(r + nw);
+    float mx = -__builtin_huge_valf();
+#pragma unroll
+    for (int k = 0; k < NC; ++k) mx = fmaxf(mx, v[k]);
+    mx = wave_max(mx);
+    float sm = 0.f;
+#pragma unroll
+    for (int k = 0; k < NC; ++k) sm += __expf(v[k] - mx);   // -inf (past V) -> 0
+    sm = wave_sum(sm);
+    const float L = mx + logf(sm);
+    if (lane == 0) {
+      lse[r] = L;
+      const int64_t t = y[r];
+      if (t != ignore) {
+        ls += (double)(L - logits[r * ldl + t]);
+        cnt += 1.0;
+      }
+    }
+  }
+  if (lane == 0) {
+    part[wv][0] = ls;
+    part[wv][1] = cnt;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double a = 0.0, c = 0.0;
+    for (int w = 0; w < 16; ++w) {
+      a += part[w][0];
+      c += part[w][1];
+    }
+    atomicAdd(loss_sum, a);
+    atomicAdd(count, c);
+  }
+}
+
 __global__ __launch_bounds__(256) void ce_fwd_kernel(const float* __restrict__ logits, int64_t R, int V, int64_t ldl,
                                                      const int64_t* __restrict__ y, int ignore, double* loss_sum,
                                                      double* count, float* __restrict__ lse) {
@@ -981,8 +1042,19 @@ extern "C" int aw_ce_fwd(const float* logits, int64_t R, int V, int64_t ldl, con
                          double* loss_sum, double* count, float* lse, void* stream) {
   AW_REQUIRE(logits && y && loss_sum && count && lse && R >= 0 && V > 0 && ldl >= V, "aw_ce_fwd: bad args");
   if (R == 0) return AW_OK;
-  hipLaunchKernelGGL(ce_fwd_kernel, dim3(gridcap(R * 64, 256, 1024)), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), logits, R,
-                     V, ldl, y, ignore_index, loss_sum, count, lse);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const dim3 gr((unsigned)std::min<int64_t>((R + 63) / 64, 256));   // <= 256 workgroups of 16 waves, ~4 rows per wave
+#define AW_CEF(NC)                                                                                                \
+  hipLaunchKernelGGL(ce_fwd_rows_kernel<NC>, gr, dim3(1024), 0, s, logits, R, V, ldl, y, ignore_index, loss_sum, \
+                     count, lse);                                                                                  \
+  return aw::check_launch("aw_ce_fwd");
+  if (V <= 256) { AW_CEF(4) }
+  if (V <= 512) { AW_CEF(8) }
+  if (V <= 576) { AW_CEF(9) }
+  if (V <= 1024) { AW_CEF(16) }
+#undef AW_CEF
+  hipLaunchKernelGGL(ce_fwd_kernel, dim3(gridcap(R * 64, 256, 1024)), dim3(256), 0, s, logits, R, V, ldl, y,
+                     ignore_index, loss_sum, count, lse);
   return aw::check_launch("aw_ce_fwd");
 }
 
