@@ -24,6 +24,15 @@ namespace {
 // embedding dim; |z|^2 and |e_k|^2 are in-order sums of squares; the distance is fl(fl(|z|^2 + |e_k|^2) - 2 * dot)
 // and the argmin the lexicographic (d, k) minimum (torch.argmin's first-index tie rule).  The register footprint
 // does not depend on D, so the stress codebook (K 8192 x D 256) runs at the same occupancy.
+// Diagnostic phase stamps (tools/probe/vq_stamps.py only: a probe build with -DAW_VQ_STAMPS; never in the library).
+#ifdef AW_VQ_STAMPS
+static __device__ uint64_t g_vq_stamps[1024 * 16];
+#define VQ_STAMP(i) do { if (threadIdx.x == 0 && blockIdx.x < 1024) \
+    g_vq_stamps[blockIdx.x * 16 + (i)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define VQ_STAMP(i) do { } while (0)
+#endif
+
 constexpr int VQ_THREADS = 512;
 constexpr int VQ_CODES = 512;
 constexpr int VQ_DC = 16;           // embedding floats per staged chunk
@@ -31,7 +40,9 @@ constexpr int VQ_DC = 16;           // embedding floats per staged chunk
 template <int D, int ROWS> struct VqLds {
   static constexpr int ZP = D + 4;                                   // z image pitch (disjoint banks per row)
   static constexpr int Z = ROWS * ZP;                                // floats
-  static constexpr int E = VQ_DC * VQ_CODES;                         // floats per stage, [d][code]
+  static constexpr int EP = VQ_CODES + 4;                            // [d][code] pitch: a staging store's 4 dims
+                                                                     // of a code land on 2-way (free) banks
+  static constexpr int E = VQ_DC * EP;                               // floats per stage, [d][code]
   static constexpr int TOTAL = Z + 2 * E + 2 * VQ_CODES + ROWS;      // + ee[2][512] + zz[ROWS]
 };
 
@@ -58,6 +69,7 @@ __global__ __launch_bounds__(VQ_THREADS, 2) void vq_fwd_kernel(const float* __re
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int lr = lane >> 3, lc = lane & 7;
   const int64_t row0 = (int64_t)blockIdx.x * ROWS;
+  VQ_STAMP(0);
 
   // ---- z tile -> LDS (rows beyond N are zero), |z|^2 per row
   for (int i = tid; i < ROWS * (D / 4); i += VQ_THREADS) {
@@ -67,39 +79,47 @@ __global__ __launch_bounds__(VQ_THREADS, 2) void vq_fwd_kernel(const float* __re
     *reinterpret_cast<float4*>(zs + r * ZP + 4 * q) = v;
   }
   __syncthreads();
+  VQ_STAMP(1);
   if (tid < ROWS) {
     float s = 0.f;
     for (int d = 0; d < D; ++d) s = __fadd_rn(s, __fmul_rn(zs[tid * ZP + d], zs[tid * ZP + d]));
     zzs[tid] = s;
   }
 
-  // ---- codebook stream: step s = (code tile s / ND, chunk s % ND); thread t stages code t of the tile
+  // ---- codebook stream: step s = (code tile s / ND, chunk s % ND).  Staging is coalesced: float4 u of thread t
+  // is quad (t & 3) of code 128u + (t >> 2) (4 lanes per 64-B chunk row, 16 cache lines per load instruction);
+  // the store transposes it into the [d][code] image.  |e_k|^2 is summed in embedding order by the thread of code
+  // k from the published image at the start of each step.
+  constexpr int EP = L::EP;
   const int ntiles = (K + VQ_CODES - 1) / VQ_CODES;
   const int nsteps = ntiles * ND;
   float4 pre[VQ_DC / 4];
   float ee_acc = 0.f;
   auto load = [&](int st) {
     const int ct = st / ND, dc = st - ct * ND;
-    const int code = ct * VQ_CODES + tid;
-    const float4* src = reinterpret_cast<const float4*>(E + (int64_t)code * D + dc * VQ_DC);
-#pragma unroll
-    for (int u = 0; u < VQ_DC / 4; ++u) pre[u] = code < K ? src[u] : make_float4(0.f, 0.f, 0.f, 0.f);
-  };
-  auto store = [&](int st) {
-    const int ct = st / ND, dc = st - ct * ND;
-    float* dst = es + (st & 1) * L::E + tid;       // transposed: element d of code t at [d][t]
-    if (dc == 0) ee_acc = 0.f;
 #pragma unroll
     for (int u = 0; u < VQ_DC / 4; ++u) {
-      dst[(4 * u + 0) * VQ_CODES] = pre[u].x;
-      dst[(4 * u + 1) * VQ_CODES] = pre[u].y;
-      dst[(4 * u + 2) * VQ_CODES] = pre[u].z;
-      dst[(4 * u + 3) * VQ_CODES] = pre[u].w;
-      ee_acc = __fadd_rn(ee_acc, __fmul_rn(pre[u].x, pre[u].x));
-      ee_acc = __fadd_rn(ee_acc, __fmul_rn(pre[u].y, pre[u].y));
-      ee_acc = __fadd_rn(ee_acc, __fmul_rn(pre[u].z, pre[u].z));
-      ee_acc = __fadd_rn(ee_acc, __fmul_rn(pre[u].w, pre[u].w));
+      const int code = ct * VQ_CODES + 128 * u + (tid >> 2);
+      pre[u] = code < K ? reinterpret_cast<const float4*>(E + (int64_t)code * D + dc * VQ_DC)[tid & 3]
+                        : make_float4(0.f, 0.f, 0.f, 0.f);
     }
+  };
+  auto store = [&](int st) {
+    float* dst = es + (st & 1) * L::E + 4 * (tid & 3) * EP + (tid >> 2);
+#pragma unroll
+    for (int u = 0; u < VQ_DC / 4; ++u) {
+      dst[0 * EP + 128 * u] = pre[u].x;
+      dst[1 * EP + 128 * u] = pre[u].y;
+      dst[2 * EP + 128 * u] = pre[u].z;
+      dst[3 * EP + 128 * u] = pre[u].w;
+    }
+  };
+  auto norms = [&](int st) {   // chunk st is published: continue this thread's code's in-order sum of squares
+    const int ct = st / ND, dc = st - ct * ND;
+    const float* src = es + (st & 1) * L::E + tid;
+    if (dc == 0) ee_acc = 0.f;
+#pragma unroll
+    for (int d = 0; d < VQ_DC; ++d) ee_acc = __fadd_rn(ee_acc, __fmul_rn(src[d * EP], src[d * EP]));
     if (dc == ND - 1) ees[(ct & 1) * VQ_CODES + tid] = ee_acc;
   };
 
@@ -119,12 +139,14 @@ __global__ __launch_bounds__(VQ_THREADS, 2) void vq_fwd_kernel(const float* __re
   load(0);
   store(0);
   __syncthreads();
+  VQ_STAMP(2);
   float zz[RPL];
 #pragma unroll
   for (int i = 0; i < RPL; ++i) zz[i] = zzs[lr + 8 * i];
 
   for (int st = 0; st < nsteps; ++st) {
     if (st + 1 < nsteps) load(st + 1);
+    norms(st);
     const int ct = st / ND, dc = st - ct * ND;
     const float* eb = es + (st & 1) * L::E + w * 64 + 8 * lc;
     const float* zb = zs + lr * ZP + dc * VQ_DC;
@@ -135,8 +157,8 @@ __global__ __launch_bounds__(VQ_THREADS, 2) void vq_fwd_kernel(const float* __re
       for (int i = 0; i < RPL; ++i) zv[i] = *reinterpret_cast<const float4*>(zb + 8 * i * ZP + 4 * q);
 #pragma unroll
       for (int dd = 0; dd < 4; ++dd) {
-        const float4 e0 = *reinterpret_cast<const float4*>(eb + (4 * q + dd) * VQ_CODES);
-        const float4 e1 = *reinterpret_cast<const float4*>(eb + (4 * q + dd) * VQ_CODES + 4);
+        const float4 e0 = *reinterpret_cast<const float4*>(eb + (4 * q + dd) * EP);
+        const float4 e1 = *reinterpret_cast<const float4*>(eb + (4 * q + dd) * EP + 4);
         const f32x2 ep[4] = {f32x2{e0.x, e0.y}, f32x2{e0.z, e0.w}, f32x2{e1.x, e1.y}, f32x2{e1.z, e1.w}};
 #pragma unroll
         for (int i = 0; i < RPL; ++i) {
@@ -147,7 +169,9 @@ __global__ __launch_bounds__(VQ_THREADS, 2) void vq_fwd_kernel(const float* __re
         }
       }
     }
-    if (dc == ND - 1) {   // the tile's dot products are complete: distances, running argmin, reset
+    if (st + 1 < nsteps) store(st + 1);
+    __syncthreads();
+    if (dc == ND - 1) {   // the tile's dot products are complete (and its norms published): distances, argmin
       const float* eet = ees + (ct & 1) * VQ_CODES + w * 64 + 8 * lc;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
@@ -168,8 +192,7 @@ __global__ __launch_bounds__(VQ_THREADS, 2) void vq_fwd_kernel(const float* __re
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = f32x2{0.f, 0.f};
     }
-    if (st + 1 < nsteps) store(st + 1);
-    __syncthreads();
+    if (st < 8) VQ_STAMP(3 + st);
   }
 
   // ---- argmin across the 8 code lanes of a row group, then across the 8 waves (LDS, the e stages are free)
@@ -195,52 +218,63 @@ __global__ __launch_bounds__(VQ_THREADS, 2) void vq_fwd_kernel(const float* __re
     }
   }
   __syncthreads();
-  if (w != 0) return;
-  const int r = lane;
-  const bool live = r < ROWS;
-  const int64_t row = row0 + r;
-  float bd = live ? rd[r] : 0.f;
-  int bk = live ? rk[r] : 0;
-#pragma unroll
-  for (int v = 1; v < 8; ++v)
-    if (live && lex_less(rd[v * ROWS + r], rk[v * ROWS + r], bd, bk)) {
-      bd = rd[v * ROWS + r];
-      bk = rk[v * ROWS + r];
-    }
+  VQ_STAMP(11);
+  // ---- epilogue over the whole workgroup: thread (row r, quad q) of the ROWS x D/4 float4 items resolves its
+  // row's winner from the 8 wave candidates (LDS broadcast reads), gathers e_k's quad and writes z_q (+ the operand
+  // copy) coalesced; the q == 0 thread of a row writes idx and counts the code.
+  constexpr int DQ = D / 4;
   double se = 0.0;
-  if (live && row < N) {
-    if (bk < 0 || bk >= K) bk = 0;  // all-NaN row guard (torch would return the NaN position)
-    idx[row] = bk;
-    atomicAdd(counts + bk, 1.0f);
-    const float4* ep = reinterpret_cast<const float4*>(E + (int64_t)bk * D);
-    const float* zr = zs + r * ZP;
-    float4* op = reinterpret_cast<float4*>(zq + row * D);
-    float s = 0.f;
-    for (int q = 0; q < D / 4; ++q) {
-      const float4 e = ep[q];
-      const float4 zv = *reinterpret_cast<const float4*>(zr + 4 * q);
-      const float d0 = __fsub_rn(e.x, zv.x), d1 = __fsub_rn(e.y, zv.y);
-      const float d2 = __fsub_rn(e.z, zv.z), d3 = __fsub_rn(e.w, zv.w);
-      float4 o;
-      o.x = __fadd_rn(zv.x, d0);  // z + (z_q - z).detach()
-      o.y = __fadd_rn(zv.y, d1);
-      o.z = __fadd_rn(zv.z, d2);
-      o.w = __fadd_rn(zv.w, d3);
-      op[q] = o;
-      if (zq2) {   // the GEMM operand copy of z_q (the decoder's first conv reads it): no separate cast launch
-        if (zq2_bf16) {
-          typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
-          reinterpret_cast<bf16x4*>(zq2)[row * (D / 4) + q] = bf16x4{(bf16)o.x, (bf16)o.y, (bf16)o.z, (bf16)o.w};
-        } else {
-          reinterpret_cast<float4*>(zq2)[row * (D / 4) + q] = o;
-        }
+  for (int it = tid; it < ROWS * DQ; it += VQ_THREADS) {
+    const int r = it / DQ, q = it - r * DQ;
+    const int64_t row = row0 + r;
+    if (row >= N) break;   // rows ascend with it
+    float bd = rd[r];
+    int bk = rk[r];
+#pragma unroll
+    for (int v = 1; v < 8; ++v)
+      if (lex_less(rd[v * ROWS + r], rk[v * ROWS + r], bd, bk)) {
+        bd = rd[v * ROWS + r];
+        bk = rk[v * ROWS + r];
       }
-      s += d0 * d0 + d1 * d1 + d2 * d2 + d3 * d3;
+    if (bk < 0 || bk >= K) bk = 0;  // all-NaN row guard (torch would return the NaN position)
+    if (q == 0) {
+      idx[row] = bk;
+      atomicAdd(counts + bk, 1.0f);
     }
-    se = s;
+    const float4 e = reinterpret_cast<const float4*>(E + (int64_t)bk * D)[q];
+    const float4 zv = *reinterpret_cast<const float4*>(zs + r * ZP + 4 * q);
+    const float d0 = __fsub_rn(e.x, zv.x), d1 = __fsub_rn(e.y, zv.y);
+    const float d2 = __fsub_rn(e.z, zv.z), d3 = __fsub_rn(e.w, zv.w);
+    float4 o;
+    o.x = __fadd_rn(zv.x, d0);  // z + (z_q - z).detach()
+    o.y = __fadd_rn(zv.y, d1);
+    o.z = __fadd_rn(zv.z, d2);
+    o.w = __fadd_rn(zv.w, d3);
+    reinterpret_cast<float4*>(zq + row * D)[q] = o;
+    if (zq2) {   // the GEMM operand copy of z_q (the decoder's first conv reads it): no separate cast launch
+      if (zq2_bf16) {
+        typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+        reinterpret_cast<bf16x4*>(zq2)[row * DQ + q] = bf16x4{(bf16)o.x, (bf16)o.y, (bf16)o.z, (bf16)o.w};
+      } else {
+        reinterpret_cast<float4*>(zq2)[row * DQ + q] = o;
+      }
+    }
+    se += (double)(d0 * d0 + d1 * d1 + d2 * d2 + d3 * d3);
   }
   se = wave_sum_d(se);
-  if (lane == 0) atomicAdd(sqerr, se);
+  double* red = reinterpret_cast<double*>(ees);   // the ee stages are free since the exchange barrier
+  if (lane == 0) red[w] = se;
+  // LDS-only barrier: __syncthreads' release fence would also wait for this workgroup's z_q stores and count atomics
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  if (tid == 0) {
+    double t = 0.0;
+#pragma unroll
+    for (int v = 0; v < 8; ++v) t += red[v];
+    atomicAdd(sqerr, t);
+  }
+  VQ_STAMP(12);
 }
 
 __global__ void vq_finalize_kernel(const float* counts, const double* sqerr, int64_t N, int K, int D, float beta,
@@ -301,6 +335,14 @@ __global__ void vq_gather_kernel(const float* E, const int64_t* idx, int64_t N, 
 }
 
 }  // namespace
+
+#ifdef AW_VQ_STAMPS
+extern "C" int aw_probe_vq_stamps(uint64_t* out, int n) {   // copies n words out, then zeroes them
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_vq_stamps), (size_t)n * 8) != hipSuccess) return -1;
+  static uint64_t zeros[1024 * 16];
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_vq_stamps), zeros, sizeof(zeros)) == hipSuccess ? n : -1;
+}
+#endif
 
 extern "C" int aw_vq_forward_ex(const float* z, const float* E, int64_t N, int K, int D, float* zq, int64_t* idx,
                                 float* counts, double* sqerr, void* zq_copy, int copy_dtype, void* stream) {
