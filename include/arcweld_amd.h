@@ -270,6 +270,9 @@ int aw_mse_bwd(const float* a, const float* b, int64_t n, const float* g, float*
 int aw_scalar_add(const float* a, const float* b, float* out, void* stream);
 /* recon = sqerr/numel as f32 -> out */
 int aw_mse_finalize(const double* sqerr, int64_t numel, float* out, void* stream);
+/* out = sqerr / numel and sum = out + addend in one launch (the training step's recon error and total loss,
+ * autencoder_lightning_base.py:80-97: loss = recon_error + embedding_loss). */
+int aw_mse_finalize_add(const double* sqerr, int64_t numel, const float* addend, float* out, float* sum, void* stream);
 
 /* ------------------------------------------------------------------------------------- optimizer
  * Multi-tensor RAdam over one flat parameter buffer (torch.optim.RAdam semantics, L2 weight decay):
@@ -306,6 +309,9 @@ int aw_radam_step_ops(float* param, float* grad, float* exp_avg, float* exp_avg_
 int aw_counter_add(int64_t* counter, int64_t v, void* stream);
 /* The same, also copying the new value to *snapshot (the per-forward dropout seed the backward re-reads). */
 int aw_counter_add_snapshot(int64_t* counter, int64_t v, int64_t* snapshot, void* stream);
+/* The same, also zeroing zero[0 .. nzero) in the one launch (a forward's f64 accumulator block). */
+int aw_counter_add_snapshot_zero(int64_t* counter, int64_t v, int64_t* snapshot, double* zero, int64_t nzero,
+                                 void* stream);
 /* Global L2 norm of the active segments of `grad` -> out_norm (f32 device scalar) and the clip coefficient
  * min(max_norm/(norm+1e-6), 1) -> out_coef (Lightning gradient_clip_val -> clip_grad_norm_).
  * ws: f64[AW_NORM_WS] scratch (per-workgroup partial sums, reduced in a fixed order: the norm is deterministic). */

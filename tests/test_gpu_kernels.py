@@ -363,6 +363,42 @@ def test_mse_loss_vs_fp64(K, n, off):
     np.testing.assert_allclose(got, ref, rtol=2e-6)
 
 
+def test_mse_finalize_add_and_counter_zero(K):
+    """aw_mse_finalize_add (recon = sq / n, loss = recon + embedding loss in one launch) and
+    aw_counter_add_snapshot_zero (dropout counter advance + snapshot + accumulator-block zeroing in one launch)."""
+    sq = torch.tensor([1234.5], device=DEV, dtype=torch.float64)
+    emb = torch.tensor([0.25], device=DEV)
+    recon, loss = torch.empty((), device=DEV), torch.empty((), device=DEV)
+    K.mse_finalize_add(sq, 1000, emb, recon, loss)
+    assert recon.item() == np.float32(1234.5 / 1000)
+    assert loss.item() == np.float32(np.float32(1234.5 / 1000) + np.float32(0.25))
+    for nz in (0, 1, 2306, 70001):     # the bench's block (K 512, H 512) and a multi-workgroup block
+        ctr = torch.tensor([41], device=DEV, dtype=torch.int64)
+        snap = torch.empty(1, device=DEV, dtype=torch.int64)
+        z = torch.full((nz + 3,), 7.0, device=DEV, dtype=torch.float64)
+        K.counter_add_snapshot(ctr, snap, v=2, zero=z[:nz])
+        assert ctr.item() == 43 and snap.item() == 43
+        assert torch.all(z[:nz] == 0) and torch.all(z[nz:] == 7.0)
+
+
+def test_grad_norm_clip_full_grid_repeated(K):
+    """aw_grad_norm_clip over the full grid of AW_NORM_WS partials and two segments, called repeatedly (as graph
+    replays do): the f64 norm and the clip coefficient every time."""
+    n = 1024 * 512 * 4 * 3 + 8
+    g = torch.tensor(gen.normal(77, (n,), 1.0), device=DEV)
+    off = torch.tensor([0, n // 2], device=DEV, dtype=torch.int64)
+    ln = torch.tensor([n // 2 - 4, n - n // 2], device=DEV, dtype=torch.int64)
+    act = torch.tensor([1, 1], device=DEV, dtype=torch.int32)
+    g[n // 2 - 4:n // 2] = 0.0                      # the padding after segment 0 is zero, as the header requires
+    ws = torch.zeros(K.NORM_WS, device=DEV, dtype=torch.float64)
+    ref = g.double().norm().item()
+    for max_norm in (1.0, 1e9, 0.5):
+        norm, coef = torch.empty((), device=DEV), torch.empty((), device=DEV)
+        K.grad_norm_clip(g, off, ln, act, 2, max_norm, ws, norm, coef)
+        np.testing.assert_allclose(norm.item(), ref, rtol=1e-6)
+        np.testing.assert_allclose(coef.item(), min(max_norm / (norm.item() + 1e-6), 1.0), rtol=1e-6)
+
+
 @pytest.mark.parametrize("policy,G,Cout,Cin,Ntok,S,ref_layout,alpha", [
     (0, 16, 512, 512, 16 * 1024, 16, False, 1.0),     # the decoder's grouped launch at full size (auto policy)
     (1, 3, 256, 128, 1024, 8, True, 1.0),             # forced at a small shape: windows of 8, (O, I, 3) column map

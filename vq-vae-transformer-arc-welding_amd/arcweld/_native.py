@@ -106,12 +106,14 @@ SIGNATURES = {
     "aw_mse_bwd": [c_p, c_p, c_i64, c_p, c_p, c_p],
     "aw_scalar_add": [c_p, c_p, c_p, c_p],
     "aw_mse_finalize": [c_p, c_i64, c_p, c_p],
+    "aw_mse_finalize_add": [c_p, c_i64, c_p, c_p, c_p, c_p],
     "aw_radam_step": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_int, c_i64, c_i64, c_f, c_f, c_f, c_f, c_p, c_p,
                       c_int, c_p],
     "aw_radam_step_ops": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_int, c_i64, c_i64, c_f, c_f, c_f, c_f, c_p, c_p,
                           c_p, c_int, c_p],
     "aw_counter_add": [c_p, c_i64, c_p],
     "aw_counter_add_snapshot": [c_p, c_i64, c_p, c_p],
+    "aw_counter_add_snapshot_zero": [c_p, c_i64, c_p, c_p, c_i64, c_p],
     "aw_grad_norm_clip": [c_p, c_p, c_p, c_p, c_int, c_i64, c_f, c_p, c_p, c_p, c_p],
     "aw_scale": [c_p, c_i64, c_p, c_p],
     "aw_layernorm_fwd": [c_p, c_i64, c_int, c_p, c_p, c_f, c_p, c_int, c_p, c_p, c_p],

@@ -327,6 +327,11 @@ def mse_finalize(sqerr, numel, out, stream=None):
     call("aw_mse_finalize", ptr(sqerr), int(numel), ptr(out), stream_ptr(stream))
 
 
+def mse_finalize_add(sqerr, numel, addend, out, total, stream=None):
+    """out = sqerr / numel and total = out + addend (device scalars), in one launch."""
+    call("aw_mse_finalize_add", ptr(sqerr), int(numel), ptr(addend), ptr(out), ptr(total), stream_ptr(stream))
+
+
 # ------------------------------------------------------------------------------------------ optimizer
 def radam_step(param, grad, m, v, seg_off, seg_len, seg_wd, seg_active, nseg, total, step, lr, beta1, beta2, eps,
                gscale=None, stream=None, step_ptr=None, ops=None, zero_grad=False):
@@ -341,9 +346,16 @@ def radam_step(param, grad, m, v, seg_off, seg_len, seg_wd, seg_active, nseg, to
         call("aw_radam_step_ops", *args, ptr(ops), int(bool(zero_grad)), stream_ptr(stream))
 
 
-def counter_add_snapshot(counter, snapshot, v=1, stream=None):
-    """counter += v and snapshot = the new value, in one launch."""
-    call("aw_counter_add_snapshot", ptr(counter), int(v), ptr(snapshot), stream_ptr(stream))
+def counter_add_snapshot(counter, snapshot, v=1, stream=None, zero=None):
+    """counter += v and snapshot = the new value, in one launch; `zero` (a contiguous float64 tensor) is zeroed by
+    the same launch."""
+    if zero is None:
+        call("aw_counter_add_snapshot", ptr(counter), int(v), ptr(snapshot), stream_ptr(stream))
+        return
+    if zero.dtype != torch.float64 or not zero.is_contiguous():
+        raise nat.NativeError("counter_add_snapshot: zero must be a contiguous float64 tensor")
+    call("aw_counter_add_snapshot_zero", ptr(counter), int(v), ptr(snapshot), ptr(zero), zero.numel(),
+         stream_ptr(stream))
 
 
 def counter_add(counter, v=1, stream=None):

@@ -39,33 +39,38 @@ def _mix(seed: int, salt: int) -> int:
     return z ^ (z >> 32)
 
 
-def rng_snapshot(m, dev, p_drop):
+def rng_snapshot(m, dev, p_drop, zero=None):
     """Advance the module's device-side dropout counter and return a device copy of it for this forward (None
     when no dropout is active).  The kernels mix it into the host seeds (aw_gemm_args.seed_ptr), so a captured
-    HIP graph draws fresh masks on every replay and the backward regenerates exactly the forward's masks."""
+    HIP graph draws fresh masks on every replay and the backward regenerates exactly the forward's masks.
+    `zero` (a float64 block, the forward's accumulators) is zeroed by the same launch."""
     if p_drop <= 0.0:
+        if zero is not None:
+            zero.zero_()
         return None
     ctr = getattr(m, "_rng_counter", None)
     if ctr is None or ctr.device != dev:
         ctr = torch.zeros(1, dtype=torch.int64, device=dev)
         m._rng_counter = ctr
     snap = torch.empty(1, dtype=torch.int64, device=dev)
-    K.counter_add_snapshot(ctr, snap)      # advance and snapshot in one launch
+    K.counter_add_snapshot(ctr, snap, zero=zero)      # advance, snapshot (and zero) in one launch
     return snap
 
 
-def accumulators(m, dev, K, H):
-    """Zeroed device accumulators of one forward, carved from one persistent block with ONE fill launch: VQ sqerr
-    (f64), MSE sqerr (f64, fused_train_step), BN column statistics (2H f64) and the VQ code counts (K f32).  Each is
-    consumed inside the call that filled it (never across a forward/backward boundary)."""
+def accumulators(m, dev, K, H, zero=True):
+    """Device accumulators of one forward, carved from one persistent f64 block (zeroed by ONE launch: here, or by
+    rng_snapshot's when zero=False and the caller passes it the "block"): VQ sqerr (f64), MSE sqerr (f64,
+    fused_train_step), BN column statistics (2H f64) and the VQ code counts (K f32).  Each is consumed inside the
+    call that filled it (never across a forward/backward boundary)."""
     key = (dev, K, H)
     st = m.__dict__.get("_acc_block")
     if st is None or st[0] != key:
         st = (key, torch.empty(2 + 4 * H + (K + 1) // 2, dtype=torch.float64, device=dev))
         m.__dict__["_acc_block"] = st
     buf = st[1]
-    buf.zero_()
-    return dict(vq_sq=buf[0:1], mse_sq=buf[1:2], colstats=buf[2:2 + 2 * H], head_gsums=buf[2 + 2 * H:2 + 4 * H],
+    if zero:
+        buf.zero_()
+    return dict(block=buf, vq_sq=buf[0:1], mse_sq=buf[1:2], colstats=buf[2:2 + 2 * H], head_gsums=buf[2 + 2 * H:2 + 4 * H],
                 counts=buf[2 + 4 * H:].view(torch.float32)[:K])
 
 
@@ -265,8 +270,8 @@ def forward(m, x, training: bool, need_backward: bool, dtype=None, seed: int = 0
     sv.sh, sv.T, sv.p_drop, sv.training = sh, T, p_drop, training
     sv.enc_seed = [_mix(seed, 100 + r) for r in range(R)]
     sv.dec_seed = [_mix(seed, 200 + r) for r in range(R)]
-    sv.ctr = rng_snapshot(m, dev, p_drop)
-    acc = accumulators(m, dev, sh.K, H)
+    acc = accumulators(m, dev, sh.K, H, zero=False)
+    sv.ctr = rng_snapshot(m, dev, p_drop, zero=acc["block"])
     sv.acc = acc
     # the head-backward sums of the block belong to one saved forward at a time: the owner is held by a weak
     # reference, released by its backward -- or by its collection when it is never backpropagated

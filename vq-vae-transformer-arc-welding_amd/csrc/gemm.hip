@@ -91,6 +91,35 @@ __global__ __launch_bounds__(256) void gemm_reduce_kernel(const float* __restric
                                                           aw_gemm_args p) {
   const int64_t n = (int64_t)M * N;
   float* C = reinterpret_cast<float*>(p.C);
+  if (p.accumulate && p.col_mod > 0 && (int64_t)p.col_mod * p.col_mul == N && (N & 3) == 0 && (p.ldc & 3) == 0 &&
+      (p.col_off & 3) == 0 && ((uintptr_t)C & 15) == 0) {
+    // transposing column map (ConvT weight gradient: column j*col_mod + o lands at o*col_mul + j): walk the
+    // DESTINATION in float4s so the read-modify-write of C is coalesced; the slab reads gather col_mul runs of
+    // consecutive o per wave instead
+    const int64_t n4 = n >> 2;
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n4; q += (int64_t)gridDim.x * blockDim.x) {
+      const int64_t e = q << 2;
+      const int64_t r = e / N;
+      const int d0 = (int)(e - r * N);
+      int64_t src[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int d = d0 + k, o = d / p.col_mul, j = d - o * p.col_mul;
+        src[k] = r * N + (int64_t)j * p.col_mod + o;
+      }
+      float acc[4] = {0.f, 0.f, 0.f, 0.f};
+      for (int s = 0; s < splits; ++s) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) acc[k] += ws[s * n + src[k]];
+      }
+      f32x4* dst = reinterpret_cast<f32x4*>(C + r * p.ldc + p.col_off + d0);
+      f32x4 v = *dst;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[k] += p.alpha * acc[k];
+      *dst = v;
+    }
+    return;
+  }
   if ((N & 3) == 0) {
     const int64_t n4 = n >> 2;
     const f32x4* w4 = reinterpret_cast<const f32x4*>(ws);

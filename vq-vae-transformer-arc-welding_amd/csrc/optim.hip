@@ -40,6 +40,18 @@ __global__ void counter_add_kernel(int64_t* c, int64_t v, int64_t* snap) {
   if (snap) snap[0] = n;
 }
 
+// the same, plus zeroing a small f64 block (a forward's accumulators) in the one launch
+__global__ __launch_bounds__(256) void counter_add_zero_kernel(int64_t* c, int64_t v, int64_t* snap, double* z,
+                                                               int64_t nz) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    const int64_t n = c[0] + v;
+    c[0] = n;
+    snap[0] = n;
+  }
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nz; i += (int64_t)gridDim.x * blockDim.x)
+    z[i] = 0.0;
+}
+
 __device__ __forceinline__ int find_seg(const int64_t* off, int nseg, int64_t e) {
   int lo = 0, hi = nseg - 1;
   while (lo < hi) {  // last segment with off <= e
@@ -407,6 +419,17 @@ extern "C" int aw_counter_add_snapshot(int64_t* counter, int64_t v, int64_t* sna
   hipLaunchKernelGGL(counter_add_kernel, dim3(1), dim3(1), 0, reinterpret_cast<hipStream_t>(stream), counter, v,
                      snapshot);
   return aw::check_launch("aw_counter_add_snapshot");
+}
+
+extern "C" int aw_counter_add_snapshot_zero(int64_t* counter, int64_t v, int64_t* snapshot, double* zero,
+                                            int64_t nzero, void* stream) {
+  AW_REQUIRE(counter && snapshot && nzero >= 0 && (zero || nzero == 0), "aw_counter_add_snapshot_zero: bad args");
+  int64_t g = (nzero + 255) / 256;
+  if (g > 1024) g = 1024;
+  if (g < 1) g = 1;
+  hipLaunchKernelGGL(counter_add_zero_kernel, dim3((int)g), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                     counter, v, snapshot, zero, nzero);
+  return aw::check_launch("aw_counter_add_snapshot_zero");
 }
 
 extern "C" int aw_grad_norm_clip(const float* grad, const int64_t* seg_off, const int64_t* seg_len,

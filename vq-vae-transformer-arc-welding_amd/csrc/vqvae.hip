@@ -1090,6 +1090,12 @@ __global__ void mse_bwd_kernel(const float* __restrict__ a, const float* __restr
 
 __global__ void scalar_add_kernel(const float* a, const float* b, float* out) { out[0] = a[0] + b[0]; }
 __global__ void mse_finalize_kernel(const double* s, int64_t n, float* out) { out[0] = (float)(s[0] / (double)n); }
+// the training step's loss in the same launch: recon = mse, loss = recon + addend (the embedding loss)
+__global__ void mse_finalize_add_kernel(const double* s, int64_t n, const float* addend, float* out, float* sum) {
+  const float r = (float)(s[0] / (double)n);
+  out[0] = r;
+  sum[0] = r + addend[0];
+}
 
 // channel-split head backward: H / 2 threads per row must divide the 1024-thread workgroup
 int head_cus() {   // the row-stream head passes run one workgroup per CU
@@ -1408,4 +1414,12 @@ extern "C" int aw_mse_finalize(const double* sqerr, int64_t numel, float* out, v
   AW_REQUIRE(sqerr && out && numel > 0, "aw_mse_finalize: bad args");
   hipLaunchKernelGGL(mse_finalize_kernel, dim3(1), dim3(1), 0, reinterpret_cast<hipStream_t>(stream), sqerr, numel, out);
   return aw::check_launch("aw_mse_finalize");
+}
+
+extern "C" int aw_mse_finalize_add(const double* sqerr, int64_t numel, const float* addend, float* out, float* sum,
+                                   void* stream) {
+  AW_REQUIRE(sqerr && addend && out && sum && numel > 0, "aw_mse_finalize_add: bad args");
+  hipLaunchKernelGGL(mse_finalize_add_kernel, dim3(1), dim3(1), 0, reinterpret_cast<hipStream_t>(stream), sqerr, numel,
+                     addend, out, sum);
+  return aw::check_launch("aw_mse_finalize_add");
 }

@@ -187,9 +187,8 @@ class VQVAEPatch(Autoencoder):
             g_xhat = torch.empty_like(x_hat)
             K.mse_bwd(x_hat, x, g, g_xhat)
         recon = torch.empty((), device=x.device)
-        K.mse_finalize(sq, x.numel(), recon)
         loss = torch.empty((), device=x.device)
-        K.scalar_add(recon.reshape(1), emb.reshape(1), loss)
+        K.mse_finalize_add(sq, x.numel(), emb.reshape(1), recon, loss)
 
         engine.backward(self, sv, g, g_xhat, slot, mid_hook=mid_hook)
         self.log('train/loss', loss, prog_bar=True)
