@@ -193,19 +193,31 @@ def transformer_workload(dev, rank, world, args, seqs, n_cycles, accumulate=1, l
             "launch": "hip-graph" if use_graph else "eager"}
 
 
+def _newest_profile(name):
+    """The newest committed profiles/r<round>/<session>*/<name>, by round then session number (s14 after s9)."""
+    import glob
+    import re
+
+    def key(path):
+        parts = os.path.relpath(path, REPO).split(os.sep)
+        nums = [int(m.group(1)) if (m := re.match(r"[rs](\d+)", q)) else -1 for q in parts[1:3]]
+        return nums, path
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "r0*", "*", name)), key=key)
+    return files[-1] if files else None
+
+
 def gemm_traffic():
     """HBM bytes of the GEMM family from the newest committed rocprofv3 PMC passes (FETCH_SIZE and WRITE_SIZE in
     separate runs, FETCH_SIZE doubled on gfx950; tools/pmc_traffic.py) of this same workload: counters cannot be
     read from inside the timed run.  Since round 3 the family is every kernel an aw_gemm / aw_gemm_grouped call
     launches (gemm_kernel, wgrad_conv3_kernel, gemm_reduce_kernel) and the file carries its bytes per traced step,
     which gemm_roofline divides by the calls per step (older files: the per-kernel-launch average)."""
-    import glob
-    files = sorted(glob.glob(os.path.join(REPO, "profiles", "r0*", "*", "pmc_gemm_traffic.json")))
-    if not files:
+    newest = _newest_profile("pmc_gemm_traffic.json")
+    if newest is None:
         return None, None
-    with open(files[-1]) as f:
+    with open(newest) as f:
         d = json.load(f)
-    src = os.path.relpath(files[-1], REPO)
+    src = os.path.relpath(newest, REPO)
     if d.get("bytes_per_step"):
         return {"bytes_per_step": d["bytes_per_step"]}, src
     return round(d["avg_bytes_per_launch"]), src
@@ -384,13 +396,12 @@ def attn_roofline(prof):
 def transformer_traffic():
     """HBM bytes per bf16 GEMM launch of the decoder train step from the committed PMC passes of the
     transformer_pretokenized workload (tools/prof_transformer.sh; FETCH_SIZE doubled per the gfx950 note)."""
-    import glob
-    files = sorted(glob.glob(os.path.join(REPO, "profiles", "r0*", "*", "pmc_transformer_gemm_traffic.json")))
-    if not files:
+    newest = _newest_profile("pmc_transformer_gemm_traffic.json")
+    if newest is None:
         return None, None
-    with open(files[-1]) as f:
+    with open(newest) as f:
         d = json.load(f)
-    src = os.path.relpath(files[-1], REPO)
+    src = os.path.relpath(newest, REPO)
     if d.get("bytes_per_step"):
         return {"bytes_per_step": d["bytes_per_step"]}, src
     return round(d["avg_bytes_per_launch"]), src

@@ -137,7 +137,9 @@ def forward(m, ids, generate: bool, training: bool, need_backward: bool, seed: i
         Wlm = ops["Wlm"]        # [Vp][d]: padded rows stay zero (K padding of the dgrad)
         logits_buf = e(R, Vp)
         logits = logits_buf[:, :V]
-        K.gemm(xf, Wlm, R, V, d, C=logits)
+        # over the padded width: the zero rows of Wlm give exact zeros in the padding columns, and N = Vp (a
+        # multiple of 8) takes the vectorised specialised epilogue instead of the generic one (N = V = 514)
+        K.gemm(xf, Wlm, R, Vp, d, C=logits_buf)
         sv.Wlm, sv.logits_buf, sv.Vp = Wlm, logits_buf, Vp
         out = logits.view(B, T, V)
     else:
@@ -170,9 +172,11 @@ def backward(m, sv, g_out, slot, mid_hook=None):
     nb = len(sv.blocks)
     if sv.generate:
         Vp = sv.Vp
-        gl = torch.zeros(R, Vp, device=dev, dtype=T_)
-        # strided cast into the zero-padded operand: GEMM epilogue with an empty contraction (v = 0 + resid)
-        K.gemm(gl, gl, R, V, 0, resid=g_out.reshape(R, V).contiguous(), C=gl[:, :V])
+        gl = getattr(sv, "gl", None)      # fused_step: the cross-entropy backward already wrote the padded operand
+        if gl is None:
+            gl = torch.zeros(R, Vp, device=dev, dtype=T_)
+            # strided cast into the zero-padded operand: GEMM epilogue with an empty contraction (v = 0 + resid)
+            K.gemm(gl, gl, R, V, 0, resid=g_out.reshape(R, V).contiguous(), C=gl[:, :V])
         # lm_head weight gradient [V][d] and input gradient (K padded to Vp with zero rows/columns)
         K.gemm(gl[:, :V], sv.xf, V, d, R, a_trans=True, b_trans=True, C=slot(m.lm_head.weight), accumulate=True)
         gxf = e(R, d)
@@ -319,7 +323,14 @@ def fused_step(m, batch, scale, slot, mid_hook=None):
     loss = torch.empty((), device=dev)
     K.ce_finalize(sums[0:1], sums[1:2], loss)
     g = torch.full((1,), float(scale), device=dev)
-    dl = torch.empty(R, V, device=dev)
+    if generate:
+        # the logits gradient straight into the zero-padded [R][Vp] operand of the lm_head GEMMs, in the operand
+        # dtype (aw_ce_bwd zeroes the padding columns): no f32 copy, no strided cast launch
+        gl = torch.empty(R, sv.Vp, device=dev, dtype=sv.Tdt)
+        dl = gl[:, :V]
+        sv.gl = gl
+    else:
+        dl = torch.empty(R, V, device=dev)
     K.ce_bwd(logits2d, V, target, ignore, lse, sums[1:2], g, dl)
     backward(m, sv, dl.view(out.shape), slot, mid_hook=mid_hook)
     return loss, out
