@@ -136,14 +136,16 @@ __global__ __launch_bounds__(256) void ln_fwd_vec_kernel(const float* __restrict
 }
 
 template <typename T2, int NV>
-__global__ __launch_bounds__(256) void ln_bwd_vec_kernel(const float* __restrict__ x, const float* __restrict__ dy,
+__global__ __launch_bounds__(512) void ln_bwd_vec_kernel(const float* __restrict__ x, const float* __restrict__ dy,
                                                          int64_t R, int D, const float* __restrict__ w,
                                                          const float* __restrict__ mean,
                                                          const float* __restrict__ rstd, float* __restrict__ dx,
                                                          int accumulate, float* __restrict__ dw,
                                                          float* __restrict__ db, T2* __restrict__ dx2, float drop_p,
                                                          uint64_t drop_seed, const uint64_t* __restrict__ seed_ptr) {
-  __shared__ float red[4][2][256 * NV];
+  // per-wave dw / db partials [wave][2][256 NV] (dynamic: blockDim.x / 64 waves), reduced in wave order at the end
+  extern __shared__ float red[];
+  const int nwv = blockDim.x >> 6;
   drop_seed = aw_seed_mix(drop_seed, seed_ptr);
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -232,15 +234,21 @@ __global__ __launch_bounds__(256) void ln_bwd_vec_kernel(const float* __restrict
       }
     }
   }
+  constexpr int C = 256 * NV;
 #pragma unroll
   for (int j = 0; j < NV; ++j) {
-    *reinterpret_cast<float4*>(&red[wv][0][4 * lane + 256 * j]) = pdw[j];
-    *reinterpret_cast<float4*>(&red[wv][1][4 * lane + 256 * j]) = pdb[j];
+    *reinterpret_cast<float4*>(&red[(wv * 2 + 0) * C + 4 * lane + 256 * j]) = pdw[j];
+    *reinterpret_cast<float4*>(&red[(wv * 2 + 1) * C + 4 * lane + 256 * j]) = pdb[j];
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < 256 * NV; i += 256) {
-    atomicAdd(dw + i, (red[0][0][i] + red[1][0][i]) + (red[2][0][i] + red[3][0][i]));
-    atomicAdd(db + i, (red[0][1][i] + red[1][1][i]) + (red[2][1][i] + red[3][1][i]));
+  for (int i = threadIdx.x; i < C; i += blockDim.x) {
+    float a = 0.f, b = 0.f;
+    for (int v = 0; v < nwv; ++v) {
+      a += red[(v * 2 + 0) * C + i];
+      b += red[(v * 2 + 1) * C + i];
+    }
+    atomicAdd(dw + i, a);
+    atomicAdd(db + i, b);
   }
 }
 
@@ -804,14 +812,21 @@ extern "C" int aw_layernorm_bwd(const float* x, const float* dy, int64_t R, int 
   // so more workgroups contend on those 2D addresses: 256 measured best at 16371 x 512 (29.4 us, 5.1 TB/s; 512:
   // 32.5 us, 1024: 40.1 us; tools/probe/ln_probe.py)
   static const int cap = [] { const char* e = getenv("AW_LN_BWD_BLOCKS"); return e ? atoi(e) : 256; }();
-  dim3 grid(gridcap(R * 64, 256, cap));
+  // waves per workgroup of the vectorised kernel (AW_LN_BWD_WAVES: 8, the kernel's launch bound, or 4): more waves
+  // keep more row loads in flight per CU at the same number of end-of-kernel dw / db atomics (8 vs 4: decoder step
+  // 5.462 vs 5.520 ms, same box)
+  static const int lnw = [] {
+    const char* e = getenv("AW_LN_BWD_WAVES");
+    return e && atoi(e) == 4 ? 4 : 8;
+  }();
+  dim3 grid(gridcap(R * 64, 64 * lnw, cap));
 #define AW_LNB(NV)                                                                                               \
   if (dx2_dtype == AW_BF16)                                                                                      \
-    hipLaunchKernelGGL((ln_bwd_vec_kernel<bf16, NV>), grid, dim3(256), 0, s, x, dy, R, D, w, mean, rstd, dx,      \
-                       accumulate, dw, db, (bf16*)dx2, drop_p, drop_seed, seed_ptr);                                       \
+    hipLaunchKernelGGL((ln_bwd_vec_kernel<bf16, NV>), grid, dim3(64 * lnw), lnw * 2 * 256 * NV * 4, s, x, dy, R, \
+                       D, w, mean, rstd, dx, accumulate, dw, db, (bf16*)dx2, drop_p, drop_seed, seed_ptr);         \
   else                                                                                                           \
-    hipLaunchKernelGGL((ln_bwd_vec_kernel<float, NV>), grid, dim3(256), 0, s, x, dy, R, D, w, mean, rstd, dx,     \
-                       accumulate, dw, db, (float*)dx2, drop_p, drop_seed, seed_ptr);                                      \
+    hipLaunchKernelGGL((ln_bwd_vec_kernel<float, NV>), grid, dim3(64 * lnw), lnw * 2 * 256 * NV * 4, s, x, dy,   \
+                       R, D, w, mean, rstd, dx, accumulate, dw, db, (float*)dx2, drop_p, drop_seed, seed_ptr);    \
   return aw::check_launch("aw_layernorm_bwd");
   const bool al = (((uintptr_t)x | (uintptr_t)dy | (uintptr_t)w | (uintptr_t)dx | (uintptr_t)dx2) & 15) == 0;
   if (al && D == 256) { AW_LNB(1) }
