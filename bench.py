@@ -51,6 +51,9 @@ def parse():
     ap.add_argument("--n-cycles", type=int, default=20)
     ap.add_argument("--only", default="all", choices=["all", "transformer_pretokenized"],
                     help="profiling aid: run one sub-line alone (the PMC passes of tools/prof_transformer.sh)")
+    ap.add_argument("--detail", default="gpurun_out/bench_detail.json",
+                    help="where the full record (every sub-line with its per-kernel objects) is written; the printed "
+                         "line keeps the compact form (empty: no file)")
     ap.add_argument("--gemm-tile", type=int, default=0, choices=[0, 128, 256],
                     help="GEMM tile policy (aw_gemm_set_tile): 0 = automatic")
     return ap.parse_args()
@@ -473,6 +476,62 @@ def _transformer_lines(extra, dev, rank, world, args):
                                                              label="configs[2], the reference's regime")
 
 
+_ROOF_KEYS = ("bound", "achieved", "peak", "unit", "frac", "traffic", "traffic_unit", "traffic_source", "kernel",
+              "launches_per_step", "avg_launch_us", "avg_algorithmic_gflop_per_launch", "gemm_ms_per_step")
+
+
+def _compact_roof(r, keys=_ROOF_KEYS):
+    return None if r is None else {k: r[k] for k in keys if k in r}
+
+
+def _sub(d):
+    """One secondary line as {value, unit, ms_per_step, frac[, attention fracs]}."""
+    out = {"value": d["value"], "unit": d["unit"], "ms_per_step": d["ms_per_step"]}
+    r = d.get("roofline")
+    if r:
+        out["gemm_frac"] = r["frac"]
+        if "tokenize_gemm_f32" in r:
+            out["tokenize_gemm_f32_frac"] = r["tokenize_gemm_f32"]["frac"]
+    for tag, a in (d.get("attention") or {}).items():
+        out[f"{tag}_us"] = a["avg_launch_us"]
+        out[f"{tag}_frac"] = a["frac"]
+    return out
+
+
+def compact_line(line, detail):
+    """The printed JSON line: the contract keys, the headline roofline and CPU baseline, and one short summary per
+    secondary line LAST (the driver keeps the tail of stdout); the full record goes to `detail`."""
+    out = {k: v for k, v in line.items() if k not in ("vq_kernel", "fp32", "stress", "transformer",
+                                                      "transformer_b16_acc5", "transformer_t257",
+                                                      "transformer_pretokenized", "roofline", "cpu_baseline")}
+    out["roofline"] = _compact_roof(line.get("roofline"))
+    cpu = line.get("cpu_baseline")
+    if cpu:
+        out["cpu_baseline"] = {k: cpu[k] for k in ("value", "unit", "cores", "kind", "sample", "cpu_model")}
+        out["cpu_baseline"]["reference"] = {k: REFERENCE_CPU[k] for k in ("value", "unit", "cores", "kind")}
+    out["detail_file"] = detail or None
+    lines = {}
+    if "vq_kernel" in line:
+        v = line["vq_kernel"]
+        lines["vq_kernel"] = {"us": v["avg_launch_us"], "frac": v["frac"], "bound": v["bound"]}
+    if "fp32" in line:
+        f = line["fp32"]
+        lines["fp32"] = {"value": f["value"], "unit": f["unit"], "ms_per_step": f["ms_per_step"],
+                         "gemm_frac_of_fp32_peak": f["roofline"]["frac"] if f.get("roofline") else None}
+    st = line.get("stress")
+    if st:
+        lines["stress_vqvae"] = {"value": st["vqvae"]["value"], "unit": "windows/s",
+                                 "ms_per_step": st["vqvae"]["ms_per_step"],
+                                 "gemm_frac": st["vqvae"]["roofline"]["frac"] if st["vqvae"].get("roofline") else None,
+                                 "vq_kernel_frac": st["vqvae"]["vq_kernel"]["frac"]}
+        lines["stress_transformer"] = _sub(st["transformer"])
+    for k in ("transformer", "transformer_b16_acc5", "transformer_t257", "transformer_pretokenized"):
+        if k in line:
+            lines[k] = _sub(line[k])
+    out["lines"] = lines
+    return out
+
+
 def main():
     args = parse()
     distributed = int(os.environ.get("WORLD_SIZE", "1")) > 1
@@ -546,7 +605,12 @@ def main():
                            "operands": "bf16 (opt-in), fp32 accumulation and master weights"},
                 "roofline": roofline, "cpu_baseline": cpu, **extra,
                 "launch": "eager" if args.no_graph else "hip-graph"}
-        print(json.dumps(line), flush=True)
+        detail = os.path.join(REPO, args.detail) if args.detail else None
+        if detail:
+            os.makedirs(os.path.dirname(detail), exist_ok=True)
+            with open(detail, "w") as f:
+                json.dump(line, f, indent=1)
+        print(json.dumps(compact_line(line, args.detail)), flush=True)
     if distributed:
         dist.destroy_process_group()
 

@@ -1,0 +1,119 @@
+"""The data-parallel step on the real RCCL backend (train_transformer_mtasks.py:31,87,149-153: DDP over
+NCCL).  One GPU box holds one device, and RCCL refuses two ranks per device, so the group has ONE rank -- but every
+collective of the path still runs through RCCL: ARCWELD_FORCE_COLLECTIVES=1 keeps the bucketed all-reduce on at
+world size 1 (arcweld/trainer.py), so the async work handles, RCCL's own stream and the waits run between the
+split graph replays exactly as they do on 8 GPUs (arcweld/graphs.py: late region between g1a and g1b, early after).
+
+A one-rank SUM is the identity, which cannot show a stream-ordering error.  So the test swaps in RCCL's pre-multiplied
+sum with factor 2 and trains with loss scale 1/2: every gradient is exact (powers of two), and the update equals a
+plain run's only if each all-reduce reads the FINISHED gradients of its region (a collective that overtook the
+backward would double a partial gradient) and the update waits for every one of them (an update that overtook a
+collective would see half of a gradient).  Reference: the same steps with no process group and scale 1."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from oracle import decoder as od
+from oracle import gen
+from oracle import vqvae as ov
+
+pytestmark = pytest.mark.gpu
+
+VQ_KW = dict(hidden_dim=512, num_embeddings=512, embedding_dim=64, n_resblocks=8, patch_size=25)
+DEC_KW = dict(d_model=512, n_classes=514, seq_len=129, n_blocks=8)
+STEPS = 6          # one eager step, two eager warm-up calls of graphed_step, the capture, two replays
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _make(name):
+    if name == "vqvae":
+        from model.vq_vae_patch_embedd import VQVAEPatch
+        m = VQVAEPatch(input_dim=2, learning_rate=1e-3, dropout_p=0.0, batch_norm=False, **VQ_KW)
+        sd = ov.det_state_dict(ov.VQVAEConfig(**VQ_KW), 2101)
+    else:
+        from model.transformer_decoder import MyTransformerDecoder
+        m = MyTransformerDecoder(n_head=8, res_dropout=0.0, att_dropout=0.0, **DEC_KW)
+        sd = od.det_state_dict(2102, **DEC_KW)
+    m.load_state_dict({k: torch.tensor(v) for k, v in sd.items()})
+    return m.cuda().train()
+
+
+def _batches(name):
+    if name == "vqvae":
+        return [torch.tensor(gen.windows(2110 + s, 128)).cuda() for s in range(STEPS)]
+    out = []
+    for s in range(STEPS):
+        ids = torch.tensor(gen.randint(2120 + s, (8, DEC_KW["seq_len"] + 1), 0, DEC_KW["n_classes"] - 2)).cuda()
+        out.append((ids[:, :-1].contiguous(), torch.zeros(8, dtype=torch.long, device="cuda"), ids[:, 1:].contiguous()))
+    return out
+
+
+def _train(name, scale):
+    from arcweld.precision import operands
+    from arcweld.trainer import Trainer
+    with operands(torch.float32):     # exact-f32 operands: no bf16 rounding flip can amplify an atomics ULP
+        m = _make(name)
+        tr = Trainer(gradient_clip_val=0.7 if name == "vqvae" else 0.8)
+        tr.setup_optimizer(m)
+        for s, b in enumerate(_batches(name)):
+            if s == 0:
+                tr.micro_step(m, b, 0, scale)
+                tr.optimizer_step(m)
+            else:
+                tr.graphed_step(m, b, scale)
+        torch.cuda.synchronize()
+        return {k: v.detach().cpu().clone() for k, v in m.named_parameters()}
+
+
+def _worker(rank, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), ARCWELD_FORCE_COLLECTIVES="1")
+    torch.cuda.set_device(0)
+    for name in ("vqvae", "decoder"):     # the plain run first, before any process group exists
+        out[("plain", name)] = _train(name, 1.0)
+    dist.init_process_group("nccl", rank=rank, world_size=1, device_id=torch.device("cuda", 0))
+    out["backend"] = dist.get_backend()
+    orig = dist.all_reduce
+    premul = dist._make_nccl_premul_sum(2.0)
+    calls = []
+
+    def doubling_all_reduce(t, op=dist.ReduceOp.SUM, group=None, async_op=False):
+        calls.append(t.numel())
+        return orig(t, op=premul, group=group, async_op=async_op)
+
+    dist.all_reduce = doubling_all_reduce
+    try:
+        probe = torch.ones(4, device="cuda")
+        dist.all_reduce(probe)           # the factor is applied by RCCL itself
+        torch.cuda.synchronize()
+        out["probe"] = probe.cpu().tolist()
+        for name in ("vqvae", "decoder"):
+            n0 = len(calls)
+            out[("rccl", name)] = _train(name, 0.5)
+            out[("calls", name)] = len(calls) - n0
+    finally:
+        dist.all_reduce = orig
+        dist.destroy_process_group()
+
+
+def test_rccl_one_rank_graphed_steps_match_plain_run():
+    port = _free_port()
+    out = mp.get_context("spawn").Manager().dict()
+    mp.spawn(_worker, args=(port, out), nprocs=1, join=True)
+    assert out["backend"] == "nccl"
+    assert out["probe"] == [2.0] * 4
+    for name in ("vqvae", "decoder"):
+        # eager step + 2 warm-up calls: one region each; captured replays: late + early regions, several buckets
+        assert out[("calls", name)] >= STEPS + 2, (name, out[("calls", name)])
+        ref, got = out[("plain", name)], out[("rccl", name)]
+        assert sorted(ref) == sorted(got)
+        for k, v in ref.items():
+            torch.testing.assert_close(got[k], v, rtol=1e-6, atol=1e-6, msg=f"{name} {k}")

@@ -5,6 +5,7 @@ current torch stream and raises on a non-zero status.  No wrapper has a CPU path
 """
 from __future__ import annotations
 
+import contextvars
 import ctypes
 
 import torch
@@ -27,7 +28,9 @@ def _ld(t):
 
 # Epilogue store policy of the GEMMs issued inside a `store_policy(...)` block (aw_gemm_args.store_policy):
 # nat.AW_STORE_NT (default) or nat.AW_STORE_WT (write-through: the VQ-VAE step, see arcweld/vqvae.py).
-_STORE_POLICY = [0]
+# The policy is context-local (a ContextVar): GEMMs issued from another thread, or from a callback that resets it
+# (the VQ-VAE backward's mid_hook), keep their own.
+_STORE_POLICY = contextvars.ContextVar("arcweld_store_policy", default=0)
 
 
 class store_policy:
@@ -37,11 +40,10 @@ class store_policy:
         self.policy = int(policy)
 
     def __enter__(self):
-        self._prev = _STORE_POLICY[0]
-        _STORE_POLICY[0] = self.policy
+        self._tok = _STORE_POLICY.set(self.policy)
 
     def __exit__(self, *exc):
-        _STORE_POLICY[0] = self._prev
+        _STORE_POLICY.reset(self._tok)
         return False
 
     def __call__(self, fn):
@@ -86,7 +88,7 @@ def _gemm_args(A, B, M, N, K, *, a_trans=False, b_trans=False, conv=None, alpha=
     a.alpha, a.beta = float(alpha), float(beta)
     a.bias = ptr(bias)
     a.act = int(act)
-    a.store_policy = _STORE_POLICY[0]
+    a.store_policy = _STORE_POLICY.get()
     a.pre, a.ld_pre = ptr(pre), _ld(pre)
     if pre is not None:
         if pre.dtype not in (torch.float32, torch.bfloat16):
@@ -299,8 +301,14 @@ def unpatch_head_bwd2(y, Q, stats, w2, g_xhat, gsums, training, g_y, db_y, strea
 
 def unpatch_head_fwd_bwd1(y, Q, stats, w2, b2, x, gscale, x_hat, g_xhat, sqerr, gsums, gw2, gb2, ggamma, gbeta,
                           stream=None):
-    """Fused training-step head: forward + MSE value / gradient + backward pass 1 in one read of y (H == 512)."""
+    """Fused training-step head: forward + MSE value / gradient + backward pass 1 in one read of y (H == 512).
+    The kernel reads x, x_hat and g_xhat as R*5 contiguous f32 values (its buffer range check would silently
+    return zeros for a shorter x), so their sizes are checked here."""
     R, H = y.shape
+    for nm, t in (("x", x), ("x_hat", x_hat), ("g_xhat", g_xhat)):
+        if t.dtype != torch.float32 or not t.is_contiguous() or t.numel() != R * 5:
+            raise nat.NativeError(f"unpatch_head_fwd_bwd1: {nm} must be a contiguous float32 tensor of R*5 = {R * 5} "
+                                  f"elements (got {tuple(t.shape)} {t.dtype}, contiguous={t.is_contiguous()})")
     call("aw_unpatch_head_fwd_bwd1", ptr(y), dtype_code(y.dtype), R, H, Q, ptr(stats), ptr(w2), ptr(b2), ptr(x),
          ptr(gscale), ptr(x_hat), ptr(g_xhat), ptr(sqerr), ptr(gsums), ptr(gw2), ptr(gb2), ptr(ggamma), ptr(gbeta),
          stream_ptr(stream))

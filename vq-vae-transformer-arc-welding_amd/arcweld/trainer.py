@@ -31,11 +31,20 @@ def world():
     return dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
 
 
+def _collectives_off():
+    """No collective at world size 1 -- unless ARCWELD_FORCE_COLLECTIVES=1 under an initialised process group: the
+    RCCL test (tests/test_rccl_gpu.py) runs the bucketed all-reduce on a one-rank RCCL group, so the async work
+    handles and their stream ordering against the captured step graphs run on the real backend."""
+    if world() > 1:
+        return False
+    return not (os.environ.get("ARCWELD_FORCE_COLLECTIVES") == "1" and dist.is_available() and dist.is_initialized())
+
+
 def allreduce_flat(flat: torch.Tensor, bucket: int = BUCKET_ELEMS, lo: int = 0, hi: int = None, wait: bool = True):
     """SUM all-reduce of flat[lo:hi] in large buckets (RCCL rings are link-bound; few large messages).  With
     wait=False the async work handles are returned (the collectives are ordered after the work already queued on
     the current stream and run on RCCL's stream)."""
-    if world() == 1:
+    if _collectives_off():
         return []
     hi = flat.numel() if hi is None else hi
     works = [dist.all_reduce(flat[o:min(o + bucket, hi)], async_op=True) for o in range(lo, hi, bucket)]
@@ -48,7 +57,7 @@ def allreduce_flat(flat: torch.Tensor, bucket: int = BUCKET_ELEMS, lo: int = 0, 
 
 def allreduce_spans(flat: torch.Tensor, spans, bucket: int = BUCKET_ELEMS):
     """Async SUM all-reduce of the [a, b) ranges of a flat buffer, each cut into buckets; returns the work handles."""
-    if world() == 1:
+    if _collectives_off():
         return []
     return [dist.all_reduce(flat[o:min(o + bucket, b)], async_op=True) for a, b in spans for o in range(a, b, bucket)]
 
@@ -122,15 +131,26 @@ class Trainer:
             broadcast_params(model, opt)
         if hasattr(model, "operand_set") and hasattr(opt, "attach_operands"):
             opt.attach_operands(model.operand_set())     # the update kernel keeps the GEMM operand copies current
-        for mod in model.modules():
-            if hasattr(mod, "sync_codebooks"):
-                # residual-VQ codebooks synchronise across ranks only when the ranks train one model together
-                mod.sync_codebooks = bool(self.data_parallel)
+        # residual-VQ codebooks synchronise across ranks only when the ranks train one model together: a devices=1
+        # Trainer under an initialised process group turns the sync off for the time it trains the model
+        # (teardown() restores the previous setting, so a model later trained data-parallel by other code is not
+        # left with drifting per-rank codebooks); data-parallel mode leaves it to follow the process group
+        self.teardown()
+        self._sync_saved = [(mod, mod.sync_codebooks) for mod in model.modules() if hasattr(mod, "sync_codebooks")]
+        for mod, _ in self._sync_saved:
+            mod.sync_codebooks = None if self.data_parallel else False
         self.optimizer = opt
         self._graphs = None          # a captured step belongs to one optimizer
         self._graph_shape = None
         self._late_key = None        # the late/early all-reduce spans follow this optimizer's flat offsets
         return opt
+
+    def teardown(self):
+        """Restore what setup_optimizer changed on the model outside the optimizer (the residual-VQ codebook
+        sync mode); fit() calls it when training ends."""
+        for mod, prev in getattr(self, "_sync_saved", ()):
+            mod.sync_codebooks = prev
+        self._sync_saved = []
 
     def micro_step(self, model, batch, batch_idx, scale):
         out = model.training_step(batch, batch_idx)
@@ -258,6 +278,7 @@ class Trainer:
             if self.should_stop or 0 < self.max_steps <= self.global_step:
                 break
         model._grad_sink = None
+        self.teardown()
         return self
 
     @torch.no_grad()

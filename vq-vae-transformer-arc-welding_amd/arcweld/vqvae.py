@@ -577,7 +577,8 @@ def backward(m, sv, g_emb, g_xhat, slot, mid_hook=None):
         K.vq_backward(sv.z, pr["E"], sv.idx, gzq, g_emb, m.vector_quantization.beta, dz, slot(pr["E"]),
                       dz_copy=None if T == F32 else dz_T)
     if mid_hook is not None:
-        mid_hook()
+        with K.store_policy(nat.AW_STORE_NT):     # the hook's own launches (e.g. collectives) keep the default policy
+            mid_hook()
     if dz_T is None:
         dz_T = _cast(dz, T)
 

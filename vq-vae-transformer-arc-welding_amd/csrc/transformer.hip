@@ -834,11 +834,13 @@ extern "C" int aw_layernorm_bwd(const float* x, const float* dy, int64_t R, int 
   if (al && D == 768) { AW_LNB(3) }
   if (al && D == 1024) { AW_LNB(4) }
 #undef AW_LNB
+  // the generic kernel runs 256-thread workgroups: its grid is sized for them, not for the 64*lnw-thread vector form
+  const dim3 grid1(gridcap(R * 64, 256, cap));
   if (dx2_dtype == AW_BF16)
-    hipLaunchKernelGGL(ln_bwd_kernel<bf16>, grid, dim3(256), 2 * D * sizeof(float), s, x, dy, R, D, w, mean, rstd, dx,
+    hipLaunchKernelGGL(ln_bwd_kernel<bf16>, grid1, dim3(256), 2 * D * sizeof(float), s, x, dy, R, D, w, mean, rstd, dx,
                        accumulate, dw, db, (bf16*)dx2, drop_p, drop_seed, seed_ptr);
   else
-    hipLaunchKernelGGL(ln_bwd_kernel<float>, grid, dim3(256), 2 * D * sizeof(float), s, x, dy, R, D, w, mean, rstd, dx,
+    hipLaunchKernelGGL(ln_bwd_kernel<float>, grid1, dim3(256), 2 * D * sizeof(float), s, x, dy, R, D, w, mean, rstd, dx,
                        accumulate, dw, db, (float*)dx2, drop_p, drop_seed, seed_ptr);
   return aw::check_launch("aw_layernorm_bwd");
 }
