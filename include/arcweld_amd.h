@@ -43,7 +43,7 @@ int aw_version(void);
  *   conv_operand = 1 (B, b_trans = 1): N = 3*conv_cin, B[k][j*cin+i] = src[(k + (j-1))*ldb + i], same mask.
  * Epilogue, per element (row r, col c), in this order:
  *   v = alpha*acc;  v += bias[c] (bias[c % bias_mod] if bias_mod > 0);  v *= act'(pre[r*ld_pre + c]) (pre f32/bf16);  v *= dropout(drop_seed, r*N+c, drop_p);
- *   v += resid[r*ld_resid + c];  v += beta * C_old (C must be f32 when beta != 0);  C[r*ldc + c] = v (c_dtype)
+ *   v += resid[r*ld_resid + c] (resid f32/bf16);  v += beta * C_old (C must be f32 when beta != 0);  C[r*ldc + c] = v (c_dtype)
  *   C2 (c2_mode): 1 = act(v), 2 = v, 3 = v * dropout(drop2_seed, r*N+c, drop2_p); stored as c2_dtype
  *   colstats (f64, 2*stats_mod): += v and v*v into slot (c % stats_mod)      (BatchNorm batch statistics)
  *   a_rowsum (f32, M): += sum_k A[m][k]                                      (bias gradients, fused)
@@ -80,6 +80,9 @@ typedef struct {
    * end-of-kernel release writes them back) or AW_STORE_WT (1, write-through: the lines leave L2 at once, so the
    * next dependent launch does not wait for that write-back; the VQ-VAE step's GEMM chain, +3 % per step). */
   int store_policy;
+  /* dtype of `resid` (AW_F32 or AW_BF16): the bf16-mode VQ-VAE keeps its ResBlock residual streams (activations and
+   * their gradients) in bf16, as autocast would (model/vq_vae_patch_embedd.py:73-74 under bf16 autocast) */
+  int resid_dtype;
 } aw_gemm_args;
 #define AW_STORE_NT 0
 #define AW_STORE_WT 1

@@ -147,6 +147,69 @@ def test_gemm_implicit_conv3(K, tile, dtype):
     torch.testing.assert_close(G.cpu(), Wg.grad, rtol=rtol, atol=atol * 30)
 
 
+@pytest.mark.parametrize("conv", [False, True], ids=["plain", "conv3"])
+@pytest.mark.parametrize("p_drop", [0.0, 0.2])
+def test_gemm_bf16_residual_stream_epilogues(K, tile, conv, p_drop):
+    """The bf16-mode ResBlock residual launches with bf16 residual streams (aw_gemm_args.resid_dtype; arcweld/vqvae.py
+    resid_dtype): forward  y = x + drop(A.W^T + b) -> C (bf16) and GELU(y) (bf16);  input gradient
+    gx' = gx + (g.W) * GELU'(x) -> C (bf16) with the dropout-masked / plain bf16 copy; and the first gradient launch
+    C (bf16) + masked copy.  Each against the same launch with an f32 residual stream (bit-identical f32 math, so the
+    bf16 outputs equal the f32 outputs rounded) and against torch fp32 at p = 0."""
+    bf = torch.bfloat16
+    Bw, S, Cin, Cout = 16, 16, 128, 128
+    M = Bw * S
+    cv = (Cin, S, 1, 0) if conv else None
+    Kd = 3 * Cin if conv else Cin
+    A = _rand((M, Cin), 61, bf)
+    W = _rand((Cout, Kd), 62, bf, 0.05)
+    bias = _rand((Cout,), 63)
+    x = _rand((M, Cout), 64, bf)
+    outs = {}
+    for rdt in (torch.float32, bf):
+        C = torch.empty(M, Cout, device=DEV, dtype=rdt)
+        C2 = torch.empty(M, Cout, device=DEV, dtype=bf)
+        K.gemm(A, W, M, Cout, Kd, conv=cv, bias=bias, drop=(p_drop, 77), resid=x.to(rdt), C=C, C2=C2, c2_mode=1)
+        outs[rdt] = (C, C2)
+    torch.testing.assert_close(outs[bf][0], outs[torch.float32][0].to(bf), rtol=0, atol=0)
+    torch.testing.assert_close(outs[bf][1], outs[torch.float32][1], rtol=0, atol=0)
+    if p_drop == 0.0:
+        if conv:
+            xr = A.float().cpu().view(Bw, S, Cin).transpose(1, 2)
+            Wr = W.float().cpu().view(Cout, 3, Cin).permute(0, 2, 1)
+            acc = F.conv1d(xr, Wr, padding=1).transpose(1, 2).reshape(M, Cout)
+        else:
+            acc = A.float().cpu() @ W.float().cpu().t()
+        v = acc + bias.cpu() + x.float().cpu()
+        torch.testing.assert_close(outs[bf][0].float().cpu(), v, rtol=8e-3, atol=2e-2)
+    # input gradient: C = gx + (g . W) * GELU'(x), C2 = masked (drop2) or plain copy
+    Wd = _rand((Cout if not conv else 3 * Cout, Cin), 66, bf, 0.05)
+    gx = _rand((M, Cin), 67, bf)
+    pre = _rand((M, Cin), 68, bf)
+    dcv = (Cout, S, -1, 0) if conv else None
+    Kb = 3 * Cout if conv else Cout
+    g = _rand((M, Cout), 65, bf)
+    for mode in (2, 3):
+        res = {}
+        for rdt in (torch.float32, bf):
+            C = torch.empty(M, Cin, device=DEV, dtype=rdt)
+            C2 = torch.empty(M, Cin, device=DEV, dtype=bf)
+            K.gemm(g, Wd, M, Cin, Kb, b_trans=True, conv=dcv, pre=pre.to(rdt), resid=gx.to(rdt), C=C, C2=C2,
+                   c2_mode=mode, drop2=(p_drop, 78))
+            res[rdt] = (C, C2)
+        torch.testing.assert_close(res[bf][0], res[torch.float32][0].to(bf), rtol=0, atol=0)
+        torch.testing.assert_close(res[bf][1], res[torch.float32][1], rtol=0, atol=0)
+    if not conv:
+        # the first gradient launch of a stack: C (bf16) + masked copy, no residual
+        res = {}
+        for rdt in (torch.float32, bf):
+            C = torch.empty(M, Cin, device=DEV, dtype=rdt)
+            C2 = torch.empty(M, Cin, device=DEV, dtype=bf)
+            K.gemm(g, Wd, M, Cin, Kb, b_trans=True, C=C, C2=C2, c2_mode=3, drop2=(p_drop, 79))
+            res[rdt] = (C, C2)
+        torch.testing.assert_close(res[bf][0], res[torch.float32][0].to(bf), rtol=0, atol=0)
+        torch.testing.assert_close(res[bf][1], res[torch.float32][1], rtol=0, atol=0)
+
+
 @pytest.mark.parametrize("tag,Kc,D,N,eseed,estd", [
     ("K512_D64_init", 512, 64, 16384, 201, None),
     ("K512_D64_trained", 512, 64, 16384, 202, 0.08),

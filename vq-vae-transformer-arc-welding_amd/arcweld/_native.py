@@ -49,6 +49,7 @@ class GemmArgs(ctypes.Structure):
         ("seed_ptr", c_p),
         ("pre_dtype", c_int),
         ("store_policy", c_int),
+        ("resid_dtype", c_int),
     ]
 
 

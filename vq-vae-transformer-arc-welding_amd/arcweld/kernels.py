@@ -95,6 +95,10 @@ def _gemm_args(A, B, M, N, K, *, a_trans=False, b_trans=False, conv=None, alpha=
             raise nat.NativeError("pre must be float32 or bfloat16")
         a.pre_dtype = dtype_code(pre.dtype)
     a.resid, a.ld_resid = ptr(resid), _ld(resid)
+    if resid is not None:
+        if resid.dtype not in (torch.float32, torch.bfloat16):
+            raise nat.NativeError("resid must be float32 or bfloat16")
+        a.resid_dtype = dtype_code(resid.dtype)
     a.drop_p, a.drop_seed = float(drop[0]), int(drop[1]) & 0xFFFFFFFFFFFFFFFF
     if C is not None:
         a.C, a.ldc, a.c_dtype = ptr(C), _ld(C), dtype_code(C.dtype)

@@ -74,6 +74,18 @@ def accumulators(m, dev, K, H, zero=True):
                 counts=buf[2 + 4 * H:].view(torch.float32)[:K])
 
 
+def resid_dtype(m, T):
+    """dtype of the ResBlock residual streams (the activations x, y and their gradients) of the fused step.
+
+    Exact-fp32 operands keep them in fp32 (the reference's numerics).  In the bf16 operand mode they are bf16, which
+    is what the reference under bf16 autocast holds: its conv outputs are bf16, so x + block(x) and its gradient are
+    bf16 tensors (model/vq_vae_patch_embedd.py:73-74) -- half the epilogue bytes of the 32 residual launches per step.
+    ``--batchnorm 1`` keeps fp32 streams (its BatchNorm kernels read f32), as does ARCWELD_RESID_F32=1 (A/B)."""
+    if T == F32 or m.batch_norm or os.environ.get("ARCWELD_RESID_F32", "0") == "1":
+        return F32
+    return T
+
+
 class VQVAEShapes:
     def __init__(self, m, B):
         self.B = B
@@ -268,6 +280,7 @@ def forward(m, x, training: bool, need_backward: bool, dtype=None, seed: int = 0
     e = lambda *s, dt=F32: torch.empty(*s, device=dev, dtype=dt)  # noqa: E731
     sv = Saved()
     sv.sh, sv.T, sv.p_drop, sv.training = sh, T, p_drop, training
+    RT = sv.RT = resid_dtype(m, T)
     sv.enc_seed = [_mix(seed, 100 + r) for r in range(R)]
     sv.dec_seed = [_mix(seed, 200 + r) for r in range(R)]
     acc = accumulators(m, dev, sh.K, H, zero=False)
@@ -292,7 +305,7 @@ def forward(m, x, training: bool, need_backward: bool, dtype=None, seed: int = 0
     # ---- patch embed
     patches = e(N, sh.ldp, dt=T)
     K.patchify(x, P, patches)
-    x0, a0 = e(N, H), e(N, H, dt=T)
+    x0, a0 = e(N, H, dt=RT), e(N, H, dt=T)
     K.gemm(patches, Wp, N, H, sh.ldp, bias=pr["pe"].bias, C=x0, C2=a0, c2_mode=1, flops=2 * N * H * P)
 
     # ---- encoder ResBlocks (per-token: centre taps)
@@ -309,7 +322,7 @@ def forward(m, x, training: bool, need_backward: bool, dtype=None, seed: int = 0
         h, a1 = e(N, H, dt=T), e(N, H, dt=T)   # pre-activation kept in the operand dtype
         K.gemm(a0s[r], enc_w[r][0], N, H, H, bias=c1.bias, C=h, C2=a1, c2_mode=1)
         if r < R - 1:
-            xn, an = e(N, H), e(N, H, dt=T)
+            xn, an = e(N, H, dt=RT), e(N, H, dt=T)
             K.gemm(a1, enc_w[r][1], N, H, H, bias=c2.bias, drop=(p_drop, sv.enc_seed[r]), seed_ptr=sv.ctr,
                    resid=xs[r], C=xn, C2=an,
                    c2_mode=1)
@@ -321,7 +334,7 @@ def forward(m, x, training: bool, need_backward: bool, dtype=None, seed: int = 0
         a0s.append(an)
         hs.append(h)
         a1s.append(a1)
-    xR_T = a0s[R] if R > 0 else (x0 if T == F32 else _cast(x0, T))
+    xR_T = a0s[R] if R > 0 else (x0 if x0.dtype == T else _cast(x0, T))
 
     # ---- SepCNNBlock -> z (B, S, D)
     z = e(N, D)
@@ -348,7 +361,7 @@ def forward(m, x, training: bool, need_backward: bool, dtype=None, seed: int = 0
         zq_T = zq if T == F32 else _cast(zq, T)
 
     # ---- decoder: 1x1 conv + ResBlocks with k=3 convs along the window
-    y0, ya0 = e(N, H), e(N, H, dt=T)
+    y0, ya0 = e(N, H, dt=RT), e(N, H, dt=T)
     K.gemm(zq_T, Wd0, N, H, D, bias=pr["dec0"].bias, C=y0, C2=ya0, c2_mode=1)
     conv = (H, S, 1, 0)
     ys, ya0s, dhs, da1s = [y0], [ya0], [], []
@@ -364,7 +377,7 @@ def forward(m, x, training: bool, need_backward: bool, dtype=None, seed: int = 0
         h, a1 = e(N, H, dt=T), e(N, H, dt=T)   # pre-activation kept in the operand dtype
         K.gemm(ya0s[r], dec_w[r][0], N, H, 3 * H, conv=conv, bias=c1.bias, C=h, C2=a1, c2_mode=1)
         if r < R - 1:
-            yn, an = e(N, H), e(N, H, dt=T)
+            yn, an = e(N, H, dt=RT), e(N, H, dt=T)
             K.gemm(a1, dec_w[r][1], N, H, 3 * H, conv=conv, bias=c2.bias, drop=(p_drop, sv.dec_seed[r]),
                    seed_ptr=sv.ctr, resid=ys[r],
                    C=yn, C2=an, c2_mode=1)
@@ -377,7 +390,7 @@ def forward(m, x, training: bool, need_backward: bool, dtype=None, seed: int = 0
         ya0s.append(an)
         dhs.append(h)
         da1s.append(a1)
-    yR_T = ya0s[R] if R > 0 else (y0 if T == F32 else _cast(y0, T))
+    yR_T = ya0s[R] if R > 0 else (y0 if y0.dtype == T else _cast(y0, T))
 
     # ---- un-patch: ConvT(H->H, k1) with BN statistics in the epilogue, then the fused head
     bn = pr["bn"]
@@ -522,7 +535,8 @@ def backward(m, sv, g_emb, g_xhat, slot, mid_hook=None):
     K.gemm(sv.yR_T, gY2, H, k1 * H, N, a_trans=True, b_trans=True, C=slot(pr["t1"].weight).view(H, H * k1),
            accumulate=True, col_map=(H, k1, 0))
     # ConvT1 input gradient -> grad of the decoder output, plus the dropout-masked operand for its last block
-    gy, go = e(N, H), e(N, H, dt=T)
+    RT = sv.RT
+    gy, go = e(N, H, dt=RT), e(N, H, dt=T)
     last = R - 1
     bnm = m.batch_norm and R > 0    # BatchNorm ResBlocks: each block applies its own dropout mask to gy
     K.gemm(gY2, sv.Wt1, N, H, k1 * H, b_trans=True, C=gy, C2=None if bnm else go, c2_mode=0 if bnm else
@@ -551,7 +565,7 @@ def backward(m, sv, g_emb, g_xhat, slot, mid_hook=None):
         gh = e(N, H, dt=T)
         K.gemm(go, W2d, N, H, 3 * H, b_trans=True, conv=dconv_in, pre=sv.dhs[r], C=gh)
         wgrads.append(wg_dec(c2, go, sv.da1s[r]))
-        gyn, gon = e(N, H), e(N, H, dt=T)
+        gyn, gon = e(N, H, dt=RT), e(N, H, dt=T)
         K.gemm(gh, W1d, N, H, 3 * H, b_trans=True, conv=dconv_in, pre=sv.ys[r], resid=gy, C=gyn, C2=gon,
                c2_mode=3 if r > 0 else 2, drop2=(p_drop, sv.dec_seed[r - 1] if r > 0 else 0),
                seed_ptr=sv.ctr)
@@ -585,7 +599,7 @@ def backward(m, sv, g_emb, g_xhat, slot, mid_hook=None):
     # ---- SepCNNBlock
     K.gemm(dz_T, sv.xR_T, D, H, N, a_trans=True, b_trans=True, C=slot(pr["sep"].weight).view(D, H), accumulate=True,
            a_rowsum=slot(pr["sep"].bias))
-    gx, gxo = e(N, H), e(N, H, dt=T)
+    gx, gxo = e(N, H, dt=RT), e(N, H, dt=T)
     K.gemm(dz_T, sv.Ws, N, H, D, b_trans=True, C=gx, C2=None if bnm else gxo, c2_mode=0 if bnm else
            (3 if R > 0 else 2), drop2=(p_drop, sv.enc_seed[R - 1] if R > 0 else 0), seed_ptr=sv.ctr)
 
@@ -610,7 +624,7 @@ def backward(m, sv, g_emb, g_xhat, slot, mid_hook=None):
         C2w, cm2 = _centre_grad(slot(c2.weight))
         wgrads.append((gxo, sv.a1s[r], H, H, N, dict(a_trans=True, b_trans=True, C=C2w, accumulate=True, col_map=cm2,
                                                      a_rowsum=slot(c2.bias))))
-        gxn, gxon = e(N, H), e(N, H, dt=T)
+        gxn, gxon = e(N, H, dt=RT), e(N, H, dt=T)
         K.gemm(gh, w1, N, H, H, b_trans=True, pre=sv.xs[r], resid=gx, C=gxn, C2=gxon, c2_mode=3 if r > 0 else 2,
                drop2=(p_drop, sv.enc_seed[r - 1] if r > 0 else 0), seed_ptr=sv.ctr)
         C1w, cm1 = _centre_grad(slot(c1.weight))

@@ -33,7 +33,7 @@ uint32_t epi_code(const aw_gemm_args& a, const GemmP& P, bool ragged) {
   if (a.pre) c |= EP_PRE | (a.pre_dtype == AW_BF16 ? EP_PREBF : 0u);
   if ((a.pre || a.c2_mode == 1) && a.act == AW_ACT_GELU_TANH) c |= EP_TANH;
   if (a.drop_p > 0.f) c |= EP_DROP;
-  if (a.resid) c |= EP_RESID;
+  if (a.resid) c |= EP_RESID | (a.resid_dtype == AW_BF16 ? EP_RESIDBF : 0u);
   if (a.beta != 0.f) c |= EP_BETA;
   if (a.C) c |= EP_C | (a.c_dtype == AW_BF16 ? EP_CBF : 0u);
   if (a.c2_mode == 1) c |= EP_C2ACT;
@@ -178,6 +178,7 @@ static int validate(const aw_gemm_args& a) {
   AW_REQUIRE(!(a.c2_mode && !a.C2), "aw_gemm: c2_mode without C2");
   AW_REQUIRE(!(a.colstats && a.stats_mod <= 0), "aw_gemm: colstats needs stats_mod > 0");
   AW_REQUIRE(a.pre_dtype == AW_F32 || a.pre_dtype == AW_BF16, "aw_gemm: bad pre_dtype %d", a.pre_dtype);
+  AW_REQUIRE(a.resid_dtype == AW_F32 || a.resid_dtype == AW_BF16, "aw_gemm: bad resid_dtype %d", a.resid_dtype);
   AW_REQUIRE(a.store_policy == AW_STORE_NT || a.store_policy == AW_STORE_WT, "aw_gemm: bad store_policy %d",
              a.store_policy);
   const bool plain = !a.bias && !a.pre && !a.resid && a.drop_p <= 0.f && !a.C2 && !a.colstats && a.C &&
@@ -240,7 +241,7 @@ static void plan(const aw_gemm_args& a, int ngroups, bool grouped, GemmP& P) {
     return ptr == nullptr || (((uintptr_t)ptr % 16) == 0 && (ld * (dt == AW_BF16 ? 2 : 4)) % 16 == 0);
   };
   P.vec = al(a.C, a.ldc, a.c_dtype) && al(a.C2, a.ldc2, a.c2_dtype) && al(a.pre, a.ld_pre, a.pre_dtype) &&
-          al(a.resid, a.ld_resid, AW_F32);
+          al(a.resid, a.ld_resid, a.resid_dtype);
   const int64_t es = a.a_dtype == AW_BF16 ? 2 : 4;
   const int64_t ka = a.K > 0 ? a.K : 1;
   // a padded transposed operand is read in whole chunks up to its padded width (see is_ragged)

@@ -94,7 +94,7 @@ enum EpiBits : uint32_t {
   EP_BIAS = 1u << 0, EP_BIASMOD = 1u << 1, EP_PRE = 1u << 2, EP_TANH = 1u << 3, EP_DROP = 1u << 4,
   EP_RESID = 1u << 5, EP_BETA = 1u << 6, EP_C = 1u << 7, EP_CBF = 1u << 8, EP_C2ACT = 1u << 9,
   EP_C2COPY = 1u << 10, EP_C2DROP = 1u << 11, EP_C2BF = 1u << 12, EP_STATS = 1u << 13, EP_ACCUM = 1u << 14,
-  EP_PREBF = 1u << 15, EP_GENERIC = 1u << 31
+  EP_PREBF = 1u << 15, EP_RESIDBF = 1u << 16, EP_GENERIC = 1u << 31
 };
 
 // Diagnostic phase stamps (tools/probe only: defined there before this file is included; never in the library).
@@ -711,6 +711,7 @@ __global__ __launch_bounds__(Cfg<BMT>::NTH, RAGGED ? 1 : Cfg<BMT>::MINB) void ge
   const bool f_tanh = EPF(EP_TANH, p.act == AW_ACT_GELU_TANH);
   const bool f_drop = EPF(EP_DROP, p.drop_p > 0.f);
   const bool f_resid = EPF(EP_RESID, p.resid != nullptr);
+  const bool f_residbf = EPF(EP_RESIDBF, p.resid_dtype == AW_BF16);
   const bool f_beta = EPF(EP_BETA, p.beta != 0.f);
   const bool f_c = EPF(EP_C, Cptr != nullptr);
   const bool f_cbf = EPF(EP_CBF, p.c_dtype == AW_BF16);
@@ -751,7 +752,15 @@ __global__ __launch_bounds__(Cfg<BMT>::NTH, RAGGED ? 1 : Cfg<BMT>::MINB) void ge
               pre4[u] = *reinterpret_cast<const float4*>(p.pre + row * p.ld_pre + col);
             }
           }
-          if (f_resid) res4[u] = *reinterpret_cast<const float4*>(p.resid + row * p.ld_resid + col);
+          if (f_resid) {
+            if (f_residbf) {
+              const uint2 h = *reinterpret_cast<const uint2*>(reinterpret_cast<const bf16*>(p.resid) + row * p.ld_resid + col);
+              res4[u] = make_float4(__uint_as_float(h.x << 16), __uint_as_float(h.x & 0xFFFF0000u),
+                                    __uint_as_float(h.y << 16), __uint_as_float(h.y & 0xFFFF0000u));
+            } else {
+              res4[u] = *reinterpret_cast<const float4*>(p.resid + row * p.ld_resid + col);
+            }
+          }
           if (f_beta) old4[u] = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(Cptr) + row * p.ldc + col);
         } else if constexpr (GEN) {
           float a[4] = {0.f, 0.f, 0.f, 0.f}, b[4] = {0.f, 0.f, 0.f, 0.f}, c[4] = {0.f, 0.f, 0.f, 0.f};
@@ -759,7 +768,7 @@ __global__ __launch_bounds__(Cfg<BMT>::NTH, RAGGED ? 1 : Cfg<BMT>::MINB) void ge
           for (int e = 0; e < 4; ++e) {
             if (col + e >= N) break;
             if (f_pre) a[e] = load_as_f32(p.pre, p.pre_dtype, row * p.ld_pre + col + e);
-            if (f_resid) b[e] = p.resid[row * p.ld_resid + col + e];
+            if (f_resid) b[e] = load_as_f32(p.resid, p.resid_dtype, row * p.ld_resid + col + e);
             if (f_beta) c[e] = reinterpret_cast<const float*>(Cptr)[row * p.ldc + col + e];
           }
           pre4[u] = make_float4(a[0], a[1], a[2], a[3]);

@@ -14,7 +14,11 @@
   X(T, LY, EP_BIAS | EP_DROP | EP_RESID | EP_C | EP_C2ACT | EP_C2BF)        \
   X(T, LY, EP_BIAS | EP_RESID | EP_C | EP_C2ACT | EP_C2BF)                  \
   X(T, LY, EP_BIAS | EP_DROP | EP_RESID | EP_C | EP_CBF)                    \
-  X(T, LY, EP_BIAS | EP_RESID | EP_C | EP_CBF)
+  X(T, LY, EP_BIAS | EP_RESID | EP_C | EP_CBF)                             \
+  X(T, LY, EP_BIAS | EP_DROP | EP_RESID | EP_RESIDBF | EP_C | EP_CBF | EP_C2ACT | EP_C2BF) \
+  X(T, LY, EP_BIAS | EP_RESID | EP_RESIDBF | EP_C | EP_CBF | EP_C2ACT | EP_C2BF)         \
+  X(T, LY, EP_BIAS | EP_DROP | EP_RESID | EP_RESIDBF | EP_C | EP_CBF)                    \
+  X(T, LY, EP_BIAS | EP_RESID | EP_RESIDBF | EP_C | EP_CBF)
 
 #define AW_FWD_PLAIN_CODES(X, T, LY)                                        \
   X(T, LY, EP_BIAS | EP_C)                                                  \
@@ -43,11 +47,15 @@
   X(T, LY, EP_PRE | EP_C | EP_CBF)                                          \
   X(T, LY, EP_PRE | EP_PREBF | EP_C | EP_CBF)                               \
   X(T, LY, EP_PRE | EP_RESID | EP_C | EP_C2DROP | EP_C2BF)                  \
-  X(T, LY, EP_PRE | EP_RESID | EP_C | EP_C2COPY | EP_C2BF)
+  X(T, LY, EP_PRE | EP_RESID | EP_C | EP_C2COPY | EP_C2BF)                  \
+  X(T, LY, EP_PRE | EP_PREBF | EP_RESID | EP_RESIDBF | EP_C | EP_CBF | EP_C2DROP | EP_C2BF) \
+  X(T, LY, EP_PRE | EP_PREBF | EP_RESID | EP_RESIDBF | EP_C | EP_CBF | EP_C2COPY | EP_C2BF)
 
 #define AW_BWD_PLAIN_CODES(X, T, LY)                                        \
   X(T, LY, EP_C | EP_C2DROP | EP_C2BF)                                      \
   X(T, LY, EP_C | EP_C2COPY | EP_C2BF)                                      \
+  X(T, LY, EP_C | EP_CBF | EP_C2DROP | EP_C2BF)                             \
+  X(T, LY, EP_C | EP_CBF | EP_C2COPY | EP_C2BF)                             \
   X(T, LY, EP_C)                                                            \
   X(T, LY, EP_C | EP_CBF)                                                   \
   X(T, LY, EP_PRE | EP_TANH | EP_C | EP_CBF)                               \
