@@ -506,6 +506,69 @@ def test_wgrad_conv3_kernel_vs_fp32_reference(policy, G, Cout, Cin, Ntok, S, ref
         torch.testing.assert_close(b, bw, rtol=1e-4, atol=2e-5 * float(bw.abs().max()))
 
 
+@pytest.mark.parametrize("case", ["transformer_half", "encoder", "ragged_small", "one_tile"])
+def test_wgrad_batch_stream_k_vs_fp32_reference(case):
+    """aw_wgrad_batch (csrc/wgrad.hip, wgrad_tt_kernel: 256 x 256 tiles, stream-K over one workgroup per CU, split tiles
+    summed by the last arriving piece) against torch fp32 on the same bf16 operands: dW[m][colmap(n)] += alpha
+    sum_k dy[k][m] x[k][n] and the bias row sums, accumulated into non-zero gradients.
+      transformer_half: the four Linear kinds of 4 blocks at d 512 (model/transformer_block.py:28-30,76-77 grads),
+                        K = 51 x 321 tokens (ragged: not a multiple of the 32-token stage), 192 tiles on 256 CUs;
+      encoder:          the 16 centre-tap convs (model/vq_vae_patch_embedd.py:65,68), K 16384, half of them through
+                        the reference's (O, I, 3) column map, alpha 0.5;
+      ragged_small:     K = 37 (two stages, the second mostly past K), mixed shapes;
+      one_tile:         a single tile over K = 8200 (its pieces all meet in one fix-up)."""
+    from arcweld import kernels as K
+    g = torch.Generator(device=DEV).manual_seed(4321)
+    d = 512
+    if case == "transformer_half":
+        Kt, alpha = 51 * 321, 1.0
+        shapes = [(3 * d, d), (d, d), (4 * d, d), (d, 4 * d)] * 4
+    elif case == "encoder":
+        Kt, alpha = 16384, 0.5
+        shapes = [(d, d)] * 16
+    elif case == "ragged_small":
+        Kt, alpha = 37, 1.0
+        shapes = [(256, 768), (512, 256), (256, 256)]
+    else:
+        Kt, alpha = 8200, 1.0
+        shapes = [(256, 256)]
+    probs, refs = [], []
+    for i, (M, N) in enumerate(shapes):
+        A = torch.randn(Kt, M, device=DEV, generator=g).to(torch.bfloat16)
+        x = torch.randn(Kt, N, device=DEV, generator=g).to(torch.bfloat16)
+        b0 = torch.randn(M, device=DEV, generator=g)
+        full = A.float().t() @ x.float()
+        if case == "encoder" and i % 2:      # contiguous (O, I, 3) conv weight: column n lands at n*3 + 1
+            C0 = torch.randn(M, N, 3, device=DEV, generator=g)
+            C = C0.clone()
+            kw = dict(C=C.view(M, 3 * N), col_map=(0, 3, 1))
+            want = C0.clone()
+            want[:, :, 1] += alpha * full
+        else:
+            C0 = torch.randn(M, N, device=DEV, generator=g)
+            C = C0.clone()
+            kw = dict(C=C)
+            want = C0 + alpha * full
+        b = b0.clone()
+        probs.append((A, x, M, N, Kt, dict(a_trans=True, b_trans=True, accumulate=True, a_rowsum=b, alpha=alpha,
+                                           **kw)))
+        refs.append((C, b, C0, want, b0, b0 + alpha * A.float().sum(0)))
+    assert K.wgrad_batch_ok(probs)
+    K.wgrad_batch(probs)
+    torch.cuda.synchronize()
+    for C, b, C0, want, b0, bw in refs:
+        scale = float(want.abs().max())
+        torch.testing.assert_close(C, want, rtol=1e-4, atol=2e-5 * scale)
+        torch.testing.assert_close(b, bw, rtol=1e-4, atol=2e-5 * float(bw.abs().max()))
+    # a second launch reuses the self-resetting per-tile arrival counters: the same sums are added again
+    K.wgrad_batch(probs)
+    torch.cuda.synchronize()
+    for C, b, C0, want, b0, bw in refs:
+        want2, bw2 = 2 * want - C0, 2 * bw - b0
+        torch.testing.assert_close(C, want2, rtol=1e-4, atol=4e-5 * float(want2.abs().max()))
+        torch.testing.assert_close(b, bw2, rtol=1e-4, atol=4e-5 * float(bw2.abs().max()))
+
+
 @pytest.mark.parametrize("training", [True, False])
 def test_unpatch_head_bf16_y_equals_f32_y(training):
     """aw_unpatch_head_*_ex with the ConvT output in bf16 (the bf16 operand mode, model/vq_vae_patch_embedd.py:24-31)

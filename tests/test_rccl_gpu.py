@@ -77,8 +77,9 @@ def _train(name, scale):
 def _worker(rank, port, out):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), ARCWELD_FORCE_COLLECTIVES="1")
     torch.cuda.set_device(0)
-    for name in ("vqvae", "decoder"):     # the plain run first, before any process group exists
+    for name in ("vqvae", "decoder"):     # the plain run first (twice: its run-to-run noise), before any group exists
         out[("plain", name)] = _train(name, 1.0)
+        out[("plain2", name)] = _train(name, 1.0)
     dist.init_process_group("nccl", rank=rank, world_size=1, device_id=torch.device("cuda", 0))
     out["backend"] = dist.get_backend()
     orig = dist.all_reduce
@@ -113,7 +114,18 @@ def test_rccl_one_rank_graphed_steps_match_plain_run():
     for name in ("vqvae", "decoder"):
         # eager step + 2 warm-up calls: one region each; captured replays: late + early regions, several buckets
         assert out[("calls", name)] >= STEPS + 2, (name, out[("calls", name)])
-        ref, got = out[("plain", name)], out[("rccl", name)]
+        ref, got, again = out[("plain", name)], out[("rccl", name)], out[("plain2", name)]
         assert sorted(ref) == sorted(got)
+        worst = []
         for k, v in ref.items():
-            torch.testing.assert_close(got[k], v, rtol=1e-6, atol=1e-6, msg=f"{name} {k}")
+            d_rccl = float((got[k] - v).abs().max())
+            d_noise = float((again[k] - v).abs().max())
+            worst.append((d_rccl, d_noise, k))
+            # the DP tests' bar (rtol 1e-5): f32 atomics (split-K tiles, bias row sums, the head's per-channel sums)
+            # add in a different order on every run, and RAdam's adaptive ratio turns a 1-ulp change of a near-zero
+            # gradient into up to lr * 1e-5; a collective that overtook the backward or an update that overtook a
+            # collective moves a parameter by O(lr) = 1e-3
+            torch.testing.assert_close(got[k], v, rtol=1e-5, atol=1e-6,
+                                       msg=f"{name} {k}: rccl-vs-plain {d_rccl:.3e}, plain-vs-plain {d_noise:.3e}")
+        worst.sort(reverse=True)
+        print(name, "largest rccl-vs-plain / plain-vs-plain differences:", worst[:3])

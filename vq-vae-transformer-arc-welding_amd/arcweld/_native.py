@@ -76,6 +76,8 @@ SIGNATURES = {
     "aw_gemm_grouped": [ctypes.POINTER(GemmArgs), c_int, c_p],
     "aw_gemm_set_tile": [c_int],
     "aw_gemm_set_wgrad_policy": [c_int],
+    "aw_wgrad_batch_workspace": [ctypes.POINTER(GemmArgs), c_int],
+    "aw_wgrad_batch": [ctypes.POINTER(GemmArgs), c_int, c_p, c_i64, c_p],
     "aw_weight_relayout_batch": [ctypes.POINTER(RelayoutJob), c_int, c_int, c_p],
     "aw_vq_forward": [c_p, c_p, c_i64, c_int, c_int, c_p, c_p, c_p, c_p, c_p],
     "aw_vq_forward_ex": [c_p, c_p, c_i64, c_int, c_int, c_p, c_p, c_p, c_p, c_p, c_int, c_p],
@@ -141,7 +143,7 @@ SIGNATURES = {
     "aw_rvq_backward": [c_p, c_p, c_p, c_p, c_int, c_i64, c_int, c_f, c_p, c_p],
 }
 
-RET_I64 = {"aw_gemm_workspace"}
+RET_I64 = {"aw_gemm_workspace", "aw_wgrad_batch_workspace"}
 
 _lib = None
 

@@ -234,13 +234,12 @@ def backward(m, sv, g_out, slot, mid_hook=None):
                         slot(blk.ln_1.bias), dx2=go, drop=(sv.p_drop, sv.seed_mlp[i - 1] if i > 0 else 0),
                         seed_ptr=sv.ctr)
         if i == half:
-            for kind in wg:
-                K.gemm_grouped(wg[kind])
-                wg[kind] = []
+            # the four kinds of the later half of the blocks: one stream-K batch (bf16) or one grouped launch per kind
+            K.wgrad_issue([pb for kind in wg for pb in wg[kind]])
+            wg = {kind: [] for kind in wg}
             if mid_hook is not None:
                 mid_hook()
-    for probs in wg.values():
-        K.gemm_grouped(probs)
+    K.wgrad_issue([pb for kind in wg for pb in wg[kind]])
     if nb == 0 and mid_hook is not None:
         mid_hook()
     K.embed_bwd(sv_ids(sv), gx, slot(m.embedding.latent_embedding.weight))

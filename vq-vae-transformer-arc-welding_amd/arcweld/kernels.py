@@ -166,6 +166,53 @@ def gemm_grouped(problems, stream=None):
         _timed(s, lambda sp: call("aw_gemm_grouped", arr, len(chunk), sp), fl, _gemm_tag(chunk[0][0]))
 
 
+def wgrad_batch_ok(problems):
+    """True when aw_wgrad_batch takes these problems (bf16 operands, M / N multiples of 256, one K) and it is not
+    switched off (ARCWELD_WGRAD_BATCH=0: the per-shape grouped launches instead, A/B)."""
+    import os
+    if os.environ.get("ARCWELD_WGRAD_BATCH", "1") == "0" or not problems or len(problems) > MAX_GROUPS:
+        return False
+    arr = (GemmArgs * len(problems))(*[_gemm_args(A, B, M, N, K, **kw) for (A, B, M, N, K, kw) in problems])
+    return nat.load().aw_wgrad_batch_workspace(arr, len(problems)) > 0
+
+
+def wgrad_batch(problems, stream=None):
+    """One aw_wgrad_batch launch over <= 16 weight-gradient problems (A, B, M, N, K, kwargs) as for ``gemm`` (M and
+    N may differ between problems; K, alpha and the dtype may not); the stream-K workspace comes from the caching
+    allocator."""
+    arr = (GemmArgs * len(problems))(*[_gemm_args(A, B, M, N, K, **kw) for (A, B, M, N, K, kw) in problems])
+    lib = nat.load()
+    wsb = lib.aw_wgrad_batch_workspace(arr, len(problems))
+    if wsb < 0:
+        raise nat.NativeError(f"aw_wgrad_batch: batch not eligible ({lib.aw_last_error().decode(errors='replace')})")
+    ws = torch.empty((wsb + 3) // 4, device=problems[0][0].device, dtype=torch.float32)
+    if PROFILE is None:
+        call("aw_wgrad_batch", arr, len(problems), ptr(ws), wsb, stream_ptr(stream))
+        return
+    s = stream if stream is not None else torch.cuda.current_stream()
+    fl = sum(_algorithmic_flops(M, N, K, None, None) for (_, _, M, N, K, _) in problems)
+    _timed(s, lambda sp: call("aw_wgrad_batch", arr, len(problems), ptr(ws), wsb, sp), fl, _gemm_tag(problems[0][0]))
+
+
+def wgrad_issue(problems, stream=None):
+    """Weight-gradient problems of one backward region that share K: in aw_wgrad_batch launches of <= 16 problems
+    when eligible (bf16, M / N multiples of 256), else one aw_gemm_grouped launch per shape."""
+    if not problems:
+        return
+    nch = (len(problems) + MAX_GROUPS - 1) // MAX_GROUPS
+    per = (len(problems) + nch - 1) // nch
+    chunks = [problems[i:i + per] for i in range(0, len(problems), per)]
+    if all(wgrad_batch_ok(c) for c in chunks):
+        for c in chunks:
+            wgrad_batch(c, stream)
+        return
+    by_shape = {}
+    for pb in problems:
+        by_shape.setdefault((pb[2], pb[3]), []).append(pb)
+    for grp in by_shape.values():
+        gemm_grouped(grp, stream)
+
+
 # ------------------------------------------------------------------------------------------------ VQ
 def vq_forward(z2d, E, zq, idx, counts, sqerr, stream=None, zq_copy=None):
     """zq_copy: optional bf16/f32 tensor that also receives z_q (aw_vq_forward_ex)."""

@@ -631,7 +631,7 @@ def backward(m, sv, g_emb, g_xhat, slot, mid_hook=None):
         wgrads.append((gh, sv.a0s[r], H, H, N, dict(a_trans=True, b_trans=True, C=C1w, accumulate=True, col_map=cm1,
                                                     a_rowsum=slot(c1.bias))))
         gx, gxo = gxn, gxon
-    K.gemm_grouped(wgrads)
+    K.wgrad_issue(wgrads)      # the 16 per-token conv weight gradients: one stream-K batch (bf16) or one grouped launch
 
     # ---- patch embed weight/bias
     K.gemm(gxo, sv.patches, H, P, N, a_trans=True, b_trans=True, C=slot(pr["pe"].weight).view(H, P),

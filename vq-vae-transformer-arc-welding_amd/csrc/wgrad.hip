@@ -23,6 +23,8 @@
 //    (the image is lane-linear per DMA instruction).
 #include "gemm_core.h"
 
+#include <algorithm>
+
 #pragma clang diagnostic ignored "-Winline-asm"
 
 namespace {
@@ -384,6 +386,340 @@ __global__ __launch_bounds__(W3_NTH, 1) void wgrad_conv3_kernel(W3Params P) {
 
 int g_policy = 0;   // aw_gemm_set_wgrad_policy: 0 automatic, 1 force, -1 off
 
+// =====================================================================================================================
+// Weight gradients of plain (1-tap) layers, a batch of problems of any (M, N) sharing K in ONE stream-K launch:
+//   dW_p[m][colmap(n)] += alpha * sum_k A_p[k][m] * B_p[k][n]      (A = dy [K][lda], B = x [K][ldb], bf16, f32 acc)
+//   rowsum_p[m]        += alpha * sum_k A_p[k][m]                  (bias gradient)
+// The transformer's four Linear kinds of half the blocks (model/transformer_block.py:28-30,76-77 grads, K = the B*T
+// tokens, ragged) and the VQ-VAE encoder's 16 centre-tap convs (model/vq_vae_patch_embedd.py:65,68 via :108-110).
+//  * Tile 256 x 256, K-stage 32 tokens, 512 threads in two wave groups that ping-pong (wgrad_conv3_kernel's schedule):
+//    each wave owns 128 x 64 outputs (8 x 4 fragments of v_mfma_f32_16x16x32_bf16); per stage a wave reads 12
+//    transposed fragments (24 ds_read_b64_tr_b16) and issues 32 MFMAs.  Four 32 KB stages (128 KB of LDS) filled by
+//    LDS-DMA three stages ahead; the tails of a ragged K read zeros from the buffer range check.
+//  * Stream-K: one workgroup per CU; the I = tiles * stages iterations of the whole batch are cut into equal
+//    contiguous ranges, so every CU does the same work whatever the tile count (the transformer's 192 tiles on 256
+//    CUs, the encoder's 64).  A tile split between workgroups is fixed up by the LAST arriving piece: every partial
+//    piece stores its accumulators write-through (sc1) into its workspace slot, drains them (vmcnt(0)), joins a
+//    workgroup barrier and takes a ticket with one agent-scope atomic add; the piece whose ticket completes the count
+//    loads the other pieces' slots with sc1 loads and does the one read-modify-write of the gradient
+//    (MI355X_MICROARCH.md, inter-workgroup hand-off, first row of the measured forms).  No piece ever waits on
+//    another, so the launch cannot deadlock whatever its residency.
+//  * Bias gradients: row sums of the A fragments by MFMA against an all-ones fragment, on the stages s with
+//    s % tiles_n == tn (spread over the row's tiles), f32 atomics per piece.
+constexpr int WT_BM = 256, WT_BN = 256, WT_BK = 32, WT_NTH = 512;
+constexpr int WT_A = WT_BK * WT_BM * 2;      // 16384 B
+constexpr int WT_B = WT_BK * WT_BN * 2;      // 16384 B
+constexpr int WT_BUF = WT_A + WT_B;          // 32768 B
+constexpr int WT_NBUF = 4;                   // 131072 B
+constexpr int WT_DMA = 4;                    // DMA instructions per thread per stage (2 A + 2 B)
+constexpr int WT_SLAB = WT_BM * WT_BN;       // f32 elements of one partial tile
+constexpr int WT_MAXTILES = 8192;
+
+struct WTProb {
+  const void* A;
+  const void* B;
+  float* C;
+  float* rowsum;
+  int64_t lda, ldb, ldc;
+  int M, N, tiles_n, tile0;
+  int col_mod, col_mul, col_off;
+};
+
+struct WTParams {
+  WTProb p[AW_GEMM_MAX_GROUPS];
+  int nprob, K, nk, G, total_tiles;
+  int64_t I;
+  float alpha;
+  float* ws;          // 2 * G slots of WT_SLAB floats
+};
+
+__device__ int g_wt_tickets[WT_MAXTILES];   // per-tile arrival counters; the last arriver resets its own to 0
+
+__device__ __forceinline__ v4i32 wt_desc(const void* base, int64_t nbytes) {
+  const uint64_t b = (uint64_t)(uintptr_t)base;
+  const int64_t nb = nbytes < 0 ? 0 : (nbytes > 0x7FFFFFF0 ? 0x7FFFFFF0 : nbytes);
+  return v4i32{(int)__builtin_amdgcn_readfirstlane((uint32_t)b),
+               (int)__builtin_amdgcn_readfirstlane((uint32_t)(b >> 32) & 0xFFFFu),
+               (int)__builtin_amdgcn_readfirstlane((uint32_t)nb), 0x00020000};
+}
+
+// first workgroup (logical index) whose range holds iteration x: max c with floor(c*I/G) <= x
+__device__ __forceinline__ int wt_owner(int64_t x, int64_t I, int G) { return (int)(((x + 1) * G - 1) / I); }
+__device__ __forceinline__ int64_t wt_start(int c, int64_t I, int G) { return (int64_t)c * I / G; }
+
+__device__ __forceinline__ void wt_st_sc1(float* p, f32x4 v) {
+  asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
+}
+
+__global__ __launch_bounds__(WT_NTH, 1) void wgrad_tt_kernel(WTParams P) {
+  __shared__ __attribute__((aligned(16))) char smem[WT_NBUF * WT_BUF];
+  __shared__ int s_last;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 2, wc = wid & 3;
+  const int g = lane >> 4, li = lane & 15, q = li >> 2, p4 = li & 3;
+  const int wcu = __builtin_amdgcn_readfirstlane(wc);
+  const int c = awg::xcd_remap(blockIdx.x, P.G);      // logical workgroup: consecutive ranges share an XCD's L2
+  const int64_t it_end = wt_start(c + 1, P.I, P.G);
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
+  const uint32_t wave_dst = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(tid & ~63)) * 16u;
+  const uint4 ones = make_uint4(0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u);
+  // fragment addresses within a stage buffer: A block mb = wr*8 + i at mb*1024, B block cb = wc*4 + f at WT_A + cb*1024
+  const int f_lo = w3_kfield(8 * g + q) + 8 * p4, f_hi = w3_kfield(8 * g + 4 + q) + 8 * p4;
+  // DMA chunk c = tid + 512 j of an image: block mb = c >> 6, k field kf = (c & 63) >> 1, half = c & 1
+  int src_row[2], src_col[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int ch = tid + WT_NTH * j;
+    const int kf = (ch & 63) >> 1;
+    src_row[j] = kf ^ (((kf >> 3) & 1) << 2);
+    src_col[j] = (ch >> 6) * 16 + (ch & 1) * 8;
+  }
+
+  for (int64_t it = wt_start(c, P.I, P.G); it < it_end;) {
+    const int tile = (int)(it / P.nk);
+    const int k0 = (int)(it - (int64_t)tile * P.nk);
+    const int k1 = (int)min((int64_t)P.nk, (int64_t)k0 + (it_end - it));
+    int pi = 0;
+    while (pi + 1 < P.nprob && tile >= P.p[pi + 1].tile0) ++pi;
+    const WTProb& pr = P.p[pi];
+    const int lt = tile - pr.tile0;
+    const int tm = lt / pr.tiles_n, tn = lt - tm * pr.tiles_n;
+    const int m0 = tm * WT_BM, n0 = tn * WT_BN;
+    const char* Ag = reinterpret_cast<const char*>(pr.A) + (int64_t)m0 * 2;
+    const char* Bg = reinterpret_cast<const char*>(pr.B) + (int64_t)n0 * 2;
+    const int64_t lda = pr.lda, ldb = pr.ldb;
+    int offA[2], offB[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      offA[j] = (int)((src_row[j] * lda + src_col[j]) * 2);
+      offB[j] = (int)((src_row[j] * ldb + src_col[j]) * 2);
+    }
+    const int64_t extA = ((int64_t)(P.K - 1) * lda + pr.M - m0) * 2;   // valid bytes from the tile's row 0
+    const int64_t extB = ((int64_t)(P.K - 1) * ldb + pr.N - n0) * 2;
+    auto dma = [&](int t) {
+      const uint32_t buf = lds0 + (uint32_t)((t & (WT_NBUF - 1)) * WT_BUF);
+      const int64_t ra = (int64_t)t * WT_BK * lda * 2, rb = (int64_t)t * WT_BK * ldb * 2;
+      const v4i32 da = wt_desc(Ag + ra, extA - ra), db = wt_desc(Bg + rb, extB - rb);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) w3_dma(buf + wave_dst + (uint32_t)(j * WT_NTH * 16), offA[j], da);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) w3_dma(buf + WT_A + wave_dst + (uint32_t)(j * WT_NTH * 16), offB[j], db);
+    };
+    float* rowptr = pr.rowsum;
+    f32x4 rs[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+    f32x4 acc[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int f = 0; f < 4; ++f) acc[i][f] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    // ---- prologue: stages k0 .. k0+2 in flight, k0 retired and published
+    const int ns = k1 - k0;
+    dma(k0);
+    if (ns > 1) dma(k0 + 1);
+    if (ns > 2) dma(k0 + 2);
+    if (ns > 2) w3_vmcnt<2 * WT_DMA>();
+    else if (ns > 1) w3_vmcnt<WT_DMA>();
+    else w3_vmcnt<0>();
+    w3_barrier();
+    if (wr == 1) w3_barrier();                 // group 1 runs one barrier behind group 0
+
+    uint4 af[8], bfr[4];
+    for (int t = k0; t < k1; ++t) {
+      // ---- read segment: fragments of stage t, the DMA of t + 3 (into the buffer of t - 1, read by both groups
+      //      before the last barrier), retire t + 1
+      const char* buf = smem + (t & (WT_NBUF - 1)) * WT_BUF;
+      {
+        const char* pa_lo = buf + wr * 8 * 1024 + f_lo;
+        const char* pa_hi = buf + wr * 8 * 1024 + f_hi;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) af[i] = w3_tr(pa_lo + i * 1024, pa_hi + i * 1024);
+        const char* pb_lo = buf + WT_A + wc * 4 * 1024 + f_lo;
+        const char* pb_hi = buf + WT_A + wc * 4 * 1024 + f_hi;
+#pragma unroll
+        for (int f = 0; f < 4; ++f) bfr[f] = w3_tr(pb_lo + f * 1024, pb_hi + f * 1024);
+      }
+      if (t + 3 < k1) dma(t + 3);
+      const int newer = min(k1 - 1, t + 3) - (t + 1);
+      if (newer >= 2) w3_vmcnt<2 * WT_DMA>();
+      else if (newer == 1) w3_vmcnt<WT_DMA>();
+      else w3_vmcnt<0>();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      w3_barrier();
+      // ---- MFMA segment
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int f = 0; f < 4; ++f)
+          acc[i][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, af[i]),
+                                                             __builtin_bit_cast(bf16x8, bfr[f]), acc[i][f], 0, 0, 0);
+      if (rowptr != nullptr && t % pr.tiles_n == tn) {
+#define WT_RS(a, b)                                                                                              \
+  rs[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, af[a]), __builtin_bit_cast(bf16x8, ones), \
+                                                  rs[0], 0, 0, 0);                                                \
+  rs[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, af[b]), __builtin_bit_cast(bf16x8, ones), \
+                                                  rs[1], 0, 0, 0);
+        switch (wcu) {
+          case 0: WT_RS(0, 1) break;
+          case 1: WT_RS(2, 3) break;
+          case 2: WT_RS(4, 5) break;
+          default: WT_RS(6, 7) break;
+        }
+#undef WT_RS
+      }
+      __builtin_amdgcn_s_setprio(0);
+      w3_barrier();
+    }
+    if (wr == 0) w3_barrier();                 // both groups end on the same barrier count
+
+    const float alpha = P.alpha;
+    if (rowptr != nullptr && li == 0) {         // column 0 of A . ones: lane 16g holds rows 4g..4g+3
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float v = rs[j][r];
+          if (v != 0.f) atomicAdd(rowptr + m0 + wr * 128 + 16 * (2 * wcu + j) + 4 * g + r, alpha * v);
+        }
+    }
+    bool write = true;
+    if (ns < P.nk) {
+      // ---- partial tile: publish, take a ticket, the last arriver sums the other pieces
+      const int64_t x0 = (int64_t)tile * P.nk, x1 = x0 + P.nk - 1;
+      const int cf = wt_owner(x0, P.I, P.G), cl = wt_owner(x1, P.I, P.G);
+      const int slot = 2 * c + (k0 == 0 ? 1 : 0);
+      float* mine = P.ws + (int64_t)slot * WT_SLAB;
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int f = 0; f < 4; ++f) wt_st_sc1(mine + ((i * 4 + f) * WT_NTH + tid) * 4, acc[i][f]);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) {
+        const int old = __hip_atomic_fetch_add(&g_wt_tickets[tile], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int last = old == cl - cf;
+        if (last) __hip_atomic_store(&g_wt_tickets[tile], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_last = last;
+      }
+      __syncthreads();
+      write = s_last != 0;
+      if (write) {
+        for (int o = cf; o <= cl; ++o) {
+          if (o == c) continue;
+          const int64_t so = wt_start(o, P.I, P.G);
+          const int oslot = 2 * o + (so <= x0 ? 1 : 0);
+          const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(P.ws + (int64_t)oslot * WT_SLAB, (short)0,
+                                                                  WT_SLAB * 4, 0x00020000);
+#pragma unroll
+          for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int f = 0; f < 4; ++f) {
+              // sc1 load (cache policy bit 4): served past this CU's L1, as the hand-off requires
+              const f32x4 v = __builtin_bit_cast(
+                  f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, ((i * 4 + f) * WT_NTH + tid) * 16, 0, 16));
+              acc[i][f] += v;
+            }
+        }
+      }
+    }
+    if (write) {
+      float* C = pr.C;
+#pragma unroll
+      for (int f = 0; f < 4; ++f) {
+        const int n = n0 + wc * 64 + 16 * f + li;
+        const int64_t oc = pr.col_mod > 0 ? (int64_t)(n % pr.col_mod) * pr.col_mul + n / pr.col_mod + pr.col_off
+                                          : (int64_t)n * (pr.col_mul > 0 ? pr.col_mul : 1) + pr.col_off;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const int row = m0 + wr * 128 + 16 * i + 4 * g;
+          float* d = C + (int64_t)row * pr.ldc + oc;
+          float v[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = d[(int64_t)r * pr.ldc];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) d[(int64_t)r * pr.ldc] = v[r] + alpha * acc[i][f][r];
+        }
+      }
+    }
+    it += ns;
+  }
+}
+
+// ---- host side of the batch
+int g_cus = 0;
+
+int wt_cus() {
+  if (g_cus == 0) {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) ==
+                                                 hipSuccess && n > 0)
+      g_cus = n;
+    else
+      g_cus = 256;
+  }
+  return g_cus;
+}
+
+// checks + launch plan; P == nullptr: only validate.  Returns AW_OK, or a negative status (with the message set)
+int wt_plan(const aw_gemm_args* args, int n, WTParams* P) {
+  AW_REQUIRE(args && n >= 1 && n <= AW_GEMM_MAX_GROUPS, "aw_wgrad_batch: need 1..%d problems", AW_GEMM_MAX_GROUPS);
+  const aw_gemm_args& a0 = args[0];
+  int tiles = 0;
+  for (int i = 0; i < n; ++i) {
+    const aw_gemm_args& a = args[i];
+    AW_REQUIRE(a.a_dtype == AW_BF16 && a.a_trans == 1 && a.b_trans == 1 && a.conv_cin == 0,
+               "aw_wgrad_batch: problem %d: bf16 operands, a_trans = b_trans = 1, no conv", i);
+    AW_REQUIRE(a.accumulate == 1 && a.c_dtype == AW_F32 && a.C && a.beta == 0.f && !a.bias && !a.pre && !a.resid &&
+                   !a.C2 && !a.colstats && a.drop_p <= 0.f,
+               "aw_wgrad_batch: problem %d: accumulate-mode f32 C only", i);
+    AW_REQUIRE(a.K == a0.K && a.alpha == a0.alpha, "aw_wgrad_batch: problem %d: K and alpha must match problem 0", i);
+    AW_REQUIRE(a.M > 0 && a.N > 0 && a.M % WT_BM == 0 && a.N % WT_BN == 0,
+               "aw_wgrad_batch: problem %d: M, N must be positive multiples of 256 (got %d x %d)", i, a.M, a.N);
+    AW_REQUIRE(a.A && a.B && ((uintptr_t)a.A % 16) == 0 && ((uintptr_t)a.B % 16) == 0 && a.lda % 8 == 0 &&
+                   a.ldb % 8 == 0 && a.lda >= a.M && a.ldb >= a.N,
+               "aw_wgrad_batch: problem %d: 16-B aligned operand rows with lda >= M, ldb >= N", i);
+    AW_REQUIRE((int64_t)WT_BK * a.lda * 2 < 0x7FFFFFF0 && (int64_t)WT_BK * a.ldb * 2 < 0x7FFFFFF0,
+               "aw_wgrad_batch: problem %d: leading dimension too large", i);
+    tiles += (a.M / WT_BM) * (a.N / WT_BN);
+  }
+  AW_REQUIRE(a0.K > 0, "aw_wgrad_batch: K must be positive");
+  AW_REQUIRE(tiles <= WT_MAXTILES, "aw_wgrad_batch: %d tiles exceed %d", tiles, WT_MAXTILES);
+  if (!P) return AW_OK;
+  memset(P, 0, sizeof(*P));
+  int t0 = 0;
+  for (int i = 0; i < n; ++i) {
+    const aw_gemm_args& a = args[i];
+    WTProb& q = P->p[i];
+    q.A = a.A;
+    q.B = a.B;
+    q.C = reinterpret_cast<float*>(a.C);
+    q.rowsum = a.a_rowsum;
+    q.lda = a.lda;
+    q.ldb = a.ldb;
+    q.ldc = a.ldc;
+    q.M = a.M;
+    q.N = a.N;
+    q.tiles_n = a.N / WT_BN;
+    q.tile0 = t0;
+    q.col_mod = a.col_mod;
+    q.col_mul = a.col_mul;
+    q.col_off = a.col_off;
+    t0 += (a.M / WT_BM) * q.tiles_n;
+  }
+  P->nprob = n;
+  P->K = a0.K;
+  P->nk = (a0.K + WT_BK - 1) / WT_BK;
+  P->total_tiles = tiles;
+  P->I = (int64_t)tiles * P->nk;
+  // one workgroup per CU, but at least a quarter of a tile's stages per workgroup: a tile is then split into at most
+  // five pieces, so the last arriver's fix-up reads at most four partial tiles (a small batch runs on fewer CUs)
+  const int64_t min_iters = std::max(1, P->nk / 4);
+  P->G = (int)std::max<int64_t>(1, std::min<int64_t>(wt_cus(), P->I / min_iters));
+  P->alpha = a0.alpha;
+  return AW_OK;
+}
+
 }  // namespace
 
 namespace awg {
@@ -452,3 +788,20 @@ extern "C" int w3_probe_stamps(uint64_t* host, int n) {
 #endif
 }
 #endif
+
+// ----------------------------------------------------------------------------------------- batched 1-tap wgrad
+extern "C" int64_t aw_wgrad_batch_workspace(const aw_gemm_args* args, int n) {
+  WTParams P;
+  if (wt_plan(args, n, &P) != AW_OK) return -1;
+  return (int64_t)2 * P.G * WT_SLAB * (int64_t)sizeof(float);
+}
+
+extern "C" int aw_wgrad_batch(const aw_gemm_args* args, int n, void* ws, int64_t ws_bytes, void* stream) {
+  WTParams P;
+  if (int st = wt_plan(args, n, &P)) return st;
+  AW_REQUIRE(ws && ((uintptr_t)ws % 16) == 0 && ws_bytes >= (int64_t)2 * P.G * WT_SLAB * (int64_t)sizeof(float),
+             "aw_wgrad_batch: workspace must be 16-B aligned and hold aw_wgrad_batch_workspace() bytes");
+  P.ws = reinterpret_cast<float*>(ws);
+  hipLaunchKernelGGL(wgrad_tt_kernel, dim3(P.G), dim3(WT_NTH), 0, reinterpret_cast<hipStream_t>(stream), P);
+  return aw::check_launch("aw_wgrad_batch");
+}
