@@ -25,7 +25,7 @@ pytestmark = pytest.mark.gpu
 
 VQ_KW = dict(hidden_dim=512, num_embeddings=512, embedding_dim=64, n_resblocks=8, patch_size=25)
 DEC_KW = dict(d_model=512, n_classes=514, seq_len=129, n_blocks=8)
-STEPS = 6          # one eager step, two eager warm-up calls of graphed_step, the capture, two replays
+STEPS = 5          # one eager step, two eager warm-up calls of graphed_step, the capture + replay, one more replay
 
 
 def _free_port():
@@ -113,7 +113,7 @@ def test_rccl_one_rank_graphed_steps_match_plain_run():
     assert out["probe"] == [2.0] * 4
     for name in ("vqvae", "decoder"):
         # eager step + 2 warm-up calls: one region each; captured replays: late + early regions, several buckets
-        assert out[("calls", name)] >= STEPS + 2, (name, out[("calls", name)])
+        assert out[("calls", name)] >= STEPS + 1, (name, out[("calls", name)])
         ref, got, again = out[("plain", name)], out[("rccl", name)], out[("plain2", name)]
         assert sorted(ref) == sorted(got)
         worst = []
@@ -121,11 +121,12 @@ def test_rccl_one_rank_graphed_steps_match_plain_run():
             d_rccl = float((got[k] - v).abs().max())
             d_noise = float((again[k] - v).abs().max())
             worst.append((d_rccl, d_noise, k))
-            # the DP tests' bar (rtol 1e-5): f32 atomics (split-K tiles, bias row sums, the head's per-channel sums)
-            # add in a different order on every run, and RAdam's adaptive ratio turns a 1-ulp change of a near-zero
-            # gradient into up to lr * 1e-5; a collective that overtook the backward or an update that overtook a
-            # collective moves a parameter by O(lr) = 1e-3
-            torch.testing.assert_close(got[k], v, rtol=1e-5, atol=1e-6,
+            # five steps keep RAdam in its un-adapted phase (rho_t <= 5 for t <= 5: the update is lr * the momentum,
+            # linear in the gradient), so the run-to-run noise of the f32 atomics (split-K tiles, bias row sums, the
+            # head's per-channel sums) stays at lr * 1 ulp; from step 6 on the adaptive ratio m / sqrt(v) turns a 1-ulp
+            # change of a near-zero gradient (the ConvT2 bias) into up to lr * 2.6e-2.  A collective that overtook the
+            # backward or an update that overtook a collective moves a parameter by lr * |g|
+            torch.testing.assert_close(got[k], v, rtol=1e-6, atol=1e-6,
                                        msg=f"{name} {k}: rccl-vs-plain {d_rccl:.3e}, plain-vs-plain {d_noise:.3e}")
         worst.sort(reverse=True)
         print(name, "largest rccl-vs-plain / plain-vs-plain differences:", worst[:3])
