@@ -1,7 +1,8 @@
 """Causal attention kernels (aw_attn_fwd / aw_attn_bwd) against a plain torch fp32 reference of
 CausalSelfAttention (model/transformer_block.py:37-63, attention dropout 0).  fp32 operands -> the VALU
 kernels (tolerance 1e-4); bf16 operands -> the MFMA kernels at head size 64 (VALU otherwise), compared on the
-same bf16-rounded inputs with bf16-output tolerance."""
+same bf16-rounded inputs with bf16-output tolerance.  At 97 <= T <= 384 the bf16 forward is the one-workgroup-per-head
+kernel (csrc/attention.hip attn_fwd_head_kernel), below and above it the row-block grid."""
 import math
 
 import pytest
@@ -60,7 +61,7 @@ def test_attention_fp32(T, hs):
     torch.testing.assert_close(dqkv, rg, rtol=1e-4, atol=2e-4)
 
 
-@pytest.mark.parametrize("T", [1, 17, 64, 65, 127, 128, 129, 200, 257, 321])
+@pytest.mark.parametrize("T", [1, 17, 64, 65, 96, 97, 127, 128, 129, 200, 257, 300, 321, 384, 385])
 @pytest.mark.parametrize("hs,nh", [(64, 2), (64, 8), (32, 4)])
 def test_attention_bf16(T, hs, nh):
     B = 3
