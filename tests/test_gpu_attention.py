@@ -1,8 +1,7 @@
 """Causal attention kernels (aw_attn_fwd / aw_attn_bwd) against a plain torch fp32 reference of
 CausalSelfAttention (model/transformer_block.py:37-63, attention dropout 0).  fp32 operands -> the VALU
 kernels (tolerance 1e-4); bf16 operands -> the MFMA kernels at head size 64 (VALU otherwise), compared on the
-same bf16-rounded inputs with bf16-output tolerance.  At 97 <= T <= 384 the bf16 forward is the one-workgroup-per-head
-kernel (csrc/attention.hip attn_fwd_head_kernel), below and above it the row-block grid."""
+same bf16-rounded inputs with bf16-output tolerance."""
 import math
 
 import pytest

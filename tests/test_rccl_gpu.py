@@ -96,6 +96,10 @@ def _worker(rank, port, out):
         dist.all_reduce(probe)           # the factor is applied by RCCL itself
         torch.cuda.synchronize()
         out["probe"] = probe.cpu().tolist()
+        odd = torch.ones(5, device="cuda")     # an odd length (recorded only: the trainer's buckets are 256-B rounded)
+        dist.all_reduce(odd)
+        torch.cuda.synchronize()
+        out["probe_odd"] = odd.cpu().tolist()
         for name in ("vqvae", "decoder"):
             n0 = len(calls)
             out[("rccl", name)] = _train(name, 0.5)
@@ -111,6 +115,7 @@ def test_rccl_one_rank_graphed_steps_match_plain_run():
     mp.spawn(_worker, args=(port, out), nprocs=1, join=True)
     assert out["backend"] == "nccl"
     assert out["probe"] == [2.0] * 4
+    print("one-rank pre-multiplied sum of 5 ones:", out["probe_odd"])
     for name in ("vqvae", "decoder"):
         # eager step + 2 warm-up calls: one region each; captured replays: late + early regions, several buckets
         assert out[("calls", name)] >= STEPS + 1, (name, out[("calls", name)])

@@ -59,6 +59,11 @@ def allreduce_spans(flat: torch.Tensor, spans, bucket: int = BUCKET_ELEMS):
     """Async SUM all-reduce of the [a, b) ranges of a flat buffer, each cut into buckets; returns the work handles."""
     if _collectives_off():
         return []
+    n = flat.numel()
+    # every span ends on a 256-B boundary: segments start 256-B aligned, so the rounding only takes in the zero
+    # padding before the next segment, and RCCL moves whole 16-B packs (an odd-length tail measured unscaled by the
+    # one-rank pre-multiplied sum of tests/test_rccl_gpu.py)
+    spans = [(a, min(n, (b + 63) // 64 * 64)) for a, b in spans]
     return [dist.all_reduce(flat[o:min(o + bucket, b)], async_op=True) for a, b in spans for o in range(a, b, bucket)]
 
 

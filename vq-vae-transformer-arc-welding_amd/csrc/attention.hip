@@ -526,131 +526,6 @@ __global__ __launch_bounds__(256, 2) void attn_dkv_ring_kernel(const bf16* __res
   }
 }
 
-// ---------------------------------------------------------------- forward, one workgroup per head
-// grid B * nh, 64 * ceil(T / 32) threads (4 .. 12 waves): wave w owns queries 32w .. 32w + 31 of one (b, h), so the
-// head's K and V are read ONCE (the row-block grid above re-reads them for every 128-query block: at 51 x 321 its
-// fetch is 65 MB against 50 MB of qkv).  K/V 64-key tiles stream through a 3-slot LDS ring by LDS-DMA (waves 0..3
-// each issue the 4 pieces of 32 rows of K or V for a tile, two tiles ahead); every wave sweeps the tiles in lock step
-// (one barrier per tile) and computes only on the tiles its causal range reaches.  The per-tile body is the row-block
-// kernel's (S^T = K.Q^T with the query on the lane, online softmax in registers, O^T += V^T.P^T).
-constexpr int FH_NB = 3;
-constexpr int FH_SLOT = 2 * IMG;   // K image, V image
-
-__global__ __launch_bounds__(768) void attn_fwd_head_kernel(const bf16* __restrict__ qkv, int T_, int nh, int d,
-                                                            bf16* __restrict__ y, float* __restrict__ lse, float c2,
-                                                            float scale) {
-  __shared__ __attribute__((aligned(16))) char L[FH_NB * FH_SLOT];
-  const int h = (int)blockIdx.x % nh, b = (int)blockIdx.x / nh;
-  const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, hf = lane >> 5;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int ldb = 6 * d;   // bytes per qkv row
-  const char* bbase = reinterpret_cast<const char*>(qkv) + (int64_t)b * T_ * ldb;
-  const bf16* base = qkv + (int64_t)b * T_ * 3 * (int64_t)d;
-  const int64_t ld = 3 * (int64_t)d;
-  const uint32_t lring = aw_lds_addr(L);
-  const int qw = WROWS * w, q = qw + r, qc = min(q, T_ - 1);
-  const int nt = (T_ + TILE - 1) / TILE;
-  const int tlast = (qw + WROWS - 1) / TILE;     // last key tile this wave's causal range reaches
-  // DMA roles: wave w < 4 loads rows 32(w & 1) .. + 31 of the K (w < 2) or V (w >= 2) image of every tile
-  const int sel = w >> 1;
-  auto issue = [&](int t) {
-    if (w >= 4 || t >= nt) return;
-    const int k0 = t * TILE;
-    const aw_v4i32 ds = aw_rdesc(bbase + (int64_t)k0 * ldb + ((1 + sel) * d + h * HS) * 2, (uint32_t)(T_ - k0) * ldb);
-    const uint32_t dst = lring + (t % FH_NB) * FH_SLOT + sel * IMG + 4096 * (w & 1);
-#pragma unroll
-    for (int u = 0; u < 4; ++u) aw_dma16(dst + 1024 * u, piece_off(4 * (w & 1) + u, lane, ldb), ds);   // offsets
-  };                                                                                // recomputed: no live VGPRs
-  issue(0);
-  issue(1);
-  uint4 qf[4];
-#pragma unroll
-  for (int s2 = 0; s2 < 4; ++s2)
-    qf[s2] = *reinterpret_cast<const uint4*>(base + (int64_t)qc * ld + h * HS + 16 * s2 + 8 * hf);
-  f32x16 o[2] = {zero16(), zero16()};
-  float m = -__builtin_huge_valf(), l = 0.f;
-  if (w < 4) {
-    if (nt > 1) aw_vm_wait<4>();
-    else aw_vm_wait<0>();
-  }
-  raw_barrier();
-  for (int t = 0; t < nt; ++t) {
-    issue(t + 2);     // into the slot of tile t - 1, which every wave finished reading before the last barrier
-    const int k0 = t * TILE;
-    if (t <= tlast && qw < T_) {
-      const char* Ks = L + (t % FH_NB) * FH_SLOT;
-      const char* Vs = Ks + IMG;
-      f32x16 s[2];
-#pragma unroll
-      for (int st = 0; st < 2; ++st) {
-        s[st] = zero16();
-#pragma unroll
-        for (int ks = 0; ks < 4; ++ks) s[st] = mfma32(row_frag(Ks, 32 * st + r, ks, hf), qf[ks], s[st]);
-      }
-      const bool edge = (k0 + TILE - 1 > qw) || (k0 + TILE > T_);
-      if (edge) {
-        asm volatile("" ::: "memory");
-        const int lim = min(q, T_ - 1) - (k0 + 4 * hf);
-#pragma unroll
-        for (int st = 0; st < 2; ++st)
-#pragma unroll
-          for (int i = 0; i < 16; ++i)
-            s[st][i] = (32 * st + 8 * (i >> 2) + (i & 3) > lim) ? -__builtin_huge_valf() : s[st][i];
-      }
-      float mx = -__builtin_huge_valf();
-#pragma unroll
-      for (int st = 0; st < 2; ++st)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) mx = fmaxf(mx, s[st][i]);
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float mn = fmaxf(m, mx);
-      const float alpha = __builtin_amdgcn_exp2f((m - mn) * c2);
-      const float mc = mn * c2;
-      m = mn;
-      f32x2 ls2 = {0.f, 0.f};
-#pragma unroll
-      for (int st = 0; st < 2; ++st)
-#pragma unroll
-        for (int i = 0; i < 16; i += 2) {
-          const f32x2 a = __builtin_elementwise_fma((f32x2){s[st][i], s[st][i + 1]}, (f32x2){c2, c2}, (f32x2){-mc, -mc});
-          const f32x2 pr = {__builtin_amdgcn_exp2f(a.x), __builtin_amdgcn_exp2f(a.y)};
-          s[st][i] = pr.x;
-          s[st][i + 1] = pr.y;
-          ls2 += pr;
-        }
-      l = l * alpha + (ls2.x + ls2.y);
-#pragma unroll
-      for (int dt = 0; dt < 2; ++dt)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) o[dt][i] *= alpha;
-#pragma unroll
-      for (int st = 0; st < 2; ++st)
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {
-          const uint4 pb = pack8(s[st], s2);
-#pragma unroll
-          for (int dt = 0; dt < 2; ++dt) o[dt] = mfma32(tr_frag(Vs, 32 * st + 16 * s2 + 4 * hf, dt, lane), pb, o[dt]);
-        }
-    }
-    if (w < 4) {      // retire tile t + 1 (tile t + 2 may stay in flight)
-      if (t + 2 < nt) aw_vm_wait<4>();
-      else aw_vm_wait<0>();
-    }
-    raw_barrier();
-  }
-  l += __shfl_xor(l, 32, 64);
-  if (q < T_) {
-    const float inv = 1.f / l;
-    bf16* yr = y + ((int64_t)b * T_ + q) * d + h * HS;
-#pragma unroll
-    for (int dt = 0; dt < 2; ++dt)
-#pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) store4_bf16(yr + 32 * dt + 8 * g4 + 4 * hf, o[dt], g4, inv);
-    if (hf == 0) lse[((int64_t)b * nh + h) * T_ + q] = m * scale + logf(l);
-  }
-}
-
-int g_fwd_head = -1;   // ARCWELD_ATTN_FWD_HEAD: 1 the per-head kernel where it applies (default), 0 the row-block grid
 
 }  // namespace
 
@@ -663,16 +538,6 @@ bool attn_mfma_supported(int dtype, int hs, int d, int64_t T) {
 
 void attn_fwd_mfma(const void* qkv, int64_t B, int T, int nh, int d, void* y, float* lse, hipStream_t s) {
   const float scale = 1.0f / sqrtf((float)HS);
-  if (g_fwd_head < 0) {
-    const char* e = getenv("ARCWELD_ATTN_FWD_HEAD");
-    g_fwd_head = e ? atoi(e) : 1;
-  }
-  const int nwv = (T + WROWS - 1) / WROWS;
-  if (g_fwd_head && nwv >= 4 && nwv <= 12) {   // 97 <= T <= 384: 4 .. 12 waves (168 VGPRs), one workgroup per head
-    hipLaunchKernelGGL(attn_fwd_head_kernel, dim3((unsigned)(B * nh)), dim3(64 * nwv), 0, s, (const bf16*)qkv, T, nh,
-                       d, (bf16*)y, lse, scale * 1.4426950408889634f, scale);
-    return;
-  }
   dim3 grid((unsigned)(((T + BLK - 1) / BLK) * (int64_t)nh * B));
   hipLaunchKernelGGL(attn_fwd_mfma_kernel, grid, dim3(256), 0, s, (const bf16*)qkv, T, nh, d, (bf16*)y, lse,
                      scale * 1.4426950408889634f, scale);

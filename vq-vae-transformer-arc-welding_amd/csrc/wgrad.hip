@@ -497,6 +497,9 @@ __global__ __launch_bounds__(WT_NTH, 1) void wgrad_tt_kernel(WTParams P) {
     const int64_t extA = ((int64_t)(P.K - 1) * lda + pr.M - m0) * 2;   // valid bytes from the tile's row 0
     const int64_t extB = ((int64_t)(P.K - 1) * ldb + pr.N - n0) * 2;
     auto dma = [&](int t) {
+#ifdef WT_SKIP_DMA
+      if (t >= k0 + 3) return;    // probe: the loop's DMA left out (operands stale)
+#endif
       const uint32_t buf = lds0 + (uint32_t)((t & (WT_NBUF - 1)) * WT_BUF);
       const int64_t ra = (int64_t)t * WT_BK * lda * 2, rb = (int64_t)t * WT_BK * ldb * 2;
       const v4i32 da = wt_desc(Ag + ra, extA - ra), db = wt_desc(Bg + rb, extB - rb);
@@ -529,6 +532,9 @@ __global__ __launch_bounds__(WT_NTH, 1) void wgrad_tt_kernel(WTParams P) {
       // ---- read segment: fragments of stage t, the DMA of t + 3 (into the buffer of t - 1, read by both groups
       //      before the last barrier), retire t + 1
       const char* buf = smem + (t & (WT_NBUF - 1)) * WT_BUF;
+#ifdef WT_SKIP_READS
+      if (t == k0)                // probe: fragments read once per piece
+#endif
       {
         const char* pa_lo = buf + wr * 8 * 1024 + f_lo;
         const char* pa_hi = buf + wr * 8 * 1024 + f_hi;
@@ -548,12 +554,19 @@ __global__ __launch_bounds__(WT_NTH, 1) void wgrad_tt_kernel(WTParams P) {
       w3_barrier();
       // ---- MFMA segment
       __builtin_amdgcn_s_setprio(1);
+#ifndef WT_SKIP_MFMA
 #pragma unroll
       for (int i = 0; i < 8; ++i)
 #pragma unroll
         for (int f = 0; f < 4; ++f)
           acc[i][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, af[i]),
                                                              __builtin_bit_cast(bf16x8, bfr[f]), acc[i][f], 0, 0, 0);
+#else
+#pragma unroll
+      for (int i = 0; i < 8; ++i) asm volatile("" ::"v"(af[i].x), "v"(af[i].w));   // probe: fragments kept live
+#pragma unroll
+      for (int f = 0; f < 4; ++f) asm volatile("" ::"v"(bfr[f].x), "v"(bfr[f].w));
+#endif
       if (rowptr != nullptr && t % pr.tiles_n == tn) {
 #define WT_RS(a, b)                                                                                              \
   rs[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, af[a]), __builtin_bit_cast(bf16x8, ones), \
@@ -584,6 +597,10 @@ __global__ __launch_bounds__(WT_NTH, 1) void wgrad_tt_kernel(WTParams P) {
         }
     }
     bool write = true;
+#ifdef WT_NO_FIX
+    if (ns < P.nk) write = false;   // probe: partial tiles neither published nor summed (results wrong)
+    else
+#endif
     if (ns < P.nk) {
       // ---- partial tile: publish, take a ticket, the last arriver sums the other pieces
       const int64_t x0 = (int64_t)tile * P.nk, x1 = x0 + P.nk - 1;
@@ -805,3 +822,10 @@ extern "C" int aw_wgrad_batch(const aw_gemm_args* args, int n, void* ws, int64_t
   hipLaunchKernelGGL(wgrad_tt_kernel, dim3(P.G), dim3(WT_NTH), 0, reinterpret_cast<hipStream_t>(stream), P);
   return aw::check_launch("aw_wgrad_batch");
 }
+
+#ifdef WT_PROBE
+// tools/probe/wgrad_tt_probe.py: the stream-K batch kernel alone (variants built with the WT_* knobs above)
+extern "C" int wt_probe_batch(const aw_gemm_args* args, int n, void* ws, int64_t ws_bytes, void* stream) {
+  return aw_wgrad_batch(args, n, ws, ws_bytes, stream);
+}
+#endif
