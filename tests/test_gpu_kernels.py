@@ -210,6 +210,57 @@ def test_gemm_bf16_residual_stream_epilogues(K, tile, conv, p_drop):
         torch.testing.assert_close(res[bf][1], res[torch.float32][1], rtol=0, atol=0)
 
 
+@pytest.mark.parametrize("seg", [8, 16, 32])
+@pytest.mark.parametrize("Bw_tiles", [1, 3])
+def test_gemm_conv3_one_image_tap3_vs_fp32(K, seg, Bw_tiles):
+    """The decoder k = 3 conv on the 256-row one-image tile (gemm_core.h CONV_TAP3: one staged x image per 64 channels
+    read with each tap's row shift and a per-lane window mask; model/vq_vae_patch_embedd.py:142-145 with :60-74)
+    against torch fp32 conv1d on the same bf16 operands: the forward with the conv1 epilogue (bias, f32 C, bf16
+    GELU copy) and the input gradient with the GELU' epilogue (bf16 pre-activation, bf16 C), at windows of 8 / 16 / 32
+    tokens; and against the row-shift tiles (aw_gemm_set_tap3(0)) on the same launch."""
+    from arcweld import _native
+    bf = torch.bfloat16
+    S, Cin, Cout = seg, 128, 256
+    M = 256 * Bw_tiles
+    Bw = M // S
+    x = _rand((M, Cin), 71, bf)
+    W = torch.tensor(gen.normal(72, (Cout, Cin, 3), 0.05))
+    bias = _rand((Cout,), 73)
+    Wk = torch.empty(Cout, 3 * Cin, device=DEV, dtype=bf)
+    K.weight_relayout(W.to(DEV), Cout, Cin, 3, 0, 1, Wk)
+    Wd = torch.empty(3 * Cout, Cin, device=DEV, dtype=bf)
+    K.weight_relayout(W.to(DEV), Cout, Cin, 3, 0, 2, Wd)
+    g = _rand((M, Cout), 74, bf)
+    pre = _rand((M, Cin), 75, bf)
+    res = {}
+    for mode in (1, 0):
+        _native.call("aw_gemm_set_tap3", mode)
+        try:
+            y = torch.empty(M, Cout, device=DEV)
+            y2 = torch.empty(M, Cout, device=DEV, dtype=bf)
+            K.gemm(x, Wk, M, Cout, 3 * Cin, conv=(Cin, S, 1, 0), bias=bias, C=y, C2=y2, c2_mode=1)
+            gin = torch.empty(M, Cin, device=DEV, dtype=bf)
+            K.gemm(g, Wd, M, Cin, 3 * Cout, b_trans=True, conv=(Cout, S, -1, 0), pre=pre, C=gin)
+            torch.cuda.synchronize()
+        finally:
+            _native.call("aw_gemm_set_tap3", 1)
+        res[mode] = (y, y2, gin)
+    xr = x.float().cpu().view(Bw, S, Cin).transpose(1, 2)
+    Wr = W.to(bf).float()
+    ref = F.conv1d(xr, Wr, padding=1).transpose(1, 2).reshape(M, Cout) + bias.cpu()
+    torch.testing.assert_close(res[1][0].cpu(), ref, rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(res[1][1].float().cpu(), F.gelu(ref), rtol=1e-2, atol=1e-2)
+    xr2 = torch.zeros_like(xr).requires_grad_(True)
+    F.conv1d(xr2, Wr, padding=1).backward(g.float().cpu().view(Bw, S, Cout).transpose(1, 2))
+    pc = pre.float().cpu()
+    gp = 0.5 * (1 + torch.erf(pc / np.sqrt(2))) + pc * torch.exp(-0.5 * pc ** 2) / np.sqrt(2 * np.pi)
+    gref = xr2.grad.transpose(1, 2).reshape(M, Cin) * gp
+    torch.testing.assert_close(res[1][2].float().cpu(), gref, rtol=1e-2, atol=2e-2)
+    # against the row-shift tiles: the same sums in another order (f32 accumulation), the same bf16 roundings
+    torch.testing.assert_close(res[1][0], res[0][0], rtol=1e-5, atol=1e-4)
+    torch.testing.assert_close(res[1][2].float(), res[0][2].float(), rtol=1e-2, atol=1e-2)
+
+
 @pytest.mark.parametrize("tag,Kc,D,N,eseed,estd", [
     ("K512_D64_init", 512, 64, 16384, 201, None),
     ("K512_D64_trained", 512, 64, 16384, 202, 0.08),
