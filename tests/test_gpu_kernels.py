@@ -604,7 +604,6 @@ def test_wgrad_batch_stream_k_vs_fp32_reference(case):
         probs.append((A, x, M, N, Kt, dict(a_trans=True, b_trans=True, accumulate=True, a_rowsum=b, alpha=alpha,
                                            **kw)))
         refs.append((C, b, C0, want, b0, b0 + alpha * A.float().sum(0)))
-    assert K.wgrad_batch_ok(probs)
     K.wgrad_batch(probs)
     torch.cuda.synchronize()
     for C, b, C0, want, b0, bw in refs:

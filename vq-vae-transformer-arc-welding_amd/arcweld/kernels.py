@@ -167,10 +167,12 @@ def gemm_grouped(problems, stream=None):
 
 
 def wgrad_batch_ok(problems):
-    """True when aw_wgrad_batch takes these problems (bf16 operands, M / N multiples of 256, one K) and it is not
-    switched off (ARCWELD_WGRAD_BATCH=0: the per-shape grouped launches instead, A/B)."""
+    """True when aw_wgrad_batch takes these problems (bf16 operands, M / N multiples of 256, one K) and it is switched
+    on (ARCWELD_WGRAD_BATCH=1).  Off by default: measured slower than the per-shape grouped launches on the bench
+    shapes (its stream-K ranges put concurrent workgroups at different k, so their operand streams
+    do not share L2 -- 3.2 GB fetched per transformer half-step)."""
     import os
-    if os.environ.get("ARCWELD_WGRAD_BATCH", "1") == "0" or not problems or len(problems) > MAX_GROUPS:
+    if os.environ.get("ARCWELD_WGRAD_BATCH", "0") != "1" or not problems or len(problems) > MAX_GROUPS:
         return False
     arr = (GemmArgs * len(problems))(*[_gemm_args(A, B, M, N, K, **kw) for (A, B, M, N, K, kw) in problems])
     return nat.load().aw_wgrad_batch_workspace(arr, len(problems)) > 0
