@@ -106,10 +106,6 @@ int aw_gemm_set_tile(int bm);
  * 0 = automatic (the 8-wave ping-pong kernel when the shape qualifies and fills the chip), 1 = force it whenever the
  * shape qualifies, -1 = always the generic grouped GEMM (tests, A/B). */
 int aw_gemm_set_wgrad_policy(int mode);
-/* The decoder's k = 3 convs (model/vq_vae_patch_embedd.py:142-145 with :60-74; forward and input gradient, bf16,
- * conv_operand 0): 1 = one 256-row tile per CU that stages ONE x image per 64 channels and reads it with each tap's
- * row shift (default; ARCWELD_TAP3 sets the initial value), 0 = the row-shift tiles that restage x per tap. */
-int aw_gemm_set_tap3(int mode);
 /* Batched weight gradients of plain (1-tap) layers: n <= AW_GEMM_MAX_GROUPS accumulate-mode problems
  *   C_i[m*ldc + colmap(n)] += alpha * sum_k A_i[k*lda + m] * B_i[k*ldb + n],  a_rowsum_i[m] += alpha * sum_k A_i[k*lda + m]
  * with bf16 operands (a_trans = b_trans = 1), f32 C, any M_i / N_i that are multiples of 256, one K (any K: ragged

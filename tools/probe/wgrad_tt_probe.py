@@ -1,7 +1,7 @@
 """The stream-K batched weight-gradient kernel (csrc/wgrad.hip, wgrad_tt_kernel) alone: time per launch at the
 transformer's half-step batch (4 blocks x {qkv, proj, fc1, fc2} at d 512, K = 51 x 321 tokens) and at the VQ-VAE
 encoder's 16 centre-tap convs (512 x 512, K 16384), for the library kernel and probe builds with parts left out
-(WT_NO_FIX: split tiles neither published nor summed; WT_SKIP_DMA / WT_SKIP_READS / WT_SKIP_MFMA; results of the probe
+(WT_NO_FIX: split pieces neither published nor summed; WT_SKIP_DMA / WT_SKIP_READS / WT_SKIP_MFMA; results of the probe
 builds are garbage by construction).  Build on the CPU first:  python tools/probe/wgrad_tt_probe.py build
 usage on the GPU box: python tools/probe/wgrad_tt_probe.py [iters]"""
 import ctypes

@@ -1,8 +1,10 @@
 set -o pipefail
 export TMPDIR=/tmp
-O=gpurun_out/r04_s7
+O=gpurun_out/r04_s8
 mkdir -p $O
-for v in 0 1; do
-ARCWELD_TAP3=$v timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/tv$v -o run --output-format csv -- python3 bench.py --no-cpu-baseline --no-fp32 --no-stress --no-profile --no-transformer --steps 10 --warmup 3 --detail "" > $O/tv$v.log 2>&1 || { tail -20 $O/tv$v.log; exit 1; }
-done
-echo done
+timeout -k 10 300 python -u -m pytest tests/test_gpu_kernels.py -x -q --timeout 200 --timeout-method thread -k "wgrad" > $O/k.log 2>&1 || { tail -40 $O/k.log; exit 1; }
+tail -1 $O/k.log
+timeout -k 10 200 python -u tools/probe/wgrad_tt_probe.py 10 > $O/wt_probe.log 2>&1 || { tail -20 $O/wt_probe.log; exit 1; }
+grep -v amdgpu.ids $O/wt_probe.log
+VAR=ARCWELD_WGRAD_BATCH bash tools/ab_env_bench.sh 0 1 2 || exit 1
+ARGS="--only transformer_pretokenized" VAR=ARCWELD_WGRAD_BATCH bash tools/ab_env_bench.sh 0 1 2 || exit 1

@@ -76,7 +76,6 @@ SIGNATURES = {
     "aw_gemm_grouped": [ctypes.POINTER(GemmArgs), c_int, c_p],
     "aw_gemm_set_tile": [c_int],
     "aw_gemm_set_wgrad_policy": [c_int],
-    "aw_gemm_set_tap3": [c_int],
     "aw_wgrad_batch_workspace": [ctypes.POINTER(GemmArgs), c_int],
     "aw_wgrad_batch": [ctypes.POINTER(GemmArgs), c_int, c_p, c_i64, c_p],
     "aw_weight_relayout_batch": [ctypes.POINTER(RelayoutJob), c_int, c_int, c_p],

@@ -44,35 +44,11 @@ uint32_t epi_code(const aw_gemm_args& a, const GemmP& P, bool ragged) {
   return c;
 }
 
-int g_tap3 = -1;   // aw_gemm_set_tap3 / ARCWELD_TAP3: 1 the one-image implicit conv where it applies, 0 never
-
-// The k = 3 implicit conv on A as one 256-row tile per CU reading ONE staged x image for its three taps
-// (gemm_core.h, CONV_TAP3): bf16, whole windows per tile (seg | 256), whole tiles of rows, 64-channel chunks,
-// no split-K, and a specialised epilogue.
-bool tap3_ok(const aw_gemm_args& a, const GemmP& P, bool ragged) {
-  if (g_tap3 < 0) {
-    const char* e = getenv("ARCWELD_TAP3");
-    g_tap3 = e ? atoi(e) : 1;
-  }
-  return g_tap3 && a.a_dtype == AW_BF16 && a.conv_cin > 0 && a.conv_operand == 0 && !a.a_trans && !ragged &&
-         a.conv_cin % 64 == 0 && a.K == 3 * a.conv_cin && a.M % 256 == 0 && a.conv_seg > 0 && 256 % a.conv_seg == 0 &&
-         P.splits == 1 && P.ngroups == 1 && !a.accumulate;
-}
-
 template <typename T>
 void dispatch(const GemmP& P, hipStream_t s, bool ragged) {
   const Layout ly = layout_of(P.a);
   uint32_t code = epi_code(P.a, P, ragged);
   constexpr bool BF = sizeof(T) == 2;
-  if constexpr (BF) {
-    if (code != EP_GENERIC && code != EP_ACCUM && (ly == L_NN_CONV || ly == L_NT_CONV) && tap3_ok(P.a, P, ragged)) {
-      GemmP P3 = P;
-      P3.bm = 256;
-      P3.tiles_per_group = (P.a.M / 256) * P.tiles_n;
-      P3.nblocks = P3.tiles_per_group;
-      if (launch_fast_256(P3, s, ly == L_NN_CONV ? L_NN_CONV3 : L_NT_CONV3, code)) return;
-    }
-  }
   if (code == EP_ACCUM) {
     switch (ly) {
       case L_TN: launch_tiled<T, L_TN, EP_ACCUM>(P, s); return;
@@ -238,12 +214,6 @@ static bool is_ragged(const aw_gemm_args& a) {
 #endif
 
 static int g_tile_override = 0;   // aw_gemm_set_tile: 0 = automatic, 128 / 256 = force (tests, tuning)
-
-extern "C" int aw_gemm_set_tap3(int mode) {
-  AW_REQUIRE(mode == 0 || mode == 1, "aw_gemm_set_tap3: mode must be 0 or 1");
-  g_tap3 = mode;
-  return AW_OK;
-}
 
 extern "C" int aw_gemm_set_tile(int bm) {
   AW_REQUIRE(bm == 0 || bm == 128 || bm == 256, "aw_gemm_set_tile: bm must be 0, 128 or 256");

@@ -86,10 +86,7 @@ struct GemmP {
   float* gRow[AW_GEMM_MAX_GROUPS];
 };
 
-// CONV_TAP3: the implicit k = 3 conv on A (L_NN_CONV3 / L_NT_CONV3, 256-row tiles): each stage holds ONE unshifted
-// image of 64 input channels of the tile's rows and the three taps' B images; the taps read the A image with their
-// row shift (see the TAP3 loop in gemm_kernel)
-enum { CONV_NONE = 0, CONV_ROWSHIFT = 1, CONV_KSHIFT = 2, CONV_TAP3 = 3 };
+enum { CONV_NONE = 0, CONV_ROWSHIFT = 1, CONV_KSHIFT = 2 };
 
 // Epilogue codes: a specialised kernel is compiled per code in use (gemm_fast_*.hip); EP_GENERIC reads every
 // feature from the argument block at run time (all other shapes / dtypes / alignments).
@@ -461,15 +458,11 @@ __global__ __launch_bounds__(Cfg<BMT>::NTH, RAGGED ? 1 : Cfg<BMT>::MINB) void ge
   constexpr int BK = TT<T>::BK;
   constexpr int A_IMG = BMT * ROWB;                // A stage image bytes; the B image follows it
   constexpr int STAGE = stage_bytes<BMT>();
-  constexpr bool TAP3 = ACONV == CONV_TAP3;
-  constexpr int B_IMG = BN * ROWB;                 // one B image (a tap's 64 k x 128 columns)
-  constexpr int STAGE3 = BMT * ROWB + 3 * B_IMG;   // TAP3 stage: the A image + the three taps' B images (80 KB)
-  static_assert(!TAP3 || (BMT == 256 && sizeof(T) == 2 && !ATR && !RAGGED), "TAP3: bf16 256-row tiles only");
   static_assert(!(RAGGED && BMT != 128), "ragged shapes use the 128-row register-staged tile");
   using SA = Stager<T, ATR, ACONV, RAGGED, BMT, NTH>;
   using SB = Stager<T, BTR, BCONV, RAGGED, BN, NTH>;
   const aw_gemm_args& p = P.a;
-  __shared__ __attribute__((aligned(16))) char smem[TAP3 ? 2 * STAGE3 : smem_bytes<BMT>()];
+  __shared__ __attribute__((aligned(16))) char smem[smem_bytes<BMT>()];
 
   AW_STAMP(0);
   const int tid = threadIdx.x;
@@ -540,61 +533,7 @@ __global__ __launch_bounds__(Cfg<BMT>::NTH, RAGGED ? 1 : Cfg<BMT>::MINB) void ge
   };
 
   const int nk = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
-  if constexpr (TAP3) {
-    // Implicit k = 3 conv along windows of `seg` rows, A[m][j*cin + c] = x[m + dir*(j - 1)][c] (zero outside the
-    // window): the three taps read ONE staged image of x's 256 tile rows, each with its row shift, so a stage of 64
-    // channels carries 32 KB of A for 3 x 256 x 128 x 64 MACs (the row-shift tile restages x per tap: 96 KB of A).
-    // Windows never straddle a tile (seg | 256), and the 16 rows of a fragment sit at window positions
-    // pos0 + 0..15, so a tap's mask is a per-lane constant: the lanes whose shifted row leaves the window read zeros.
-    // Two 80 KB stages (the whole LDS): the DMA of chunk c + 1 flies under the 96 MFMAs per wave of chunk c.
-    const int cin = p.conv_cin, seg = p.conv_seg, dir = p.conv_dir;
-    const int nc = cin / BK;
-    auto issue = [&](int c, uint32_t so) {
-      sa.dma(c * BK, so);
-#pragma unroll
-      for (int j = 0; j < 3; ++j) sb.dma(j * cin + c * BK, so + (uint32_t)(j * B_IMG));
-    };
-    const int li = lane & 15, g = lane >> 4;
-    bool okm[FM], okp[FM];   // the row at shift -1 / +1 lies in the lane's window
-#pragma unroll
-    for (int f = 0; f < FM; ++f) {
-      const int pos = (wm * WR + f * 16 + li) % seg;
-      okm[f] = pos > 0;
-      okp[f] = pos < seg - 1;
-    }
-    issue(0, 0u);
-    wait_vmcnt<0>();
-    __syncthreads();
-    AW_STAMP(1);
-    for (int c = 0; c < nc; ++c) {
-      const char* a_l = smem + (c & 1) * STAGE3;
-      if (c + 1 < nc) issue(c + 1, (uint32_t)(((c + 1) & 1) * STAGE3));
-#pragma unroll
-      for (int j = 0; j < 3; ++j) {
-        const int sft = dir * (j - 1);
-        const char* b_l = a_l + BMT * ROWB + j * B_IMG;
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          uint4 af[FM], bfr[4];
-#pragma unroll
-          for (int f = 0; f < FM; ++f) {
-            const int r = wm * WR + f * 16 + li;
-            const bool ok = sft == 0 || (sft < 0 ? okm[f] : okp[f]);
-            const uint4 v = *reinterpret_cast<const uint4*>(a_l + nt_off(ok ? r + sft : r, 4 * u + g));
-            af[f] = ok ? v : make_uint4(0u, 0u, 0u, 0u);
-          }
-#pragma unroll
-          for (int f = 0; f < 4; ++f) bfr[f] = frag<T, BTR, BN * (int)sizeof(T)>(b_l, wn * 64 + f * 16, lane, u);
-#pragma unroll
-          for (int i = 0; i < FM; ++i)
-#pragma unroll
-            for (int jj = 0; jj < 4; ++jj) Mfma<T>::run(acc[i][jj], af[i], bfr[jj]);
-        }
-      }
-      wait_vmcnt<0>();      // chunk c + 1 landed
-      __syncthreads();      // ... for every wave; every read of chunk c retired before its stage is refilled
-    }
-  } else if constexpr (use_dma && Cfg<BMT>::NSTAGE == 2) {
+  if constexpr (use_dma && Cfg<BMT>::NSTAGE == 2) {
     // two stages: the loads of step t+1 fly into the other stage while step t computes
     char* L0 = smem;
     char* L1 = smem + STAGE;
@@ -910,8 +849,7 @@ __global__ __launch_bounds__(Cfg<BMT>::NTH, RAGGED ? 1 : Cfg<BMT>::MINB) void ge
 }
 
 // operand-layout variants of the kernel
-enum Layout { L_NN = 0, L_NN_CONV = 1, L_NT = 2, L_NT_CONV = 3, L_TN = 4, L_TT = 5, L_TT_KCONV = 6, L_NN_CONV3 = 7,
-              L_NT_CONV3 = 8 };
+enum Layout { L_NN = 0, L_NN_CONV = 1, L_NT = 2, L_NT_CONV = 3, L_TN = 4, L_TT = 5, L_TT_KCONV = 6 };
 
 template <Layout LY> struct LayoutArgs;
 template <> struct LayoutArgs<L_NN> { static constexpr bool ATR = false, BTR = false; static constexpr int AC = CONV_NONE, BC = CONV_NONE; };
@@ -921,8 +859,6 @@ template <> struct LayoutArgs<L_NT_CONV> { static constexpr bool ATR = false, BT
 template <> struct LayoutArgs<L_TN> { static constexpr bool ATR = true, BTR = false; static constexpr int AC = CONV_NONE, BC = CONV_NONE; };
 template <> struct LayoutArgs<L_TT> { static constexpr bool ATR = true, BTR = true; static constexpr int AC = CONV_NONE, BC = CONV_NONE; };
 template <> struct LayoutArgs<L_TT_KCONV> { static constexpr bool ATR = true, BTR = true; static constexpr int AC = CONV_NONE, BC = CONV_KSHIFT; };
-template <> struct LayoutArgs<L_NN_CONV3> { static constexpr bool ATR = false, BTR = false; static constexpr int AC = CONV_TAP3, BC = CONV_NONE; };
-template <> struct LayoutArgs<L_NT_CONV3> { static constexpr bool ATR = false, BTR = true; static constexpr int AC = CONV_TAP3, BC = CONV_NONE; };
 
 template <typename T, Layout LY, bool RAGGED, uint32_t EPI, int BMT>
 inline void launch_kernel(const GemmP& P, hipStream_t s) {

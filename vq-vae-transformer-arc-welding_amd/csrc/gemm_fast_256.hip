@@ -32,16 +32,6 @@ bool launch_fast_256(const GemmP& P, hipStream_t s, Layout ly, uint32_t code) {
         AW_BWD_CONV_CODES(AW_FAST_CASE256, bf16, L_NT_CONV)
         default: return false;
       }
-    case L_NN_CONV3:      // the decoder's k = 3 convs, one staged x image for the three taps
-      switch (code) {
-        AW_FWD_CODES(AW_FAST_CASE256, bf16, L_NN_CONV3)
-        default: return false;
-      }
-    case L_NT_CONV3:
-      switch (code) {
-        AW_BWD_CONV_CODES(AW_FAST_CASE256, bf16, L_NT_CONV3)
-        default: return false;
-      }
     default:
       return false;
   }

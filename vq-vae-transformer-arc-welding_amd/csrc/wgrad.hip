@@ -396,14 +396,18 @@ int g_policy = 0;   // aw_gemm_set_wgrad_policy: 0 automatic, 1 force, -1 off
 //    each wave owns 128 x 64 outputs (8 x 4 fragments of v_mfma_f32_16x16x32_bf16); per stage a wave reads 12
 //    transposed fragments (24 ds_read_b64_tr_b16) and issues 32 MFMAs.  Four 32 KB stages (128 KB of LDS) filled by
 //    LDS-DMA three stages ahead; the tails of a ragged K read zeros from the buffer range check.
-//  * Stream-K: one workgroup per CU; the I = tiles * stages iterations of the whole batch are cut into equal
-//    contiguous ranges, so every CU does the same work whatever the tile count (the transformer's 192 tiles on 256
-//    CUs, the encoder's 64).  A tile split between workgroups is fixed up by the LAST arriving piece: every partial
-//    piece stores its accumulators write-through (sc1) into its workspace slot, drains them (vmcnt(0)), joins a
-//    workgroup barrier and takes a ticket with one agent-scope atomic add; the piece whose ticket completes the count
-//    loads the other pieces' slots with sc1 loads and does the one read-modify-write of the gradient
-//    (MI355X_MICROARCH.md, inter-workgroup hand-off, first row of the measured forms).  No piece ever waits on
-//    another, so the launch cannot deadlock whatever its residency.
+//  * Split-K with k-ALIGNED units: tile t is cut into S equal token ranges (S = 4 at the bench shapes: the
+//    transformer's 192 tiles -> 768 units = three full rounds of 256 CUs, the encoder's 64 -> one round); persistent
+//    workgroups (one per CU) take units u = c, c + G, ... in split-major order, so the workgroups that run together
+//    are at the same k of their ranges, and the tiles that share an operand block sit on one XCD: their operand
+//    streams meet in that XCD's L2.  (A stream-K cut into equal contiguous ranges, measured first, put concurrent
+//    workgroups at different k: 3.2 GB fetched per transformer half-step, slower than the per-kind launches.)
+//  * A tile's S partial pieces are summed by the LAST arriving piece: every piece stores its accumulators
+//    write-through (sc1) into its workspace slot, drains them (vmcnt(0)), joins a workgroup barrier and takes a
+//    ticket with one agent-scope atomic add; the piece whose ticket completes the count loads the other pieces' slots
+//    with sc1 loads and does the one read-modify-write of the gradient (MI355X_MICROARCH.md, inter-workgroup hand-off,
+//    first row of the measured forms).  No piece ever waits on another, so the launch cannot deadlock whatever its
+//    residency.  The read-modify-write goes through LDS in two 128-row halves: float4 per lane, 16 row loads in flight.
 //  * Bias gradients: row sums of the A fragments by MFMA against an all-ones fragment, on the stages s with
 //    s % tiles_n == tn (spread over the row's tiles), f32 atomics per piece.
 constexpr int WT_BM = 256, WT_BN = 256, WT_BK = 32, WT_NTH = 512;
@@ -427,10 +431,9 @@ struct WTProb {
 
 struct WTParams {
   WTProb p[AW_GEMM_MAX_GROUPS];
-  int nprob, K, nk, G, total_tiles;
-  int64_t I;
+  int nprob, K, nk, G, total_tiles, S, units;
   float alpha;
-  float* ws;          // 2 * G slots of WT_SLAB floats
+  float* ws;          // one slot of WT_SLAB floats per unit
 };
 
 __device__ int g_wt_tickets[WT_MAXTILES];   // per-tile arrival counters; the last arriver resets its own to 0
@@ -443,9 +446,6 @@ __device__ __forceinline__ v4i32 wt_desc(const void* base, int64_t nbytes) {
                (int)__builtin_amdgcn_readfirstlane((uint32_t)nb), 0x00020000};
 }
 
-// first workgroup (logical index) whose range holds iteration x: max c with floor(c*I/G) <= x
-__device__ __forceinline__ int wt_owner(int64_t x, int64_t I, int G) { return (int)(((x + 1) * G - 1) / I); }
-__device__ __forceinline__ int64_t wt_start(int c, int64_t I, int G) { return (int64_t)c * I / G; }
 
 __device__ __forceinline__ void wt_st_sc1(float* p, f32x4 v) {
   asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
@@ -459,7 +459,6 @@ __global__ __launch_bounds__(WT_NTH, 1) void wgrad_tt_kernel(WTParams P) {
   const int g = lane >> 4, li = lane & 15, q = li >> 2, p4 = li & 3;
   const int wcu = __builtin_amdgcn_readfirstlane(wc);
   const int c = awg::xcd_remap(blockIdx.x, P.G);      // logical workgroup: consecutive ranges share an XCD's L2
-  const int64_t it_end = wt_start(c + 1, P.I, P.G);
   const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
   const uint32_t wave_dst = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(tid & ~63)) * 16u;
   const uint4 ones = make_uint4(0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u);
@@ -475,10 +474,9 @@ __global__ __launch_bounds__(WT_NTH, 1) void wgrad_tt_kernel(WTParams P) {
     src_col[j] = (ch >> 6) * 16 + (ch & 1) * 8;
   }
 
-  for (int64_t it = wt_start(c, P.I, P.G); it < it_end;) {
-    const int tile = (int)(it / P.nk);
-    const int k0 = (int)(it - (int64_t)tile * P.nk);
-    const int k1 = (int)min((int64_t)P.nk, (int64_t)k0 + (it_end - it));
+  for (int unit = c; unit < P.units; unit += P.G) {
+    const int sp = unit / P.total_tiles, tile = unit - sp * P.total_tiles;
+    const int k0 = (int)((int64_t)sp * P.nk / P.S), k1 = (int)((int64_t)(sp + 1) * P.nk / P.S);
     int pi = 0;
     while (pi + 1 < P.nprob && tile >= P.p[pi + 1].tile0) ++pi;
     const WTProb& pr = P.p[pi];
@@ -598,15 +596,12 @@ __global__ __launch_bounds__(WT_NTH, 1) void wgrad_tt_kernel(WTParams P) {
     }
     bool write = true;
 #ifdef WT_NO_FIX
-    if (ns < P.nk) write = false;   // probe: partial tiles neither published nor summed (results wrong)
+    if (P.S > 1) write = false;   // probe: split tiles neither published nor summed (results wrong)
     else
 #endif
-    if (ns < P.nk) {
-      // ---- partial tile: publish, take a ticket, the last arriver sums the other pieces
-      const int64_t x0 = (int64_t)tile * P.nk, x1 = x0 + P.nk - 1;
-      const int cf = wt_owner(x0, P.I, P.G), cl = wt_owner(x1, P.I, P.G);
-      const int slot = 2 * c + (k0 == 0 ? 1 : 0);
-      float* mine = P.ws + (int64_t)slot * WT_SLAB;
+    if (P.S > 1) {
+      // ---- one piece of S: publish, take a ticket, the last arriver sums the other pieces
+      float* mine = P.ws + (int64_t)unit * WT_SLAB;
 #pragma unroll
       for (int i = 0; i < 8; ++i)
 #pragma unroll
@@ -615,19 +610,17 @@ __global__ __launch_bounds__(WT_NTH, 1) void wgrad_tt_kernel(WTParams P) {
       __syncthreads();
       if (tid == 0) {
         const int old = __hip_atomic_fetch_add(&g_wt_tickets[tile], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const int last = old == cl - cf;
+        const int last = old == P.S - 1;
         if (last) __hip_atomic_store(&g_wt_tickets[tile], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         s_last = last;
       }
       __syncthreads();
       write = s_last != 0;
       if (write) {
-        for (int o = cf; o <= cl; ++o) {
-          if (o == c) continue;
-          const int64_t so = wt_start(o, P.I, P.G);
-          const int oslot = 2 * o + (so <= x0 ? 1 : 0);
-          const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(P.ws + (int64_t)oslot * WT_SLAB, (short)0,
-                                                                  WT_SLAB * 4, 0x00020000);
+        for (int o = 0; o < P.S; ++o) {
+          if (o == sp) continue;
+          const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(P.ws + ((int64_t)o * P.total_tiles + tile) * WT_SLAB,
+                                                              (short)0, WT_SLAB * 4, 0x00020000);
 #pragma unroll
           for (int i = 0; i < 8; ++i)
 #pragma unroll
@@ -641,25 +634,58 @@ __global__ __launch_bounds__(WT_NTH, 1) void wgrad_tt_kernel(WTParams P) {
       }
     }
     if (write) {
+      // ---- the tile's one read-modify-write of the gradient, through LDS in two 128-row halves (the stage ring is
+      //      free: every wave passed the loop's last barrier): lane-contiguous float4 columns, 16 rows in flight
       float* C = pr.C;
+      float* T = reinterpret_cast<float*>(smem);                // [128][WT_BN] f32 = 128 KB
+      const bool vec = pr.col_mod == 0 && pr.col_mul <= 1 && (pr.ldc & 3) == 0 && (pr.col_off & 3) == 0 &&
+                       (((uintptr_t)C) & 15) == 0;
 #pragma unroll
-      for (int f = 0; f < 4; ++f) {
-        const int n = n0 + wc * 64 + 16 * f + li;
-        const int64_t oc = pr.col_mod > 0 ? (int64_t)(n % pr.col_mod) * pr.col_mul + n / pr.col_mod + pr.col_off
-                                          : (int64_t)n * (pr.col_mul > 0 ? pr.col_mul : 1) + pr.col_off;
+      for (int hh = 0; hh < 2; ++hh) {
+        if (hh) __syncthreads();                                 // the first half's reads are done
+        if (wr == hh) {
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const int row = m0 + wr * 128 + 16 * i + 4 * g;
-          float* d = C + (int64_t)row * pr.ldc + oc;
-          float v[4];
+          for (int i = 0; i < 8; ++i)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = d[(int64_t)r * pr.ldc];
+            for (int f = 0; f < 4; ++f)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) d[(int64_t)r * pr.ldc] = v[r] + alpha * acc[i][f][r];
+              for (int r = 0; r < 4; ++r) T[(16 * i + 4 * g + r) * WT_BN + wc * 64 + 16 * f + li] = acc[i][f][r];
+        }
+        __syncthreads();
+        const int row0 = m0 + 128 * hh;
+        if (vec) {
+          const int c4 = (tid & 63) * 4, rr = tid >> 6;           // 64 float4 per row, 8 rows per pass
+#pragma unroll
+          for (int k0r = 0; k0r < 16; k0r += 8) {                 // 8 rows of loads in flight per lane
+            f32x4 old[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+              old[k] = *reinterpret_cast<const f32x4*>(C + (int64_t)(row0 + rr + 8 * (k0r + k)) * pr.ldc + pr.col_off +
+                                                       n0 + c4);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+              const f32x4 a = *reinterpret_cast<const f32x4*>(T + (rr + 8 * (k0r + k)) * WT_BN + c4);
+              *reinterpret_cast<f32x4*>(C + (int64_t)(row0 + rr + 8 * (k0r + k)) * pr.ldc + pr.col_off + n0 + c4) =
+                  old[k] + alpha * a;
+            }
+          }
+        } else {
+          const int cc = tid & 255, rr = tid >> 8;                // one column per lane, 2 rows per pass
+          const int n = n0 + cc;
+          const int64_t oc = pr.col_mod > 0 ? (int64_t)(n % pr.col_mod) * pr.col_mul + n / pr.col_mod + pr.col_off
+                                            : (int64_t)n * (pr.col_mul > 0 ? pr.col_mul : 1) + pr.col_off;
+          for (int k = 0; k < 64; k += 8) {
+            float old[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) old[e] = C[(int64_t)(row0 + rr + 2 * (k + e)) * pr.ldc + oc];
+#pragma unroll
+            for (int e = 0; e < 8; ++e)
+              C[(int64_t)(row0 + rr + 2 * (k + e)) * pr.ldc + oc] = old[e] + alpha * T[(rr + 2 * (k + e)) * WT_BN + cc];
+          }
         }
       }
     }
-    it += ns;
+    __syncthreads();     // the epilogue's LDS reads are done before the next unit's DMA refills the ring
   }
 }
 
@@ -728,11 +754,23 @@ int wt_plan(const aw_gemm_args* args, int n, WTParams* P) {
   P->K = a0.K;
   P->nk = (a0.K + WT_BK - 1) / WT_BK;
   P->total_tiles = tiles;
-  P->I = (int64_t)tiles * P->nk;
-  // one workgroup per CU, but at least a quarter of a tile's stages per workgroup: a tile is then split into at most
-  // five pieces, so the last arriver's fix-up reads at most four partial tiles (a small batch runs on fewer CUs)
-  const int64_t min_iters = std::max(1, P->nk / 4);
-  P->G = (int)std::max<int64_t>(1, std::min<int64_t>(wt_cus(), P->I / min_iters));
+  // split count: the fewest stages per CU over whole rounds of units, S <= 4 (the last arriver then reads at most
+  // three partial tiles) and >= 16 stages per unit; ties go to the smaller S
+  const int cus = wt_cus();
+  int best = 1;
+  int64_t best_cost = INT64_MAX;
+  for (int S = 1; S <= 4; S *= 2) {
+    if (S > 1 && P->nk / S < 16) break;
+    const int64_t units = (int64_t)tiles * S, rounds = (units + cus - 1) / cus;
+    const int64_t cost = rounds * ((P->nk + S - 1) / S);
+    if (cost < best_cost) {
+      best_cost = cost;
+      best = S;
+    }
+  }
+  P->S = best;
+  P->units = tiles * best;
+  P->G = std::min(cus, P->units);
   P->alpha = a0.alpha;
   return AW_OK;
 }
@@ -810,13 +848,14 @@ extern "C" int w3_probe_stamps(uint64_t* host, int n) {
 extern "C" int64_t aw_wgrad_batch_workspace(const aw_gemm_args* args, int n) {
   WTParams P;
   if (wt_plan(args, n, &P) != AW_OK) return -1;
-  return (int64_t)2 * P.G * WT_SLAB * (int64_t)sizeof(float);
+  return P.S > 1 ? (int64_t)P.units * WT_SLAB * (int64_t)sizeof(float) : 16;
 }
 
 extern "C" int aw_wgrad_batch(const aw_gemm_args* args, int n, void* ws, int64_t ws_bytes, void* stream) {
   WTParams P;
   if (int st = wt_plan(args, n, &P)) return st;
-  AW_REQUIRE(ws && ((uintptr_t)ws % 16) == 0 && ws_bytes >= (int64_t)2 * P.G * WT_SLAB * (int64_t)sizeof(float),
+  AW_REQUIRE(ws && ((uintptr_t)ws % 16) == 0 &&
+                 ws_bytes >= (P.S > 1 ? (int64_t)P.units * WT_SLAB * (int64_t)sizeof(float) : 16),
              "aw_wgrad_batch: workspace must be 16-B aligned and hold aw_wgrad_batch_workspace() bytes");
   P.ws = reinterpret_cast<float*>(ws);
   hipLaunchKernelGGL(wgrad_tt_kernel, dim3(P.G), dim3(WT_NTH), 0, reinterpret_cast<hipStream_t>(stream), P);
