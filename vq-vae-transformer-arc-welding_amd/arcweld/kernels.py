@@ -167,15 +167,20 @@ def gemm_grouped(problems, stream=None):
 
 
 def wgrad_batch_ok(problems):
-    """True when aw_wgrad_batch takes these problems (bf16 operands, M / N multiples of 256, one K) and it is switched
-    on (ARCWELD_WGRAD_BATCH=1).  Off by default: measured slower than the per-shape grouped launches on the bench
-    shapes (its stream-K ranges put concurrent workgroups at different k, so their operand streams
-    do not share L2 -- 3.2 GB fetched per transformer half-step)."""
+    """True when aw_wgrad_batch takes these problems (bf16 operands, M / N multiples of 256, one K) and pays: at least
+    128 of its 256 x 256 tiles (the transformer's half-step batch of four Linear kinds, 192 tiles: 656 -> 532 us per
+    launch in tools/probe/wgrad_tt_probe.py, the decoder step 5.58 -> 5.44 ms same box).  Below that its split-K
+    fix-up costs more than it saves (the VQ-VAE encoder's 64 tiles: 214 vs 184 us for the grouped launch), and the
+    per-shape grouped launches run instead.  ARCWELD_WGRAD_BATCH=0 / 1 forces them off / on (A/B, tests)."""
     import os
-    if os.environ.get("ARCWELD_WGRAD_BATCH", "0") != "1" or not problems or len(problems) > MAX_GROUPS:
+    mode = os.environ.get("ARCWELD_WGRAD_BATCH", "auto")
+    if mode == "0" or not problems or len(problems) > MAX_GROUPS:
         return False
     arr = (GemmArgs * len(problems))(*[_gemm_args(A, B, M, N, K, **kw) for (A, B, M, N, K, kw) in problems])
-    return nat.load().aw_wgrad_batch_workspace(arr, len(problems)) > 0
+    if nat.load().aw_wgrad_batch_workspace(arr, len(problems)) <= 0:
+        return False
+    tiles = sum((M // 256) * (N // 256) for (_, _, M, N, _, _) in problems)
+    return mode == "1" or tiles >= 128
 
 
 def wgrad_batch(problems, stream=None):

@@ -402,12 +402,13 @@ int g_policy = 0;   // aw_gemm_set_wgrad_policy: 0 automatic, 1 force, -1 off
 //    are at the same k of their ranges, and the tiles that share an operand block sit on one XCD: their operand
 //    streams meet in that XCD's L2.  (A stream-K cut into equal contiguous ranges, measured first, put concurrent
 //    workgroups at different k: 3.2 GB fetched per transformer half-step, slower than the per-kind launches.)
-//  * A tile's S partial pieces are summed by the LAST arriving piece: every piece stores its accumulators
-//    write-through (sc1) into its workspace slot, drains them (vmcnt(0)), joins a workgroup barrier and takes a
-//    ticket with one agent-scope atomic add; the piece whose ticket completes the count loads the other pieces' slots
-//    with sc1 loads and does the one read-modify-write of the gradient (MI355X_MICROARCH.md, inter-workgroup hand-off,
-//    first row of the measured forms).  No piece ever waits on another, so the launch cannot deadlock whatever its
-//    residency.  The read-modify-write goes through LDS in two 128-row halves: float4 per lane, 16 row loads in flight.
+//  * A tile's S partial pieces are summed by the LAST arriving piece: each piece takes an arrival ticket (one agent-
+//    scope atomic add) when its loop ends; every piece but the last stores its accumulators write-through (sc1) into
+//    its workspace slot, drains them (vmcnt(0)), joins a workgroup barrier and counts itself published (one more
+//    atomic add); the last polls the published count with sc1 loads, then loads the other slots with sc1 loads and
+//    does the one read-modify-write of the gradient (MI355X_MICROARCH.md, inter-workgroup hand-off, first row of the
+//    measured forms).  It waits only for pieces that already hold tickets, i.e. are running and only store: no
+//    deadlock whatever the residency.  The read-modify-write goes through LDS in two 128-row halves: float4 per lane, 16 row loads in flight.
 //  * Bias gradients: row sums of the A fragments by MFMA against an all-ones fragment, on the stages s with
 //    s % tiles_n == tn (spread over the row's tiles), f32 atomics per piece.
 constexpr int WT_BM = 256, WT_BN = 256, WT_BK = 32, WT_NTH = 512;
@@ -436,7 +437,9 @@ struct WTParams {
   float* ws;          // one slot of WT_SLAB floats per unit
 };
 
-__device__ int g_wt_tickets[WT_MAXTILES];   // per-tile arrival counters; the last arriver resets its own to 0
+// per-tile counters of arrived and of published pieces; the last arriver resets both of its tile to 0
+__device__ int g_wt_arrive[WT_MAXTILES];
+__device__ int g_wt_pub[WT_MAXTILES];
 
 __device__ __forceinline__ v4i32 wt_desc(const void* base, int64_t nbytes) {
   const uint64_t b = (uint64_t)(uintptr_t)base;
@@ -600,23 +603,33 @@ __global__ __launch_bounds__(WT_NTH, 1) void wgrad_tt_kernel(WTParams P) {
     else
 #endif
     if (P.S > 1) {
-      // ---- one piece of S: publish, take a ticket, the last arriver sums the other pieces
-      float* mine = P.ws + (int64_t)unit * WT_SLAB;
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int f = 0; f < 4; ++f) wt_st_sc1(mine + ((i * 4 + f) * WT_NTH + tid) * 4, acc[i][f]);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (tid == 0) {
-        const int old = __hip_atomic_fetch_add(&g_wt_tickets[tile], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const int last = old == P.S - 1;
-        if (last) __hip_atomic_store(&g_wt_tickets[tile], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        s_last = last;
-      }
+      // ---- one piece of S: take an arrival ticket first; the last to arrive sums the other pieces once they have
+      //      published (they took their tickets before it, so they are resident and only store, drain and count: the
+      //      wait is bounded whatever the residency), the others publish their accumulators and leave
+      if (tid == 0) s_last = __hip_atomic_fetch_add(&g_wt_arrive[tile], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                             P.S - 1;
       __syncthreads();
       write = s_last != 0;
-      if (write) {
+      if (!write) {
+        float* mine = P.ws + (int64_t)unit * WT_SLAB;
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+          for (int f = 0; f < 4; ++f) wt_st_sc1(mine + ((i * 4 + f) * WT_NTH + tid) * 4, acc[i][f]);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) __hip_atomic_fetch_add(&g_wt_pub[tile], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+        if (tid == 0) {
+          // sc1 poll of the published count (a bounded spin: the publishers are running)
+          for (int it = 0; it < (1 << 26); ++it) {
+            if (__hip_atomic_load(&g_wt_pub[tile], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= P.S - 1) break;
+            __builtin_amdgcn_s_sleep(1);
+          }
+          __hip_atomic_store(&g_wt_pub[tile], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(&g_wt_arrive[tile], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        __syncthreads();
         for (int o = 0; o < P.S; ++o) {
           if (o == sp) continue;
           const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(P.ws + ((int64_t)o * P.total_tiles + tile) * WT_SLAB,
