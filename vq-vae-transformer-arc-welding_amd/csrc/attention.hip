@@ -260,24 +260,25 @@ __device__ __forceinline__ int piece_off(int jj, int lane, int ldb) {
 __device__ __forceinline__ void lgkm_wait0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
 // dQ on the ring.  Wave w fills bytes [4 KiB w, 4 KiB w + 4 KiB) of every slot: K rows 32w.. (w < 2) or V
-// rows 32(w - 2).. (w >= 2).  The stationary operands of a wave are its own 32 rows only, so they are staged where
-// nothing but that wave's own later DMA lands: Q in bytes [4 KiB w, +4 KiB) of slot NB - 1 (a 128-row image over
-// the slot; the wave's first DMA into it follows its reads), dO and O in two 128-row images of their own.  It also
-// computes delta_i = dO_i . O_i for its rows and writes it (after its loop) for the dK/dV launch that follows.
+// rows 32(w - 2).. (w >= 2).  The stationary operands of a wave are its own 32 rows only: Q is staged where nothing
+// but that wave's own later DMA lands (bytes [4 KiB w, +4 KiB) of slot NB - 1: a 128-row image over the slot; the
+// wave's first DMA into it follows its reads); dO and O go straight to registers (the dO fragments are the B operand
+// of dP^T as they are; O only meets dO in delta_i = dO_i . O_i, which the wave writes after its loop for the dK/dV
+// launch).  48 KB of LDS: three workgroups per CU (the dO / O images of round 3 held it to two at 80 KB).
 __global__ __launch_bounds__(256, 2) void attn_dq_ring_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ dy,
                                                            const bf16* __restrict__ y, const float* __restrict__ lse,
                                                            float* __restrict__ delta, int T_, int nh, int d,
                                                            bf16* __restrict__ dqkv, float c2, float scale) {
-  __shared__ __attribute__((aligned(16))) char L[NB * SLOT + 4 * IMG];   // ring, dO image, O image
+  __shared__ __attribute__((aligned(16))) char L[NB * SLOT];   // the K / V ring (Q of the own rows in slot NB - 1)
   const int nqb = (T_ + BLK - 1) / BLK;
   const BlockId id(nqb, nh);
   const int qb = nqb - 1 - id.x;
   const int h = id.h, b = id.b;
   const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, hf = lane >> 5;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int ldb = 6 * d, ldg = 2 * d;   // bytes per qkv / dy / y row
+  const int ldb = 6 * d;   // bytes per qkv row
   const char* bbase = reinterpret_cast<const char*>(qkv) + (int64_t)b * T_ * ldb;
-  const uint32_t lring = aw_lds_addr(L), lg = lring + NB * SLOT, ly = lg + 2 * IMG;
+  const uint32_t lring = aw_lds_addr(L);
   const int q0 = qb * BLK, qw = q0 + w * WROWS, q = qw + r;
   const int kend = min(T_, q0 + BLK);
   const int nt = (kend + TILE - 1) / TILE;
@@ -285,19 +286,24 @@ __global__ __launch_bounds__(256, 2) void attn_dq_ring_kernel(const bf16* __rest
   int off[4];
 #pragma unroll
   for (int u = 0; u < 4; ++u) off[u] = piece_off(4 * (w & 1) + u, lane, ldb);
-  {   // own rows of Q, dO, O
+  // dO and O of the lane's row (clamped past T: those rows are never stored), 16 B per k-step as row_frag reads;
+  // issued before the DMAs so that the counted waits below cover them
+  uint4 qf[4], gf[4], yf[4];
+  {
+    const int qc = min(q, T_ - 1);
+    const bf16* grow = dy + ((int64_t)b * T_ + qc) * d + h * HS + 8 * hf;
+    const bf16* yrow = y + ((int64_t)b * T_ + qc) * d + h * HS + 8 * hf;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      gf[s] = *reinterpret_cast<const uint4*>(grow + 16 * s);
+      yf[s] = *reinterpret_cast<const uint4*>(yrow + 16 * s);
+    }
+  }
+  {   // own rows of Q (LDS-DMA)
     const aw_v4i32 dq = aw_rdesc(bbase + (int64_t)q0 * ldb + h * HS * 2, (uint32_t)(T_ - q0) * ldb);
-    const int64_t gro = ((int64_t)b * T_ + q0) * ldg + h * HS * 2;
-    const aw_v4i32 dg = aw_rdesc(reinterpret_cast<const char*>(dy) + gro, (uint32_t)(T_ - q0) * ldg);
-    const aw_v4i32 dyv = aw_rdesc(reinterpret_cast<const char*>(y) + gro, (uint32_t)(T_ - q0) * ldg);
     const uint32_t sq = lring + (NB - 1) * SLOT;
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const uint32_t o = (4 * w + u) * 1024;
-      aw_dma16(sq + o, piece_off(4 * w + u, lane, ldb), dq);
-      aw_dma16(lg + o, piece_off(4 * w + u, lane, ldg), dg);
-      aw_dma16(ly + o, piece_off(4 * w + u, lane, ldg), dyv);
-    }
+    for (int u = 0; u < 4; ++u) aw_dma16(sq + (4 * w + u) * 1024, piece_off(4 * w + u, lane, ldb), dq);
   }
   auto issue = [&](int t) {
     const int k0 = t * TILE;
@@ -309,24 +315,23 @@ __global__ __launch_bounds__(256, 2) void attn_dq_ring_kernel(const bf16* __rest
   };
 #pragma unroll
   for (int t = 0; t < NB - 1; ++t) issue(t);
-  aw_vm_wait<4 * (NB - 2)>();
+  aw_vm_wait<4 * (NB - 2)>();   // dO / O, the Q pieces and ring tile 0 landed
   raw_barrier();
-  uint4 qf[4], gf[4];
   float Dl = 0.f;
   {
-    const char* Qs = L + (NB - 1) * SLOT;
-    const char* Gs = L + NB * SLOT;
-    const char* Ys = Gs + 2 * IMG;
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-      qf[s] = row_frag(Qs, 32 * w + r, s, hf);
-      gf[s] = row_frag(Gs, 32 * w + r, s, hf);
-      const bf16x8 yv = __builtin_bit_cast(bf16x8, row_frag(Ys, 32 * w + r, s, hf));
+      const bf16x8 yv = __builtin_bit_cast(bf16x8, yf[s]);
       const bf16x8 gv = __builtin_bit_cast(bf16x8, gf[s]);
 #pragma unroll
       for (int e = 0; e < 8; ++e) Dl = fmaf((float)gv[e], (float)yv[e], Dl);
     }
     Dl += __shfl_xor(Dl, 32, 64);
+  }
+  {
+    const char* Qs = L + (NB - 1) * SLOT;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) qf[s] = row_frag(Qs, 32 * w + r, s, hf);
     lgkm_wait0();   // the Q reads retire before this wave's DMA of tile NB - 1 overwrites them
   }
   const int64_t st_i = ((int64_t)b * nh + h) * T_ + min(q, T_ - 1);
@@ -387,13 +392,14 @@ __global__ __launch_bounds__(256, 2) void attn_dq_ring_kernel(const bf16* __rest
 // delta row; wave w fills bytes [4 KiB w, +4 KiB) of the two images (Q rows 32w.. for w < 2, dO rows 32(w - 2)..
 // for w >= 2) and one 256-byte row (lse for even w, delta for odd w: two waves load each row, the same bytes), so
 // every wave issues five pieces per tile.  The wave's own K rows are staged in slot NB - 1 (as Q in the dQ kernel),
-// its V rows in an image of their own.
+// its V rows go straight to registers (they are only ever the B operand of dP).  49.5 KB of LDS and at most 168
+// VGPRs: three workgroups per CU (round 3: 65.5 KB and 202 VGPRs, two).
 constexpr int DSLOT = 2 * IMG + 2 * TILE * 4;
-__global__ __launch_bounds__(256, 2) void attn_dkv_ring_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ dy,
+__global__ __launch_bounds__(256, 3) void attn_dkv_ring_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ dy,
                                                             const float* __restrict__ lse,
                                                             const float* __restrict__ delta, int T_, int nh, int d,
                                                             bf16* __restrict__ dqkv, float c2, float scale) {
-  __shared__ __attribute__((aligned(16))) char L[NB * DSLOT + 2 * IMG];
+  __shared__ __attribute__((aligned(16))) char L[NB * DSLOT];
   const BlockId id((T_ + BLK - 1) / BLK, nh);
   const int kb = id.x;
   const int h = id.h, b = id.b;
@@ -402,7 +408,7 @@ __global__ __launch_bounds__(256, 2) void attn_dkv_ring_kernel(const bf16* __res
   const int ldb = 6 * d, ldg = 2 * d;
   const char* bbase = reinterpret_cast<const char*>(qkv) + (int64_t)b * T_ * ldb;
   const char* gbase = reinterpret_cast<const char*>(dy) + (int64_t)b * T_ * ldg;
-  const uint32_t lring = aw_lds_addr(L), lv = lring + NB * DSLOT;
+  const uint32_t lring = aw_lds_addr(L);
   const int k0b = kb * BLK, kw = k0b + w * WROWS, key = kw + r;
   const int qstart = k0b;   // BLK is a multiple of TILE
   const int nqt = (T_ - qstart + TILE - 1) / TILE;
@@ -413,16 +419,18 @@ __global__ __launch_bounds__(256, 2) void attn_dkv_ring_kernel(const bf16* __res
   for (int u = 0; u < 4; ++u) off[u] = piece_off(4 * (w & 1) + u, lane, lds_src);
   const int64_t sbase = ((int64_t)b * nh + h) * T_;
   const float* vec = (w & 1) ? delta : lse;
-  {   // own rows of K (into slot NB - 1) and V
+  // V of the lane's key row to registers (clamped past T: those keys are never stored), issued before the DMAs
+  uint4 kf[4], vf[4];
+  {
+    const bf16* vrow = qkv + ((int64_t)b * T_ + min(key, T_ - 1)) * (3 * (int64_t)d) + 2 * d + h * HS + 8 * hf;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) vf[s] = *reinterpret_cast<const uint4*>(vrow + 16 * s);
+  }
+  {   // own rows of K (into slot NB - 1)
     const aw_v4i32 dk = aw_rdesc(bbase + (int64_t)k0b * ldb + (d + h * HS) * 2, (uint32_t)(T_ - k0b) * ldb);
-    const aw_v4i32 dv = aw_rdesc(bbase + (int64_t)k0b * ldb + (2 * d + h * HS) * 2, (uint32_t)(T_ - k0b) * ldb);
     const uint32_t sk = lring + (NB - 1) * DSLOT;
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const uint32_t o = (4 * w + u) * 1024;
-      aw_dma16(sk + o, piece_off(4 * w + u, lane, ldb), dk);
-      aw_dma16(lv + o, piece_off(4 * w + u, lane, ldb), dv);
-    }
+    for (int u = 0; u < 4; ++u) aw_dma16(sk + (4 * w + u) * 1024, piece_off(4 * w + u, lane, ldb), dk);
   }
   auto issue = [&](int i) {
     const int q0 = qstart + TILE * i;
@@ -439,15 +447,10 @@ __global__ __launch_bounds__(256, 2) void attn_dkv_ring_kernel(const bf16* __res
   for (int i = 0; i < NB - 1; ++i) issue(i);
   aw_vm_wait<5 * (NB - 2)>();
   raw_barrier();
-  uint4 kf[4], vf[4];
   {
     const char* Ksg = L + (NB - 1) * DSLOT;
-    const char* Vsg = L + NB * DSLOT;
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      kf[s] = row_frag(Ksg, 32 * w + r, s, hf);
-      vf[s] = row_frag(Vsg, 32 * w + r, s, hf);
-    }
+    for (int s = 0; s < 4; ++s) kf[s] = row_frag(Ksg, 32 * w + r, s, hf);
     lgkm_wait0();
   }
   f32x16 dk[2] = {zero16(), zero16()}, dv[2] = {zero16(), zero16()};
@@ -476,17 +479,11 @@ __global__ __launch_bounds__(256, 2) void attn_dkv_ring_kernel(const bf16* __res
         dp = mfma32(row_frag(Gs, 32 * qs + r, ks, hf), vf[ks], dp);
       }
       f32x16 p;
-      float Dv[16];
 #pragma unroll
       for (int g4 = 0; g4 < 4; ++g4) {
         const int ql = 32 * qs + 8 * g4 + 4 * hf;
         const float4 L4 = *reinterpret_cast<const float4*>(Ls + ql);
-        const float4 D4 = *reinterpret_cast<const float4*>(Ds + ql);
         const float Lv[4] = {L4.x, L4.y, L4.z, L4.w};
-        Dv[4 * g4] = D4.x;
-        Dv[4 * g4 + 1] = D4.y;
-        Dv[4 * g4 + 2] = D4.z;
-        Dv[4 * g4 + 3] = D4.w;
 #pragma unroll
         for (int e = 0; e < 4; ++e)
           p[4 * g4 + e] = __builtin_amdgcn_exp2f(fmaf(s[4 * g4 + e], c2, -Lv[e] * 1.4426950408889634f));
@@ -499,8 +496,14 @@ __global__ __launch_bounds__(256, 2) void attn_dkv_ring_kernel(const bf16* __res
           p[e] = (qq < key || qq >= T_) ? 0.f : p[e];
         }
       }
+      // dS = P (dP - delta): the delta rows are read from the slot per 4-row group (no 16-register copy)
 #pragma unroll
-      for (int e = 0; e < 16; ++e) s[e] = p[e] * (dp[e] - Dv[e]);
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const float4 D4 = *reinterpret_cast<const float4*>(Ds + 32 * qs + 8 * g4 + 4 * hf);
+        const float Dv[4] = {D4.x, D4.y, D4.z, D4.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) s[4 * g4 + e] = p[4 * g4 + e] * (dp[4 * g4 + e] - Dv[e]);
+      }
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) {
         const uint4 pb = pack8(p, s2), db = pack8(s, s2);
