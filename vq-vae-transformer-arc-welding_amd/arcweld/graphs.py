@@ -20,6 +20,12 @@ from __future__ import annotations
 
 import torch
 
+# Capture mode "thread_local": only this thread's unsafe calls are refused while it captures.  The default
+# ("global") also refuses every other thread's -- including the RCCL process group's watchdog, which polls the
+# completion events of earlier all-reduces from its own thread and terminates the process when the poll is refused
+# (seen on the GPU box: "operation not permitted when stream is capturing" from WorkNCCL::isCompleted).
+_MODE = "thread_local"
+
 
 def _clone_static(batch):
     if isinstance(batch, torch.Tensor):
@@ -56,12 +62,12 @@ class StepGraphs:
         self.g2 = torch.cuda.CUDAGraph()
         if self.split:
             self.g1a, self.g1b = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-            state = {"ctx": torch.cuda.graph(self.g1a, pool=pool)}
+            state = {"ctx": torch.cuda.graph(self.g1a, pool=pool, capture_error_mode=_MODE)}
             state["ctx"].__enter__()
 
             def mid():   # end the first capture where the decoder-side gradients are final, start the second
                 state["ctx"].__exit__(None, None, None)
-                state["ctx"] = torch.cuda.graph(self.g1b, pool=pool)
+                state["ctx"] = torch.cuda.graph(self.g1b, pool=pool, capture_error_mode=_MODE)
                 state["ctx"].__enter__()
 
             try:
@@ -70,9 +76,9 @@ class StepGraphs:
                 state["ctx"].__exit__(None, None, None)
         else:
             self.g1 = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self.g1, pool=pool):
+            with torch.cuda.graph(self.g1, pool=pool, capture_error_mode=_MODE):
                 self.loss = self.trainer.micro_step(self.model, self.static, 0, self.scale)
-        with torch.cuda.graph(self.g2, pool=pool):
+        with torch.cuda.graph(self.g2, pool=pool, capture_error_mode=_MODE):
             self.trainer._update(self.model)
 
     def run(self, batch):
