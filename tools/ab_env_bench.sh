@@ -6,8 +6,10 @@ A=$1; B=$2; R=${3:-2}
 ARGS=${ARGS:---no-cpu-baseline --no-profile --no-transformer --no-fp32 --no-stress}
 mkdir -p gpurun_out/abenv
 for i in $(seq 1 $R); do
-  for v in $A $B; do
-    env $VAR=$v timeout -k 10 200 python bench.py $ARGS --no-profile --detail "" > gpurun_out/abenv/$VAR$v$i.log 2>&1 || { tail -5 gpurun_out/abenv/$VAR$v$i.log; exit 1; }
-    tail -1 gpurun_out/abenv/$VAR$v$i.log | python -c "import json,sys;d=json.loads(sys.stdin.read());print('$VAR=$v', d['value'], d['ms_per_step'])"
+  for t in A B; do
+    [ $t = A ] && v=$A || v=$B
+    log=gpurun_out/abenv/$VAR-$t$i.log
+    env $VAR=$v timeout -k 10 200 python bench.py $ARGS --no-profile --detail "" > $log 2>&1 || { tail -5 $log; exit 1; }
+    tail -1 $log | python -c "import json,sys;d=json.loads(sys.stdin.read());print('$VAR=$t', d['value'], d['ms_per_step'])"
   done
 done
