@@ -19,7 +19,7 @@ if has smoke; then
   tail -1 $OUT/smoke.log
 fi
 if has bench; then
-  timeout -k 10 500 python -u bench.py ${BENCH_ARGS:-} > $OUT/bench.log 2>&1 || { tail -30 $OUT/bench.log; exit 1; }
+  timeout -k 10 500 python -u bench.py --detail $OUT/bench_detail.json ${BENCH_ARGS:-} > $OUT/bench.log 2>&1 || { tail -30 $OUT/bench.log; exit 1; }
   tail -1 $OUT/bench.log > $OUT/bench.json
   cat $OUT/bench.json | cut -c1-600
 fi

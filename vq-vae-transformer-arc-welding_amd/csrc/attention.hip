@@ -120,6 +120,34 @@ __device__ __forceinline__ void tile_store(const TileRegs& tr, char* img, int ti
   }
 }
 
+// A wave's 32 rows x 64 head dims (an accumulator pair with the row on the lane, the dims in the registers) stored as
+// whole 128-byte rows: the fragments go to the wave's own 4 KB of LDS (16-byte chunks XOR-swizzled by row), then
+// every lane writes 16-byte chunks, 8 lanes per row.  Stored straight from the registers, each 8-byte wave store
+// touched 32 rows at a 128-byte stride (MI355X_MICROARCH.md: a store-issue-bound tail).
+__device__ __forceinline__ void store_rows(const f32x16 (&a)[2], float s, char* reg, bf16* out0, int64_t ld,
+                                           int nrows, int lane) {
+  const int r = lane & 31, hf = lane >> 5;
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      bf16 v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = (bf16)(a[dt][4 * g4 + e] * s);
+      uint2 u;
+      memcpy(&u, v, 8);
+      *reinterpret_cast<uint2*>(reg + r * ROWB + (((4 * dt + g4) ^ (r & 7)) << 4) + 8 * hf) = u;
+    }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int row = (lane >> 3) + 8 * j, c = lane & 7;
+    if (row < nrows)
+      *reinterpret_cast<uint4*>(out0 + row * ld + 8 * c) =
+          *reinterpret_cast<const uint4*>(reg + row * ROWB + ((c ^ (row & 7)) << 4));
+  }
+}
+
 __device__ __forceinline__ void store4_bf16(bf16* dst, const f32x16& a, int g4, float s) {
   bf16 v[4];
 #pragma unroll
@@ -224,15 +252,16 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_mfma_kernel(const bf16* __res
       }
   }
   l += __shfl_xor(l, 32, 64);
-  if (q < T_) {
-    const float inv = 1.f / l;
-    bf16* yr = y + ((int64_t)b * T_ + q) * d + h * HS;
+  // 1 / l per lane: lanes past T carry l = 0 (every score masked); their rows are not stored
+  const float inv = q < T_ ? 1.f / l : 0.f;
 #pragma unroll
-    for (int dt = 0; dt < 2; ++dt)
+  for (int dt = 0; dt < 2; ++dt)
 #pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) store4_bf16(yr + 32 * dt + 8 * g4 + 4 * hf, o[dt], g4, inv);
-    if (hf == 0) lse[((int64_t)b * nh + h) * T_ + q] = m * scale + logf(l);
-  }
+    for (int i = 0; i < 16; ++i) o[dt][i] *= inv;
+  if (q < T_ && hf == 0) lse[((int64_t)b * nh + h) * T_ + q] = m * scale + logf(l);
+  __syncthreads();   // every wave's reads of the K / V images are done: the images become store staging
+  if (qw < T_)
+    store_rows(o, 1.f, KV + w * 4096, y + ((int64_t)b * T_ + qw) * d + h * HS, d, min(WROWS, T_ - qw), lane);
 }
 
 // ---------------------------------------------------------------- backward: LDS-DMA tile ring
@@ -378,14 +407,11 @@ __global__ __launch_bounds__(256, 2) void attn_dq_ring_kernel(const bf16* __rest
     }
   }
   aw_vm_wait<0>();
-  if (q < T_) {
-    if (hf == 0) delta[st_i] = Dl;
-    bf16* out = dqkv + ((int64_t)b * T_ + q) * (3 * (int64_t)d) + h * HS;
-#pragma unroll
-    for (int dt = 0; dt < 2; ++dt)
-#pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) store4_bf16(out + 32 * dt + 8 * g4 + 4 * hf, acc[dt], g4, scale);
-  }
+  if (q < T_ && hf == 0) delta[st_i] = Dl;
+  raw_barrier();   // every wave's reads of the ring are done; bytes [4 KiB w, +4 KiB) of slot 0 take only w's DMAs
+  if (qw < T_)
+    store_rows(acc, scale, L + 4096 * w, dqkv + ((int64_t)b * T_ + qw) * (3 * (int64_t)d) + h * HS, 3 * (int64_t)d,
+               min(WROWS, T_ - qw), lane);
 }
 
 // dK, dV on the ring, key-stationary.  A slot holds the query tile's Q image, dO image, lse row and
@@ -517,15 +543,12 @@ __global__ __launch_bounds__(256, 3) void attn_dkv_ring_kernel(const bf16* __res
     }
   }
   aw_vm_wait<0>();
-  if (key < T_) {
-    bf16* out = dqkv + ((int64_t)b * T_ + key) * (3 * (int64_t)d) + h * HS;
-#pragma unroll
-    for (int dt = 0; dt < 2; ++dt)
-#pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        store4_bf16(out + d + 32 * dt + 8 * g4 + 4 * hf, dk[dt], g4, scale);
-        store4_bf16(out + 2 * d + 32 * dt + 8 * g4 + 4 * hf, dv[dt], g4, 1.f);
-      }
+  raw_barrier();   // every wave's reads of the ring are done; bytes [4 KiB w, +4 KiB) of a slot take only w's DMAs
+  if (kw < T_) {
+    bf16* out = dqkv + ((int64_t)b * T_ + kw) * (3 * (int64_t)d) + h * HS;
+    const int n = min(WROWS, T_ - kw);
+    store_rows(dk, scale, L + 4096 * w, out + d, 3 * (int64_t)d, n, lane);
+    store_rows(dv, 1.f, L + DSLOT + 4096 * w, out + 2 * d, 3 * (int64_t)d, n, lane);
   }
 }
 
