@@ -190,11 +190,12 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_mfma_kernel(const bf16* __res
     char* Vs = Ks + IMG;
     tile_store(kr, Ks, tid);
     tile_store(vr, Vs, tid);
-    __syncthreads();
+    // the next tile's loads go out before the barrier: their latency runs under the barrier wait too
     if (t + 1 < nt) {
       tile_load(kr, base, ld, d + h * HS, k0 + TILE, T_, tid);
       tile_load(vr, base, ld, 2 * d + h * HS, k0 + TILE, T_, tid);
     }
+    __syncthreads();
     if (k0 > qw + WROWS - 1) continue;  // wave-uniform: the whole tile lies after this wave's queries
     f32x16 s[2];
 #pragma unroll
@@ -222,9 +223,15 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_mfma_kernel(const bf16* __res
       for (int i = 0; i < 16; ++i) mx = fmaxf(mx, s[st][i]);
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
     const float mn = fmaxf(m, mx);
-    const float alpha = __builtin_amdgcn_exp2f((m - mn) * c2);   // v_exp_f32: arguments <= 0, -inf -> 0
-    const float mc = mn * c2;
-    m = mn;
+    // the running max moves only when some lane's grows by more than 2^8 in P: below that the stale max keeps
+    // every P <= 256 (same products, other roundings) and the rescale of o and l is skipped (wave-uniform)
+    const bool resc = __builtin_amdgcn_ballot_w64((mn - m) * c2 > 8.f) != 0;
+    float alpha = 1.f;
+    if (resc) {
+      alpha = __builtin_amdgcn_exp2f((m - mn) * c2);
+      m = mn;
+    }
+    const float mc = m * c2;
     // exponent arguments and the row sum as f32 pairs (v_pk_fma_f32 / v_pk_add_f32)
     f32x2 ls2 = {0.f, 0.f};
 #pragma unroll
@@ -237,11 +244,14 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_mfma_kernel(const bf16* __res
         s[st][i + 1] = p.y;
         ls2 += p;
       }
-    l = l * alpha + (ls2.x + ls2.y);
+    if (resc) {
+      l *= alpha;
 #pragma unroll
-    for (int dt = 0; dt < 2; ++dt)
+      for (int dt = 0; dt < 2; ++dt)
 #pragma unroll
-      for (int i = 0; i < 16; ++i) o[dt][i] *= alpha;
+        for (int i = 0; i < 16; ++i) o[dt][i] *= alpha;
+    }
+    l += ls2.x + ls2.y;
 #pragma unroll
     for (int st = 0; st < 2; ++st)
 #pragma unroll
