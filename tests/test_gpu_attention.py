@@ -78,13 +78,14 @@ def test_attention_bf16(T, hs, nh):
         assert (a - r).norm().item() <= 1e-2 * r.norm().item() + 1e-4, j   # dq is exactly 0 at T = 1
 
 
-@pytest.mark.parametrize("R", [1000, 5000])
-@pytest.mark.parametrize("D", [64, 512])
+@pytest.mark.parametrize("R", [5, 1000, 5000, 16371])
+@pytest.mark.parametrize("D", [64, 512, 1024])
 @pytest.mark.parametrize("out_dtype", [torch.float32, torch.bfloat16])
 def test_layernorm_fwd_bwd(R, D, out_dtype):
     """aw_layernorm_fwd / aw_layernorm_bwd (vectorised at D % 256 == 0) vs torch layer_norm in fp32, including
-    the accumulate-into-dx form and the dropout-masked operand copy dx2 (regenerated mask).  R = 5000 exceeds
-    the backward's 2048 waves, so each wave walks several rows (the next-row prefetch path)."""
+    the accumulate-into-dx form and the dropout-masked operand copy dx2 (regenerated mask).  R = 5000 and 16371
+    (the decoder's 51 x 321 rows) exceed the backward's 2048 waves, so each wave walks several rows (the next-row
+    prefetch path); R = 5 leaves most waves without a row."""
     from arcweld import kernels as K
     g = torch.Generator(device="cuda").manual_seed(D)
     x = torch.randn(R, D, device="cuda", generator=g) * 3 + 1
@@ -110,7 +111,7 @@ def test_layernorm_fwd_bwd(R, D, out_dtype):
     torch.testing.assert_close(db, br.grad, rtol=1e-4, atol=1e-3)
     kept = dx2.float() != 0
     frac = kept.float().mean().item()
-    assert 0.72 < frac < 0.78
+    assert abs(frac - 0.75) < max(0.03, 4 * (0.1875 / kept.numel()) ** 0.5), frac   # 4 sigma at small R
     torch.testing.assert_close(dx2.float()[kept], (dx / 0.75)[kept], rtol=tol, atol=tol)
 
 

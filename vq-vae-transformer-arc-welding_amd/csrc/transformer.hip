@@ -99,13 +99,20 @@ __global__ __launch_bounds__(256) void ln_fwd_vec_kernel(const float* __restrict
   const int lane = threadIdx.x & 63;
   const int64_t r = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   if (r >= R) return;
-  float4 v[NV];
-  float s = 0.f;
+  float4 v[NV], w4[NV], b4[NV];
+#pragma unroll
+  for (int j = 0; j < NV; ++j) v[j] = *reinterpret_cast<const float4*>(x + r * D + 4 * lane + 256 * j);
+  // the affine parameters load beside the row (issued after the load of x, waited for only after the reductions;
+  // loaded after the reductions, their latency followed the two wave sums of every row)
 #pragma unroll
   for (int j = 0; j < NV; ++j) {
-    v[j] = *reinterpret_cast<const float4*>(x + r * D + 4 * lane + 256 * j);
-    s += (v[j].x + v[j].y) + (v[j].z + v[j].w);
+    w4[j] = *reinterpret_cast<const float4*>(w + 4 * lane + 256 * j);
+    b4[j] = *reinterpret_cast<const float4*>(b + 4 * lane + 256 * j);
   }
+  __builtin_amdgcn_sched_barrier(0);   // keep the loads issued here, ahead of the reductions
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < NV; ++j) s += (v[j].x + v[j].y) + (v[j].z + v[j].w);
   const float mu = wave_sum(s) / (float)D;
   float q = 0.f;
 #pragma unroll
@@ -117,9 +124,8 @@ __global__ __launch_bounds__(256) void ln_fwd_vec_kernel(const float* __restrict
 #pragma unroll
   for (int j = 0; j < NV; ++j) {
     const int c = 4 * lane + 256 * j;
-    const float4 w4 = *reinterpret_cast<const float4*>(w + c), b4 = *reinterpret_cast<const float4*>(b + c);
-    const float o[4] = {(v[j].x - mu) * rs * w4.x + b4.x, (v[j].y - mu) * rs * w4.y + b4.y,
-                        (v[j].z - mu) * rs * w4.z + b4.z, (v[j].w - mu) * rs * w4.w + b4.w};
+    const float o[4] = {(v[j].x - mu) * rs * w4[j].x + b4[j].x, (v[j].y - mu) * rs * w4[j].y + b4[j].y,
+                        (v[j].z - mu) * rs * w4[j].z + b4[j].z, (v[j].w - mu) * rs * w4[j].w + b4[j].w};
     if constexpr (sizeof(T) == 2) {
       bf16 h[4] = {(bf16)o[0], (bf16)o[1], (bf16)o[2], (bf16)o[3]};
       uint2 u;
