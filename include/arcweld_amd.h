@@ -106,15 +106,17 @@ int aw_gemm_set_tile(int bm);
  * 0 = automatic (the 8-wave ping-pong kernel when the shape qualifies and fills the chip), 1 = force it whenever the
  * shape qualifies, -1 = always the generic grouped GEMM (tests, A/B). */
 int aw_gemm_set_wgrad_policy(int mode);
-/* Batched weight gradients of plain (1-tap) layers: n <= AW_GEMM_MAX_GROUPS accumulate-mode problems
+/* Batched weight gradients of plain (1-tap) layers: n <= AW_WGRAD_BATCH_MAX accumulate-mode problems
  *   C_i[m*ldc + colmap(n)] += alpha * sum_k A_i[k*lda + m] * B_i[k*ldb + n],  a_rowsum_i[m] += alpha * sum_k A_i[k*lda + m]
  * with bf16 operands (a_trans = b_trans = 1), f32 C, any M_i / N_i that are multiples of 256, one K (any K: ragged
  * token counts) and one alpha for all problems.  Replaces the weight / bias gradients of the transformer's Linear
- * layers, one launch for the four kinds of half the blocks (model/transformer_block.py:28-30,76-77), and of the
+ * layers, one launch for the four kinds of all 8 blocks (half of them per launch when a data-parallel step reduces
+ * the later half's gradients early) (model/transformer_block.py:28-30,76-77), and of the
  * VQ-VAE encoder's per-token convs (model/vq_vae_patch_embedd.py:65,68 via :108-110).  One stream-K launch (one
  * workgroup per CU, equal work per CU whatever the tile count); tiles split between workgroups are summed through
  * `ws` (aw_wgrad_batch_workspace bytes, 16-B aligned, no initial contents).  One batch at a time per device (the
  * per-tile arrival counters are the library's).  aw_wgrad_batch_workspace returns -1 when the batch is not eligible. */
+#define AW_WGRAD_BATCH_MAX 32
 int64_t aw_wgrad_batch_workspace(const aw_gemm_args* args, int n);
 int aw_wgrad_batch(const aw_gemm_args* args, int n, void* ws, int64_t ws_bytes, void* stream);
 

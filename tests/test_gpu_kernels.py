@@ -506,13 +506,14 @@ def test_wgrad_conv3_kernel_vs_fp32_reference(policy, G, Cout, Cin, Ntok, S, ref
         torch.testing.assert_close(b, bw, rtol=1e-4, atol=2e-5 * float(bw.abs().max()))
 
 
-@pytest.mark.parametrize("case", ["transformer_half", "encoder", "ragged_small", "one_tile"])
+@pytest.mark.parametrize("case", ["transformer_half", "transformer_full", "encoder", "ragged_small", "one_tile"])
 def test_wgrad_batch_split_k_vs_fp32_reference(case):
     """aw_wgrad_batch (csrc/wgrad.hip, wgrad_tt_kernel: 256 x 256 tiles, k-aligned split-K units over persistent
     workgroups, split tiles summed by the last arriving piece) against torch fp32 on the same bf16 operands: dW[m][colmap(n)] += alpha
     sum_k dy[k][m] x[k][n] and the bias row sums, accumulated into non-zero gradients.
       transformer_half: the four Linear kinds of 4 blocks at d 512 (model/transformer_block.py:28-30,76-77 grads),
                         K = 51 x 321 tokens (ragged: not a multiple of the 32-token stage), 192 tiles x 4 splits;
+      transformer_full: all 8 blocks in one launch (32 problems, the single-GPU step's batch): 384 tiles x 2 splits;
       encoder:          the 16 centre-tap convs (model/vq_vae_patch_embedd.py:65,68), K 16384, half of them through
                         the reference's (O, I, 3) column map (the scalar epilogue), alpha 0.5;
       ragged_small:     K = 37 (two stages, the second mostly past K), mixed shapes, no split;
@@ -520,9 +521,9 @@ def test_wgrad_batch_split_k_vs_fp32_reference(case):
     from arcweld import kernels as K
     g = torch.Generator(device=DEV).manual_seed(4321)
     d = 512
-    if case == "transformer_half":
+    if case in ("transformer_half", "transformer_full"):
         Kt, alpha = 51 * 321, 1.0
-        shapes = [(3 * d, d), (d, d), (4 * d, d), (d, 4 * d)] * 4
+        shapes = [(3 * d, d), (d, d), (4 * d, d), (d, 4 * d)] * (4 if case == "transformer_half" else 8)
     elif case == "encoder":
         Kt, alpha = 16384, 0.5
         shapes = [(d, d)] * 16

@@ -2,7 +2,8 @@
 NCCL).  One GPU box holds one device, and RCCL refuses two ranks per device, so the group has ONE rank -- but every
 collective of the path still runs through RCCL: ARCWELD_FORCE_COLLECTIVES=1 keeps the bucketed all-reduce on at
 world size 1 (arcweld/trainer.py), so the async work handles, RCCL's own stream and the waits run between the
-split graph replays exactly as they do on 8 GPUs (arcweld/graphs.py: late region between g1a and g1b, early after).
+split graph replays exactly as they do on 8 GPUs (arcweld/graphs.py: the late region after the graph piece that ends at
+the mid-backward hook, the early region after the last piece).
 
 A one-rank SUM is the identity, which cannot show a stream-ordering error.  So the test swaps in RCCL's pre-multiplied
 sum with factor 2 and trains with loss scale 1/2: every gradient is exact (powers of two), and the update equals a

@@ -195,8 +195,10 @@ def backward(m, sv, g_out, slot, mid_hook=None):
     last = nb - 1
     K.layernorm_bwd(sv.x_last, gxf, lnf.weight, sv.muf, sv.rsf, gx, False, slot(lnf.weight), slot(lnf.bias),
                     dx2=go, drop=(sv.p_drop, sv.seed_mlp[last] if nb else 0), seed_ptr=sv.ctr)
-    # per-layer-kind weight gradients are deferred and issued as grouped launches per kind: once for the later
-    # half of the blocks (before the mid-backward hook), once for the rest
+    # the weight gradients are deferred and issued as one batch per half, the first before the mid-backward hook (a
+    # data-parallel step reduces the later half's gradients while the earlier blocks run); with no collective
+    # (m._wgrad_merge, set by the step graphs) or no hook, all blocks in one batch at the end (384 tiles split in two
+    # pieces instead of 2 x 192 in four: a third of the split-K slab traffic and one launch fewer)
     wg = {"fc2": [], "fc1": [], "proj": [], "qkv": []}
     half = nb // 2
     for i in reversed(range(nb)):
@@ -233,12 +235,12 @@ def backward(m, sv, g_out, slot, mid_hook=None):
         K.layernorm_bwd(c["x"], ga, blk.ln_1.weight, c["mu1"], c["rs1"], gx, True, slot(blk.ln_1.weight),
                         slot(blk.ln_1.bias), dx2=go, drop=(sv.p_drop, sv.seed_mlp[i - 1] if i > 0 else 0),
                         seed_ptr=sv.ctr)
-        if i == half:
-            # the four kinds of the later half of the blocks: one stream-K batch (bf16) or one grouped launch per kind
-            K.wgrad_issue([pb for kind in wg for pb in wg[kind]])
-            wg = {kind: [] for kind in wg}
-            if mid_hook is not None:
-                mid_hook()
+        if i == half and mid_hook is not None:
+            if not m.__dict__.get("_wgrad_merge", False):
+                # the four kinds of the later half of the blocks: one batch (bf16) or one grouped launch per kind
+                K.wgrad_issue([pb for kind in wg for pb in wg[kind]])
+                wg = {kind: [] for kind in wg}
+            mid_hook()
     K.wgrad_issue([pb for kind in wg for pb in wg[kind]])
     if nb == 0 and mid_hook is not None:
         mid_hook()

@@ -18,6 +18,9 @@ batch it was given.
 """
 from __future__ import annotations
 
+import inspect
+import os
+
 import torch
 
 # Capture mode "thread_local": only this thread's unsafe calls are refused while it captures.  The default
@@ -43,14 +46,22 @@ def _copy_into(dst, src):
 
 class StepGraphs:
     """allreduce(region) launches the SUM all-reduce of a flat-gradient region ("all", "late" = the part final at
-    the mid-backward split, "early" = the rest) and returns the async work handles."""
+    the mid-backward split, "early" = the rest) and returns the async work handles; collective=False (no process
+    group) lets the model defer the late weight gradients past the split (model._wgrad_merge)."""
 
-    def __init__(self, trainer, model, scale, allreduce, warmup=2):
+    def __init__(self, trainer, model, scale, allreduce, warmup=2, collective=True):
         self.trainer, self.model, self.scale, self.allreduce = trainer, model, scale, allreduce
         self.warmup = warmup
         self.calls = 0
         self.static = None
-        self.split = hasattr(model, "fused_train_step") and hasattr(model, "backward_late_parameters")
+        # The forward/backward is captured as two graphs split at the model's mid-backward hook, with or without a
+        # collective between them: the split measured faster on its own (VQ-VAE step 3.152 / 3.167 vs 3.222 / 3.202
+        # ms unsplit, same box).  Without a collective nothing needs the late gradients at the hook, so the decoder
+        # issues the weight gradients of all its blocks as one batch at the end (model._wgrad_merge, arcweld/decoder.py
+        # backward).  ARCWELD_SPLIT_GRAPHS=0 captures one graph (A/B runs).
+        self.split = hasattr(model, "fused_train_step") and hasattr(model, "backward_late_parameters") and \
+            os.environ.get("ARCWELD_SPLIT_GRAPHS") != "0"
+        model.__dict__["_wgrad_merge"] = not collective and os.environ.get("ARCWELD_WGRAD_MERGE") != "0"
 
     def _capture(self, batch):
         self.static = _clone_static(batch)
@@ -61,17 +72,28 @@ class StepGraphs:
         pool = torch.cuda.graph_pool_handle()
         self.g2 = torch.cuda.CUDAGraph()
         if self.split:
-            self.g1a, self.g1b = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-            state = {"ctx": torch.cuda.graph(self.g1a, pool=pool, capture_error_mode=_MODE)}
+            # the forward/backward as a list of graph pieces: cut at the mid-backward hook (the late all-reduce is
+            # launched after that piece), and -- ARCWELD_EXTRA_SPLIT=1, models that take a split_hook -- at more seams
+            self.pieces, self.late_after = [torch.cuda.CUDAGraph()], None
+            state = {"ctx": torch.cuda.graph(self.pieces[0], pool=pool, capture_error_mode=_MODE)}
             state["ctx"].__enter__()
 
-            def mid():   # end the first capture where the decoder-side gradients are final, start the second
+            def cut():
                 state["ctx"].__exit__(None, None, None)
-                state["ctx"] = torch.cuda.graph(self.g1b, pool=pool, capture_error_mode=_MODE)
+                self.pieces.append(torch.cuda.CUDAGraph())
+                state["ctx"] = torch.cuda.graph(self.pieces[-1], pool=pool, capture_error_mode=_MODE)
                 state["ctx"].__enter__()
 
+            def mid():   # the decoder-side gradients are final here: the late all-reduce follows this piece
+                self.late_after = len(self.pieces) - 1
+                cut()
+
+            kw = {"mid_hook": mid}
+            if os.environ.get("ARCWELD_EXTRA_SPLIT") == "1" and \
+                    "split_hook" in inspect.signature(self.model.fused_train_step).parameters:
+                kw["split_hook"] = cut
             try:
-                self.loss = self.model.fused_train_step(self.static, self.scale, mid_hook=mid)
+                self.loss = self.model.fused_train_step(self.static, self.scale, **kw)
             finally:
                 state["ctx"].__exit__(None, None, None)
         else:
@@ -102,11 +124,13 @@ class StepGraphs:
         for j, b in enumerate(batches):
             _copy_into(self.static, b)        # ordered after the previous replay on this stream
             if self.split:
-                self.g1a.replay()
+                for i, g in enumerate(self.pieces):
+                    g.replay()
+                    if j == last and i == self.late_after:
+                        works = self.allreduce("late")   # decoder side: overlaps the encoder-side backward below
                 if j == last:
-                    works = self.allreduce("late")       # decoder side: overlaps the encoder-side backward below
-                self.g1b.replay()
-                if j == last:
+                    if self.late_after is None:
+                        works = self.allreduce("late")
                     works += self.allreduce("early")
             else:
                 self.g1.replay()

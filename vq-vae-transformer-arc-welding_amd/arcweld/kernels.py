@@ -166,6 +166,9 @@ def gemm_grouped(problems, stream=None):
         _timed(s, lambda sp: call("aw_gemm_grouped", arr, len(chunk), sp), fl, _gemm_tag(chunk[0][0]))
 
 
+WGRAD_BATCH_MAX = 32     # aw_wgrad_batch problems per launch (include/arcweld_amd.h AW_WGRAD_BATCH_MAX)
+
+
 def wgrad_batch_ok(problems):
     """True when aw_wgrad_batch takes these problems (bf16 operands, M / N multiples of 256, one K) and pays: at least
     128 of its 256 x 256 tiles (the transformer's half-step batch of four Linear kinds, 192 tiles: 656 -> 532 us per
@@ -174,7 +177,7 @@ def wgrad_batch_ok(problems):
     per-shape grouped launches run instead.  ARCWELD_WGRAD_BATCH=0 / 1 forces them off / on (A/B, tests)."""
     import os
     mode = os.environ.get("ARCWELD_WGRAD_BATCH", "auto")
-    if mode == "0" or not problems or len(problems) > MAX_GROUPS:
+    if mode == "0" or not problems or len(problems) > WGRAD_BATCH_MAX:
         return False
     arr = (GemmArgs * len(problems))(*[_gemm_args(A, B, M, N, K, **kw) for (A, B, M, N, K, kw) in problems])
     if nat.load().aw_wgrad_batch_workspace(arr, len(problems)) <= 0:
@@ -184,7 +187,7 @@ def wgrad_batch_ok(problems):
 
 
 def wgrad_batch(problems, stream=None):
-    """One aw_wgrad_batch launch over <= 16 weight-gradient problems (A, B, M, N, K, kwargs) as for ``gemm`` (M and
+    """One aw_wgrad_batch launch over <= 32 weight-gradient problems (A, B, M, N, K, kwargs) as for ``gemm`` (M and
     N may differ between problems; K, alpha and the dtype may not); the stream-K workspace comes from the caching
     allocator."""
     arr = (GemmArgs * len(problems))(*[_gemm_args(A, B, M, N, K, **kw) for (A, B, M, N, K, kw) in problems])
@@ -202,11 +205,11 @@ def wgrad_batch(problems, stream=None):
 
 
 def wgrad_issue(problems, stream=None):
-    """Weight-gradient problems of one backward region that share K: in aw_wgrad_batch launches of <= 16 problems
+    """Weight-gradient problems of one backward region that share K: in aw_wgrad_batch launches of <= 32 problems
     when eligible (bf16, M / N multiples of 256), else one aw_gemm_grouped launch per shape."""
     if not problems:
         return
-    nch = (len(problems) + MAX_GROUPS - 1) // MAX_GROUPS
+    nch = (len(problems) + WGRAD_BATCH_MAX - 1) // WGRAD_BATCH_MAX
     per = (len(problems) + nch - 1) // nch
     chunks = [problems[i:i + per] for i in range(0, len(problems), per)]
     if all(wgrad_batch_ok(c) for c in chunks):

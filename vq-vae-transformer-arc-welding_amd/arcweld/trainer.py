@@ -190,7 +190,8 @@ class Trainer:
         The first calls warm up eagerly and capture.  Returns the (static) loss tensor."""
         from .graphs import StepGraphs
         if getattr(self, "_graphs", None) is None or self._graphs.model is not model:
-            self._graphs = StepGraphs(self, model, scale, lambda region: self._allreduce_region(model, region))
+            self._graphs = StepGraphs(self, model, scale, lambda region: self._allreduce_region(model, region),
+                                      collective=self.data_parallel and not _collectives_off())
         return self._graphs.run(batch)
 
     def _allreduce_region(self, model, region):

@@ -279,6 +279,17 @@ __global__ void embed_bwd_kernel(const int64_t* __restrict__ ids, int64_t B, int
   }
 }
 
+// One workgroup per row (grid-stride): the row's id is one scalar load, its D columns are consecutive lanes (every
+// wave-instruction of atomics covers 256 contiguous bytes), and there is no per-element 64-bit division or id load.
+__global__ __launch_bounds__(256) void embed_bwd_rows_kernel(const int64_t* __restrict__ ids, int64_t R, int D,
+                                                             const float* __restrict__ dx, float* __restrict__ dw) {
+  for (int64_t r = blockIdx.x; r < R; r += gridDim.x) {
+    const float* src = dx + r * D;
+    float* dst = dw + ids[r] * D;
+    for (int c = threadIdx.x; c < D; c += blockDim.x) atomicAdd(dst + c, src[c]);
+  }
+}
+
 // ---------------------------------------------------------------- causal attention
 // Two lanes per query (or key) row, each holding half of the head dimension; partial dot products are combined
 // with one xor-1 shuffle.  Key/value (resp. query) tiles of 32 rows are staged in LDS and read as broadcasts.
@@ -863,8 +874,16 @@ extern "C" int aw_embed_fwd(const int64_t* ids, int64_t B, int T, int D, const f
 extern "C" int aw_embed_bwd(const int64_t* ids, int64_t B, int T, int D, const float* dx, float* dwtok, void* stream) {
   AW_REQUIRE(ids && dx && dwtok && B >= 0 && T > 0 && D > 0, "aw_embed_bwd: bad args");
   if (B == 0) return AW_OK;
-  hipLaunchKernelGGL(embed_bwd_kernel, dim3(gridcap(B * T * D)), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
-                     ids, B, T, D, dx, dwtok);
+  // AW_EMBED_BWD_ROWS=0: the element-wise form (A/B)
+  static const bool rows = [] { const char* e = getenv("AW_EMBED_BWD_ROWS"); return !(e && atoi(e) == 0); }();
+  if (rows) {
+    const int64_t R = B * T;
+    hipLaunchKernelGGL(embed_bwd_rows_kernel, dim3((unsigned)(R < 4096 ? R : 4096)), dim3(256), 0,
+                       reinterpret_cast<hipStream_t>(stream), ids, R, D, dx, dwtok);
+  } else {
+    hipLaunchKernelGGL(embed_bwd_kernel, dim3(gridcap(B * T * D)), dim3(256), 0,
+                       reinterpret_cast<hipStream_t>(stream), ids, B, T, D, dx, dwtok);
+  }
   return aw::check_launch("aw_embed_bwd");
 }
 

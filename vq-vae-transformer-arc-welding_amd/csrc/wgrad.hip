@@ -431,7 +431,7 @@ struct WTProb {
 };
 
 struct WTParams {
-  WTProb p[AW_GEMM_MAX_GROUPS];
+  WTProb p[AW_WGRAD_BATCH_MAX];   // 32 x 88 B: the kernel-argument block stays under 3 KB
   int nprob, K, nk, G, total_tiles, S, units;
   float alpha;
   float* ws;          // one slot of WT_SLAB floats per unit
@@ -719,7 +719,7 @@ int wt_cus() {
 
 // checks + launch plan; P == nullptr: only validate.  Returns AW_OK, or a negative status (with the message set)
 int wt_plan(const aw_gemm_args* args, int n, WTParams* P) {
-  AW_REQUIRE(args && n >= 1 && n <= AW_GEMM_MAX_GROUPS, "aw_wgrad_batch: need 1..%d problems", AW_GEMM_MAX_GROUPS);
+  AW_REQUIRE(args && n >= 1 && n <= AW_WGRAD_BATCH_MAX, "aw_wgrad_batch: need 1..%d problems", AW_WGRAD_BATCH_MAX);
   const aw_gemm_args& a0 = args[0];
   int tiles = 0;
   for (int i = 0; i < n; ++i) {
