@@ -158,13 +158,12 @@ class VQVAEPatch(Autoencoder):
         return emb, x_hat, perp
 
     @torch.no_grad()
-    def fused_train_step(self, x, scale, mid_hook=None, split_hook=None):
+    def fused_train_step(self, x, scale, mid_hook=None):
         """One training micro-step on the kernels without autograd: the same work as ``training_step`` followed by
         ``(loss * scale).backward()`` (loss = mse(x_hat, x) + embedding loss, autencoder_lightning_base.py:80-97).
         Gradients accumulate into each parameter's ``.grad`` (the flat optimizer views when a Trainer installed
         ``_grad_sink``).  ``mid_hook`` is called between the decoder-side and the encoder-side backward (see
-        arcweld.vqvae.backward): the data-parallel step starts the decoder-side all-reduce there; ``split_hook`` (if
-        given) between the forward and the backward, where the step graphs may cut.  Returns the loss."""
+        arcweld.vqvae.backward): the data-parallel step starts the decoder-side all-reduce there.  Returns the loss."""
         x = x.contiguous()
         sink = getattr(self, "_grad_sink", None)
 
@@ -179,8 +178,6 @@ class VQVAEPatch(Autoencoder):
         emb, x_hat, perp, idx, sv = engine.forward(self, x, self.training, need_backward=True, seed=self._next_seed(),
                                                    head=False)
         self._last_indices = idx
-        if split_hook is not None:
-            split_hook()
         sq = sv.acc["mse_sq"]            # zeroed with the forward's other accumulators (one fill launch)
         g = self._loss_scale_tensor(float(scale), x.device)
         if sv.head_fused:
