@@ -66,7 +66,7 @@ def operand_set(m, T=None):
     return operands.peek(m, ("decoder", T_), lambda: _operand_jobs(m, T_))
 
 
-def forward(m, ids, generate: bool, training: bool, need_backward: bool, seed: int = 0, dtype=None):
+def forward(m, ids, generate: bool, training: bool, need_backward: bool, seed: int = 0, dtype=None, zero=None):
     """ids (B, T) int64 -> logits (B, T, V) [generate] or (B, 2) [classify]."""
     T_ = operand_dtype(dtype)
     B, T = ids.shape
@@ -93,7 +93,7 @@ def forward(m, ids, generate: bool, training: bool, need_backward: bool, seed: i
     sv.seed_attn = [_mix(seed, 300 + i) for i in range(nb)]
     sv.seed_mlp = [_mix(seed, 400 + i) for i in range(nb)]
     sv.seed_probs = [_mix(seed, 500 + i) for i in range(nb)]
-    sv.ctr = rng_snapshot(m, dev, max(p_drop, sv.p_att))
+    sv.ctr = rng_snapshot(m, dev, max(p_drop, sv.p_att), zero=zero)   # zero: a caller's f64 accumulators
     ids = ids.contiguous()
 
     x = e(R, d)
@@ -309,9 +309,10 @@ def fused_step(m, batch, scale, slot, mid_hook=None):
     (loss, logits)."""
     x, cond, y = batch
     generate = m.task == "generate"
-    out, sv = forward(m, x, generate, m.training, need_backward=True, seed=m._next_seed())
-    sv.ids = x.contiguous()
     dev = x.device
+    sums = torch.empty(2, device=dev, dtype=torch.float64)    # zeroed by the forward's dropout-counter launch
+    out, sv = forward(m, x, generate, m.training, need_backward=True, seed=m._next_seed(), zero=sums)
+    sv.ids = x.contiguous()
     if generate:
         logits2d = out.view(-1, out.shape[-1])          # rows of stride Vp (the padded logits buffer)
         target, ignore = y.reshape(-1).contiguous(), -1
@@ -319,11 +320,11 @@ def fused_step(m, batch, scale, slot, mid_hook=None):
         logits2d, target, ignore = out, cond.reshape(-1).contiguous(), -100
     R, V = logits2d.shape
     lse = torch.empty(R, device=dev)
-    sums = torch.zeros(2, device=dev, dtype=torch.float64)
     K.ce_fwd(logits2d, V, target, ignore, sums[0:1], sums[1:2], lse)
     loss = torch.empty((), device=dev)
     K.ce_finalize(sums[0:1], sums[1:2], loss)
-    g = torch.full((1,), float(scale), device=dev)
+    g = m._loss_scale_tensor(float(scale), dev) if hasattr(m, "_loss_scale_tensor") else \
+        torch.full((1,), float(scale), device=dev)
     if generate:
         # the logits gradient straight into the zero-padded [R][Vp] operand of the lm_head GEMMs, in the operand
         # dtype (aw_ce_bwd zeroes the padding columns): no f32 copy, no strided cast launch

@@ -35,12 +35,26 @@ def _clone_static(batch):
     return type(batch)(_clone_static(b) for b in batch)
 
 
+def _flatten(batch, out):
+    if isinstance(batch, torch.Tensor):
+        out.append(batch)
+    else:
+        for b in batch:
+            _flatten(b, out)
+    return out
+
+
 def _copy_into(dst, src):
-    if isinstance(dst, torch.Tensor):
-        dst.copy_(src, non_blocking=True)
-        return
-    for d, s in zip(dst, src):
-        _copy_into(d, s)
+    """The batch into the static input buffers: one multi-tensor copy launch for all of its tensors (the decoder's
+    ids / condition / targets took three copy launches)."""
+    d, s = _flatten(dst, []), _flatten(src, [])
+    if len(d) == 1:
+        d[0].copy_(s[0], non_blocking=True)
+    elif all(a.dtype == b.dtype and a.device == b.device for a, b in zip(d, s)):
+        torch._foreach_copy_(d, s, non_blocking=True)
+    else:
+        for a, b in zip(d, s):
+            a.copy_(b, non_blocking=True)
 
 
 class StepGraphs:

@@ -394,11 +394,12 @@ def forward(m, x, training: bool, need_backward: bool, dtype=None, seed: int = 0
 
     # ---- un-patch: ConvT(H->H, k1) with BN statistics in the epilogue, then the fused head
     bn = pr["bn"]
-    # The ConvT output stays f32.  A bf16 Y (ARCWELD_HEAD_BF16=1: half the bytes for the head's three passes, the BN
-    # statistics still from the f32 values in the epilogue) measured slower end to end on one box: the ConvT GEMM
-    # 84.5 -> 79.1 us, but head fwd / bwd1 / bwd2 58.7 / 82.5 / 74.8 -> 64.3 / 87.7 / 82.3 us -- the passes are
-    # VALU-bound (BN + erf-GELU + its derivative per element), not HBM-bound
-    bf_y = T != F32 and K.head_bf16_ok(H) and os.environ.get("ARCWELD_HEAD_BF16", "0") == "1"
+    # In the bf16 operand mode the ConvT output Y is bf16 (what autocast keeps for a ConvTranspose1d output; the BN
+    # statistics still come from the f32 values in the epilogue): half the bytes of the GEMM's output and of the head's
+    # passes over Y.  Round 3 measured it even over the step (the head passes are VALU-bound); on the round-4 step it
+    # measured 3.162 / 3.155 / 3.157 vs 3.170 / 3.170 / 3.193 ms for an f32 Y (alternating, same box).
+    # ARCWELD_HEAD_BF16=0 keeps Y in f32.
+    bf_y = T != F32 and K.head_bf16_ok(H) and os.environ.get("ARCWELD_HEAD_BF16", "1") == "1"
     Y = e(N, k1 * H, dt=T if bf_y else F32)
     colstats = acc["colstats"] if training else None
     K.gemm(yR_T, Wt1, N, k1 * H, H, bias=pr["t1"].bias, bias_mod=H, C=Y, colstats=colstats, stats_mod=H)

@@ -135,6 +135,15 @@ class MyTransformerDecoder(LightningModule):
         out, _ = engine.forward(self, x, generate, self.training, need_backward=False, seed=self._next_seed())
         return out
 
+    def _loss_scale_tensor(self, scale, dev):
+        """Persistent device scalar holding the loss scale (refilled only when the value changes; the step graphs
+        make it before their capture, so the captured step has no fill launch for it)."""
+        st = self.__dict__.get("_gscale")
+        if st is None or st[0] != scale or st[1].device != dev:
+            st = (scale, torch.full((1,), scale, device=dev))
+            self.__dict__["_gscale"] = st
+        return st[1]
+
     @torch.no_grad()
     def fused_train_step(self, batch, scale, mid_hook=None):
         """One training micro-step on the kernels without autograd: training_step followed by
