@@ -1,11 +1,11 @@
 #!/bin/bash
-# session script: bf16 ConvT output by default (bf16 mode), decoder fills folded, one multi-tensor input copy
+# session script: epilogue store policy of the decoder step's GEMMs (NT default / write-through / plain)
 set -o pipefail
 export TMPDIR=/tmp
-mkdir -p gpurun_out/s24
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/s24/pytest_gpu.log 2>&1 || { tail -30 gpurun_out/s24/pytest_gpu.log; exit 1; }
-tail -1 gpurun_out/s24/pytest_gpu.log
-timeout -k 10 500 python -u bench.py --no-cpu-baseline --detail gpurun_out/s24/detail.json > gpurun_out/s24/bench.log 2>&1 || { tail -20 gpurun_out/s24/bench.log; exit 1; }
-tail -1 gpurun_out/s24/bench.log | cut -c1-300
-python -c "import json;d=json.loads(open('gpurun_out/s24/bench.log').read().strip().splitlines()[-1]);print({k:v.get('ms_per_step') for k,v in d['lines'].items() if isinstance(v,dict)})"
+A="--no-cpu-baseline --only transformer_pretokenized"
+VAR=ARCWELD_QKV_STORE ARGS="$A" bash tools/ab_env_bench.sh 0 2 2 || exit 1
+VAR=ARCWELD_DEC_STORE ARGS="$A" bash tools/ab_env_bench.sh 0 2 2 || exit 1
+VAR=ARCWELD_DEC_STORE ARGS="$A" bash tools/ab_env_bench.sh 0 1 2 || exit 1
 echo done
+VAR=ARCWELD_VQ_STORE bash tools/ab_env_bench.sh 1 2 2 || exit 1
+echo done2
