@@ -1,11 +1,9 @@
 #!/bin/bash
-# session script: epilogue store policy of the decoder step's GEMMs (NT default / write-through / plain)
+# session script: non-temporal output stores in the LayerNorm and attention kernels (probe libraries, A/B)
 set -o pipefail
 export TMPDIR=/tmp
 A="--no-cpu-baseline --only transformer_pretokenized"
-VAR=ARCWELD_QKV_STORE ARGS="$A" bash tools/ab_env_bench.sh 0 2 2 || exit 1
-VAR=ARCWELD_DEC_STORE ARGS="$A" bash tools/ab_env_bench.sh 0 2 2 || exit 1
-VAR=ARCWELD_DEC_STORE ARGS="$A" bash tools/ab_env_bench.sh 0 1 2 || exit 1
+D=$PWD/vq-vae-transformer-arc-welding_amd/lib/libarcweld_amd.so
+VAR=ARCWELD_LIB ARGS="$A" bash tools/ab_env_bench.sh $D $PWD/ablib/lnnt/libarcweld_amd.so 3 || exit 1
+VAR=ARCWELD_LIB ARGS="$A" bash tools/ab_env_bench.sh $D $PWD/ablib/attnt/libarcweld_amd.so 3 || exit 1
 echo done
-VAR=ARCWELD_VQ_STORE bash tools/ab_env_bench.sh 1 2 2 || exit 1
-echo done2

@@ -142,9 +142,12 @@ __device__ __forceinline__ void store_rows(const f32x16 (&a)[2], float s, char* 
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int row = (lane >> 3) + 8 * j, c = lane & 7;
-    if (row < nrows)
-      *reinterpret_cast<uint4*>(out0 + row * ld + 8 * c) =
-          *reinterpret_cast<const uint4*>(reg + row * ROWB + ((c ^ (row & 7)) << 4));
+    if (row < nrows) {
+      const uint4 u = *reinterpret_cast<const uint4*>(reg + row * ROWB + ((c ^ (row & 7)) << 4));
+      // non-temporal, as the GEMM epilogues: the next launch reads them (decoder step 5.314 / 5.315 / 5.315 ->
+      // 5.306 / 5.309 / 5.300 ms against ordinary stores, same box)
+      __builtin_nontemporal_store(__builtin_bit_cast(aw_v4i32, u), reinterpret_cast<aw_v4i32*>(out0 + row * ld + 8 * c));
+    }
   }
 }
 
