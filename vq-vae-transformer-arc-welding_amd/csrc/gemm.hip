@@ -213,6 +213,11 @@ static bool is_ragged(const aw_gemm_args& a) {
 #define AW_GROUPED_MAXSPLIT 8
 #endif
 
+// fewest K steps of one split-K slice of a plain 128-tile launch (its slab write + reduce stay small against them)
+#ifndef AW_SPLIT_MIN_KSTEPS
+#define AW_SPLIT_MIN_KSTEPS 12
+#endif
+
 static int g_tile_override = 0;   // aw_gemm_set_tile: 0 = automatic, 128 / 256 = force (tests, tuning)
 
 extern "C" int aw_gemm_set_tile(int bm) {
@@ -275,7 +280,7 @@ static void plan(const aw_gemm_args& a, int ngroups, bool grouped, GemmP& P) {
     if (plain && nb < 384 && a.K >= 24 * BK) {
       // two co-resident blocks per CU (256 CUs); keep >= 12 K-steps per split so the slab write + reduce is small
       splits = 512 / nb;
-      const int max_splits = a.K / (12 * BK);
+      const int max_splits = a.K / (AW_SPLIT_MIN_KSTEPS * BK);
       if (splits > max_splits) splits = max_splits;
       if (grouped && splits > AW_GROUPED_MAXSPLIT) splits = AW_GROUPED_MAXSPLIT;
       if (splits < 1) splits = 1;
