@@ -1,15 +1,9 @@
 #!/bin/bash
-# session script: ConvT forward variants + skinny weight gradients at split-K floors 12 / 6 / 4 K steps (isolated
-# probe per library), then the VQ-VAE step A/B of the 4-step floor
+# session script: LayerNorm backward with bf16 input gradients -- GPU suite, then the decoder step A/B
 set -o pipefail
 export TMPDIR=/tmp
-mkdir -p gpurun_out/s28
-D=$PWD/vq-vae-transformer-arc-welding_amd/lib/libarcweld_amd.so
-for i in 1 2; do
-  for L in $D $PWD/ablib/ks6/libarcweld_amd.so $PWD/ablib/ks4/libarcweld_amd.so; do
-    echo "== $(basename $(dirname $L))"
-    ARCWELD_LIB=$L timeout -k 10 120 python tools/probe/skinny_probe.py 30 2>&1 | grep -v amdgpu.ids || exit 1
-  done
-done
-VAR=ARCWELD_LIB bash tools/ab_env_bench.sh $D $PWD/ablib/ks4/libarcweld_amd.so 2 || exit 1
+mkdir -p gpurun_out/s29
+timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread > gpurun_out/s29/tests.log 2>&1 || { tail -30 gpurun_out/s29/tests.log; exit 1; }
+tail -1 gpurun_out/s29/tests.log
+VAR=ARCWELD_LN_DY_F32 ARGS="--no-cpu-baseline --only transformer_pretokenized" bash tools/ab_env_bench.sh 1 0 3 || exit 1
 echo done
