@@ -2,7 +2,8 @@
 
 A step is captured as graphs on the current stream:
   g_fwd_bwd : forward + backward of one micro-batch (gradients accumulate into the flat buffer)
-  g_update  : clip-norm + RAdam + zero_grad
+  g_update  : clip-norm + RAdam + zero_grad (captured into the last forward/backward piece when no collective and
+              no accumulation separate them)
 With data parallelism the RCCL all-reduce of the flat gradient buffer runs eagerly between the two.  A model
 with ``fused_train_step`` (VQVAEPatch, MyTransformerDecoder) is captured as TWO forward/backward graphs split
 where its ``backward_late_parameters()`` are final (VQ-VAE: the decoder side; Transformer: the task head, ln_f and
@@ -75,6 +76,11 @@ class StepGraphs:
         self.split = hasattr(model, "fused_train_step") and hasattr(model, "backward_late_parameters") and \
             os.environ.get("ARCWELD_SPLIT_GRAPHS") != "0"
         model.__dict__["_wgrad_merge"] = not collective and os.environ.get("ARCWELD_WGRAD_MERGE") != "0"
+        # Without a collective and without accumulation nothing runs between the last forward/backward piece and the
+        # update, so the update is captured into that piece: one graph launch (and its ~8.5 us gap on the stream)
+        # fewer per step.  ARCWELD_FUSE_UPDATE=0 keeps it a graph of its own (A/B runs).
+        self.fuse_update = self.split and not collective and getattr(trainer, "accumulate", 1) == 1 and \
+            os.environ.get("ARCWELD_FUSE_UPDATE") != "0"
 
     def _capture(self, batch):
         self.static = _clone_static(batch)
@@ -104,8 +110,12 @@ class StepGraphs:
 
             try:
                 self.loss = self.model.fused_train_step(self.static, self.scale, mid_hook=mid)
+                if self.fuse_update:
+                    self.trainer._update(self.model)
             finally:
                 state["ctx"].__exit__(None, None, None)
+            if self.fuse_update:
+                return
         else:
             self.g1 = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self.g1, pool=pool, capture_error_mode=_MODE):
@@ -118,6 +128,8 @@ class StepGraphs:
         forward/backward graph is replayed once per micro-batch, gradients accumulating in the flat buffer; the
         all-reduce runs once, split around the last micro-batch's backward -- DDP's no_sync accumulation)."""
         batches = batch if isinstance(batch, list) else [batch]
+        if self.fuse_update and len(batches) > 1:
+            raise ValueError("StepGraphs: the update is captured with the backward; one micro-batch per step")
         self.calls += 1
         if self.calls <= self.warmup:
             for j, b in enumerate(batches):
@@ -148,6 +160,7 @@ class StepGraphs:
                     works = self.allreduce("all")
         for w in works:
             w.wait()
-        self.g2.replay()
+        if not self.fuse_update:
+            self.g2.replay()
         self.trainer.global_step += 1
         return self.loss
