@@ -270,6 +270,25 @@ __global__ void embed_fwd_kernel(const int64_t* __restrict__ ids, int64_t B, int
   }
 }
 
+// Vectorised form (D % 4 == 0, 16-B aligned tables): one wave per row, float4 columns; the row's id and position are
+// computed once per row instead of per element (the element-wise form: 21 us at 16371 x 512, 1.6 TB/s).
+__global__ __launch_bounds__(256) void embed_fwd_rows_kernel(const int64_t* __restrict__ ids, int64_t R, int T, int D,
+                                                             const float* __restrict__ wtok,
+                                                             const float* __restrict__ pe, float* __restrict__ x) {
+  const int lane = threadIdx.x & 63;
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  const int d4 = D >> 2;
+  for (int64_t r = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; r < R; r += nw) {
+    const float4* a = reinterpret_cast<const float4*>(wtok + ids[r] * D);
+    const float4* b = reinterpret_cast<const float4*>(pe + (r % T) * D);
+    float4* o = reinterpret_cast<float4*>(x + r * D);
+    for (int c = lane; c < d4; c += 64) {
+      const float4 u = a[c], v = b[c];
+      o[c] = make_float4(u.x + v.x, u.y + v.y, u.z + v.z, u.w + v.w);
+    }
+  }
+}
+
 __global__ void embed_bwd_kernel(const int64_t* __restrict__ ids, int64_t B, int T, int D, const float* __restrict__ dx,
                                  float* __restrict__ dw) {
   const int64_t n = B * T * D;
@@ -866,6 +885,12 @@ extern "C" int aw_embed_fwd(const int64_t* ids, int64_t B, int T, int D, const f
                             void* stream) {
   AW_REQUIRE(ids && wtok && pe && x && B >= 0 && T > 0 && D > 0, "aw_embed_fwd: bad args");
   if (B == 0) return AW_OK;
+  if ((D & 3) == 0 && (((uintptr_t)wtok | (uintptr_t)pe | (uintptr_t)x) & 15) == 0) {
+    const int64_t R = B * T;
+    hipLaunchKernelGGL(embed_fwd_rows_kernel, dim3((unsigned)std::min<int64_t>((R + 3) / 4, 4096)), dim3(256), 0,
+                       reinterpret_cast<hipStream_t>(stream), ids, R, T, D, wtok, pe, x);
+    return aw::check_launch("aw_embed_fwd");
+  }
   hipLaunchKernelGGL(embed_fwd_kernel, dim3(gridcap(B * T * D)), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
                      ids, B, T, D, wtok, pe, x);
   return aw::check_launch("aw_embed_fwd");
