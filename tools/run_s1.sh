@@ -1,2 +1,2 @@
 #!/bin/bash
-TAG=r04_s22 STAGES="tests smoke bench prof proft" bash tools/evidence.sh
+TAG=r04_s35 STAGES="tests smoke bench prof proft" bash tools/evidence.sh
