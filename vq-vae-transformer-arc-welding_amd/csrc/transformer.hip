@@ -606,12 +606,16 @@ __global__ __launch_bounds__(1024) void ce_fwd_rows_kernel(const float* __restri
   const int64_t nw = (int64_t)gridDim.x * 16;
   double ls = 0.0, cnt = 0.0;
   float nv[NC];
+  int64_t ny = ignore;
+  // the row's logits AND its target id load one row ahead; the target logit is then taken from the registers (its
+  // own dependent load after the target id's, both exposed per row, was most of this kernel's time)
   auto load = [&](int64_t r) {
 #pragma unroll
     for (int k = 0; k < NC; ++k) {
       const int i = lane + 64 * k;
       nv[k] = (r < R && i < V) ? logits[r * ldl + i] : -__builtin_huge_valf();
     }
+    ny = r < R ? y[r] : ignore;
   };
   int64_t r = (int64_t)blockIdx.x * 16 + wv;
   load(r);
@@ -619,6 +623,7 @@ __global__ __launch_bounds__(1024) void ce_fwd_rows_kernel(const float* __restri
     float v[NC];
 #pragma unroll
     for (int k = 0; k < NC; ++k) v[k] = nv[k];
+    const int64_t t = ny;
     load(r + nw);
     float mx = -__builtin_huge_valf();
 #pragma unroll
@@ -629,15 +634,17 @@ __global__ __launch_bounds__(1024) void ce_fwd_rows_kernel(const float* __restri
     for (int k = 0; k < NC; ++k) sm += __expf(v[k] - mx);   // -inf (past V) -> 0
     sm = wave_sum(sm);
     const float L = mx + logf(sm);
-    if (lane == 0) {
-      lse[r] = L;
-      const int64_t t = y[r];
-      if (t != ignore) {
-        ls += (double)(L - logits[r * ldl + t]);
-        cnt += 1.0;
-      }
+    if (lane == 0) lse[r] = L;
+    if (t != ignore) {   // wave-uniform; the lane holding column t adds the row's term
+      const int tk = (int)(t >> 6);
+      float tv = v[0];
+#pragma unroll
+      for (int k = 1; k < NC; ++k) tv = k == tk ? v[k] : tv;
+      if (lane == (int)(t & 63)) ls += (double)(L - tv);
+      cnt += 1.0;
     }
   }
+  ls = wave_sum_d(ls);
   if (lane == 0) {
     part[wv][0] = ls;
     part[wv][1] = cnt;
