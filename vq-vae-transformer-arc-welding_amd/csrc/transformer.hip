@@ -14,6 +14,10 @@ void attn_bwd_mfma(const void* qkv, const void* y, const void* dy, const float* 
                    int nh, int d, void* dqkv, hipStream_t s);   // delta computed by its dQ launch
 }  // namespace aw
 
+#ifndef AW_ATOMIC_ROTATE
+#define AW_ATOMIC_ROTATE 1
+#endif
+
 namespace {
 
 // ---------------------------------------------------------------- LayerNorm (one wave per row)
@@ -247,7 +251,14 @@ __global__ __launch_bounds__(512) void ln_bwd_vec_kernel(const float* __restrict
     *reinterpret_cast<float4*>(&red[(wv * 2 + 1) * C + 4 * lane + 256 * j]) = pdb[j];
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < C; i += blockDim.x) {
+  // every workgroup adds into the same 2C addresses: each starts its walk at its own offset, so that at any moment
+  // they queue on different addresses (AW_ATOMIC_ROTATE=0 in the build: all from column 0)
+  for (int i0 = threadIdx.x; i0 < C; i0 += blockDim.x) {
+#if AW_ATOMIC_ROTATE
+    const int i = (i0 + (int)(blockIdx.x & 7) * (C / 8)) % C;
+#else
+    const int i = i0;
+#endif
     float a = 0.f, b = 0.f;
     for (int v = 0; v < nwv; ++v) {
       a += red[(v * 2 + 0) * C + i];

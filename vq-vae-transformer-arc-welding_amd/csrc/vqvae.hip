@@ -676,6 +676,9 @@ __global__ __launch_bounds__(1024) void head_bwd2_cs_kernel(const TY* __restrict
 // HB rows through a ring of three batches (two in flight while one computes), without VGPRs held by loads and
 // without barriers (nothing is shared between waves until the final per-channel reduction).  The x row (5 floats)
 // comes the same way.
+#ifndef AW_ATOMIC_ROTATE
+#define AW_ATOMIC_ROTATE 1
+#endif
 constexpr int HB = 4;          // rows per wave below which the grid shrinks
 constexpr int HFW = 8;         // waves per workgroup (one workgroup per CU: its per-channel atomics end the launch)
 template <typename TY> struct HeadRows {
@@ -879,12 +882,32 @@ __global__ __launch_bounds__(64 * HFW, 1) void head_fwd_bwd1_kernel(
       mine[5 * H + o] = accg[p][e];
       mine[6 * H + o] = accgx[p][e];
     }
+  // the two scalar sums per workgroup (one atomic each), not per wave: 2 x 2048 same-address atomics serialised
+  // into ~12 us of the launch's tail (fused head 88.7 -> 74.8-76.6 us isolated, tools/probe/head_probe.py)
+  __shared__ double scal[HFW][2];
   if (lane == 0) {
-    atomicAdd(gb2, gbs);
-    atomicAdd(sqerr, sq);
+    scal[wv][0] = sq;
+    scal[wv][1] = (double)gbs;
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < 7 * H; i += 64 * HFW) {
+  if (threadIdx.x == 0) {
+    double a = 0.0, b = 0.0;
+#pragma unroll
+    for (int q = 0; q < HFW; ++q) {
+      a += scal[q][0];
+      b += scal[q][1];
+    }
+    atomicAdd(sqerr, a);
+    atomicAdd(gb2, (float)b);
+  }
+  // per-channel sums: every workgroup adds into the same 7H addresses; starting each workgroup's walk at its own
+  // offset keeps them on different addresses at any moment (AW_ATOMIC_ROTATE=0 in the build: all from entry 0)
+  for (int i0 = threadIdx.x; i0 < 7 * H; i0 += 64 * HFW) {
+#if AW_ATOMIC_ROTATE
+    const int i = (i0 + (int)(blockIdx.x % 7) * H) % (7 * H);
+#else
+    const int i = i0;
+#endif
     float t = 0.f;
 #pragma unroll
     for (int q = 0; q < HFW; ++q) t += part[q * 7 * H + i];
@@ -1038,7 +1061,12 @@ __global__ __launch_bounds__(64 * HFW, 1) void head_bwd2_rows_kernel(const TY* _
     part[wv * H + HR::chan(lane, 2 * p + 1)] = accd[p].y;
   }
   __syncthreads();
-  for (int o = threadIdx.x; o < H; o += 64 * HFW) {
+  for (int o0 = threadIdx.x; o0 < H; o0 += 64 * HFW) {
+#if AW_ATOMIC_ROTATE
+    const int o = (o0 + (int)(blockIdx.x & 7) * (H / 8)) % H;   // see head_fwd_bwd1_kernel
+#else
+    const int o = o0;
+#endif
     float t = 0.f;
 #pragma unroll
     for (int q = 0; q < HFW; ++q) t += part[q * H + o];
