@@ -37,6 +37,12 @@ constexpr int VQ_THREADS = 512;
 constexpr int VQ_CODES = 512;
 constexpr int VQ_DC = 16;           // embedding floats per staged chunk
 
+// code counts gathered per workgroup in LDS (1) or added per row (0: A/B builds).  Isolated at the configs[1] shape:
+// 39.1 -> 28.0 us (a probe build without the count atomics: 26.4 us; tools/probe/vq_probe.py)
+#ifndef AW_VQ_LDS_COUNTS
+#define AW_VQ_LDS_COUNTS 1
+#endif
+
 template <int D, int ROWS> struct VqLds {
   static constexpr int ZP = D + 4;                                   // z image pitch (disjoint banks per row)
   static constexpr int Z = ROWS * ZP;                                // floats
@@ -224,6 +230,17 @@ __global__ __launch_bounds__(VQ_THREADS, 2) void vq_fwd_kernel(const float* __re
   // copy) coalesced; the q == 0 thread of a row writes idx and counts the code.
   constexpr int DQ = D / 4;
   double se = 0.0;
+#if AW_VQ_LDS_COUNTS
+  // the workgroup's code counts gather in LDS (the e stages past rd / rk are free now) and go out as one sweep of
+  // the K bins: one atomic per distinct code, issued bin-contiguous, instead of one per row from the epilogue
+  constexpr int HCAP = 2 * L::E - 16 * ROWS;
+  float* hist = es + 16 * ROWS;
+  const bool lds_counts = K <= HCAP;
+  if (lds_counts) {
+    for (int i = tid; i < K; i += VQ_THREADS) hist[i] = 0.f;
+    __syncthreads();
+  }
+#endif
   for (int it = tid; it < ROWS * DQ; it += VQ_THREADS) {
     const int r = it / DQ, q = it - r * DQ;
     const int64_t row = row0 + r;
@@ -239,6 +256,11 @@ __global__ __launch_bounds__(VQ_THREADS, 2) void vq_fwd_kernel(const float* __re
     if (bk < 0 || bk >= K) bk = 0;  // all-NaN row guard (torch would return the NaN position)
     if (q == 0) {
       idx[row] = bk;
+#if AW_VQ_LDS_COUNTS
+      if (lds_counts)
+        atomicAdd(hist + bk, 1.0f);
+      else
+#endif
 #ifndef AW_VQ_NO_COUNTS_PROBE
       atomicAdd(counts + bk, 1.0f);
 #endif
@@ -270,6 +292,13 @@ __global__ __launch_bounds__(VQ_THREADS, 2) void vq_fwd_kernel(const float* __re
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
+#if AW_VQ_LDS_COUNTS
+  if (lds_counts)
+    for (int i = tid; i < K; i += VQ_THREADS) {
+      const float c = hist[i];
+      if (c != 0.f) atomicAdd(counts + i, c);
+    }
+#endif
   if (tid == 0) {
     double t = 0.0;
 #pragma unroll
