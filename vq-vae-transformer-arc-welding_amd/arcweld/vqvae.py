@@ -311,7 +311,27 @@ def forward(m, x, training: bool, need_backward: bool, dtype=None, seed: int = 0
     # ---- encoder ResBlocks (per-token: centre taps)
     xs, a0s, hs, a1s = [x0], [a0], [], []
     sv.enc_bs, sv.dec_bs = [], []
-    for r, (c1, c2) in enumerate(pr["enc"]):
+    sv.enc_chain = R > 0 and pr["enc_bn"][0] is None and K.enc_chain_ok(H, R, T, RT)
+    if sv.enc_chain:
+        # bf16: the whole ResBlock stack as ONE persistent launch (csrc/encchain.hip), the same tensors bit for bit
+        sb = need_backward
+        hs = [e(N, H, dt=T) if sb else None for _ in range(R)]
+        a1s = [e(N, H, dt=T) if sb else None for _ in range(R)]
+        xo = [e(N, H, dt=RT) if sb and r < R - 1 else None for r in range(R)]
+        ao = [e(N, H, dt=T) for _ in range(R)]
+        # fragment-packed weight copies, from the optimizer-maintained [out][in] copies (one launch; the backward's
+        # transposed ones come out of the same launch)
+        wsrc = [w for pair in enc_w for w in pair]
+        pk = [e(H, H, dt=T) for _ in wsrc]
+        sv.enc_pk_bwd = [e(H, H, dt=T) for _ in wsrc] if sb else None
+        K.enc_pack_weights(wsrc, pk, sv.enc_pk_bwd)
+        sv.enc_masks = K.enc_dropout_masks(N, (p_drop, sv.enc_seed), sv.ctr)   # both directions' dropout bits
+        K.enc_chain_fwd(a0, x0, pk[0::2], pk[1::2], [c1.bias for c1, _ in pr["enc"]],
+                        [c2.bias for _, c2 in pr["enc"]], hs, a1s, xo, ao, drop=(p_drop, sv.enc_seed),
+                        seed_ptr=sv.ctr, masks=sv.enc_masks)
+        xs += xo
+        a0s += ao
+    for r, (c1, c2) in enumerate(pr["enc"] if not sv.enc_chain else []):
         if pr["enc_bn"][r] is not None:   # BatchNorm ResBlocks: per-token statistics (G = S)
             xn, an, bs = _bn_block_fwd(a0s[r], xs[r], enc_w[r][0], enc_w[r][1], H, {}, c1, c2, pr["enc_bn"][r], S,
                                        training, p_drop, sv.enc_seed[r], sv.ctr, T, last=r == R - 1)
@@ -612,7 +632,26 @@ def backward(m, sv, g_emb, g_xhat, slot, mid_hook=None):
         return (A, B, H, H, N, dict(a_trans=True, b_trans=True, C=Cw, accumulate=True, col_map=cm,
                                     a_rowsum=slot(c.bias)))
 
-    for r in reversed(range(R)):
+    if getattr(sv, "enc_chain", False):
+        # bf16: the input-gradient chain of all R blocks in one launch, on the packed transposed weight copies the
+        # forward made
+        wt = sv.enc_pk_bwd
+        gh = [e(N, H, dt=T) for _ in range(R)]
+        go = [e(N, H, dt=T) for _ in range(R)]
+        K.enc_chain_bwd(gx, gxo, wt[0::2], wt[1::2], sv.hs, sv.xs[:R], gh, go, drop=(p_drop, sv.enc_seed),
+                        seed_ptr=sv.ctr, masks=sv.enc_masks)
+        sv.enc_pk_bwd = sv.enc_masks = None
+        for r in reversed(range(R)):
+            c1, c2 = pr["enc"][r]
+            gin = gxo if r == R - 1 else go[r + 1]
+            C2w, cm2 = _centre_grad(slot(c2.weight))
+            wgrads.append((gin, sv.a1s[r], H, H, N, dict(a_trans=True, b_trans=True, C=C2w, accumulate=True,
+                                                         col_map=cm2, a_rowsum=slot(c2.bias))))
+            C1w, cm1 = _centre_grad(slot(c1.weight))
+            wgrads.append((gh[r], sv.a0s[r], H, H, N, dict(a_trans=True, b_trans=True, C=C1w, accumulate=True,
+                                                           col_map=cm1, a_rowsum=slot(c1.bias))))
+        gxo = go[0]
+    for r in reversed(range(R)) if not getattr(sv, "enc_chain", False) else ():
         c1, c2 = pr["enc"][r]
         w1, w2 = sv.enc_w[r]
         if bnm:

@@ -165,6 +165,16 @@ __device__ __forceinline__ float gelu_tanh_grad(float x) {
   return s + 2.0f * x * s * (1.0f - s) * du;
 }
 
+// The GEMM epilogue's  x * m + r  (m = the last of act' / dropout scale, r = the residual): fused when both are
+// present, so the rounding does not depend on the compiler's contraction choices (gemm_core.h and the fused encoder
+// chain, encchain.hip, must agree bit for bit).
+__device__ __forceinline__ float aw_epi_mad(float x, float m, bool has_m, float r, bool has_r) {
+  if (has_m && has_r) return __builtin_fmaf(x, m, r);
+  if (has_m) x = __fmul_rn(x, m);
+  if (has_r) x = __fadd_rn(x, r);
+  return x;
+}
+
 // ---------------------------------------------------------------- counter-based RNG (dropout masks)
 // One splitmix64 draw per aligned group of 4 elements (g = e >> 2) of a launch with seed s; element e takes the
 // 16-bit uniform in bits [16*(e & 3), 16*(e & 3) + 16) and is dropped iff u < round(p * 65536).  Forward and
@@ -175,7 +185,7 @@ __device__ __forceinline__ uint64_t aw_hash_group(uint64_t seed, uint64_t g) {
   z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
   return z ^ (z >> 31);
 }
-__device__ __forceinline__ uint32_t aw_drop_threshold(float p) { return (uint32_t)(p * 65536.f + 0.5f); }
+__host__ __device__ __forceinline__ uint32_t aw_drop_threshold(float p) { return (uint32_t)(p * 65536.f + 0.5f); }
 // Effective seed when a device-side per-step counter is supplied (seed_ptr in the ABI).
 __device__ __forceinline__ uint64_t aw_seed_mix_value(uint64_t salt, uint64_t ctr) {
   uint64_t z = salt ^ (ctr * 0xD1B54A32D192ED03ull + 0x8CB92BA72F3D8DD7ull);

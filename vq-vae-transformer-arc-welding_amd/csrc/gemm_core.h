@@ -794,9 +794,17 @@ __global__ __launch_bounds__(Cfg<BMT>::NTH, RAGGED ? 1 : Cfg<BMT>::MINB) void ge
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           float x = alpha * av[e] + bias[e];
-          if (f_pre) x *= f_tanh ? gelu_tanh_grad(pv[e]) : (FASTGELU ? gelu_erf_grad_fast(pv[e]) : gelu_erf_grad(pv[e]));
-          if (f_drop) x *= ds[e];
-          if (f_resid) x += rv[e];
+          // x * act' * ds + resid with the last multiply fused into the add (aw_epi_mad): one rounding order that the
+          // encoder chain (encchain.hip) reproduces exactly, whatever FMA contraction the compiler would choose
+          float m = 1.f;
+          bool has_m = false;
+          if (f_pre) {
+            const float a = f_tanh ? gelu_tanh_grad(pv[e]) : (FASTGELU ? gelu_erf_grad_fast(pv[e]) : gelu_erf_grad(pv[e]));
+            if (f_drop) x *= a;
+            else m = a, has_m = true;
+          }
+          if (f_drop) m = ds[e], has_m = true;
+          x = aw_epi_mad(x, m, has_m, f_resid ? rv[e] : 0.f, f_resid);
           if (f_beta) x += p.beta * ov[e];
           v[e] = x;
           float y = x;
