@@ -10,7 +10,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(os.path.dirname(HERE))
 SRC = os.path.join(REPO, "vq-vae-transformer-arc-welding_amd", "csrc")
-VARIANTS = {"base": 0, "no_store": 1, "w_l1": 2, "no_store_w_l1": 3, "stamps": 4}
+VARIANTS = {"base": 0, "no_store": 1, "stamps": 4}
 
 
 def build():
@@ -67,7 +67,7 @@ def main(iters=20):
     masks = torch.empty(R * (N // 64) * 512 * 8, device="cuda", dtype=torch.uint8)
     keep.append(masks)
     fa.drop_masks = ba.drop_masks = masks.data_ptr()
-    pol = int(os.environ.get("EC_STORE_POLICY", "1"))
+    pol = int(os.environ.get("EC_STORE_POLICY", "0"))
     fa.store_policy = ba.store_policy = pol
     print(f"store policy {'WT (sc1)' if pol else 'NT'}")
     for name in VARIANTS:
@@ -91,15 +91,17 @@ def main(iters=20):
             res.append(t0.elapsed_time(t1) * 1000 / iters)
             if name.startswith("stamps"):
                 import numpy as np
-                buf = (ctypes.c_uint64 * (256 * 32 * 3))()
-                lib.aw_probe_ec_stamps(buf, 256 * 32 * 3)
-                st = np.frombuffer(buf, dtype=np.uint64).reshape(256, 32, 3).astype(np.int64)[:, :2 * R]
+                buf = (ctypes.c_uint64 * (256 * 32 * 4))()
+                lib.aw_probe_ec_stamps(buf, 256 * 32 * 4)
+                st = np.frombuffer(buf, dtype=np.uint64).reshape(256, 32, 4).astype(np.int64)[:, :2 * R]
                 loop = np.median(st[:, :, 1] - st[:, :, 0], axis=0)
-                epi = np.median(st[:, :, 2] - st[:, :, 1], axis=0)
+                pub = np.median(st[:, :-1, 3] - st[:, :-1, 1], axis=0)
+                epi = np.median(st[:, :-1, 2] - st[:, :-1, 3], axis=0)
                 gap = np.median(st[:, 1:, 0] - st[:, :-1, 2], axis=0)
                 print(f"  {'fwd' if args is fa else 'bwd'} stamps (cycles, median over WGs) k-loop {loop.astype(int).tolist()}")
-                print(f"      epilogue {epi.astype(int).tolist()}")
-                print(f"      barrier  {gap.astype(int).tolist()}")
+                print(f"      k-loop end -> published {pub.astype(int).tolist()}")
+                print(f"      published -> epilogue end {epi.astype(int).tolist()}")
+                print(f"      -> next k-loop  {gap.astype(int).tolist()}")
         print(f"{name:14s} fwd {res[0]:7.1f} us   bwd {res[1]:7.1f} us", flush=True)
 
 

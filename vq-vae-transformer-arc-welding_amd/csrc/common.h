@@ -151,6 +151,17 @@ __device__ __forceinline__ f32x2 gelu_erf_grad_fast2(f32x2 x) {
   return dg;
 }
 
+// Four values at a time (two packed pairs): the form the bf16 GEMM epilogues and the fused encoder chain share, so
+// that both round identically (tests/test_enc_chain.py compares them bit for bit).
+__device__ __forceinline__ void aw_gelu4(const float (&x)[4], float (&y)[4]) {
+  const f32x2 a = gelu_erf_fast2((f32x2){x[0], x[1]}), b = gelu_erf_fast2((f32x2){x[2], x[3]});
+  y[0] = a.x, y[1] = a.y, y[2] = b.x, y[3] = b.y;
+}
+__device__ __forceinline__ void aw_gelu_grad4(const float (&x)[4], float (&g)[4]) {
+  const f32x2 a = gelu_erf_grad_fast2((f32x2){x[0], x[1]}), b = gelu_erf_grad_fast2((f32x2){x[2], x[3]});
+  g[0] = a.x, g[1] = a.y, g[2] = b.x, g[3] = b.y;
+}
+
 // GELU tanh form (model/transformer_block.py:8-15): 0.5*x*(1 + tanh(u)) == x * sigmoid(2u), u = sqrt(2/pi)(x +
 // 0.044715 x^3) -- one exp and one division instead of tanhf (same value to fp32 rounding).
 #define AW_SQRT_2_OVER_PI 0.79788456080286535588f

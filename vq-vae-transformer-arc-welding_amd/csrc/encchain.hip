@@ -43,12 +43,12 @@
 // Probe builds only (tools/probe/enc_chain_variants.py compiles this file alone with -DEC_PROBE_FLAGS=n; the
 // library never sets it): 1 = no global stores, 2 = every weight load reads the first 64 KB of its matrix
 // (L1/L2-resident), 4 = per-conv s_memtime stamps of wave 0 into g_ec_stamps (K loop start, K loop end, epilogue
-// end).  Results of the probe builds are garbage by construction.
+// end, slice published).  Results of the probe builds are garbage by construction.
 #ifndef EC_PROBE_FLAGS
 #define EC_PROBE_FLAGS 0
 #endif
 #if EC_PROBE_FLAGS & 4
-__device__ uint64_t g_ec_stamps[1024 * 32 * 3];
+__device__ uint64_t g_ec_stamps[1024 * 32 * 4];
 extern "C" int aw_probe_ec_stamps(uint64_t* out, int n) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ec_stamps), (size_t)n * 8) == hipSuccess ? n : -1;
 }
@@ -59,7 +59,7 @@ namespace {
 __device__ __forceinline__ void ec_stamp(int conv, int k) {
 #if EC_PROBE_FLAGS & 4
   if (threadIdx.x == 0 && blockIdx.x < 1024 && conv < 32)
-    g_ec_stamps[(blockIdx.x * 32 + conv) * 3 + k] = __builtin_amdgcn_s_memtime();
+    g_ec_stamps[(blockIdx.x * 32 + conv) * 4 + k] = __builtin_amdgcn_s_memtime();
 #else
   (void)conv;
   (void)k;
@@ -73,7 +73,8 @@ constexpr int EC_ROWB = EC_H * 2;           // bytes per image row (bf16)
 constexpr int EC_IMG = EC_ROWS * EC_ROWB;   // 64 KB per activation image
 constexpr int EC_SCR = 2048;                // per-wave scratch: 16 tokens x 64 channels bf16, [token][128 B]
 constexpr int EC_FLAGS = 2 * EC_IMG + 8 * EC_SCR;   // 8 per-wave "epilogues done" counters
-constexpr int EC_LDS = EC_FLAGS + 64;
+constexpr int EC_BIAS = EC_FLAGS + 64;              // per-wave bias slot: the wave's 64 channels of the current conv
+constexpr int EC_LDS = EC_BIAS + 8 * 256;
 constexpr uint32_t EC_WBYTES = EC_H * EC_H * 2;     // one weight matrix
 
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
@@ -142,7 +143,19 @@ __device__ __forceinline__ void ec_load_image(char* img, const void* src, int64_
   }
 }
 
+// Waves 4-7 (the SIMD partners of waves 0-3) start ~10 k cycles (about half a conv) late, so that on every SIMD
+// one wave's epilogue (VALU, LDS, stores) tends to run under the other's MFMAs; the slice hand-offs keep the phase
+// shift (the early waves' K steps 8-15 read the late waves' slices).  Probe, same box: forward 257 -> 223 us,
+// backward 265 -> 247 us.
+__device__ __forceinline__ void ec_stagger(int tid) {
+  if ((tid >> 6) >= 4) {
+    __builtin_amdgcn_s_sleep(127);
+    __builtin_amdgcn_s_sleep(40);
+  }
+}
+
 // ---------------------------------------------------------------- inter-wave hand-off through LDS
+__device__ __forceinline__ void ec_stamp_pub(int conv) { ec_stamp(conv, 3); }
 typedef __attribute__((address_space(3))) volatile int lds_vint;
 __device__ __forceinline__ lds_vint* ec_flag(char* smem, int wv) {
   // an LDS pointer (ds_read / ds_write): through a generic pointer the flags compiled to flat accesses
@@ -155,6 +168,7 @@ __device__ __forceinline__ void ec_wait(char* smem, int wv, int target) {
 }
 // publish this wave's slice of the next image (every LDS write of it performed first)
 __device__ __forceinline__ void ec_publish(char* smem, int w, int lane, int count) {
+  ec_stamp_pub(count - 1);
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   if (lane == 0) *ec_flag(smem, w) = count;
 }
@@ -308,6 +322,7 @@ __global__ __launch_bounds__(EC_NTH) void enc_chain_fwd_kernel(aw_enc_chain_fwd_
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __syncthreads();
+  ec_stagger(tid);
 
   for (int c = 0; c < NC; ++c) {
     const int r = c >> 1;
@@ -319,8 +334,12 @@ __global__ __launch_bounds__(EC_NTH) void enc_chain_fwd_kernel(aw_enc_chain_fwd_
     f32x4 acc[4][4];
     ec_stamp(c, 0);
     u32x2 keep = {0u, 0u};
+    // this conv's bias, one value per lane (the wave's 64 channels), loaded ahead of the K loop and parked in the
+    // wave's LDS slot at its end (read in the epilogue as a 16-B broadcast per fragment row: no L2 latency there)
+    const float bias_l = (second ? P.b2[r] : P.b1[r])[64 * L.w + L.lane];
     // the dropout keep bits of a conv2 epilogue, loaded behind the last K step's weight loads
     auto load_keep = [&] {
+      *reinterpret_cast<float*>(smem + EC_BIAS + 256 * L.w + 4 * L.lane) = bias_l;
       if (DROP && second) keep = ec_keep(P.drop_masks, r, tid);
     };
     ec_conv(acc, wf, smem, L.rb0 + io, rc, rn, has_next, L.wl, L.w, c, load_keep);
@@ -329,9 +348,8 @@ __global__ __launch_bounds__(EC_NTH) void enc_chain_fwd_kernel(aw_enc_chain_fwd_
 #pragma unroll
     for (int i = 0; i < 4; ++i) nwb[i] = L.wb(i) + no;
 
-    const float* bp = (second ? P.b2[r] : P.b1[r]) + 64 * L.w + 4 * L.g;
-    auto bias = [&](int i, float (&bv)[4]) {   // reloaded per fragment (L1 hits): fewer registers across the epilogue
-      const float4 b4 = *reinterpret_cast<const float4*>(bp + 16 * i);
+    auto bias = [&](int i, float (&bv)[4]) {   // channels 64w + 16i + 4g .. +3 from the wave's LDS slot
+      const float4 b4 = *reinterpret_cast<const float4*>(smem + EC_BIAS + 256 * L.w + 64 * i + 16 * L.g);
       bv[0] = b4.x, bv[1] = b4.y, bv[2] = b4.z, bv[3] = b4.w;
     };
     const EcStore S(tid, row0);
@@ -346,10 +364,8 @@ __global__ __launch_bounds__(EC_NTH) void enc_chain_fwd_kernel(aw_enc_chain_fwd_
           float v[4], y[4], bv[4];
           bias(i, bv);
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            v[e] = acc[i][j][e] + bv[e];
-            y[e] = gelu_erf_fast(v[e]);
-          }
+          for (int e = 0; e < 4; ++e) v[e] = acc[i][j][e] + bv[e];
+          aw_gelu4(v, y);
           ec_lds_w8(smem, S.sw[i], ec_pack(v));
           ec_lds_w8(smem, nwb[i] + 16384 * j, ec_pack(y));
           __builtin_amdgcn_sched_barrier(0);   // one fragment at a time: bounded live ranges
@@ -381,8 +397,7 @@ __global__ __launch_bounds__(EC_NTH) void enc_chain_fwd_kernel(aw_enc_chain_fwd_
           for (int i = 0; i < 4; ++i) {
             float v[4], y[4];
             resid(i, j, v);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) y[e] = gelu_erf_fast(v[e]);
+            aw_gelu4(v, y);
             ec_lds_w8(smem, S.sw[i], xr[i][j]);
             ec_lds_w8(smem, nwb[i] + 16384 * j, ec_pack(y));
             __builtin_amdgcn_sched_barrier(0);   // one fragment at a time: bounded live ranges
@@ -433,6 +448,7 @@ __global__ __launch_bounds__(EC_NTH) void enc_chain_bwd_kernel(aw_enc_chain_bwd_
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __syncthreads();
+  ec_stagger(tid);
 
   for (int c = 0; c < NC; ++c) {
     const int r = R - 1 - (c >> 1);
@@ -464,10 +480,11 @@ __global__ __launch_bounds__(EC_NTH) void enc_chain_bwd_kernel(aw_enc_chain_bwd_
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          float pv[4], v[4];
+          float pv[4], v[4], ag[4];
           ec_unpack(pre[i][j], pv);
+          aw_gelu_grad4(pv, ag);
 #pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = aw_epi_mad(acc[i][j][e], gelu_erf_grad_fast(pv[e]), true, 0.f, false);
+          for (int e = 0; e < 4; ++e) v[e] = aw_epi_mad(acc[i][j][e], ag[e], true, 0.f, false);
           ec_lds_w8(smem, nwb[i] + 16384 * j, ec_pack(v));
           __builtin_amdgcn_sched_barrier(0);   // one fragment at a time: bounded live ranges
         }
@@ -477,11 +494,12 @@ __global__ __launch_bounds__(EC_NTH) void enc_chain_bwd_kernel(aw_enc_chain_bwd_
       // gx = gx' + (W1^T gh) * GELU'(x); go = gx * mask(block r - 1) (block r - 1's conv2 operand: the next operand
       // image) or, for r = 0, gx itself (the patch-embed weight-gradient operand, staged in the image)
       auto grad = [&](int i, int j, float (&v)[4]) {
-        float pv[4], gv[4];
+        float pv[4], gv[4], ag[4];
         ec_unpack(pre[i][j], pv);
         ec_unpack(gr[i][j], gv);
+        aw_gelu_grad4(pv, ag);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = aw_epi_mad(acc[i][j][e], gelu_erf_grad_fast(pv[e]), true, gv[e], true);
+        for (int e = 0; e < 4; ++e) v[e] = aw_epi_mad(acc[i][j][e], ag[e], true, gv[e], true);
         gr[i][j] = ec_pack(v);
       };
       if (r > 0) {
@@ -526,42 +544,56 @@ struct PackJobs {
   void* bwd[AW_ENC_PACK_MAX];
 };
 
-// blockIdx = (16-row block mb, job, kind): kind 0 packs W's rows 16 mb .. +15, kind 1 W's columns 16 mb .. +15
+// blockIdx = (64-row / 64-column group b, job, kind).  Both kinds stage through LDS so that the global reads and
+// writes are whole lines (the first form, one 16-row block per workgroup with 16-B accesses at 256-B to 1-KB
+// strides, took 28.7 us for the step's 16 matrices).
+//  kind 0: W's rows 64 b .. +63, 16 rows (one packed block row, 16 KB in and out) at a time: the packed block row is
+//          a permutation of the 16 rows' 16-B chunks;
+//  kind 1: W's columns 64 b .. +63 (512 rows x 128 B) -> the 4 packed block rows of W^T they make.
+constexpr int PK_PITCH0 = EC_ROWB + 16;   // kind 0 staging row pitch (conflict-free column-of-chunks reads)
+constexpr int PK_PITCH1 = 128 + 16;       // kind 1 staging row pitch
 __global__ __launch_bounds__(256) void enc_pack_kernel(PackJobs J) {
-  __shared__ uint16_t t[EC_H][16 + 2];
-  const int mb = blockIdx.x, job = blockIdx.y, tid = threadIdx.x;
-  const uint16_t* __restrict__ W = reinterpret_cast<const uint16_t*>(J.src[job]);
+  __shared__ __attribute__((aligned(16))) char t[EC_H * PK_PITCH1];
+  const int b = blockIdx.x, job = blockIdx.y, tid = threadIdx.x;
+  const char* __restrict__ W = reinterpret_cast<const char*>(J.src[job]);
   if (blockIdx.z == 0) {
     uint4* __restrict__ out = reinterpret_cast<uint4*>(J.fwd[job]);
     if (!out) return;
+    for (int mb = 4 * b; mb < 4 * b + 4; ++mb) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {   // 16 rows x 64 chunks of 8
-      const int c = tid + 256 * q, row = c >> 6, kc = c & 63;
-      const uint4 v = reinterpret_cast<const uint4*>(W + (size_t)(16 * mb + row) * EC_H)[kc];
-      out[(size_t)(mb * 16 + (kc >> 2)) * 64 + (kc & 3) * 16 + row] = v;
+      for (int q = 0; q < 4; ++q) {   // 16 rows x 64 chunks, row-major: coalesced
+        const int c = tid + 256 * q, row = c >> 6, kc = c & 63;
+        *reinterpret_cast<uint4*>(t + row * PK_PITCH0 + kc * 16) =
+            *reinterpret_cast<const uint4*>(W + (size_t)(16 * mb + row) * EC_ROWB + kc * 16);
+      }
+      __syncthreads();
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {   // output chunk o = (s, lane): row lane & 15, chunk 4s + (lane >> 4)
+        const int o = tid + 256 * q, st = o >> 6, l = o & 63;
+        out[(size_t)mb * 1024 + o] = *reinterpret_cast<const uint4*>(t + (l & 15) * PK_PITCH0 + (4 * st + (l >> 4)) * 16);
+      }
+      __syncthreads();
     }
   } else {
     uint4* __restrict__ out = reinterpret_cast<uint4*>(J.bwd[job]);
     if (!out) return;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {   // W[o][16 mb .. +15] for all 512 o: 512 x 32 B
-      const int c = tid + 256 * q, o = c >> 1, h = c & 1;
-      const uint4 v = reinterpret_cast<const uint4*>(W + (size_t)o * EC_H + 16 * mb)[h];
-      uint16_t e[8];
-      memcpy(e, &v, 16);
-#pragma unroll
-      for (int x = 0; x < 8; ++x) t[o][8 * h + x] = e[x];
+    for (int q = 0; q < 16; ++q) {    // W[o][64 b .. +63]: 512 rows x 8 chunks
+      const int c = tid + 256 * q, o = c >> 3, kc = c & 7;
+      *reinterpret_cast<uint4*>(t + o * PK_PITCH1 + kc * 16) =
+          *reinterpret_cast<const uint4*>(W + (size_t)o * EC_ROWB + 128 * b + kc * 16);
     }
     __syncthreads();
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {   // 16 blocks (s) x 64 lanes
-      const int c = tid + 256 * q, s = c >> 6, l = c & 63, li = l & 15, g = l >> 4;
+#pragma unroll 4
+    for (int q = 0; q < 16; ++q) {    // 4 block rows x 16 blocks x 64 lanes, in output order
+      const int o = tid + 256 * q, mb = o >> 10, st = (o >> 6) & 15, l = o & 63, li = l & 15, g = l >> 4;
       uint16_t e[8];
 #pragma unroll
-      for (int x = 0; x < 8; ++x) e[x] = t[32 * s + 8 * g + x][li];
+      for (int x = 0; x < 8; ++x)
+        e[x] = *reinterpret_cast<const uint16_t*>(t + (32 * st + 8 * g + x) * PK_PITCH1 + (16 * mb + li) * 2);
       uint4 v;
       memcpy(&v, e, 16);
-      out[(size_t)(mb * 16 + s) * 64 + l] = v;
+      out[(size_t)(4 * b + mb) * 1024 + (o & 1023)] = v;
     }
   }
 }
@@ -654,7 +686,7 @@ extern "C" int aw_enc_pack_weights(const void* const* src, void* const* fwd, voi
     J.fwd[i] = fwd[i];
     J.bwd[i] = bwd[i];
   }
-  hipLaunchKernelGGL(enc_pack_kernel, dim3(EC_H / 16, n, 2), dim3(256), 0, (hipStream_t)stream, J);
+  hipLaunchKernelGGL(enc_pack_kernel, dim3(EC_H / 64, n, 2), dim3(256), 0, (hipStream_t)stream, J);
   return aw::check_launch("aw_enc_pack_weights");
 }
 

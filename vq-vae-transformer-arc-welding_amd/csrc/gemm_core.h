@@ -790,7 +790,9 @@ __global__ __launch_bounds__(Cfg<BMT>::NTH, RAGGED ? 1 : Cfg<BMT>::MINB) void ge
         float ds[4] = {1.f, 1.f, 1.f, 1.f}, ds2[4] = {1.f, 1.f, 1.f, 1.f};
         if (f_drop) aw_dropout_scale4(dseed, e0, p.drop_p, ds);
         if (c2m == 3) aw_dropout_scale4(dseed2, e0, p.drop2_p, ds2);
-        float v[4], w[4];
+        float v[4], w[4], ag[4];
+        // bf16 operands: GELU and GELU' in packed pairs (aw_gelu4 / aw_gelu_grad4, shared with the encoder chain)
+        if (FASTGELU && f_pre && !f_tanh) aw_gelu_grad4(pv, ag);
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           float x = alpha * av[e] + bias[e];
@@ -799,7 +801,7 @@ __global__ __launch_bounds__(Cfg<BMT>::NTH, RAGGED ? 1 : Cfg<BMT>::MINB) void ge
           float m = 1.f;
           bool has_m = false;
           if (f_pre) {
-            const float a = f_tanh ? gelu_tanh_grad(pv[e]) : (FASTGELU ? gelu_erf_grad_fast(pv[e]) : gelu_erf_grad(pv[e]));
+            const float a = f_tanh ? gelu_tanh_grad(pv[e]) : (FASTGELU ? ag[e] : gelu_erf_grad(pv[e]));
             if (f_drop) x *= a;
             else m = a, has_m = true;
           }
@@ -808,7 +810,7 @@ __global__ __launch_bounds__(Cfg<BMT>::NTH, RAGGED ? 1 : Cfg<BMT>::MINB) void ge
           if (f_beta) x += p.beta * ov[e];
           v[e] = x;
           float y = x;
-          if (c2m == 1) y = f_tanh ? gelu_tanh(x) : (FASTGELU ? gelu_erf_fast(x) : gelu_erf(x));
+          if (c2m == 1 && (f_tanh || !FASTGELU)) y = f_tanh ? gelu_tanh(x) : gelu_erf(x);
           else if (c2m == 3) y = x * ds2[e];
           w[e] = y;
           if (f_stats && col + e < N) {
@@ -816,6 +818,7 @@ __global__ __launch_bounds__(Cfg<BMT>::NTH, RAGGED ? 1 : Cfg<BMT>::MINB) void ge
             csq[e] += x * x;
           }
         }
+        if (FASTGELU && c2m == 1 && !f_tanh) aw_gelu4(v, w);
         if (vec) {
           if (f_c) store4(Cptr, f_cbf, row * p.ldc + col, v, wt);
           if (c2m) store4(p.C2, f_c2bf, row * p.ldc2 + col, w, wt);
