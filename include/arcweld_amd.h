@@ -120,76 +120,85 @@ int aw_gemm_set_wgrad_policy(int mode);
 int64_t aw_wgrad_batch_workspace(const aw_gemm_args* args, int n);
 int aw_wgrad_batch(const aw_gemm_args* args, int n, void* ws, int64_t ws_bytes, void* stream);
 
-/* Fused encoder ResBlock chain, bf16 operands, H = 512, no BatchNorm (model/vq_vae_patch_embedd.py:60-74 through
- * CNNBlock(seperate=True) :103-110: every encoder conv sees a length-1 token slice, so it is its centre tap, a
- * [H][H] contraction per token, and token rows are independent through all R blocks).  One persistent launch of
- * N / 64 workgroups walks each 64-token row block through the 2R convs with its activations resident in LDS; it
+/* Fused ResBlock chain, bf16 operands, H = 512, no BatchNorm: the whole ResBlock stack of the encoder or of the
+ * decoder (model/vq_vae_patch_embedd.py:60-74 ResBlock, :103-110 CNNBlock) as ONE persistent launch of N / 64
+ * workgroups, each walking a 64-token row block through the 2R convs with its activations resident in LDS; it
  * replaces the 2R aw_gemm launches of either direction and produces the same tensors bit for bit.
- * Forward, per block r (x_0 = x0, a_0 = a0 = GELU(x_0)):
- *   h_r = W1_r a_r + b1_r,  a1_r = GELU(h_r),  x_{r+1} = x_r + Dropout(W2_r a1_r + b2_r; drop_seed[r], group
- *   row*H + c as aw_gemm's epilogue),  a_{r+1} = GELU(x_{r+1}) for r < R-1 and x_R for r = R-1.
+ *   taps = 1: the encoder (CNNBlock(seperate=True)): every conv sees a length-1 token slice, so it is its centre tap,
+ *             a [H][H] contraction per token; weights are [H][H] (packed).
+ *   taps = 3: the decoder (CNNBlock(seperate=False)): k = 3, padding 1 convs along windows of seg = 16 consecutive
+ *             rows (the rows of one welding window; rows outside the window read as zero, aw_gemm's implicit conv
+ *             with conv_seg = 16); weights are [H][3H] with column j*H + i = tap j, input channel i (packed).
+ * Forward, per block r (x_0 = x0, a_0 = a0 = GELU(x_0)), conv(W, v)[t] = sum_j W_j v[t + j - 1] (taps = 3) or W v[t]:
+ *   h_r = conv(W1_r, a_r) + b1_r,  a1_r = GELU(h_r),  x_{r+1} = x_r + Dropout(conv(W2_r, a1_r) + b2_r; drop_seed[r],
+ *   group row*H + c as aw_gemm's epilogue),  a_{r+1} = GELU(x_{r+1}) for r < R-1 and x_R for r = R-1.
  *   Stored: h[r] = h_r, a1[r] = a1_r, x[r] = x_{r+1} (r < R-1), a[r] = a_{r+1}; h / a1 / x may be NULL (not stored:
- *   eval forwards).  Weights w1 / w2 are the forward copies of aw_enc_pack_weights (W packed), biases f32.
- * Backward, per block r = R-1 .. 0, from gx = dL/dx_R (bf16) and gxo = gx * mask_{R-1} (bf16):
- *   gh_r = (W2_r^T go_r) * GELU'(h_r),  gx_r = gx_{r+1} + (W1_r^T gh_r) * GELU'(x_r),
+ *   eval forwards).  Weights w1 / w2 are the forward copies of aw_res_pack_weights, biases f32.  With drop_p > 0
+ *   and drop_masks != NULL the launch also writes the keep bits of every block there (aw_res_dropout_masks_bytes;
+ *   the masks aw_res_dropout_masks makes), for the backward.
+ * Backward, per block r = R-1 .. 0, from gx = dL/dx_R (bf16) and gxo = gx * mask_{R-1} (bf16), with
+ * convT(W, v)[t] = sum_j W_j^T v[t - j + 1] (taps = 3) or W^T v[t]:
+ *   gh_r = convT(W2_r, go_r) * GELU'(h_r),  gx_r = gx_{r+1} + convT(W1_r, gh_r) * GELU'(x_r),
  *   gxo_out[r] = gx_r * mask_{r-1} (r > 0: block r-1's conv2 operand) or gx_0 (r = 0); gh[r] = gh_r.
- *   w1t / w2t are the backward copies of aw_enc_pack_weights (W^T packed); h / x are the forward's saved tensors
- *   with x[0] = x_0 and x[r] = the forward's x[r-1].
- * All activations are [N][H] bf16 with row stride H, 16-B aligned; N * H * 2 < 2^31; 1 <= R <= AW_ENC_CHAIN_MAX.
- * Dropout (drop_p > 0): drop_masks holds the keep bits of every block (aw_enc_dropout_masks with the same N, R,
- * drop_p, drop_seed and seed_ptr -- the masks aw_gemm's epilogue draws for the same seeds); drop_seed / seed_ptr
- * are informational here.  store_policy AW_STORE_WT (sc1) or AW_STORE_NT for every global store. */
-#define AW_ENC_CHAIN_MAX 16
+ *   w1t / w2t are the backward copies of aw_res_pack_weights; h / x are the forward's saved tensors with x[0] = x_0
+ *   and x[r] = the forward's x[r-1]; drop_masks (drop_p > 0) = what the forward wrote.
+ * All activations are [N][H] bf16 with row stride H, 16-B aligned; N * H * 2 < 2^31; 1 <= R <= AW_RES_CHAIN_MAX;
+ * taps = 3 needs seg = 16 and N % 16 == 0.  drop_seed / seed_ptr select the masks (forward); store_policy AW_STORE_WT
+ * (sc1) or AW_STORE_NT for every global store. */
+#define AW_RES_CHAIN_MAX 16
 typedef struct {
   int64_t N;
   int H, R;
+  int taps, seg;
   const void* a0;
   const void* x0;
-  const void* w1[AW_ENC_CHAIN_MAX];
-  const void* w2[AW_ENC_CHAIN_MAX];
-  const float* b1[AW_ENC_CHAIN_MAX];
-  const float* b2[AW_ENC_CHAIN_MAX];
-  void* h[AW_ENC_CHAIN_MAX];
-  void* a1[AW_ENC_CHAIN_MAX];
-  void* x[AW_ENC_CHAIN_MAX];
-  void* a[AW_ENC_CHAIN_MAX];
+  const void* w1[AW_RES_CHAIN_MAX];
+  const void* w2[AW_RES_CHAIN_MAX];
+  const float* b1[AW_RES_CHAIN_MAX];
+  const float* b2[AW_RES_CHAIN_MAX];
+  void* h[AW_RES_CHAIN_MAX];
+  void* a1[AW_RES_CHAIN_MAX];
+  void* x[AW_RES_CHAIN_MAX];
+  void* a[AW_RES_CHAIN_MAX];
   float drop_p;
-  uint64_t drop_seed[AW_ENC_CHAIN_MAX];
+  uint64_t drop_seed[AW_RES_CHAIN_MAX];
   const uint64_t* seed_ptr;
   int store_policy;
-  const uint64_t* drop_masks;
-} aw_enc_chain_fwd_args;
+  uint64_t* drop_masks;
+} aw_res_chain_fwd_args;
 typedef struct {
   int64_t N;
   int H, R;
+  int taps, seg;
   const void* gx;
   const void* gxo;
-  const void* w1t[AW_ENC_CHAIN_MAX];
-  const void* w2t[AW_ENC_CHAIN_MAX];
-  const void* h[AW_ENC_CHAIN_MAX];
-  const void* x[AW_ENC_CHAIN_MAX];
-  void* gh[AW_ENC_CHAIN_MAX];
-  void* gxo_out[AW_ENC_CHAIN_MAX];
+  const void* w1t[AW_RES_CHAIN_MAX];
+  const void* w2t[AW_RES_CHAIN_MAX];
+  const void* h[AW_RES_CHAIN_MAX];
+  const void* x[AW_RES_CHAIN_MAX];
+  void* gh[AW_RES_CHAIN_MAX];
+  void* gxo_out[AW_RES_CHAIN_MAX];
   float drop_p;
-  uint64_t drop_seed[AW_ENC_CHAIN_MAX];
-  const uint64_t* seed_ptr;
   int store_policy;
   const uint64_t* drop_masks;
-} aw_enc_chain_bwd_args;
-int aw_enc_chain_fwd(const aw_enc_chain_fwd_args* args, void* stream);
-int aw_enc_chain_bwd(const aw_enc_chain_bwd_args* args, void* stream);
-/* The chain's dropout keep bits for R blocks at N tokens: aw_enc_dropout_masks_bytes(N, R) bytes (16-B aligned), one
+} aw_res_chain_bwd_args;
+int aw_res_chain_fwd(const aw_res_chain_fwd_args* args, void* stream);
+int aw_res_chain_bwd(const aw_res_chain_bwd_args* args, void* stream);
+/* The chain's dropout keep bits for R blocks at N tokens: aw_res_dropout_masks_bytes(N, R) bytes (16-B aligned), one
  * 64-bit word per chain thread and block (block r's mask: the keep decision of aw_gemm's dropout epilogue with seed
- * drop_seed[r] mixed with *seed_ptr, on element row * 512 + c).  Made once per step, read by both directions. */
-int64_t aw_enc_dropout_masks_bytes(int64_t N, int R);
-int aw_enc_dropout_masks(int64_t N, int R, float drop_p, const uint64_t* drop_seed, const uint64_t* seed_ptr,
+ * drop_seed[r] mixed with *seed_ptr, on element row * 512 + c).  aw_res_chain_fwd writes the same words itself;
+ * this standalone form serves a backward without a chain forward (and the tests). */
+int64_t aw_res_dropout_masks_bytes(int64_t N, int R);
+int aw_res_dropout_masks(int64_t N, int R, float drop_p, const uint64_t* drop_seed, const uint64_t* seed_ptr,
                          void* masks, void* stream);
-/* Fragment-packed weight copies of the chain (n <= AW_ENC_PACK_MAX [512][512] bf16 [out][in] matrices src[i]):
- * fwd[i] packs A = W, bwd[i] packs A = W^T (either may be NULL).  Packed layout of A (row m, k): the 1-KB block
- * (m / 16, k / 32) at byte ((m / 16) * 16 + k / 32) * 1024 holds lane l = (m % 16) + 16 ((k % 32) / 8) at 16 l,
- * element k % 8 within -- one MFMA A-fragment, so a wave reads each fragment as one contiguous KB. */
-#define AW_ENC_PACK_MAX 32
-int aw_enc_pack_weights(const void* const* src, void* const* fwd, void* const* bwd, int n, void* stream);
+/* Fragment-packed weight copies of the chain: n <= AW_RES_PACK_MAX bf16 matrices src[i] = W of shape
+ * [512][taps * 512] ([out][(tap, in)], the forward operand layout; taps 1 or 3).  fwd[i] packs A = W, bwd[i] packs
+ * the backward operand A[i][(j, o)] = W[o][j * 512 + i] (W^T for taps = 1); either may be NULL.  Packed layout of a
+ * [512][K] A (row m, column k): the 1-KB block (m / 16, k / 32) at byte ((m / 16) * (K / 32) + k / 32) * 1024 holds
+ * lane l = (m % 16) + 16 ((k % 32) / 8) at 16 l, element k % 8 within -- one MFMA A-fragment, so a wave reads each
+ * fragment as one contiguous KB. */
+#define AW_RES_PACK_MAX 32
+int aw_res_pack_weights(const void* const* src, void* const* fwd, void* const* bwd, int n, int taps, void* stream);
 
 /* -------------------------------------------------------------------------------- vector quantizer
  * VectorQuantizer.forward (model/vector_quantizer.py:76-119), fp32, codebook staged in LDS, no MFMA:

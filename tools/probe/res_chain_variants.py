@@ -1,7 +1,7 @@
-"""Probe builds of csrc/encchain.hip (EC_PROBE_FLAGS, see the top of that file): the chain kernels alone at the
+"""Probe builds of csrc/reschain.hip (EC_PROBE_FLAGS, see the top of that file): the chain kernels alone at the
 configs[1] shape with parts left out, and per-conv s_memtime stamps.  Results of the probe builds are garbage by
-construction.  Build on the CPU first:  python tools/probe/enc_chain_variants.py build
-usage on the GPU box: python tools/probe/enc_chain_variants.py [iters]"""
+construction.  Build on the CPU first:  python tools/probe/res_chain_variants.py build
+usage on the GPU box: python tools/probe/res_chain_variants.py [iters] [taps]   (taps 1: encoder, 3: decoder)"""
 import ctypes
 import os
 import subprocess
@@ -20,13 +20,13 @@ def build():
         out = os.path.join(HERE, "build", f"ec_{name}.so")
         procs.append(subprocess.Popen(
             ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-fPIC", "-shared", "-std=c++17", "-Wl,-Bsymbolic",
-             f"-DEC_PROBE_FLAGS={fl}", "-I" + os.path.join(REPO, "include"), os.path.join(SRC, "encchain.hip"),
+             f"-DEC_PROBE_FLAGS={fl}", "-I" + os.path.join(REPO, "include"), os.path.join(SRC, "reschain.hip"),
              os.path.join(SRC, "runtime.hip"), "-o", out]))
     for p in procs:
         assert p.wait() == 0
 
 
-def main(iters=20):
+def main(iters=20, taps=1):
     import torch
     sys.path.insert(0, os.path.join(REPO, "vq-vae-transformer-arc-welding_amd"))
     from arcweld import _native as nat
@@ -36,8 +36,8 @@ def main(iters=20):
     rnd = lambda *s, sc=1.0, dt=BF: (torch.randn(*s, device="cuda", generator=g) * sc).to(dt)  # noqa: E731
     e = lambda: torch.empty(N, H, device="cuda", dtype=BF)  # noqa: E731
     keep = []
-    fa = nat.EncChainFwdArgs()
-    fa.N, fa.H, fa.R, fa.drop_p = N, H, R, p
+    fa = nat.ResChainFwdArgs()
+    fa.N, fa.H, fa.R, fa.drop_p, fa.taps, fa.seg = N, H, R, p, taps, 16
     a0, x0 = rnd(N, H), rnd(N, H)
     keep += [a0, x0]
     fa.a0, fa.x0 = a0.data_ptr(), x0.data_ptr()
@@ -45,15 +45,16 @@ def main(iters=20):
     keep.append(ctr)
     fa.seed_ptr = ctr.data_ptr()
     fa.store_policy = 1
-    ba = nat.EncChainBwdArgs()
-    ba.N, ba.H, ba.R, ba.drop_p, ba.seed_ptr, ba.store_policy = N, H, R, p, ctr.data_ptr(), 1
+    ba = nat.ResChainBwdArgs()
+    ba.N, ba.H, ba.R, ba.drop_p, ba.store_policy, ba.taps, ba.seg = N, H, R, p, 1, taps, 16
+    TH = taps * H
     gx, gxo = rnd(N, H, sc=0.01), rnd(N, H, sc=0.01)
     keep += [gx, gxo]
     ba.gx, ba.gxo = gx.data_ptr(), gxo.data_ptr()
     for r in range(R):
-        ts = [rnd(H, H, sc=H ** -0.5), rnd(H, H, sc=H ** -0.5), rnd(H, sc=0.1, dt=torch.float32),
-              rnd(H, sc=0.1, dt=torch.float32), e(), e(), e(), e(), rnd(H, H, sc=H ** -0.5), rnd(H, H, sc=H ** -0.5),
-              e(), e()]
+        ts = [rnd(H, TH, sc=TH ** -0.5), rnd(H, TH, sc=TH ** -0.5), rnd(H, sc=0.1, dt=torch.float32),
+              rnd(H, sc=0.1, dt=torch.float32), e(), e(), e(), e(), rnd(H, TH, sc=TH ** -0.5),
+              rnd(H, TH, sc=TH ** -0.5), e(), e()]
         keep += ts
         fa.w1[r], fa.w2[r], fa.b1[r], fa.b2[r] = (t.data_ptr() for t in ts[:4])
         fa.h[r], fa.a1[r], fa.a[r] = ts[4].data_ptr(), ts[5].data_ptr(), ts[7].data_ptr()
@@ -62,23 +63,22 @@ def main(iters=20):
         ba.w1t[r], ba.w2t[r] = ts[8].data_ptr(), ts[9].data_ptr()
         ba.h[r], ba.x[r], ba.gh[r], ba.gxo_out[r] = ts[4].data_ptr(), ts[6].data_ptr(), ts[10].data_ptr(), \
             ts[11].data_ptr()
-        ba.drop_seed[r] = r + 1
     s = torch.cuda.current_stream().cuda_stream
     masks = torch.empty(R * (N // 64) * 512 * 8, device="cuda", dtype=torch.uint8)
     keep.append(masks)
     fa.drop_masks = ba.drop_masks = masks.data_ptr()
     pol = int(os.environ.get("EC_STORE_POLICY", "0"))
     fa.store_policy = ba.store_policy = pol
-    print(f"store policy {'WT (sc1)' if pol else 'NT'}")
+    print(f"taps {taps}, store policy {'WT (sc1)' if pol else 'NT'}")
     for name in VARIANTS:
         lib = ctypes.CDLL(os.path.join(HERE, "build", f"ec_{name}.so"))
-        for fn in (lib.aw_enc_chain_fwd, lib.aw_enc_chain_bwd):
+        for fn in (lib.aw_res_chain_fwd, lib.aw_res_chain_bwd):
             fn.restype = ctypes.c_int
         sd = (ctypes.c_uint64 * R)(*range(1, R + 1))
-        assert lib.aw_enc_dropout_masks(ctypes.c_int64(N), R, ctypes.c_float(p), sd, ctypes.c_void_p(ctr.data_ptr()),
+        assert lib.aw_res_dropout_masks(ctypes.c_int64(N), R, ctypes.c_float(p), sd, ctypes.c_void_p(ctr.data_ptr()),
                                         ctypes.c_void_p(masks.data_ptr()), ctypes.c_void_p(s)) == 0
         res = []
-        for fn, args in ((lib.aw_enc_chain_fwd, fa), (lib.aw_enc_chain_bwd, ba)):
+        for fn, args in ((lib.aw_res_chain_fwd, fa), (lib.aw_res_chain_bwd, ba)):
             for _ in range(3):
                 assert fn(ctypes.byref(args), ctypes.c_void_p(s)) == 0
             torch.cuda.synchronize()

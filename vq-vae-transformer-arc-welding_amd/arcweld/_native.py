@@ -67,27 +67,26 @@ class OperandDesc(ctypes.Structure):
 
 OPS_PER_SEG = 2     # AW_OPS_PER_SEG
 
-ENC_CHAIN_MAX = 16  # AW_ENC_CHAIN_MAX
-ENC_PACK_MAX = 32   # AW_ENC_PACK_MAX
-_E = ENC_CHAIN_MAX
+RES_CHAIN_MAX = 16  # AW_RES_CHAIN_MAX
+RES_PACK_MAX = 32   # AW_RES_PACK_MAX
+_E = RES_CHAIN_MAX
 
 
-class EncChainFwdArgs(ctypes.Structure):
-    """aw_enc_chain_fwd_args (include/arcweld_amd.h)."""
-    _fields_ = [("N", c_i64), ("H", c_int), ("R", c_int), ("a0", c_p), ("x0", c_p),
+class ResChainFwdArgs(ctypes.Structure):
+    """aw_res_chain_fwd_args (include/arcweld_amd.h)."""
+    _fields_ = [("N", c_i64), ("H", c_int), ("R", c_int), ("taps", c_int), ("seg", c_int), ("a0", c_p), ("x0", c_p),
                 ("w1", c_p * _E), ("w2", c_p * _E), ("b1", c_p * _E), ("b2", c_p * _E),
                 ("h", c_p * _E), ("a1", c_p * _E), ("x", c_p * _E), ("a", c_p * _E),
                 ("drop_p", c_f), ("drop_seed", ctypes.c_uint64 * _E), ("seed_ptr", c_p), ("store_policy", c_int),
                 ("drop_masks", c_p)]
 
 
-class EncChainBwdArgs(ctypes.Structure):
-    """aw_enc_chain_bwd_args (include/arcweld_amd.h)."""
-    _fields_ = [("N", c_i64), ("H", c_int), ("R", c_int), ("gx", c_p), ("gxo", c_p),
+class ResChainBwdArgs(ctypes.Structure):
+    """aw_res_chain_bwd_args (include/arcweld_amd.h)."""
+    _fields_ = [("N", c_i64), ("H", c_int), ("R", c_int), ("taps", c_int), ("seg", c_int), ("gx", c_p), ("gxo", c_p),
                 ("w1t", c_p * _E), ("w2t", c_p * _E), ("h", c_p * _E), ("x", c_p * _E),
                 ("gh", c_p * _E), ("gxo_out", c_p * _E),
-                ("drop_p", c_f), ("drop_seed", ctypes.c_uint64 * _E), ("seed_ptr", c_p), ("store_policy", c_int),
-                ("drop_masks", c_p)]
+                ("drop_p", c_f), ("store_policy", c_int), ("drop_masks", c_p)]
 
 # name -> argtypes (every entry returns int status except aw_last_error)
 SIGNATURES = {
@@ -100,11 +99,11 @@ SIGNATURES = {
     "aw_gemm_set_wgrad_policy": [c_int],
     "aw_wgrad_batch_workspace": [ctypes.POINTER(GemmArgs), c_int],
     "aw_wgrad_batch": [ctypes.POINTER(GemmArgs), c_int, c_p, c_i64, c_p],
-    "aw_enc_chain_fwd": [ctypes.POINTER(EncChainFwdArgs), c_p],
-    "aw_enc_chain_bwd": [ctypes.POINTER(EncChainBwdArgs), c_p],
-    "aw_enc_pack_weights": [ctypes.POINTER(c_p), ctypes.POINTER(c_p), ctypes.POINTER(c_p), c_int, c_p],
-    "aw_enc_dropout_masks_bytes": [c_i64, c_int],
-    "aw_enc_dropout_masks": [c_i64, c_int, c_f, ctypes.POINTER(ctypes.c_uint64), c_p, c_p, c_p],
+    "aw_res_chain_fwd": [ctypes.POINTER(ResChainFwdArgs), c_p],
+    "aw_res_chain_bwd": [ctypes.POINTER(ResChainBwdArgs), c_p],
+    "aw_res_pack_weights": [ctypes.POINTER(c_p), ctypes.POINTER(c_p), ctypes.POINTER(c_p), c_int, c_int, c_p],
+    "aw_res_dropout_masks_bytes": [c_i64, c_int],
+    "aw_res_dropout_masks": [c_i64, c_int, c_f, ctypes.POINTER(ctypes.c_uint64), c_p, c_p, c_p],
     "aw_weight_relayout_batch": [ctypes.POINTER(RelayoutJob), c_int, c_int, c_p],
     "aw_vq_forward": [c_p, c_p, c_i64, c_int, c_int, c_p, c_p, c_p, c_p, c_p],
     "aw_vq_forward_ex": [c_p, c_p, c_i64, c_int, c_int, c_p, c_p, c_p, c_p, c_p, c_int, c_p],
@@ -170,7 +169,7 @@ SIGNATURES = {
     "aw_rvq_backward": [c_p, c_p, c_p, c_p, c_int, c_i64, c_int, c_f, c_p, c_p],
 }
 
-RET_I64 = {"aw_gemm_workspace", "aw_wgrad_batch_workspace", "aw_enc_dropout_masks_bytes"}
+RET_I64 = {"aw_gemm_workspace", "aw_wgrad_batch_workspace", "aw_res_dropout_masks_bytes"}
 
 _lib = None
 

@@ -224,24 +224,26 @@ def wgrad_issue(problems, stream=None):
 
 
 # ------------------------------------------------------------------------------------------------ encoder chain
-ENC_CHAIN_MAX = nat.ENC_CHAIN_MAX
+RES_CHAIN_MAX = nat.RES_CHAIN_MAX
 
 
-def enc_chain_ok(H, R, T, RT):
-    """aw_enc_chain_fwd / _bwd serve the bf16 operand mode with bf16 residual streams, H == 512 and 1 <= R <= 16
-    (the per-token encoder ResBlocks without BatchNorm).  ARCWELD_ENC_CHAIN=0 keeps the per-conv GEMM launches
-    (A/B runs, and the tests that compare the two)."""
+def res_chain_ok(H, R, T, RT, taps=1, seg=16, which="ENC"):
+    """aw_res_chain_fwd / _bwd serve the bf16 operand mode with bf16 residual streams, H == 512 and 1 <= R <= 16
+    (ResBlocks without BatchNorm): the encoder's per-token stack (taps 1) and the decoder's k = 3 stack over 16-token
+    windows (taps 3, seg 16).  ARCWELD_ENC_CHAIN=0 / ARCWELD_DEC_CHAIN=0 keep the per-conv GEMM launches of that
+    stack (A/B runs, and the tests that compare the two)."""
     import os
-    if os.environ.get("ARCWELD_ENC_CHAIN", "1") == "0":
+    if os.environ.get(f"ARCWELD_{which}_CHAIN", "1") == "0":
         return False
-    return H == 512 and 1 <= R <= ENC_CHAIN_MAX and T == torch.bfloat16 and RT == torch.bfloat16
+    return (H == 512 and 1 <= R <= RES_CHAIN_MAX and T == torch.bfloat16 and RT == torch.bfloat16
+            and (taps == 1 or (taps == 3 and seg == 16)))
 
 
 def _chain_store_policy():
-    """The chain's store policy: non-temporal (ARCWELD_ENC_CHAIN_STORE=wt: write-through, for A/B runs).  Same-box
+    """The chain's store policy: non-temporal (ARCWELD_CHAIN_STORE=wt: write-through, for A/B runs).  Same-box
     A/B of the VQ-VAE step: 2.932 / 2.914 ms nt vs 2.971 / 2.959 ms wt (the GEMM launches it replaces use wt)."""
     import os
-    return nat.AW_STORE_WT if os.environ.get("ARCWELD_ENC_CHAIN_STORE", "nt") == "wt" else nat.AW_STORE_NT
+    return nat.AW_STORE_WT if os.environ.get("ARCWELD_CHAIN_STORE", "nt") == "wt" else nat.AW_STORE_NT
 
 
 def _chk_rows(ts, N, H, who):
@@ -252,36 +254,49 @@ def _chk_rows(ts, N, H, who):
             raise nat.NativeError(f"{who}: activations must be contiguous ({N}, {H}) bfloat16 tensors")
 
 
-def enc_dropout_masks(N, drop, seed_ptr=None, stream=None):
-    """The chain's dropout keep bits for drop = (p, R seeds) at N tokens (aw_enc_dropout_masks): a uint8 device
-    tensor to pass to enc_chain_fwd / enc_chain_bwd, or None when p == 0."""
+def res_dropout_masks_empty(N, R, device):
+    """An uninitialised buffer for the chain's dropout keep bits of R blocks at N tokens (res_chain_fwd fills it)."""
+    nb = nat.load().aw_res_dropout_masks_bytes(int(N), int(R))
+    if nb <= 0:
+        raise nat.NativeError("res_dropout_masks: bad N / R")
+    return torch.empty(nb, device=device, dtype=torch.uint8)
+
+
+def res_dropout_masks(N, drop, seed_ptr=None, stream=None):
+    """The chain's dropout keep bits for drop = (p, R seeds) at N tokens (aw_res_dropout_masks, the standalone form of
+    what res_chain_fwd writes): a uint8 device tensor, or None when p == 0."""
     p, seeds = float(drop[0]), list(drop[1] or [])
     if p <= 0.0:
         return None
     R = len(seeds)
-    nb = nat.load().aw_enc_dropout_masks_bytes(int(N), R)
-    if nb <= 0:
-        raise nat.NativeError("enc_dropout_masks: bad N / R")
-    out = torch.empty(nb, device=torch.cuda.current_device() if seed_ptr is None else seed_ptr.device,
-                      dtype=torch.uint8)
+    out = res_dropout_masks_empty(N, R, torch.cuda.current_device() if seed_ptr is None else seed_ptr.device)
     sd = (ctypes.c_uint64 * R)(*[int(v) & 0xFFFFFFFFFFFFFFFF for v in seeds])
-    call("aw_enc_dropout_masks", int(N), R, p, sd, ptr(seed_ptr), ptr(out), stream_ptr(stream))
+    call("aw_res_dropout_masks", int(N), R, p, sd, ptr(seed_ptr), ptr(out), stream_ptr(stream))
     return out
 
 
-def enc_chain_fwd(a0, x0, w1, w2, b1, b2, h, a1, x, a, drop=(0.0, None), seed_ptr=None, masks=None, stream=None):
-    """One aw_enc_chain_fwd launch over the R = len(w1) encoder ResBlocks (see include/arcweld_amd.h).
+def _chain_flops(R, N, H, taps, seg):
+    """Algorithmic flops of one chain launch: 2R convs of 2 N H (taps H) -- for taps 3 only the taps that touch a
+    real row (the window edges lose one tap each, as _algorithmic_flops counts the implicit conv GEMMs)."""
+    if taps == 1:
+        return 4.0 * R * N * H * H
+    return 4.0 * R * N * H * H * (3 - 2.0 / seg)
 
-    a0 / x0: (N, H) bf16; w1 / w2: R packed weight copies (enc_pack_weights); b1 / b2: R f32 biases; h / a1 / x / a: R output
-    tensors each (h, a1, x entries may be None: not stored; x[R-1] is never stored); drop = (p, R seeds); masks =
-    enc_dropout_masks(N, drop, seed_ptr) (made here when None and p > 0)."""
+
+def res_chain_fwd(a0, x0, w1, w2, b1, b2, h, a1, x, a, drop=(0.0, None), seed_ptr=None, masks=None, taps=1, seg=16,
+                  stream=None):
+    """One aw_res_chain_fwd launch over the R = len(w1) ResBlocks (see include/arcweld_amd.h).
+
+    a0 / x0: (N, H) bf16; w1 / w2: R packed weight copies (res_pack_weights); b1 / b2: R f32 biases; h / a1 / x / a: R
+    output tensors each (h, a1, x entries may be None: not stored; x[R-1] is never stored); drop = (p, R seeds); masks:
+    None or a res_dropout_masks_empty(N, R) buffer the launch fills with the keep bits (for res_chain_bwd)."""
     N, H = a0.shape
     R = len(w1)
-    if not (1 <= R <= ENC_CHAIN_MAX) or not all(len(v) == R for v in (w2, b1, b2, h, a1, x, a)):
-        raise nat.NativeError("enc_chain_fwd: need R (1..16) entries in every per-block list")
-    _chk_rows([a0, x0] + list(h) + list(a1) + list(x) + list(a), N, H, "enc_chain_fwd")
-    g = nat.EncChainFwdArgs()
-    g.N, g.H, g.R = N, H, R
+    if not (1 <= R <= RES_CHAIN_MAX) or not all(len(v) == R for v in (w2, b1, b2, h, a1, x, a)):
+        raise nat.NativeError("res_chain_fwd: need R (1..16) entries in every per-block list")
+    _chk_rows([a0, x0] + list(h) + list(a1) + list(x) + list(a), N, H, "res_chain_fwd")
+    g = nat.ResChainFwdArgs()
+    g.N, g.H, g.R, g.taps, g.seg = N, H, R, int(taps), int(seg)
     g.a0, g.x0 = ptr(a0), ptr(x0)
     for r in range(R):
         g.w1[r], g.w2[r], g.b1[r], g.b2[r] = ptr(w1[r]), ptr(w2[r]), ptr(b1[r]), ptr(b2[r])
@@ -290,53 +305,50 @@ def enc_chain_fwd(a0, x0, w1, w2, b1, b2, h, a1, x, a, drop=(0.0, None), seed_pt
     g.drop_p = float(drop[0])
     g.seed_ptr = ptr(seed_ptr)
     g.store_policy = _chain_store_policy()
-    if g.drop_p > 0 and masks is None:
-        masks = enc_dropout_masks(N, drop, seed_ptr, stream)
     g.drop_masks = ptr(masks)
-    _maybe_timed(stream, "gemm_bf16", 4.0 * R * N * H * H, lambda sp: call("aw_enc_chain_fwd", ctypes.byref(g), sp))
+    _maybe_timed(stream, "gemm_bf16", _chain_flops(R, N, H, taps, seg),
+                 lambda sp: call("aw_res_chain_fwd", ctypes.byref(g), sp))
 
 
-def enc_chain_bwd(gx, gxo, w1t, w2t, h, x, gh, gxo_out, drop=(0.0, None), seed_ptr=None, masks=None, stream=None):
-    """One aw_enc_chain_bwd launch (see include/arcweld_amd.h): w1t / w2t are the packed W^T copies, h / x
-    the forward's saved pre-activations and residual streams (x[0] = x_0), gh / gxo_out the R outputs each."""
+def res_chain_bwd(gx, gxo, w1t, w2t, h, x, gh, gxo_out, drop_p=0.0, masks=None, taps=1, seg=16, stream=None):
+    """One aw_res_chain_bwd launch (see include/arcweld_amd.h): w1t / w2t are the packed backward copies, h / x
+    the forward's saved pre-activations and residual streams (x[0] = x_0), gh / gxo_out the R outputs each; masks
+    (drop_p > 0, R > 1): the keep bits res_chain_fwd wrote (or res_dropout_masks made)."""
     N, H = gx.shape
     R = len(w1t)
-    if not (1 <= R <= ENC_CHAIN_MAX) or not all(len(v) == R for v in (w2t, h, x, gh, gxo_out)):
-        raise nat.NativeError("enc_chain_bwd: need R (1..16) entries in every per-block list")
-    _chk_rows([gx, gxo] + list(h) + list(x) + list(gh) + list(gxo_out), N, H, "enc_chain_bwd")
-    g = nat.EncChainBwdArgs()
-    g.N, g.H, g.R = N, H, R
+    if not (1 <= R <= RES_CHAIN_MAX) or not all(len(v) == R for v in (w2t, h, x, gh, gxo_out)):
+        raise nat.NativeError("res_chain_bwd: need R (1..16) entries in every per-block list")
+    _chk_rows([gx, gxo] + list(h) + list(x) + list(gh) + list(gxo_out), N, H, "res_chain_bwd")
+    g = nat.ResChainBwdArgs()
+    g.N, g.H, g.R, g.taps, g.seg = N, H, R, int(taps), int(seg)
     g.gx, g.gxo = ptr(gx), ptr(gxo)
     for r in range(R):
         g.w1t[r], g.w2t[r], g.h[r], g.x[r] = ptr(w1t[r]), ptr(w2t[r]), ptr(h[r]), ptr(x[r])
         g.gh[r], g.gxo_out[r] = ptr(gh[r]), ptr(gxo_out[r])
-        g.drop_seed[r] = int(drop[1][r]) & 0xFFFFFFFFFFFFFFFF if drop[0] > 0 else 0
-    g.drop_p = float(drop[0])
-    g.seed_ptr = ptr(seed_ptr)
+    g.drop_p = float(drop_p)
     g.store_policy = _chain_store_policy()
-    if g.drop_p > 0 and masks is None:
-        masks = enc_dropout_masks(N, drop, seed_ptr, stream)
     g.drop_masks = ptr(masks)
-    _maybe_timed(stream, "gemm_bf16", 4.0 * R * N * H * H, lambda sp: call("aw_enc_chain_bwd", ctypes.byref(g), sp))
+    _maybe_timed(stream, "gemm_bf16", _chain_flops(R, N, H, taps, seg),
+                 lambda sp: call("aw_res_chain_bwd", ctypes.byref(g), sp))
 
 
-def enc_pack_weights(src, fwd=None, bwd=None, stream=None):
-    """Fragment-packed copies of [512][512] bf16 [out][in] weights for the encoder chain (aw_enc_pack_weights):
-    fwd[i] <- W packed (aw_enc_chain_fwd's w1 / w2), bwd[i] <- W^T packed (aw_enc_chain_bwd's w1t / w2t); either list
-    may be None.  One launch per 32 matrices."""
+def res_pack_weights(src, fwd=None, bwd=None, taps=1, stream=None):
+    """Fragment-packed copies of [512][taps*512] bf16 [out][(tap, in)] weights for the chain (aw_res_pack_weights):
+    fwd[i] <- W packed (aw_res_chain_fwd's w1 / w2), bwd[i] <- the backward operand packed (aw_res_chain_bwd's w1t /
+    w2t); either list may be None.  One launch per 32 matrices."""
     n = len(src)
     fwd = fwd if fwd is not None else [None] * n
     bwd = bwd if bwd is not None else [None] * n
     if len(fwd) != n or len(bwd) != n:
-        raise nat.NativeError("enc_pack_weights: list lengths differ")
+        raise nat.NativeError("res_pack_weights: list lengths differ")
     for t in list(src) + [t for t in fwd + bwd if t is not None]:
-        if t.dtype != torch.bfloat16 or tuple(t.shape) != (512, 512) or not t.is_contiguous():
-            raise nat.NativeError("enc_pack_weights: need contiguous (512, 512) bfloat16 tensors")
-    for c0 in range(0, n, nat.ENC_PACK_MAX):
-        sl = slice(c0, c0 + nat.ENC_PACK_MAX)
+        if t.dtype != torch.bfloat16 or t.numel() != 512 * 512 * taps or not t.is_contiguous():
+            raise nat.NativeError(f"res_pack_weights: need contiguous 512 x {512 * taps} bfloat16 tensors")
+    for c0 in range(0, n, nat.RES_PACK_MAX):
+        sl = slice(c0, c0 + nat.RES_PACK_MAX)
         m = len(src[sl])
         arr = lambda ts: (ctypes.c_void_p * m)(*[ptr(t) for t in ts])  # noqa: E731
-        call("aw_enc_pack_weights", arr(src[sl]), arr(fwd[sl]), arr(bwd[sl]), m, stream_ptr(stream))
+        call("aw_res_pack_weights", arr(src[sl]), arr(fwd[sl]), arr(bwd[sl]), m, int(taps), stream_ptr(stream))
 
 
 # ------------------------------------------------------------------------------------------------ VQ

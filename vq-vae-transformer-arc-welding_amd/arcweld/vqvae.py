@@ -256,6 +256,54 @@ def _bn_block_bwd(gy, x, a0, bs, w1d, w2d, Kd, dgemm_kw, wg, c1, c2, bns, G, tra
     return gx, gxo
 
 
+def _chain_fwd(ws, convs, a0, x0, N, H, T, RT, p_drop, seeds, ctr, need_backward, taps, seg):
+    """Forward of a ResBlock stack through aw_res_chain_fwd (encoder: taps 1, decoder: taps 3).  ws: the R pairs of
+    optimizer-maintained operand copies ([O][I] or [O][3I]); convs: the R (conv1, conv2) modules.  Returns (h, a1, x,
+    a lists as the per-conv loop makes them -- h / a1 / x None without a backward --, the packed backward weight
+    copies or None, the dropout keep bits for the backward or None)."""
+    R = len(ws)
+    dev = a0.device
+    e = lambda dt: torch.empty(N, H, device=dev, dtype=dt)  # noqa: E731
+    sb = need_backward
+    hs = [e(T) if sb else None for _ in range(R)]
+    a1s = [e(T) if sb else None for _ in range(R)]
+    xo = [e(RT) if sb and r < R - 1 else None for r in range(R)]
+    ao = [e(T) for _ in range(R)]
+    # fragment-packed weight copies, from the operand copies (one launch; the backward's come out of the same launch)
+    wsrc = [w for pair in ws for w in pair]
+    pk = [torch.empty(H, taps * H, device=dev, dtype=T) for _ in wsrc]
+    pk_bwd = [torch.empty(H, taps * H, device=dev, dtype=T) for _ in wsrc] if sb else None
+    K.res_pack_weights(wsrc, pk, pk_bwd, taps=taps)
+    masks = K.res_dropout_masks_empty(N, R, dev) if sb and p_drop > 0 and R > 1 else None
+    K.res_chain_fwd(a0, x0, pk[0::2], pk[1::2], [c1.bias for c1, _ in convs], [c2.bias for _, c2 in convs], hs, a1s,
+                    xo, ao, drop=(p_drop, seeds), seed_ptr=ctr, masks=masks, taps=taps, seg=seg)
+    return hs, a1s, xo, ao, pk_bwd, masks
+
+
+def _chain_bwd(sv, convs, gx, gxo, hs, xs, a0s, a1s, pk_bwd, masks, wgrad_target, slot, taps, seg):
+    """Backward of a ResBlock stack through aw_res_chain_bwd; returns (weight-gradient problems in the per-conv
+    loop's order, the stack input's operand gradient gxo_out[0]).  wgrad_target(c) = (C, col_map) of conv c's
+    weight gradient, taps 3 adds the implicit conv form (wconv) to each problem."""
+    N, H = gx.shape
+    R = len(hs)
+    dev = gx.device
+    T = gxo.dtype
+    gh = [torch.empty(N, H, device=dev, dtype=T) for _ in range(R)]
+    go = [torch.empty(N, H, device=dev, dtype=T) for _ in range(R)]
+    K.res_chain_bwd(gx, gxo, pk_bwd[0::2], pk_bwd[1::2], hs, xs[:R], gh, go, drop_p=sv.p_drop, masks=masks, taps=taps,
+                    seg=seg)
+    extra = dict(conv=(H, seg, 1, 1)) if taps == 3 else {}
+    wgrads = []
+    for r in reversed(range(R)):
+        c1, c2 = convs[r]
+        gin = gxo if r == R - 1 else go[r + 1]
+        for c, A, B in ((c2, gin, a1s[r]), (c1, gh[r], a0s[r])):
+            Cw, cm = wgrad_target(c)
+            wgrads.append((A, B, H, taps * H, N, dict(a_trans=True, b_trans=True, C=Cw, accumulate=True, col_map=cm,
+                                                      a_rowsum=slot(c.bias), **extra)))
+    return wgrads, go[0]
+
+
 # The step's GEMM chain stores its epilogue outputs write-through (aw_gemm_args.store_policy): with 64 dependent
 # class-A launches per step, each launch otherwise waits for the previous one's end-of-kernel L2 write-back of up to
 # 32 MB of dirty output lines (same-box A/B: +3 % windows/s)
@@ -311,24 +359,11 @@ def forward(m, x, training: bool, need_backward: bool, dtype=None, seed: int = 0
     # ---- encoder ResBlocks (per-token: centre taps)
     xs, a0s, hs, a1s = [x0], [a0], [], []
     sv.enc_bs, sv.dec_bs = [], []
-    sv.enc_chain = R > 0 and pr["enc_bn"][0] is None and K.enc_chain_ok(H, R, T, RT)
+    sv.enc_chain = R > 0 and pr["enc_bn"][0] is None and K.res_chain_ok(H, R, T, RT)
     if sv.enc_chain:
-        # bf16: the whole ResBlock stack as ONE persistent launch (csrc/encchain.hip), the same tensors bit for bit
-        sb = need_backward
-        hs = [e(N, H, dt=T) if sb else None for _ in range(R)]
-        a1s = [e(N, H, dt=T) if sb else None for _ in range(R)]
-        xo = [e(N, H, dt=RT) if sb and r < R - 1 else None for r in range(R)]
-        ao = [e(N, H, dt=T) for _ in range(R)]
-        # fragment-packed weight copies, from the optimizer-maintained [out][in] copies (one launch; the backward's
-        # transposed ones come out of the same launch)
-        wsrc = [w for pair in enc_w for w in pair]
-        pk = [e(H, H, dt=T) for _ in wsrc]
-        sv.enc_pk_bwd = [e(H, H, dt=T) for _ in wsrc] if sb else None
-        K.enc_pack_weights(wsrc, pk, sv.enc_pk_bwd)
-        sv.enc_masks = K.enc_dropout_masks(N, (p_drop, sv.enc_seed), sv.ctr)   # both directions' dropout bits
-        K.enc_chain_fwd(a0, x0, pk[0::2], pk[1::2], [c1.bias for c1, _ in pr["enc"]],
-                        [c2.bias for _, c2 in pr["enc"]], hs, a1s, xo, ao, drop=(p_drop, sv.enc_seed),
-                        seed_ptr=sv.ctr, masks=sv.enc_masks)
+        # bf16: the whole ResBlock stack as ONE persistent launch (csrc/reschain.hip), the same tensors bit for bit
+        hs, a1s, xo, ao, sv.enc_pk_bwd, sv.enc_masks = _chain_fwd(enc_w, pr["enc"], a0, x0, N, H, T, RT, p_drop,
+                                                                  sv.enc_seed, sv.ctr, need_backward, 1, S)
         xs += xo
         a0s += ao
     for r, (c1, c2) in enumerate(pr["enc"] if not sv.enc_chain else []):
@@ -385,7 +420,14 @@ def forward(m, x, training: bool, need_backward: bool, dtype=None, seed: int = 0
     K.gemm(zq_T, Wd0, N, H, D, bias=pr["dec0"].bias, C=y0, C2=ya0, c2_mode=1)
     conv = (H, S, 1, 0)
     ys, ya0s, dhs, da1s = [y0], [ya0], [], []
-    for r, (c1, c2) in enumerate(pr["dec"]):
+    sv.dec_chain = R > 0 and pr["dec_bn"][0] is None and K.res_chain_ok(H, R, T, RT, 3, S, "DEC")
+    if sv.dec_chain:
+        # bf16: the decoder's k = 3 ResBlock stack as one persistent launch (csrc/reschain.hip, taps = 3)
+        dhs, da1s, yo, yao, sv.dec_pk_bwd, sv.dec_masks = _chain_fwd(dec_w, pr["dec"], ya0, y0, N, H, T, RT, p_drop,
+                                                                     sv.dec_seed, sv.ctr, need_backward, 3, S)
+        ys += yo
+        ya0s += yao
+    for r, (c1, c2) in enumerate(pr["dec"] if not sv.dec_chain else []):
         if pr["dec_bn"][r] is not None:   # BatchNorm ResBlocks: statistics over all B*S positions (G = 1)
             yn, an, bs = _bn_block_fwd(ya0s[r], ys[r], dec_w[r][0], dec_w[r][1], 3 * H, dict(conv=conv), c1, c2,
                                        pr["dec_bn"][r], 1, training, p_drop, sv.dec_seed[r], sv.ctr, T,
@@ -575,7 +617,11 @@ def backward(m, sv, g_emb, g_xhat, slot, mid_hook=None):
         return (A, B, H, 3 * H, N, dict(a_trans=True, b_trans=True, conv=wconv, C=Cw, accumulate=True, col_map=cm,
                                         a_rowsum=slot(c.bias)))
 
-    for r in reversed(range(R)):
+    if getattr(sv, "dec_chain", False):
+        wgrads, go = _chain_bwd(sv, pr["dec"], gy, go, sv.dhs, sv.ys, sv.ya0s, sv.da1s, sv.dec_pk_bwd, sv.dec_masks,
+                                lambda c: _conv3_grad(slot(c.weight)), slot, 3, S)
+        sv.dec_pk_bwd = sv.dec_masks = None
+    for r in reversed(range(R)) if not getattr(sv, "dec_chain", False) else ():
         c1, c2 = pr["dec"][r]
         W1d, W2d = dgw[r]
         if bnm:
@@ -633,24 +679,11 @@ def backward(m, sv, g_emb, g_xhat, slot, mid_hook=None):
                                     a_rowsum=slot(c.bias)))
 
     if getattr(sv, "enc_chain", False):
-        # bf16: the input-gradient chain of all R blocks in one launch, on the packed transposed weight copies the
+        # bf16: the input-gradient chain of all R blocks in one launch, on the packed backward weight copies the
         # forward made
-        wt = sv.enc_pk_bwd
-        gh = [e(N, H, dt=T) for _ in range(R)]
-        go = [e(N, H, dt=T) for _ in range(R)]
-        K.enc_chain_bwd(gx, gxo, wt[0::2], wt[1::2], sv.hs, sv.xs[:R], gh, go, drop=(p_drop, sv.enc_seed),
-                        seed_ptr=sv.ctr, masks=sv.enc_masks)
+        wgrads, gxo = _chain_bwd(sv, pr["enc"], gx, gxo, sv.hs, sv.xs, sv.a0s, sv.a1s, sv.enc_pk_bwd, sv.enc_masks,
+                                 lambda c: _centre_grad(slot(c.weight)), slot, 1, S)
         sv.enc_pk_bwd = sv.enc_masks = None
-        for r in reversed(range(R)):
-            c1, c2 = pr["enc"][r]
-            gin = gxo if r == R - 1 else go[r + 1]
-            C2w, cm2 = _centre_grad(slot(c2.weight))
-            wgrads.append((gin, sv.a1s[r], H, H, N, dict(a_trans=True, b_trans=True, C=C2w, accumulate=True,
-                                                         col_map=cm2, a_rowsum=slot(c2.bias))))
-            C1w, cm1 = _centre_grad(slot(c1.weight))
-            wgrads.append((gh[r], sv.a0s[r], H, H, N, dict(a_trans=True, b_trans=True, C=C1w, accumulate=True,
-                                                           col_map=cm1, a_rowsum=slot(c1.bias))))
-        gxo = go[0]
     for r in reversed(range(R)) if not getattr(sv, "enc_chain", False) else ():
         c1, c2 = pr["enc"][r]
         w1, w2 = sv.enc_w[r]

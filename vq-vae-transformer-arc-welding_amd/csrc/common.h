@@ -152,7 +152,7 @@ __device__ __forceinline__ f32x2 gelu_erf_grad_fast2(f32x2 x) {
 }
 
 // Four values at a time (two packed pairs): the form the bf16 GEMM epilogues and the fused encoder chain share, so
-// that both round identically (tests/test_enc_chain.py compares them bit for bit).
+// that both round identically (tests/test_res_chain.py compares them bit for bit).
 __device__ __forceinline__ void aw_gelu4(const float (&x)[4], float (&y)[4]) {
   const f32x2 a = gelu_erf_fast2((f32x2){x[0], x[1]}), b = gelu_erf_fast2((f32x2){x[2], x[3]});
   y[0] = a.x, y[1] = a.y, y[2] = b.x, y[3] = b.y;
@@ -178,7 +178,7 @@ __device__ __forceinline__ float gelu_tanh_grad(float x) {
 
 // The GEMM epilogue's  x * m + r  (m = the last of act' / dropout scale, r = the residual): fused when both are
 // present, so the rounding does not depend on the compiler's contraction choices (gemm_core.h and the fused encoder
-// chain, encchain.hip, must agree bit for bit).
+// chain, reschain.hip, must agree bit for bit).
 __device__ __forceinline__ float aw_epi_mad(float x, float m, bool has_m, float r, bool has_r) {
   if (has_m && has_r) return __builtin_fmaf(x, m, r);
   if (has_m) x = __fmul_rn(x, m);

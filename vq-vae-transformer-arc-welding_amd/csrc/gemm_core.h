@@ -797,7 +797,7 @@ __global__ __launch_bounds__(Cfg<BMT>::NTH, RAGGED ? 1 : Cfg<BMT>::MINB) void ge
         for (int e = 0; e < 4; ++e) {
           float x = alpha * av[e] + bias[e];
           // x * act' * ds + resid with the last multiply fused into the add (aw_epi_mad): one rounding order that the
-          // encoder chain (encchain.hip) reproduces exactly, whatever FMA contraction the compiler would choose
+          // encoder chain (reschain.hip) reproduces exactly, whatever FMA contraction the compiler would choose
           float m = 1.f;
           bool has_m = false;
           if (f_pre) {
