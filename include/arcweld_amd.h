@@ -115,7 +115,9 @@ int aw_gemm_set_wgrad_policy(int mode);
  * VQ-VAE encoder's per-token convs (model/vq_vae_patch_embedd.py:65,68 via :108-110).  One stream-K launch (one
  * workgroup per CU, equal work per CU whatever the tile count); tiles split between workgroups are summed through
  * `ws` (aw_wgrad_batch_workspace bytes, 16-B aligned, no initial contents).  One batch at a time per device (the
- * per-tile arrival counters are the library's).  aw_wgrad_batch_workspace returns -1 when the batch is not eligible. */
+ * per-tile arrival counters are the library's).  Each tile adds into C with one plain read-modify-write (not
+ * atomics, unlike aw_gemm's accumulate mode): the problems' C ranges [C, C + M*ldc) must not overlap (rejected).
+ * aw_wgrad_batch_workspace returns -1 when the batch is not eligible. */
 #define AW_WGRAD_BATCH_MAX 32
 int64_t aw_wgrad_batch_workspace(const aw_gemm_args* args, int n);
 int aw_wgrad_batch(const aw_gemm_args* args, int n, void* ws, int64_t ws_bytes, void* stream);

@@ -97,10 +97,13 @@ def _worker(rank, port, out):
         dist.all_reduce(probe)           # the factor is applied by RCCL itself
         torch.cuda.synchronize()
         out["probe"] = probe.cpu().tolist()
-        odd = torch.ones(5, device="cuda")     # an odd length (recorded only: the trainer's buckets are 256-B rounded)
+        odd = torch.ones(5, device="cuda")     # an odd length: scaled like the rest (measured, asserted below)
         dist.all_reduce(odd)
+        one = torch.ones(1, device="cuda")     # a 1-element tail: what came back unscaled (recorded only)
+        dist.all_reduce(one)
         torch.cuda.synchronize()
         out["probe_odd"] = odd.cpu().tolist()
+        out["probe_one"] = one.cpu().tolist()
         for name in ("vqvae", "decoder"):
             n0 = len(calls)
             out[("rccl", name)] = _train(name, 0.5)
@@ -116,7 +119,10 @@ def test_rccl_one_rank_graphed_steps_match_plain_run():
     mp.spawn(_worker, args=(port, out), nprocs=1, join=True)
     assert out["backend"] == "nccl"
     assert out["probe"] == [2.0] * 4
-    print("one-rank pre-multiplied sum of 5 ones:", out["probe_odd"])
+    # a 5-element bucket is scaled; the hazard DESIGN.md section 7 records was a bucket ENDING on a 1-element segment
+    # (the ConvT2 bias), which the trainer's 256-B bucket rounding (arcweld/trainer.py allreduce_spans) avoids
+    assert out["probe_odd"] == [2.0] * 5
+    print("one-rank pre-multiplied sum of 1 one:", out["probe_one"])
     for name in ("vqvae", "decoder"):
         # eager step + 2 warm-up calls: one region each; captured replays: late + early regions, several buckets
         assert out[("calls", name)] >= STEPS + 1, (name, out[("calls", name)])

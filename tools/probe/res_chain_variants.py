@@ -10,7 +10,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(os.path.dirname(HERE))
 SRC = os.path.join(REPO, "vq-vae-transformer-arc-welding_amd", "csrc")
-VARIANTS = {"base": 0, "no_store": 1, "stamps": 4}
+VARIANTS = {"base": 0, "no_store": 1, "small_w": 2, "stamps": 4}
 
 
 def build():

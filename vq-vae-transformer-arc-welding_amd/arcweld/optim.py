@@ -178,11 +178,13 @@ class RAdam(torch.optim.Optimizer):
         return [tuple(x) for x in spans]
 
     def live_spans_excluding(self, spans):
-        """live_spans() minus the given [a, b) ranges."""
+        """live_spans() minus the given [a, b) ranges, each taken with its end rounded up to 64 elements as
+        arcweld.trainer.allreduce_spans moves it: the zero padding after an excluded range is not all-reduced twice."""
+        al = lambda n: (n + 63) // 64 * 64   # noqa: E731
         out = []
         for a, b in self.live_spans():
             cur = a
-            for x, y in sorted(spans):
+            for x, y in sorted((x, al(y)) for x, y in spans):
                 if y <= cur or x >= b:
                     continue
                 if x > cur:

@@ -405,7 +405,8 @@ int g_policy = 0;   // aw_gemm_set_wgrad_policy: 0 automatic, 1 force, -1 off
 //  * A tile's S partial pieces are summed by the LAST arriving piece: each piece takes an arrival ticket (one agent-
 //    scope atomic add) when its loop ends; every piece but the last stores its accumulators write-through (sc1) into
 //    its workspace slot, drains them (vmcnt(0)), joins a workgroup barrier and counts itself published (one more
-//    atomic add); the last polls the published count with sc1 loads, then loads the other slots with sc1 loads and
+//    atomic add); the last polls the published count with sc1 loads (a poll that never completes traps instead of
+//    summing unwritten slots), then loads the other slots with sc1 loads and
 //    does the one read-modify-write of the gradient (MI355X_MICROARCH.md, inter-workgroup hand-off, first row of the
 //    measured forms).  It waits only for pieces that already hold tickets, i.e. are running and only store: no
 //    deadlock whatever the residency.  The read-modify-write goes through LDS in two 128-row halves: float4 per lane, 16 row loads in flight.
@@ -616,20 +617,30 @@ __global__ __launch_bounds__(WT_NTH, 1) void wgrad_tt_kernel(WTParams P) {
         for (int i = 0; i < 8; ++i)
 #pragma unroll
           for (int f = 0; f < 4; ++f) wt_st_sc1(mine + ((i * 4 + f) * WT_NTH + tid) * 4, acc[i][f]);
+        // the sc1 hand-off form of MI355X_MICROARCH.md (valid forms, first table row): every storing wave drains its
+        // write-through stores, a workgroup barrier, then ONE lane's agent-scope add.  Not the memory model's
+        // release / acquire fences: their L2 write-back (buffer_wbl2) and invalidates cost the decoder step
+        // 5.34 -> 6.29 ms (same-box A/B, four alternating runs)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (tid == 0) __hip_atomic_fetch_add(&g_wt_pub[tile], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       } else {
         if (tid == 0) {
-          // sc1 poll of the published count (a bounded spin: the publishers are running)
-          for (int it = 0; it < (1 << 26); ++it) {
+          // poll of the published count: a bounded spin (the publishers took their tickets first, so they are
+          // resident and only store, drain and count); running out of it means a broken hand-off, which must not
+          // turn into a silently wrong gradient: trap
+          int it = 0;   // relaxed agent loads = sc1 loads: past this CU's L1
+          for (; it < (1 << 26); ++it) {
             if (__hip_atomic_load(&g_wt_pub[tile], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= P.S - 1) break;
             __builtin_amdgcn_s_sleep(1);
           }
+          // a broken hand-off poisons the tile (NaN: loud in the loss, the clip norm and every check) instead of
+          // summing unwritten slots silently
+          if (it == (1 << 26)) acc[0][0] = f32x4{__builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""), 0.f};
           __hip_atomic_store(&g_wt_pub[tile], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           __hip_atomic_store(&g_wt_arrive[tile], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-        __syncthreads();
+        __syncthreads();   // the polling wave joins: every wave's slot loads (all sc1) come after the poll matched
         for (int o = 0; o < P.S; ++o) {
           if (o == sp) continue;
           const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(P.ws + ((int64_t)o * P.total_tiles + tile) * WT_SLAB,
@@ -740,6 +751,14 @@ int wt_plan(const aw_gemm_args* args, int n, WTParams* P) {
     tiles += (a.M / WT_BM) * (a.N / WT_BN);
   }
   AW_REQUIRE(a0.K > 0, "aw_wgrad_batch: K must be positive");
+  // each tile read-modify-writes its block of C once, without atomics: problems must not share C storage (the
+  // extent of problem i's rows: [C, C + M * ldc) floats)
+  for (int i = 0; i < n; ++i)
+    for (int j = i + 1; j < n; ++j) {
+      const uintptr_t bi = (uintptr_t)args[i].C, ei = bi + (uintptr_t)args[i].M * args[i].ldc * sizeof(float);
+      const uintptr_t bj = (uintptr_t)args[j].C, ej = bj + (uintptr_t)args[j].M * args[j].ldc * sizeof(float);
+      AW_REQUIRE(ei <= bj || ej <= bi, "aw_wgrad_batch: problems %d and %d write overlapping C storage", i, j);
+    }
   AW_REQUIRE(tiles <= WT_MAXTILES, "aw_wgrad_batch: %d tiles exceed %d", tiles, WT_MAXTILES);
   if (!P) return AW_OK;
   memset(P, 0, sizeof(*P));

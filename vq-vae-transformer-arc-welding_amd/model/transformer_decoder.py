@@ -136,13 +136,14 @@ class MyTransformerDecoder(LightningModule):
         return out
 
     def _loss_scale_tensor(self, scale, dev):
-        """Persistent device scalar holding the loss scale (refilled only when the value changes; the step graphs
-        make it before their capture, so the captured step has no fill launch for it)."""
-        st = self.__dict__.get("_gscale")
-        if st is None or st[0] != scale or st[1].device != dev:
-            st = (scale, torch.full((1,), scale, device=dev))
-            self.__dict__["_gscale"] = st
-        return st[1]
+        """Persistent device scalar holding the loss scale, one per (scale, device) and never freed: the step graphs
+        make it before their capture (the captured step has no fill launch for it) and keep reading its address, so a
+        later call with another scale gets a tensor of its own instead of replacing one a graph still holds."""
+        cache = self.__dict__.setdefault("_gscale", {})
+        key = (float(scale), str(dev))
+        if key not in cache:
+            cache[key] = torch.full((1,), scale, device=dev)
+        return cache[key]
 
     @torch.no_grad()
     def fused_train_step(self, batch, scale, mid_hook=None):

@@ -197,12 +197,13 @@ class VQVAEPatch(Autoencoder):
         return loss
 
     def _loss_scale_tensor(self, scale, dev):
-        """Persistent device scalar holding the loss scale (refilled only when the value changes)."""
-        st = self.__dict__.get("_gscale")
-        if st is None or st[0] != scale or st[1].device != dev:
-            st = (scale, torch.full((1,), scale, device=dev))
-            self.__dict__["_gscale"] = st
-        return st[1]
+        """Persistent device scalar holding the loss scale, one per (scale, device) and never freed (a captured step
+        graph keeps reading the one it was made with)."""
+        cache = self.__dict__.setdefault("_gscale", {})
+        key = (float(scale), str(dev))
+        if key not in cache:
+            cache[key] = torch.full((1,), scale, device=dev)
+        return cache[key]
 
     def operand_set(self):
         """The persistent GEMM operand copies of the training step (arcweld.operands), for the optimizer to keep
