@@ -49,7 +49,7 @@ def parse():
                     help="skip the configs[4] line (codebook 8192x256, T 1025, 16-block Transformer)")
     ap.add_argument("--seqs", type=int, default=51, help="Transformer sequences per GPU per step (configs[2])")
     ap.add_argument("--n-cycles", type=int, default=20)
-    ap.add_argument("--only", default="all", choices=["all", "transformer_pretokenized"],
+    ap.add_argument("--only", default="all", choices=["all", "transformer_pretokenized", "transformer_b16_acc5"],
                     help="profiling aid: run one sub-line alone (the PMC passes of tools/prof_transformer.sh)")
     ap.add_argument("--detail", default="gpurun_out/bench_detail.json",
                     help="where the full record (every sub-line with its per-kernel objects) is written; the printed "
@@ -124,7 +124,7 @@ def transformer_workload(dev, rank, world, args, seqs, n_cycles, accumulate=1, l
     def train(w):
         ids = tokenize.encode_ids(vq, w)
         x, y, _ = tokenize.autoregressive_pairs(ids, start_token=K)
-        return (x, cond, y)
+        return (x, cond if w.shape[0] == seqs else torch.zeros(w.shape[0], dtype=torch.long, device=dev), y)
 
     batches = [train(w) for w in wins] if pretokenized else None
 
@@ -154,7 +154,7 @@ def transformer_workload(dev, rank, world, args, seqs, n_cycles, accumulate=1, l
         # replays: the fused step with the mid-backward all-reduce split)
         orig, orig_fused = dec.training_step, dec.fused_train_step
         dec.training_step = lambda w, i: orig(train(w), i)
-        dec.fused_train_step = lambda w, scale, mid_hook=None: orig_fused(train(w), scale, mid_hook=mid_hook)
+        dec.fused_train_step = lambda w, scale, mid_hook=None, **kw: orig_fused(train(w), scale, mid_hook=mid_hook, **kw)
     el = _timed_steps(step, max(args.warmup, 3 if use_graph else 0), args.steps, world)
     windows = world * seqs * accumulate * nc * args.steps
     flops = transformer_flops_per_seq(T, n_blocks, 512, V) * seqs * accumulate * world * args.steps
@@ -549,11 +549,15 @@ def main():
     from arcweld import _native
     _native.call("aw_gemm_set_tile", args.gemm_tile)
 
-    if args.only == "transformer_pretokenized":
+    if args.only != "all":
         from arcweld.precision import operands
         with operands(torch.bfloat16):
-            line = transformer_workload(dev, rank, world, args, args.seqs, args.n_cycles, pretokenized=True,
-                                        label="configs[2], the reference's regime")
+            if args.only == "transformer_pretokenized":
+                line = transformer_workload(dev, rank, world, args, args.seqs, args.n_cycles, pretokenized=True,
+                                            label="configs[2], the reference's regime")
+            else:
+                line = transformer_workload(dev, rank, world, args, 16, args.n_cycles, accumulate=5,
+                                            label="configs[2], reference batch 16 x accumulate 5")
         if rank == 0:
             print(json.dumps({"only": args.only, **line}), flush=True)
         if distributed:

@@ -24,8 +24,9 @@ pytestmark = pytest.mark.gpu
 @pytest.mark.parametrize("graphs", [False, True])
 def test_accumulate5_clip08_two_stage_trajectory_matches_reference(graphs):
     """graphs: Trainer(hip_graphs=True) -- the first two accumulation groups of a stage run eagerly (warm-up), the
-    third is captured and replayed (the forward/backward graph once per micro-batch, then the captured clip + RAdam),
-    so stage 0's last optimizer step comes from the graphs; the captured clip reports no norm to Python."""
+    third is captured and replayed (the group's five micro-batches as ONE forward/backward with a loss mean per
+    micro-batch, arcweld/graphs.py grouped accumulation, then the captured clip + RAdam), so stage 0's last optimizer
+    step comes from the graphs; the captured clip reports no norm to Python."""
     from arcweld.precision import operands
     from arcweld.trainer import Trainer
     from model.transformer_decoder import MyTransformerDecoder
@@ -64,3 +65,42 @@ def test_accumulate5_clip08_two_stage_trajectory_matches_reference(graphs):
             for n, p in m.named_parameters():
                 np.testing.assert_allclose(p.detach().cpu().numpy(), g[f"s{si}/param/{n}"], rtol=1e-5, atol=1e-6,
                                            err_msg=f"stage {si} {n}")
+
+
+@pytest.mark.parametrize("task", ["generate", "classification"])
+def test_grouped_accumulation_equals_micro_batch_sum(task):
+    """fused_train_step(groups=5) on the five micro-batches side by side (arcweld/decoder.py fused_step, what the
+    captured accumulation step runs) == five fused_train_step calls accumulating into the same gradients, each
+    micro-batch with its own valid-token count (ignore_index rows differ per micro-batch here); fp32 operands,
+    no dropout: the same per-token math, only the weight-gradient reduction order differs."""
+    from arcweld.precision import operands
+    from model.transformer_decoder import MyTransformerDecoder
+    torch.manual_seed(0)
+    kw = dict(d_model=128, n_classes=40, seq_len=33, n_blocks=2, n_head=4, res_dropout=0.0, att_dropout=0.0)
+    m = MyTransformerDecoder(**kw).cuda().train()
+    (m.switch_to_generate if task == "generate" else m.switch_to_classification)()
+    g = torch.Generator(device="cpu").manual_seed(5)
+    mbs = []
+    for j in range(5):
+        x = torch.randint(0, 38, (6, 33), generator=g)
+        y = torch.randint(0, 38, (6, 33), generator=g)
+        y[:, 33 - 3 * j:] = -1                       # a different number of ignored targets per micro-batch
+        cond = torch.randint(0, 2, (6,), generator=g)
+        if task == "classification":
+            cond[: j % 3] = -100
+        mbs.append((x.cuda(), cond.cuda(), y.cuda()))
+    grads, losses = [], []
+    with operands(torch.float32):
+        for grouped in (False, True):
+            m.zero_grad(set_to_none=True)
+            if grouped:
+                cat = tuple(torch.cat([b[i] for b in mbs], 0) for i in range(3))
+                losses.append(float(m.fused_train_step(cat, 0.2, groups=5)))
+            else:
+                losses.append(sum(float(m.fused_train_step(b, 0.2)) for b in mbs) / 5)
+            torch.cuda.synchronize()
+            grads.append({n: p.grad.detach().clone() for n, p in m.named_parameters() if p.grad is not None})
+    assert abs(losses[0] - losses[1]) <= 1e-5 * abs(losses[0])
+    assert grads[0].keys() == grads[1].keys()
+    for n, g0 in grads[0].items():
+        torch.testing.assert_close(grads[1][n], g0, rtol=1e-5, atol=1e-7, msg=n)

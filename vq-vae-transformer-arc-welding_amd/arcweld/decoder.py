@@ -303,14 +303,23 @@ class _CrossEntropy(torch.autograd.Function):
         return dl, None, None
 
 
-def fused_step(m, batch, scale, slot, mid_hook=None):
+def fused_step(m, batch, scale, slot, mid_hook=None, groups=1):
     """forward + cross-entropy + backward of one micro-batch of the current task, without autograd: the work of
     training_step followed by (loss * scale).backward() (model/transformer_decoder.py:139-155, 226-230).  Returns
-    (loss, logits)."""
+    (loss, logits).
+
+    groups = G > 1: the batch is the G equal micro-batches of one accumulation group, concatenated along the
+    sequences (accumulate_grad_batches, train_transformer_mtasks.py:32): each micro-batch's loss is its own mean
+    over its own valid tokens (one cross-entropy reduction per group), so the summed gradient is Lightning's sum of
+    the G micro-batch gradients; the returned loss is the mean of the G losses.  Every row draws its own dropout
+    mask from the one counter range of this forward."""
     x, cond, y = batch
     generate = m.task == "generate"
     dev = x.device
-    sums = torch.empty(2, device=dev, dtype=torch.float64)    # zeroed by the forward's dropout-counter launch
+    G = int(groups)
+    if G < 1 or x.shape[0] % G:
+        raise ValueError(f"fused_step: {x.shape[0]} sequences do not split into {G} equal micro-batches")
+    sums = torch.empty(G, 2, device=dev, dtype=torch.float64)  # zeroed by the forward's dropout-counter launch
     out, sv = forward(m, x, generate, m.training, need_backward=True, seed=m._next_seed(), zero=sums)
     sv.ids = x.contiguous()
     if generate:
@@ -319,10 +328,15 @@ def fused_step(m, batch, scale, slot, mid_hook=None):
     else:
         logits2d, target, ignore = out, cond.reshape(-1).contiguous(), -100
     R, V = logits2d.shape
+    Rg = R // G
+    rows = [slice(j * Rg, (j + 1) * Rg) for j in range(G)]
     lse = torch.empty(R, device=dev)
-    K.ce_fwd(logits2d, V, target, ignore, sums[0:1], sums[1:2], lse)
-    loss = torch.empty((), device=dev)
-    K.ce_finalize(sums[0:1], sums[1:2], loss)
+    for j, sl in enumerate(rows):
+        K.ce_fwd(logits2d[sl], V, target[sl], ignore, sums[j, 0:1], sums[j, 1:2], lse[sl])
+    losses = torch.empty(G, device=dev)
+    for j in range(G):
+        K.ce_finalize(sums[j, 0:1], sums[j, 1:2], losses[j:j + 1])
+    loss = losses[0] if G == 1 else losses.mean()
     g = m._loss_scale_tensor(float(scale), dev) if hasattr(m, "_loss_scale_tensor") else \
         torch.full((1,), float(scale), device=dev)
     if generate:
@@ -333,7 +347,8 @@ def fused_step(m, batch, scale, slot, mid_hook=None):
         sv.gl = gl
     else:
         dl = torch.empty(R, V, device=dev)
-    K.ce_bwd(logits2d, V, target, ignore, lse, sums[1:2], g, dl)
+    for j, sl in enumerate(rows):
+        K.ce_bwd(logits2d[sl], V, target[sl], ignore, lse[sl], sums[j, 1:2], g, dl[sl])
     backward(m, sv, dl.view(out.shape), slot, mid_hook=mid_hook)
     return loss, out
 

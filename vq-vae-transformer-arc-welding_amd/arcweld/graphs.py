@@ -11,7 +11,10 @@ the later half of the blocks): their all-reduce is launched (async, RCCL stream)
 overlaps the rest of the backward; the remaining gradients' all-reduce follows.  Replay needs no host values: dropout masks come from
 a device counter (aw_gemm_args.seed_ptr), the RAdam step number and clip coefficient live on the device.  Inputs
 are copied into static buffers before each replay; with gradient accumulation the forward/backward graphs are
-replayed once per micro-batch before the update.
+replayed once per micro-batch before the update -- or, for a model with ``grouped_accumulation`` (the Transformer
+decoder), the group's micro-batches are copied side by side into one static batch and the step is captured as ONE
+forward/backward over all of them (``fused_train_step(groups=G)``: each micro-batch keeps its own loss mean), so the
+reference's 16-sequence micro-batches (train_transformer_mtasks.py:32) no longer run as five under-filled passes.
 
 The first `warmup` calls run eagerly on their own batches (lazy device state -- RNG counters, optimizer
 buffers -- is created there); the next call captures and replays, so every call is exactly one step on the
@@ -45,6 +48,33 @@ def _flatten(batch, out):
     return out
 
 
+def _concat(batches):
+    """The micro-batches of a group side by side (dim 0 of every tensor)."""
+    if isinstance(batches[0], torch.Tensor):
+        return torch.cat(batches, 0)
+    return type(batches[0])(_concat([b[i] for b in batches]) for i in range(len(batches[0])))
+
+
+def _same_shapes(batches):
+    shp = lambda b: [(t.shape, t.dtype) for t in _flatten(b, [])]  # noqa: E731
+    return all(shp(b) == shp(batches[0]) for b in batches[1:])
+
+
+def _copy_group_into(dst, batches):
+    """The group's micro-batches into their row slices of the static buffers: one multi-tensor copy launch."""
+    d, s = [], []
+    for t_dst, *t_src in zip(_flatten(dst, []), *[_flatten(b, []) for b in batches]):
+        n = t_src[0].shape[0]
+        for j, t in enumerate(t_src):
+            d.append(t_dst[j * n:(j + 1) * n])
+            s.append(t)
+    if all(a.dtype == b.dtype and a.device == b.device for a, b in zip(d, s)):
+        torch._foreach_copy_(d, s, non_blocking=True)
+    else:
+        for a, b in zip(d, s):
+            a.copy_(b, non_blocking=True)
+
+
 def _copy_into(dst, src):
     """The batch into the static input buffers: one multi-tensor copy launch for all of its tensors (the decoder's
     ids / condition / targets took three copy launches)."""
@@ -76,13 +106,18 @@ class StepGraphs:
         self.split = hasattr(model, "fused_train_step") and hasattr(model, "backward_late_parameters") and \
             os.environ.get("ARCWELD_SPLIT_GRAPHS") != "0"
         model.__dict__["_wgrad_merge"] = not collective and os.environ.get("ARCWELD_WGRAD_MERGE") != "0"
+        # an accumulation group as one captured batch (see the module docstring); ARCWELD_GROUP_ACCUM=0 replays the
+        # per-micro-batch graph instead (A/B runs)
+        self.group_accum = self.split and getattr(model, "grouped_accumulation", False) and \
+            getattr(trainer, "accumulate", 1) > 1 and os.environ.get("ARCWELD_GROUP_ACCUM") != "0"
+        self.G = 1
         # Without a collective and without accumulation nothing runs between the last forward/backward piece and the
         # update, so the update is captured into that piece: one graph launch (and its ~8.5 us gap on the stream)
         # fewer per step.  ARCWELD_FUSE_UPDATE=0 keeps it a graph of its own (A/B runs).
-        self.fuse_update = self.split and not collective and getattr(trainer, "accumulate", 1) == 1 and \
-            os.environ.get("ARCWELD_FUSE_UPDATE") != "0"
+        self.fuse_update = self.split and not collective and \
+            (getattr(trainer, "accumulate", 1) == 1 or self.group_accum) and os.environ.get("ARCWELD_FUSE_UPDATE") != "0"
 
-    def _capture(self, batch):
+    def _capture(self, batch, G=1):
         self.static = _clone_static(batch)
         if hasattr(self.model, "_loss_scale_tensor"):       # persistent scalars are made outside the capture
             dev = next(self.model.parameters()).device
@@ -109,7 +144,8 @@ class StepGraphs:
                 cut()
 
             try:
-                self.loss = self.model.fused_train_step(self.static, self.scale, mid_hook=mid)
+                kw = {"groups": G} if G > 1 else {}
+                self.loss = self.model.fused_train_step(self.static, self.scale, mid_hook=mid, **kw)
                 if self.fuse_update:
                     self.trainer._update(self.model)
             finally:
@@ -128,7 +164,8 @@ class StepGraphs:
         forward/backward graph is replayed once per micro-batch, gradients accumulating in the flat buffer; the
         all-reduce runs once, split around the last micro-batch's backward -- DDP's no_sync accumulation)."""
         batches = batch if isinstance(batch, list) else [batch]
-        if self.fuse_update and len(batches) > 1:
+        G = len(batches) if len(batches) > 1 and self.group_accum and _same_shapes(batches) else 1
+        if self.fuse_update and len(batches) > 1 and G == 1:
             raise ValueError("StepGraphs: the update is captured with the backward; one micro-batch per step")
         self.calls += 1
         if self.calls <= self.warmup:
@@ -140,11 +177,18 @@ class StepGraphs:
             self.trainer.global_step += 1
             return loss
         if self.static is None:
-            self._capture(batches[0])
+            self.G = G
+            self._capture(_concat(batches) if G > 1 else batches[0], G)
+        if G != self.G:
+            raise ValueError(f"StepGraphs: captured for groups of {self.G} micro-batches, got {len(batches)}")
+        if G > 1:
+            _copy_group_into(self.static, batches)
+            batches = [None]      # one replay of the group's forward/backward
         last = len(batches) - 1
         works = []
         for j, b in enumerate(batches):
-            _copy_into(self.static, b)        # ordered after the previous replay on this stream
+            if b is not None:
+                _copy_into(self.static, b)    # ordered after the previous replay on this stream
             if self.split:
                 for i, g in enumerate(self.pieces):
                     g.replay()

@@ -24,24 +24,13 @@ namespace {
 // embedding dim; |z|^2 and |e_k|^2 are in-order sums of squares; the distance is fl(fl(|z|^2 + |e_k|^2) - 2 * dot)
 // and the argmin the lexicographic (d, k) minimum (torch.argmin's first-index tie rule).  The register footprint
 // does not depend on D, so the stress codebook (K 8192 x D 256) runs at the same occupancy.
-// Diagnostic phase stamps (tools/probe/vq_stamps.py only: a probe build with -DAW_VQ_STAMPS; never in the library).
-#ifdef AW_VQ_STAMPS
-static __device__ uint64_t g_vq_stamps[1024 * 16];
-#define VQ_STAMP(i) do { if (threadIdx.x == 0 && blockIdx.x < 1024) \
-    g_vq_stamps[blockIdx.x * 16 + (i)] = __builtin_amdgcn_s_memrealtime(); } while (0)
-#else
-#define VQ_STAMP(i) do { } while (0)
-#endif
 
 constexpr int VQ_THREADS = 512;
 constexpr int VQ_CODES = 512;
 constexpr int VQ_DC = 16;           // embedding floats per staged chunk
 
-// code counts gathered per workgroup in LDS (1) or added per row (0: A/B builds).  Isolated at the configs[1] shape:
-// 39.1 -> 28.0 us (a probe build without the count atomics: 26.4 us; tools/probe/vq_probe.py)
-#ifndef AW_VQ_LDS_COUNTS
-#define AW_VQ_LDS_COUNTS 1
-#endif
+// Code counts are gathered per workgroup in LDS, not added per row: isolated at the configs[1] shape 39.1 -> 28.0 us
+// (a build without the count atomics: 26.4 us; round-4 probes).
 
 template <int D, int ROWS> struct VqLds {
   static constexpr int ZP = D + 4;                                   // z image pitch (disjoint banks per row)
@@ -75,7 +64,6 @@ __global__ __launch_bounds__(VQ_THREADS, 2) void vq_fwd_kernel(const float* __re
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int lr = lane >> 3, lc = lane & 7;
   const int64_t row0 = (int64_t)blockIdx.x * ROWS;
-  VQ_STAMP(0);
 
   // ---- z tile -> LDS (rows beyond N are zero), |z|^2 per row
   for (int i = tid; i < ROWS * (D / 4); i += VQ_THREADS) {
@@ -85,7 +73,6 @@ __global__ __launch_bounds__(VQ_THREADS, 2) void vq_fwd_kernel(const float* __re
     *reinterpret_cast<float4*>(zs + r * ZP + 4 * q) = v;
   }
   __syncthreads();
-  VQ_STAMP(1);
   if (tid < ROWS) {
     float s = 0.f;
     for (int d = 0; d < D; ++d) s = __fadd_rn(s, __fmul_rn(zs[tid * ZP + d], zs[tid * ZP + d]));
@@ -145,7 +132,6 @@ __global__ __launch_bounds__(VQ_THREADS, 2) void vq_fwd_kernel(const float* __re
   load(0);
   store(0);
   __syncthreads();
-  VQ_STAMP(2);
   float zz[RPL];
 #pragma unroll
   for (int i = 0; i < RPL; ++i) zz[i] = zzs[lr + 8 * i];
@@ -198,7 +184,6 @@ __global__ __launch_bounds__(VQ_THREADS, 2) void vq_fwd_kernel(const float* __re
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = f32x2{0.f, 0.f};
     }
-    if (st < 8) VQ_STAMP(3 + st);
   }
 
   // ---- argmin across the 8 code lanes of a row group, then across the 8 waves (LDS, the e stages are free)
@@ -224,13 +209,11 @@ __global__ __launch_bounds__(VQ_THREADS, 2) void vq_fwd_kernel(const float* __re
     }
   }
   __syncthreads();
-  VQ_STAMP(11);
   // ---- epilogue over the whole workgroup: thread (row r, quad q) of the ROWS x D/4 float4 items resolves its
   // row's winner from the 8 wave candidates (LDS broadcast reads), gathers e_k's quad and writes z_q (+ the operand
   // copy) coalesced; the q == 0 thread of a row writes idx and counts the code.
   constexpr int DQ = D / 4;
   double se = 0.0;
-#if AW_VQ_LDS_COUNTS
   // the workgroup's code counts gather in LDS (the e stages past rd / rk are free now) and go out as one sweep of
   // the K bins: one atomic per distinct code, issued bin-contiguous, instead of one per row from the epilogue
   constexpr int HCAP = 2 * L::E - 16 * ROWS;
@@ -240,7 +223,6 @@ __global__ __launch_bounds__(VQ_THREADS, 2) void vq_fwd_kernel(const float* __re
     for (int i = tid; i < K; i += VQ_THREADS) hist[i] = 0.f;
     __syncthreads();
   }
-#endif
   for (int it = tid; it < ROWS * DQ; it += VQ_THREADS) {
     const int r = it / DQ, q = it - r * DQ;
     const int64_t row = row0 + r;
@@ -256,14 +238,10 @@ __global__ __launch_bounds__(VQ_THREADS, 2) void vq_fwd_kernel(const float* __re
     if (bk < 0 || bk >= K) bk = 0;  // all-NaN row guard (torch would return the NaN position)
     if (q == 0) {
       idx[row] = bk;
-#if AW_VQ_LDS_COUNTS
       if (lds_counts)
         atomicAdd(hist + bk, 1.0f);
       else
-#endif
-#ifndef AW_VQ_NO_COUNTS_PROBE
       atomicAdd(counts + bk, 1.0f);
-#endif
     }
     const float4 e = reinterpret_cast<const float4*>(E + (int64_t)bk * D)[q];
     const float4 zv = *reinterpret_cast<const float4*>(zs + r * ZP + 4 * q);
@@ -292,24 +270,17 @@ __global__ __launch_bounds__(VQ_THREADS, 2) void vq_fwd_kernel(const float* __re
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
-#if AW_VQ_LDS_COUNTS
   if (lds_counts)
     for (int i = tid; i < K; i += VQ_THREADS) {
       const float c = hist[i];
       if (c != 0.f) atomicAdd(counts + i, c);
     }
-#endif
   if (tid == 0) {
     double t = 0.0;
 #pragma unroll
     for (int v = 0; v < 8; ++v) t += red[v];
-#ifndef AW_VQ_NO_SQERR_PROBE
     atomicAdd(sqerr, t);
-#else
-    if (t == 12345.0) sqerr[0] = t;   // probe build only
-#endif
   }
-  VQ_STAMP(12);
 }
 
 __global__ void vq_finalize_kernel(const float* counts, const double* sqerr, int64_t N, int K, int D, float beta,
@@ -371,13 +342,6 @@ __global__ void vq_gather_kernel(const float* E, const int64_t* idx, int64_t N, 
 
 }  // namespace
 
-#ifdef AW_VQ_STAMPS
-extern "C" int aw_probe_vq_stamps(uint64_t* out, int n) {   // copies n words out, then zeroes them
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_vq_stamps), (size_t)n * 8) != hipSuccess) return -1;
-  static uint64_t zeros[1024 * 16];
-  return hipMemcpyToSymbol(HIP_SYMBOL(g_vq_stamps), zeros, sizeof(zeros)) == hipSuccess ? n : -1;
-}
-#endif
 
 extern "C" int aw_vq_forward_ex(const float* z, const float* E, int64_t N, int K, int D, float* zq, int64_t* idx,
                                 float* counts, double* sqerr, void* zq_copy, int copy_dtype, void* stream) {

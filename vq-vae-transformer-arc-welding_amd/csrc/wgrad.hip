@@ -38,11 +38,8 @@ constexpr int W3_B = W3_BK * W3_CB * 2;    // 8192 B: x image
 constexpr int W3_BUF = W3_A + W3_B;        // 40960 B
 constexpr int W3_NBUF = 4;                 // 163840 B = the whole LDS of a CU
 constexpr int W3_DMA = 5;                  // DMA instructions per thread per K-tile (4 dy + 1 x)
-// where the DMA is issued (probe knob; 1 measured fastest): 0 = K-tile t + 3 inside the MFMA segment, 1 = t + 3 in the
-// read segment (which then retires its reads before the barrier), 2 = t + 2 in the read segment
-#ifndef W3_SCHED
-#define W3_SCHED 1
-#endif
+// The DMA of K-tile t + 3 is issued in the read segment of tile t (which then retires its reads before the barrier):
+// measured faster than issuing it inside the MFMA segment, or t + 2 in the read segment (round-3 probes).
 
 struct W3Params {
   int M, cin, K, seg, ngroups, tiles_m, tiles_i, nblocks;
@@ -90,18 +87,6 @@ __device__ __forceinline__ void w3_barrier() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
-#ifdef W3_STAMPS
-// probe: s_memtime at the segment boundaries of K-tiles [W3_T0, W3_T0 + 4) for waves 0 and 4 of workgroups 0..7
-#define W3_T0 96
-__device__ uint64_t g_w3_stamps[8 * 2 * 4 * 6];
-#define W3_STAMP(k)                                                                                             \
-  do {                                                                                                          \
-    if (blockIdx.x < 8 && (wid & 3) == 0 && lane == 0 && t >= W3_T0 && t < W3_T0 + 4)                           \
-      g_w3_stamps[((blockIdx.x * 2 + (wid >> 2)) * 4 + (t - W3_T0)) * 6 + (k)] = __builtin_amdgcn_s_memtime();   \
-  } while (0)
-#else
-#define W3_STAMP(k) do { } while (0)
-#endif
 
 __global__ __launch_bounds__(W3_NTH, 1) void wgrad_conv3_kernel(W3Params P) {
   __shared__ __attribute__((aligned(16))) char smem[W3_NBUF * W3_BUF];
@@ -142,9 +127,6 @@ __global__ __launch_bounds__(W3_NTH, 1) void wgrad_conv3_kernel(W3Params P) {
   const int64_t a_step = (int64_t)W3_BK * P.lda * 2, b_step = (int64_t)W3_BK * P.ldb * 2;
 
   auto dma = [&](int t) {
-#ifdef W3_SKIP_DMA
-    if (t >= 3) return;       // probe: the loop's DMA left out (operands stale), prologue kept
-#endif
     const uint32_t buf = lds0 + (uint32_t)((t & (W3_NBUF - 1)) * W3_BUF);
     const v4i32 da = w3_desc(Ag + t * a_step);
     const v4i32 db = w3_desc(Bg + t * b_step);
@@ -163,7 +145,6 @@ __global__ __launch_bounds__(W3_NTH, 1) void wgrad_conv3_kernel(W3Params P) {
   // rows that leave the image (r = -1 or 64: tap 0 / tap 2 at a window edge) only feed masked elements, and their
   // addresses stay inside this buffer
   int b_base[3][2];
-  int b_addr[3][2][2];   // (W3_SKIP_READS probe only)
   int tap[3];
 #pragma unroll
   for (int f = 0; f < 3; ++f) {
@@ -172,10 +153,6 @@ __global__ __launch_bounds__(W3_NTH, 1) void wgrad_conv3_kernel(W3Params P) {
     tap[f] = j;
 #pragma unroll
     for (int h = 0; h < 2; ++h) b_base[f][h] = W3_A + cb * 2048 + w3_kfield((8 * g + 4 * h + q + j - 1) & 63) + 8 * p;
-#pragma unroll
-    for (int u = 0; u < 2; ++u)
-#pragma unroll
-      for (int h = 0; h < 2; ++h) b_addr[f][u][h] = b_base[f][h] + 1024 * u;
   }
   // window masks: element 0 of the fragment (token 32u + 8g) for tap 0, element 7 (token 32u + 8g + 7) for tap 2;
   // branch-free per fragment (all-ones for the other taps)
@@ -209,26 +186,17 @@ __global__ __launch_bounds__(W3_NTH, 1) void wgrad_conv3_kernel(W3Params P) {
   // ---- prologue: K-tiles 0..2 in flight, tile 0 retired and published
   dma(0);
   if (nk > 1) dma(1);
-#if W3_SCHED == 2
-  if (nk > 1) w3_vmcnt<W3_DMA>();
-  else w3_vmcnt<0>();
-#else
   if (nk > 2) dma(2);
   if (nk > 2) w3_vmcnt<2 * W3_DMA>();
   else if (nk > 1) w3_vmcnt<W3_DMA>();
   else w3_vmcnt<0>();
-#endif
   w3_barrier();
-#ifndef W3_NO_STAGGER
   if (wr == 1) w3_barrier();                         // group 1 runs one barrier behind group 0
-#endif
 
   uint4 af[2][8], bfr[2][3];
   for (int t = 0; t < nk; ++t) {
     // ---- read segment: this group's fragments of K-tile t, the DMA of t + 3, retire t + 1
-    W3_STAMP(0);
     const char* buf = smem + (t & (W3_NBUF - 1)) * W3_BUF;
-#ifndef W3_SKIP_READS
     {
       // one lane base per read kind, the rest as immediate offsets of the ds_read instructions
       const char* pa_lo = buf + wr * 8 * 2048 + a_lo;
@@ -245,34 +213,14 @@ __global__ __launch_bounds__(W3_NTH, 1) void wgrad_conv3_kernel(W3Params P) {
         for (int u = 0; u < 2; ++u) bfr[u][f] = w3_tr(pb_lo + 1024 * u, pb_hi + 1024 * u);
       }
     }
-#else
-    if (t == 0) {             // probe: fragments read once, the loop's LDS reads left out
-      for (int u = 0; u < 2; ++u)
-        for (int i = 0; i < 8; ++i) af[u][i] = w3_tr(buf + (wr * 8 + i) * 2048 + 1024 * u + a_lo, buf + a_hi);
-      for (int u = 0; u < 2; ++u)
-        for (int f = 0; f < 3; ++f) bfr[u][f] = w3_tr(buf + b_addr[f][u][0], buf + b_addr[f][u][1]);
-    }
-#endif
-#if W3_SCHED == 1
     // DMA of K-tile t + 3 into buffer (t - 1) % 4: the other group read tile t - 1 in the previous segment and retired
     // those reads before the barrier (the lgkmcnt(0) below), so the buffer is free
     if (t + 3 < nk) dma(t + 3);
     const int newer = min(nk - 1, t + 3) - (t + 1);   // tiles issued after t + 1 (still allowed in flight)
-#elif W3_SCHED == 2
-    // DMA of K-tile t + 2 into buffer (t - 2) % 4, consumed by both groups' MFMAs before the last barrier
-    if (t + 2 < nk) dma(t + 2);
-    const int newer = min(nk - 1, t + 2) - (t + 1);
-#else
-    // the DMA of K-tile t + 3 goes out in this tile's MFMA segment (see there); tiles t + 1 and t + 2 are in flight
-    const int newer = min(nk - 1, t + 2) - (t + 1);
-#endif
     if (newer >= 2) w3_vmcnt<2 * W3_DMA>();
     else if (newer == 1) w3_vmcnt<W3_DMA>();
     else w3_vmcnt<0>();
-#if W3_SCHED == 1
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this buffer's reads retire before the barrier (WAR)
-#endif
-#if W3_SCHED == 1 && !defined(W3_MASK_IN_M)
     // the window masks while the reads are retired anyway: the MFMA segment opens with MFMAs (no VALU head)
 #pragma unroll
     for (int u = 0; u < 2; ++u)
@@ -281,26 +229,11 @@ __global__ __launch_bounds__(W3_NTH, 1) void wgrad_conv3_kernel(W3Params P) {
         bfr[u][f].x &= mlo[f];
         bfr[u][f].w &= mhi[f];
       }
-#endif
     // otherwise the reads' own lgkmcnt waits come at their first use in the MFMA segment: their latency overlaps the
     // barrier and the other group's MFMAs
-    W3_STAMP(1);
     w3_barrier();
-    W3_STAMP(2);
     // ---- MFMA segment
-#if W3_SCHED != 1 || defined(W3_MASK_IN_M)
-#pragma unroll
-    for (int u = 0; u < 2; ++u)
-#pragma unroll
-      for (int f = 0; f < 3; ++f) {
-        bfr[u][f].x &= mlo[f];
-        bfr[u][f].w &= mhi[f];
-      }
-#endif
-#ifndef W3_NO_PRIO
     __builtin_amdgcn_s_setprio(1);
-#endif
-#ifndef W3_SKIP_MFMA
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
 #pragma unroll
@@ -309,23 +242,7 @@ __global__ __launch_bounds__(W3_NTH, 1) void wgrad_conv3_kernel(W3Params P) {
         for (int f = 0; f < 3; ++f)
           acc[i][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, af[u][i]),
                                                              __builtin_bit_cast(bf16x8, bfr[u][f]), acc[i][f], 0, 0, 0);
-#if W3_SCHED == 0
-      // K-tile t + 3 -> buffer (t - 1) % 4, issued behind the first 24 MFMAs: both groups finished reading tile
-      // t - 1 before the barrier that opened this segment (the other group's MFMAs of t - 1 consumed them), so the
-      // DMA cannot overwrite data still being read (WAR); its issue cost hides among the MFMAs
-      if (u == 0 && t + 3 < nk) dma(t + 3);
-#endif
     }
-#else
-#pragma unroll
-    for (int u = 0; u < 2; ++u)     // probe: MFMAs left out, the fragments kept live
-#pragma unroll
-      for (int i = 0; i < 8; ++i) asm volatile("" ::"v"(af[u][i].x), "v"(af[u][i].w));
-#pragma unroll
-    for (int u = 0; u < 2; ++u)
-#pragma unroll
-      for (int f = 0; f < 3; ++f) asm volatile("" ::"v"(bfr[u][f].x), "v"(bfr[u][f].w));
-#endif
     const bool rs_now = tile_rowsum && rs_count == 0;
     rs_count = rs_count == 0 ? P.tiles_i - 1 : rs_count - 1;
     if (rs_now) {
@@ -344,17 +261,10 @@ __global__ __launch_bounds__(W3_NTH, 1) void wgrad_conv3_kernel(W3Params P) {
       }
 #undef W3_RS
     }
-#ifndef W3_NO_PRIO
     __builtin_amdgcn_s_setprio(0);
-#endif
-    W3_STAMP(3);
-    W3_STAMP(4);
     w3_barrier();
-    W3_STAMP(5);
   }
-#ifndef W3_NO_STAGGER
   if (wr == 0) w3_barrier();                         // both groups end on the same barrier count
-#endif
 
   // ---- epilogue: this tile owns its output block -> plain read-modify-write of the f32 gradient
   const float alpha = P.alpha;
@@ -499,9 +409,6 @@ __global__ __launch_bounds__(WT_NTH, 1) void wgrad_tt_kernel(WTParams P) {
     const int64_t extA = ((int64_t)(P.K - 1) * lda + pr.M - m0) * 2;   // valid bytes from the tile's row 0
     const int64_t extB = ((int64_t)(P.K - 1) * ldb + pr.N - n0) * 2;
     auto dma = [&](int t) {
-#ifdef WT_SKIP_DMA
-      if (t >= k0 + 3) return;    // probe: the loop's DMA left out (operands stale)
-#endif
       const uint32_t buf = lds0 + (uint32_t)((t & (WT_NBUF - 1)) * WT_BUF);
       const int64_t ra = (int64_t)t * WT_BK * lda * 2, rb = (int64_t)t * WT_BK * ldb * 2;
       const v4i32 da = wt_desc(Ag + ra, extA - ra), db = wt_desc(Bg + rb, extB - rb);
@@ -534,9 +441,6 @@ __global__ __launch_bounds__(WT_NTH, 1) void wgrad_tt_kernel(WTParams P) {
       // ---- read segment: fragments of stage t, the DMA of t + 3 (into the buffer of t - 1, read by both groups
       //      before the last barrier), retire t + 1
       const char* buf = smem + (t & (WT_NBUF - 1)) * WT_BUF;
-#ifdef WT_SKIP_READS
-      if (t == k0)                // probe: fragments read once per piece
-#endif
       {
         const char* pa_lo = buf + wr * 8 * 1024 + f_lo;
         const char* pa_hi = buf + wr * 8 * 1024 + f_hi;
@@ -556,19 +460,12 @@ __global__ __launch_bounds__(WT_NTH, 1) void wgrad_tt_kernel(WTParams P) {
       w3_barrier();
       // ---- MFMA segment
       __builtin_amdgcn_s_setprio(1);
-#ifndef WT_SKIP_MFMA
 #pragma unroll
       for (int i = 0; i < 8; ++i)
 #pragma unroll
         for (int f = 0; f < 4; ++f)
           acc[i][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, af[i]),
                                                              __builtin_bit_cast(bf16x8, bfr[f]), acc[i][f], 0, 0, 0);
-#else
-#pragma unroll
-      for (int i = 0; i < 8; ++i) asm volatile("" ::"v"(af[i].x), "v"(af[i].w));   // probe: fragments kept live
-#pragma unroll
-      for (int f = 0; f < 4; ++f) asm volatile("" ::"v"(bfr[f].x), "v"(bfr[f].w));
-#endif
       if (rowptr != nullptr && t % pr.tiles_n == tn) {
 #define WT_RS(a, b)                                                                                              \
   rs[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, af[a]), __builtin_bit_cast(bf16x8, ones), \
@@ -599,10 +496,6 @@ __global__ __launch_bounds__(WT_NTH, 1) void wgrad_tt_kernel(WTParams P) {
         }
     }
     bool write = true;
-#ifdef WT_NO_FIX
-    if (P.S > 1) write = false;   // probe: split tiles neither published nor summed (results wrong)
-    else
-#endif
     if (P.S > 1) {
       // ---- one piece of S: take an arrival ticket first; the last to arrive sums the other pieces once they have
       //      published (they took their tickets before it, so they are resident and only store, drain and count: the
@@ -861,20 +754,6 @@ extern "C" int aw_gemm_set_wgrad_policy(int mode) {
   return AW_OK;
 }
 
-#ifdef W3_PROBE
-// tools/probe/wgrad3_probe.py: the kernel alone (variants built with the W3_SKIP_* / W3_NO_STAGGER knobs above)
-extern "C" int w3_probe_grouped(const aw_gemm_args* args, int n, void* stream) {
-  g_policy = 1;
-  return awg::wgrad_conv3_try(args, n, reinterpret_cast<hipStream_t>(stream)) ? aw::check_launch("w3") : -1;
-}
-extern "C" int w3_probe_stamps(uint64_t* host, int n) {
-#ifdef W3_STAMPS
-  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_w3_stamps), n * sizeof(uint64_t)) == hipSuccess ? n : -1;
-#else
-  return 0;
-#endif
-}
-#endif
 
 // ----------------------------------------------------------------------------------------- batched 1-tap wgrad
 extern "C" int64_t aw_wgrad_batch_workspace(const aw_gemm_args* args, int n) {
@@ -894,9 +773,3 @@ extern "C" int aw_wgrad_batch(const aw_gemm_args* args, int n, void* ws, int64_t
   return aw::check_launch("aw_wgrad_batch");
 }
 
-#ifdef WT_PROBE
-// tools/probe/wgrad_tt_probe.py: the stream-K batch kernel alone (variants built with the WT_* knobs above)
-extern "C" int wt_probe_batch(const aw_gemm_args* args, int n, void* ws, int64_t ws_bytes, void* stream) {
-  return aw_wgrad_batch(args, n, ws, ws_bytes, stream);
-}
-#endif

@@ -145,12 +145,17 @@ class MyTransformerDecoder(LightningModule):
             cache[key] = torch.full((1,), scale, device=dev)
         return cache[key]
 
+    # the captured step may run a whole accumulation group as one batch (fused_train_step(groups=G),
+    # arcweld.graphs.StepGraphs)
+    grouped_accumulation = True
+
     @torch.no_grad()
-    def fused_train_step(self, batch, scale, mid_hook=None):
+    def fused_train_step(self, batch, scale, mid_hook=None, groups=1):
         """One training micro-step on the kernels without autograd: training_step followed by
         ``(loss * scale).backward()``.  Gradients accumulate into each parameter's ``.grad`` (the flat optimizer
         views when a Trainer installed ``_grad_sink``); ``mid_hook`` runs once backward_late_parameters() are final
-        (arcweld.decoder.backward).  Returns the loss."""
+        (arcweld.decoder.backward).  groups = G: `batch` is the G micro-batches of an accumulation group concatenated
+        along the sequences, each with its own loss mean (arcweld.decoder.fused_step).  Returns the loss."""
         sink = getattr(self, "_grad_sink", None)
 
         def slot(p):
@@ -160,7 +165,7 @@ class MyTransformerDecoder(LightningModule):
                 p.grad = torch.zeros_like(p)
             return p.grad
 
-        loss, logits = engine.fused_step(self, batch, scale, slot, mid_hook=mid_hook)
+        loss, logits = engine.fused_step(self, batch, scale, slot, mid_hook=mid_hook, groups=groups)
         if self.task == "generate":
             self.log('train/loss', loss, prog_bar=True)
         else:
