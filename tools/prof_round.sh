@@ -2,12 +2,12 @@
 # One GPU call: rocprofv3 kernel trace + stats of the bench (VQ-VAE configs[1] and the configs[2] Transformer line),
 # then three PMC passes of the same command (SQ timing / MFMA / LDS counters; FETCH_SIZE; WRITE_SIZE), each its own
 # run as MI355X_MICROARCH.md prescribes.  usage: TAG=r02 [EXTRA="--no-transformer"] bash tools/prof_round.sh
-# -> gpurun_out/prof_$TAG/
+# -> gpurun_out/prof_$TAG/   (CMD="python3 tools/probe/res_chain_probe.py 5 3" profiles another program instead)
 set -o pipefail
 export TMPDIR=/tmp
 OUT=gpurun_out/prof_${TAG:-run}
 mkdir -p $OUT
-CMD="python3 bench.py --no-cpu-baseline --no-fp32 --no-stress --no-profile --steps ${STEPS:-10} --warmup 3 ${EXTRA:-}"
+CMD=${CMD:-"python3 bench.py --no-cpu-baseline --no-fp32 --no-stress --no-profile --steps ${STEPS:-10} --warmup 3 ${EXTRA:-}"}
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- $CMD > $OUT/trace.log 2>&1 || { tail -20 $OUT/trace.log; exit 1; }
 timeout -s KILL 200 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CU_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE -d $OUT/pmc_sq -o run --output-format csv -- $CMD > $OUT/pmc_sq.log 2>&1 || { tail -20 $OUT/pmc_sq.log; exit 1; }
 timeout -s KILL 200 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_fetch -o run --output-format csv -- $CMD > $OUT/pmc_fetch.log 2>&1 || { tail -20 $OUT/pmc_fetch.log; exit 1; }

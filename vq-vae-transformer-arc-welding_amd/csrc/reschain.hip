@@ -421,12 +421,13 @@ __global__ __launch_bounds__(EC_NTH) void res_chain_fwd_kernel(aw_res_chain_fwd_
       bv[0] = b4.x, bv[1] = b4.y, bv[2] = b4.z, bv[3] = b4.w;
     };
     const EcStore<G> S(tid, row0);
+    // The slice is published as soon as the next operand image holds it (the other waves' next K loops wait for
+    // it); the saved tensor that goes through the scratch (h, x') follows the publish.
     if (!second) {
-      // h = conv1 + b1 (saved pre-activation, via the scratch), a1 = GELU(h) (the next operand image; stored from
-      // there once the slice is published)
-      const rsrc_t rh = ec_rsrc(P.h[r], nbytes);
+      // a1 = GELU(h), h = conv1 + b1: a1 into the next operand image (stored from there once published), then h
+      // (the saved pre-activation) recomputed from the accumulators through the scratch
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
+      for (int j = 0; j < 4; ++j)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           float v[4], y[4], bv[4];
@@ -434,14 +435,24 @@ __global__ __launch_bounds__(EC_NTH) void res_chain_fwd_kernel(aw_res_chain_fwd_
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[e] = acc[i][j][e] + bv[e];
           aw_gelu4(v, y);
-          ec_lds_w8(smem, S.sw[i], ec_pack(v));
           ec_lds_w8(smem, nwb[i] + G::JS * j, ec_pack(y));
           __builtin_amdgcn_sched_barrier(0);   // one fragment at a time: bounded live ranges
+        }
+      ec_publish<G>(smem, L.w, L.lane, c + 1);
+      const rsrc_t rh = ec_rsrc(P.h[r], nbytes);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          float v[4], bv[4];
+          bias(i, bv);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = acc[i][j][e] + bv[e];
+          ec_lds_w8(smem, S.sw[i], ec_pack(v));
         }
         ec_store_scratch<G, WT>(smem, j, S, rh);
         __builtin_amdgcn_sched_barrier(0);
       }
-      ec_publish<G>(smem, L.w, L.lane, c + 1);
       ec_store_slice<G, WT>(smem, no, S, ec_rsrc(P.a1[r], nbytes));
     } else {
       // x' = x + Dropout(conv2 + b2): x' (saved for GELU', via the scratch) and a' = GELU(x') (the next operand
@@ -458,22 +469,25 @@ __global__ __launch_bounds__(EC_NTH) void res_chain_fwd_kernel(aw_res_chain_fwd_
         xr[i][j] = ec_pack(v);
       };
       if (!last) {
-        const rsrc_t rx = ec_rsrc(P.x[r], nbytes);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
+        for (int j = 0; j < 4; ++j)
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             float v[4], y[4];
             resid(i, j, v);
             aw_gelu4(v, y);
-            ec_lds_w8(smem, S.sw[i], xr[i][j]);
             ec_lds_w8(smem, nwb[i] + G::JS * j, ec_pack(y));
             __builtin_amdgcn_sched_barrier(0);   // one fragment at a time: bounded live ranges
           }
+        ec_publish<G>(smem, L.w, L.lane, c + 1);
+        const rsrc_t rx = ec_rsrc(P.x[r], nbytes);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) ec_lds_w8(smem, S.sw[i], xr[i][j]);
           ec_store_scratch<G, WT>(smem, j, S, rx);
           __builtin_amdgcn_sched_barrier(0);
         }
-        ec_publish<G>(smem, L.w, L.lane, c + 1);
       } else {
 #pragma unroll
         for (int i = 0; i < 4; ++i)
