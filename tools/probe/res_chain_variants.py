@@ -10,17 +10,21 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(os.path.dirname(HERE))
 SRC = os.path.join(REPO, "vq-vae-transformer-arc-welding_amd", "csrc")
-VARIANTS = {"base": 0, "no_store": 1, "small_w": 2, "stamps": 4}
+# name -> EC_PROBE_FLAGS, or (EC_PROBE_FLAGS, extra -D defines)
+VARIANTS = {"base": 0, "base2": 0, "no_gelu": 16, "stag0": (0, ["-DEC_STAGGER=0"]),
+            "stag80": (0, ["-DEC_STAGGER=80"]), "stag300": (0, ["-DEC_STAGGER=300"]),
+            "stag500": (0, ["-DEC_STAGGER=500"])}
 
 
 def build():
     os.makedirs(os.path.join(HERE, "build"), exist_ok=True)
     procs = []
     for name, fl in VARIANTS.items():
+        fl, extra = fl if isinstance(fl, tuple) else (fl, [])
         out = os.path.join(HERE, "build", f"ec_{name}.so")
         procs.append(subprocess.Popen(
             ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-fPIC", "-shared", "-std=c++17", "-Wl,-Bsymbolic",
-             f"-DEC_PROBE_FLAGS={fl}", "-I" + os.path.join(REPO, "include"), os.path.join(SRC, "reschain.hip"),
+             f"-DEC_PROBE_FLAGS={fl}", *extra, "-I" + os.path.join(REPO, "include"), os.path.join(SRC, "reschain.hip"),
              os.path.join(SRC, "runtime.hip"), "-o", out]))
     for p in procs:
         assert p.wait() == 0

@@ -22,7 +22,9 @@
 //    instruction;
 //  * no workgroup barrier between convs: wave w publishes its 64-channel slice of the next image with an LDS flag,
 //    and a K step of the next conv waits only for the slice it reads (K steps 2w', 2w' + 1 of the first tap = wave
-//    w''s slice).  The waves drift apart, so one wave's epilogue (VALU, stores) runs under its SIMD partner's MFMAs.
+//    w''s slice).  The waves drift apart, so one wave's epilogue (VALU, stores) runs under its SIMD partner's MFMAs
+//    (an initial half-conv delay of waves 4-7 helped an earlier form of the epilogues by 10 %; with the early
+//    publish and line-loaded pre-activations it costs 2-5 %, so all waves start together).
 //    The image ring stays safe: a wave writing image (c + 2) & 1 in conv c + 1's epilogue has read all of conv c's
 //    slices, so every wave is past conv c's K loop (the one that read that image);
 //  * the product is computed transposed, C^T = W X^T (v_mfma_f32_16x16x32_bf16, A = weight rows, B = tokens), so a
@@ -47,7 +49,8 @@
 // Probe builds only (tools/probe/res_chain_variants.py compiles this file alone with -DEC_PROBE_FLAGS=n; the
 // library never sets it): 1 = no global stores, 2 = every weight load reads the first 64 KB of its matrix
 // (L1/L2-resident), 4 = per-conv s_memtime stamps of wave 0 into g_ec_stamps (K loop start, K loop end, epilogue
-// end, slice published).  Results of the probe builds are garbage by construction.
+// end, slice published), 8 = no slice-flag waits, 16 = GELU / GELU' replaced by the identity / one, 32 = no saved
+// tensor through the scratch (forward).  Results of the probe builds are garbage by construction.
 #ifndef EC_PROBE_FLAGS
 #define EC_PROBE_FLAGS 0
 #endif
@@ -173,17 +176,6 @@ __device__ __forceinline__ void ec_load_image(char* img, const void* src, int64_
   }
 }
 
-// Waves 4-7 (the SIMD partners of waves 0-3) start ~10 k cycles (about half an encoder conv) late, so that on every
-// SIMD one wave's epilogue (VALU, LDS, stores) tends to run under the other's MFMAs; the slice hand-offs keep the
-// phase shift (the early waves' K steps 8-15 read the late waves' slices).  Probe, same box: forward 257 -> 223 us,
-// backward 265 -> 247 us (encoder).
-__device__ __forceinline__ void ec_stagger(int tid) {
-  if ((tid >> 6) >= 4) {
-    __builtin_amdgcn_s_sleep(127);
-    __builtin_amdgcn_s_sleep(40);
-  }
-}
-
 // ---------------------------------------------------------------- inter-wave hand-off through LDS
 typedef __attribute__((address_space(3))) volatile int lds_vint;
 template <class G> __device__ __forceinline__ lds_vint* ec_flag(char* smem, int wv) {
@@ -192,6 +184,7 @@ template <class G> __device__ __forceinline__ lds_vint* ec_flag(char* smem, int 
 }
 // wait until wave wv has published `target` epilogues (its slice of the image this conv reads is written)
 template <class G> __device__ __forceinline__ void ec_wait(char* smem, int wv, int target) {
+  if constexpr ((EC_PROBE_FLAGS & 8) != 0) return;
   while (__builtin_amdgcn_readfirstlane(*ec_flag<G>(smem, wv)) < target) __builtin_amdgcn_s_sleep(1);
   asm volatile("" ::: "memory");   // the image reads that follow stay behind the flag read
 }
@@ -200,6 +193,26 @@ template <class G> __device__ __forceinline__ void ec_publish(char* smem, int w,
   ec_stamp(count - 1, 3);
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   if (lane == 0) *ec_flag<G>(smem, w) = count;
+}
+
+// One epilogue scheduling region per fragment: bounded live ranges (regions of 2, 4 or 16 fragments, letting the
+// scheduler interleave their VALU chains, measured within 1-3 %: the epilogue is bound by its VALU issue, not by
+// dependency latency).
+__device__ __forceinline__ void ec_frag_fence(int) { __builtin_amdgcn_sched_barrier(0); }
+
+__device__ __forceinline__ void ec_gelu4(const float (&v)[4], float (&y)[4]) {
+  if constexpr ((EC_PROBE_FLAGS & 16) != 0) {
+    for (int e = 0; e < 4; ++e) y[e] = v[e];
+  } else {
+    aw_gelu4(v, y);
+  }
+}
+__device__ __forceinline__ void ec_gelu_grad4(const float (&v)[4], float (&y)[4]) {
+  if constexpr ((EC_PROBE_FLAGS & 16) != 0) {
+    for (int e = 0; e < 4; ++e) y[e] = 1.f;
+  } else {
+    aw_gelu_grad4(v, y);
+  }
 }
 
 // Weight fragment (i, s) of wave w (rows 64w + 16i .. +15, k 32s .. 32s + 31) in the fragment-packed layout: block
@@ -384,7 +397,6 @@ __global__ __launch_bounds__(EC_NTH) void res_chain_fwd_kernel(aw_res_chain_fwd_
   const uint64_t grp0 = (uint64_t)(row0 + L.li) * (EC_H / 4) + 16 * L.w + L.g;
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __syncthreads();
-  ec_stagger(tid);
 
   for (int c = 0; c < NC; ++c) {
     const int r = c >> 1;
@@ -434,14 +446,14 @@ __global__ __launch_bounds__(EC_NTH) void res_chain_fwd_kernel(aw_res_chain_fwd_
           bias(i, bv);
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[e] = acc[i][j][e] + bv[e];
-          aw_gelu4(v, y);
+          ec_gelu4(v, y);
           ec_lds_w8(smem, nwb[i] + G::JS * j, ec_pack(y));
-          __builtin_amdgcn_sched_barrier(0);   // one fragment at a time: bounded live ranges
+          ec_frag_fence(4 * j + i);
         }
       ec_publish<G>(smem, L.w, L.lane, c + 1);
       const rsrc_t rh = ec_rsrc(P.h[r], nbytes);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
+      for (int j = 0; j < ((EC_PROBE_FLAGS & 32) ? 0 : 4); ++j) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           float v[4], bv[4];
@@ -475,14 +487,14 @@ __global__ __launch_bounds__(EC_NTH) void res_chain_fwd_kernel(aw_res_chain_fwd_
           for (int i = 0; i < 4; ++i) {
             float v[4], y[4];
             resid(i, j, v);
-            aw_gelu4(v, y);
+            ec_gelu4(v, y);
             ec_lds_w8(smem, nwb[i] + G::JS * j, ec_pack(y));
-            __builtin_amdgcn_sched_barrier(0);   // one fragment at a time: bounded live ranges
+            ec_frag_fence(4 * j + i);
           }
         ec_publish<G>(smem, L.w, L.lane, c + 1);
         const rsrc_t rx = ec_rsrc(P.x[r], nbytes);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
+        for (int j = 0; j < ((EC_PROBE_FLAGS & 32) ? 0 : 4); ++j) {
 #pragma unroll
           for (int i = 0; i < 4; ++i) ec_lds_w8(smem, S.sw[i], xr[i][j]);
           ec_store_scratch<G, WT>(smem, j, S, rx);
@@ -496,7 +508,7 @@ __global__ __launch_bounds__(EC_NTH) void res_chain_fwd_kernel(aw_res_chain_fwd_
             float v[4];
             resid(i, j, v);
             ec_lds_w8(smem, nwb[i] + G::JS * j, xr[i][j]);
-            __builtin_amdgcn_sched_barrier(0);   // one fragment at a time: bounded live ranges
+            ec_frag_fence(4 * i + j);
           }
       }
       ec_store_slice<G, WT>(smem, no, S, ec_rsrc(P.a[r], nbytes));
@@ -531,7 +543,6 @@ __global__ __launch_bounds__(EC_NTH) void res_chain_bwd_kernel(aw_res_chain_bwd_
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __syncthreads();
-  ec_stagger(tid);
 
   for (int c = 0; c < NC; ++c) {
     const int r = R - 1 - (c >> 1);
@@ -542,13 +553,22 @@ __global__ __launch_bounds__(EC_NTH) void res_chain_bwd_kernel(aw_res_chain_bwd_
     const int io = (c & 1) * G::IMG, no = ((c + 1) & 1) * G::IMG;
     f32x4 acc[4][4];
     ec_stamp(c, 0);
-    // the epilogue's pre-activation (h_r for conv2's gradient, x_r for conv1's) and, for conv1's, block r - 1's
-    // dropout keep bits, loaded behind the last K step's weight loads: issued earlier, a load would hold up (in
-    // vmcnt order) the weight loads issued after it, and held across the whole K loop it cost 32 registers
-    u32x2 pre[4][4];
+    // the epilogue's pre-activation (h_r for conv2's gradient, x_r for conv1's) as whole 128-B lines (the wave's
+    // 64-channel slice of 8 tokens per load, as the stores), turned into fragments through the wave's scratch in
+    // the epilogue; and, for conv1's, block r - 1's dropout keep bits.  Loaded behind the last K step's weight loads:
+    // issued earlier, a load would hold up (in vmcnt order) the weight loads issued after it.  Loaded in the
+    // fragment layout (16 rows x 32 B per instruction, every line touched by four instructions) the backward ran
+    // 40 % slower than with the pre-activations left out (probe), against 7 % for the forward's GELU alone.
+    uint4 pl[8];
     u32x2 keep = {0u, 0u};
     auto load_pre = [&] {
-      ec_load_frags(pre, ec_rsrc(second ? P.x[r] : P.h[r], nbytes), fo);
+      const rsrc_t rp = ec_rsrc(second ? P.x[r] : P.h[r], nbytes);
+      const uint32_t gs = (uint32_t)(((row0 + (L.lane >> 3)) * EC_H + 64 * L.w + 8 * (L.lane & 7)) * 2);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rp, gs, 8192 * q, 0);
+        memcpy(&pl[q], &v, 16);
+      }
       if (DROP && second && r > 0) keep = ec_keep(P.drop_masks, r - 1, tid);
     };
     ec_conv<G>(acc, wf, smem, L.rb, io, rc, rn, has_next, L.wl, L.w, c, load_pre, [](int) {});
@@ -556,31 +576,40 @@ __global__ __launch_bounds__(EC_NTH) void res_chain_bwd_kernel(aw_res_chain_bwd_
     int nwb[4];   // this lane's write positions in the next image (fragment i; + JS j)
 #pragma unroll
     for (int i = 0; i < 4; ++i) nwb[i] = L.wb(i) + no;
+    const EcStore<G> S(tid, row0);
+    // tokens 16 j .. 16 j + 15 of the pre lines into the scratch (read back below as this lane's fragments (i, j))
+    auto stage_pre = [&](int j) {
+      *reinterpret_cast<uint4*>(smem + S.sr) = pl[2 * j];
+      *reinterpret_cast<uint4*>(smem + S.sr + 1024) = pl[2 * j + 1];
+    };
+    auto pre_frag = [&](int i, float (&pv)[4]) { ec_unpack(*reinterpret_cast<const u32x2*>(smem + S.sw[i]), pv); };
 
     if (!second) {
       // gh = (W2^T go) * GELU'(h): the next operand image, stored from there (conv1's weight-gradient operand)
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int j = 0; j < 4; ++j) {
+        stage_pre(j);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
+        for (int i = 0; i < 4; ++i) {
           float pv[4], v[4], ag[4];
-          ec_unpack(pre[i][j], pv);
-          aw_gelu_grad4(pv, ag);
+          pre_frag(i, pv);
+          ec_gelu_grad4(pv, ag);
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[e] = aw_epi_mad(acc[i][j][e], ag[e], true, 0.f, false);
           ec_lds_w8(smem, nwb[i] + G::JS * j, ec_pack(v));
-          __builtin_amdgcn_sched_barrier(0);   // one fragment at a time: bounded live ranges
+          ec_frag_fence(4 * j + i);
         }
+      }
       ec_publish<G>(smem, L.w, L.lane, c + 1);
-      ec_store_slice<G, WT>(smem, no, EcStore<G>(tid, row0), ec_rsrc(P.gh[r], nbytes));
+      ec_store_slice<G, WT>(smem, no, S, ec_rsrc(P.gh[r], nbytes));
     } else {
       // gx = gx' + (W1^T gh) * GELU'(x); go = gx * mask(block r - 1) (block r - 1's conv2 operand: the next operand
       // image) or, for r = 0, gx itself (the previous stage's weight-gradient operand, staged in the image)
       auto grad = [&](int i, int j, float (&v)[4]) {
         float pv[4], gv[4], ag[4];
-        ec_unpack(pre[i][j], pv);
+        pre_frag(i, pv);
         ec_unpack(gr[i][j], gv);
-        aw_gelu_grad4(pv, ag);
+        ec_gelu_grad4(pv, ag);
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] = aw_epi_mad(acc[i][j][e], ag[e], true, gv[e], true);
         gr[i][j] = ec_pack(v);
@@ -588,30 +617,34 @@ __global__ __launch_bounds__(EC_NTH) void res_chain_bwd_kernel(aw_res_chain_bwd_
       if (r > 0) {
         const float dk = DROP ? 1.f / (1.f - P.drop_p) : 1.f;
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j) {
+          stage_pre(j);
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
+          for (int i = 0; i < 4; ++i) {
             float v[4], ds[4] = {1.f, 1.f, 1.f, 1.f}, o[4];
             grad(i, j, v);
             if constexpr (DROP) ec_scales(keep, i, j, dk, ds);
 #pragma unroll
             for (int e = 0; e < 4; ++e) o[e] = v[e] * ds[e];
             ec_lds_w8(smem, nwb[i] + G::JS * j, ec_pack(o));
-            __builtin_amdgcn_sched_barrier(0);   // one fragment at a time: bounded live ranges
+            ec_frag_fence(4 * j + i);
           }
+        }
         ec_publish<G>(smem, L.w, L.lane, c + 1);
       } else {
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j) {
+          stage_pre(j);
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
+          for (int i = 0; i < 4; ++i) {
             float v[4];
             grad(i, j, v);
             ec_lds_w8(smem, nwb[i] + G::JS * j, gr[i][j]);
-            __builtin_amdgcn_sched_barrier(0);   // one fragment at a time: bounded live ranges
+            ec_frag_fence(4 * j + i);
           }
+        }
       }
-      ec_store_slice<G, WT>(smem, no, EcStore<G>(tid, row0), ec_rsrc(P.gxo_out[r], nbytes));
+      ec_store_slice<G, WT>(smem, no, S, ec_rsrc(P.gxo_out[r], nbytes));
     }
     ec_stamp(c, 2);
   }
