@@ -11,9 +11,9 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(os.path.dirname(HERE))
 SRC = os.path.join(REPO, "vq-vae-transformer-arc-welding_amd", "csrc")
 # name -> EC_PROBE_FLAGS, or (EC_PROBE_FLAGS, extra -D defines)
-VARIANTS = {"base": 0, "base2": 0, "no_gelu": 16, "stag0": (0, ["-DEC_STAGGER=0"]),
-            "stag80": (0, ["-DEC_STAGGER=80"]), "stag300": (0, ["-DEC_STAGGER=300"]),
-            "stag500": (0, ["-DEC_STAGGER=500"])}
+VARIANTS = {"base": 0, "base2": 0, "no_gelu": 16, "scalar": (0, ["-DEC_SCALAR_GELU=1"]),
+            "scalar_noslp": (0, ["-DEC_SCALAR_GELU=1", "-fno-slp-vectorize"]),
+            "noslp": (0, ["-fno-slp-vectorize"])}
 
 
 def build():

@@ -200,18 +200,23 @@ template <class G> __device__ __forceinline__ void ec_publish(char* smem, int w,
 // dependency latency).
 __device__ __forceinline__ void ec_frag_fence(int) { __builtin_amdgcn_sched_barrier(0); }
 
+// GELU / GELU' of a fragment's 4 values, element by element (the same operations as aw_gelu4 / aw_gelu_grad4, so
+// the same bits as the unfused GEMM epilogues): written per element, the compiler packs only where it pays (the
+// fully packed pair form measured 3 % slower here, MI355X_MICROARCH.md: packed f32 VALU beside MFMAs)
 __device__ __forceinline__ void ec_gelu4(const float (&v)[4], float (&y)[4]) {
   if constexpr ((EC_PROBE_FLAGS & 16) != 0) {
     for (int e = 0; e < 4; ++e) y[e] = v[e];
   } else {
-    aw_gelu4(v, y);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) y[e] = gelu_erf_fast(v[e]);
   }
 }
 __device__ __forceinline__ void ec_gelu_grad4(const float (&v)[4], float (&y)[4]) {
   if constexpr ((EC_PROBE_FLAGS & 16) != 0) {
     for (int e = 0; e < 4; ++e) y[e] = 1.f;
   } else {
-    aw_gelu_grad4(v, y);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) y[e] = gelu_erf_grad_fast(v[e]);
   }
 }
 
