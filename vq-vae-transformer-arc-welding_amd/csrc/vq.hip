@@ -1,11 +1,12 @@
 // Vector quantizer (model/vector_quantizer.py:59-131) for gfx950.
 //
-// Forward: register-blocked distance tiles with the codebook streamed through LDS (see vq_fwd_kernel).
-// Distances follow the reference expression exactly in fp32:
+// Forward: distances follow the reference expression exactly in fp32:
 //     d_k = fl( fl(|z|^2 + |e_k|^2) - 2 * dot(z, e_k) ),  dot = k-ordered fmaf chain over the embedding dim
 // (torch's CPU sgemm on this shape is bit-identical to that chain -- measured), so the
-// argmin (lexicographic (d, k) minimum == torch.argmin first-index tie rule) is bit-exact.
-// No MFMA (the north-star design): fp32 VALU, whose rate equals the f32-input MFMA's on gfx950.
+// argmin (lexicographic (d, k) minimum == torch.argmin first-index tie rule) is bit-exact.  Two kernels:
+//   * vq_fwd_pinned_kernel (K <= 512, D <= 64, the configs[1] codebook): the codebook pinned in LDS, the dot
+//     products on the f32-input MFMA, which is bit for bit the same fmaf chain;
+//   * vq_fwd_kernel (any K, D <= 256): register-blocked fp32 VALU tiles with the codebook streamed through LDS.
 #include <stdlib.h>
 
 #include "common.h"
@@ -299,10 +300,39 @@ __global__ __launch_bounds__(VQ_THREADS, 2) void vq_fwd_kernel(const float* __re
 }
 
 // Codebook-pinned form (K <= 512, D <= 64: the configs[1] codebook, 512 x 64 fp32 = 128 KB): ONE workgroup per CU
-// of 64 rows stages the whole codebook into LDS once ([d][code], transposed on the way in, as the streaming
-// kernel's chunks) beside its z tile, then runs the full embedding dim without a barrier -- no per-chunk staging,
-// no load latency per chunk.  Same per-lane register blocks, same in-order fma chains, norms and (d, k) argmin as
-// vq_fwd_kernel, so the same bits.
+// of 64 rows keeps the whole codebook in LDS and runs the dot products on the f32-input MFMA
+// (v_mfma_f32_32x32x2_f32).  That instruction is bit for bit a k-ordered fmaf chain -- D = fma(a_k1, b_k1,
+// fma(a_k0, b_k0, C)) with one rounding per product (cdna_hip_programming.md, 'FP32-input MFMA') -- so step s over
+// dims (2s, 2s + 1) continues exactly the chain the VALU kernel runs, at the vector rate but off the vector pipe,
+// with four steps' operands per 16-B LDS read.  Wave w owns codes 64w .. 64w + 63 (M, two 32-code tiles) x all 64
+// rows (N, two 32-row tiles); lane l ends with row (l & 31) of each row tile against 32 of the wave's codes.
+//
+// The codebook arrives in 16-dim chunks: all of its loads are issued at once, and each chunk is stored and its MFMA
+// steps run as soon as its data is in (one LDS barrier per chunk), so the load latency overlaps the matrix work;
+// the norms |e_k|^2 and |z|^2 accumulate chunk by chunk beside the MFMAs.  The codebook stays in LDS to the end:
+// the epilogue gathers z_q's code rows from it (no dependent global load).
+template <int D> struct VqPinLds {
+  static constexpr int ROWS = 64;
+  static constexpr int ES = 0, ZS = ES + VQ_CODES * D, EES = ZS + ROWS * D, ZZS = EES + VQ_CODES;
+  static constexpr int RD = ZZS + ROWS, RK = RD + 8 * ROWS, HIST = RK + 8 * ROWS, RED = HIST + VQ_CODES;
+  static constexpr int TOTAL = RED + 16;                     // floats (RED: 8 doubles)
+  static_assert(TOTAL * 4 <= 160 * 1024, "pinned VQ LDS");
+};
+
+// Float offset of permuted position p of row c in a [c][D] image.  Positions: dim d sits at (d & 1) * D/2 + (d >> 1)
+// (even dims, then odd), so MFMA lane half h reads steps s .. s + 3 (dims 2s + h, ...) as one float4 at h * D/2 + s;
+// 16-B quads are XOR-swizzled by the row, so the 16 lanes of a ds_read_b128 group (rows distinct mod 16) hit 16
+// distinct quads = all 64 banks (for D = 64; 2- / 4-way at D = 32 / 16).
+template <int D> __device__ __forceinline__ int vq_pos(int c, int p) {
+  return c * D + ((((p >> 2) ^ c) & (D / 4 - 1)) << 2) + (p & 3);
+}
+
+__device__ __forceinline__ void vq_lds_barrier() {   // LDS-only: no wait for the global loads still in flight
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
 template <int D>
 __global__ __launch_bounds__(VQ_THREADS, 1) void vq_fwd_pinned_kernel(const float* __restrict__ z,
                                                                      const float* __restrict__ E, int64_t N, int K,
@@ -310,123 +340,213 @@ __global__ __launch_bounds__(VQ_THREADS, 1) void vq_fwd_pinned_kernel(const floa
                                                                      float* __restrict__ counts,
                                                                      double* __restrict__ sqerr, void* __restrict__ zq2,
                                                                      int zq2_bf16) {
-  constexpr int RPL = 8, ROWS = 64, ZP = D + 4, EP = VQ_CODES + 4, NQ = D / 4;
-  constexpr int ZF = ROWS * ZP, EF = D * EP;
+  typedef __attribute__((ext_vector_type(16))) float f32x16;
+  using L = VqPinLds<D>;
+  constexpr int ROWS = L::ROWS, NQ = D / 4, NCH = D / 16, H2 = D / 2;
+  constexpr int ZPT = (ROWS * NQ + VQ_THREADS - 1) / VQ_THREADS;   // z float4 per thread
   static_assert(D % 16 == 0 && D <= 64, "pinned codebook: D 16..64");
-  __shared__ __attribute__((aligned(16))) float smem[ZF + EF + VQ_CODES + ROWS];
-  float* zs = smem;
-  float* es = smem + ZF;                   // [D][VQ_CODES (+4)]
-  float* ees = es + EF;                    // [VQ_CODES]
-  float* zzs = ees + VQ_CODES;             // [ROWS]
+  __shared__ __attribute__((aligned(16))) float smem[L::TOTAL];
+  float* es = smem + L::ES;                // [VQ_CODES][D] permuted + swizzled (vq_pos)
+  float* zs = smem + L::ZS;                // [ROWS][D] likewise
+  float* ees = smem + L::EES;              // [VQ_CODES]: |e_k|^2, NaN for k >= K
+  float* zzs = smem + L::ZZS;              // [ROWS]
+  float* rd = smem + L::RD;                // [8 waves][ROWS] per-wave row minima
+  int* rk = reinterpret_cast<int*>(smem + L::RK);
+  float* hist = smem + L::HIST;            // [VQ_CODES] this workgroup's code counts
+  double* red = reinterpret_cast<double*>(smem + L::RED);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int lr = lane >> 3, lc = lane & 7;
+  const int h = lane >> 5, jr = lane & 31;
   const int64_t row0 = (int64_t)blockIdx.x * ROWS;
 
-  // ---- the codebook: float4 (u, dc) of thread t = quad t & 3 of dims 16 dc .. of code 128 u + (t >> 2), all in
-  //      flight at once (codes >= K read as zero), then stored transposed; the z tile behind them
-  float4 pre[4][D / 16];
+  // ---- loads: the z tile first, then the codebook chunk by chunk (float4 (dc, u) of thread t = quad t & 3 of dims
+  //      16 dc .. of code 128 u + (t >> 2)), all in flight at once.  Addresses are clamped instead of predicated:
+  //      codes >= K hold a copy of code K - 1 and are excluded by their NaN norm, rows >= N a copy of row N - 1 and
+  //      are never written.
+  float4 zr[ZPT];
 #pragma unroll
-  for (int dc = 0; dc < D / 16; ++dc)
+  for (int i = 0; i < ZPT; ++i) {
+    const int it = tid + i * VQ_THREADS, r = it / NQ, q = it - r * NQ;
+    const int64_t gr = min(row0 + r, N - 1);
+    if (it < ROWS * NQ) zr[i] = reinterpret_cast<const float4*>(z + gr * D)[q];
+  }
+  float4 pe[NCH][4];
+#pragma unroll
+  for (int dc = 0; dc < NCH; ++dc)
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      const int code = 128 * u + (tid >> 2);
-      pre[u][dc] = code < K ? reinterpret_cast<const float4*>(E + (int64_t)code * D + dc * 16)[tid & 3]
-                            : make_float4(0.f, 0.f, 0.f, 0.f);
+      const int code = min(128 * u + (tid >> 2), K - 1);
+      pe[dc][u] = reinterpret_cast<const float4*>(E + (int64_t)code * D + dc * 16)[tid & 3];
+      if (u == 3) __builtin_amdgcn_sched_barrier(0);   // issue in chunk order: chunk dc waits only for its own
     }
-  for (int i = tid; i < ROWS * NQ; i += VQ_THREADS) {
-    const int r = i / NQ, q = i - r * NQ;
-    const int64_t gr = row0 + r;
-    const float4 v = gr < N ? reinterpret_cast<const float4*>(z + gr * D)[q] : make_float4(0.f, 0.f, 0.f, 0.f);
-    *reinterpret_cast<float4*>(zs + r * ZP + 4 * q) = v;
-  }
+  // a float4 of dims 4q .. 4q + 3 goes to the image as two 8-B halves: (4q, 4q + 2) at 2q, (4q + 1, 4q + 3) at D/2 + 2q
+  auto put4 = [&](float* img, int c, int q, const float4& v) {
+    *reinterpret_cast<float2*>(img + vq_pos<D>(c, 2 * q)) = make_float2(v.x, v.z);
+    *reinterpret_cast<float2*>(img + vq_pos<D>(c, H2 + 2 * q)) = make_float2(v.y, v.w);
+  };
 #pragma unroll
-  for (int dc = 0; dc < D / 16; ++dc)
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      float* dst = es + (16 * dc + 4 * (tid & 3)) * EP + 128 * u + (tid >> 2);
-      dst[0 * EP] = pre[u][dc].x;
-      dst[1 * EP] = pre[u][dc].y;
-      dst[2 * EP] = pre[u][dc].z;
-      dst[3 * EP] = pre[u][dc].w;
-    }
-  __syncthreads();
-  // ---- |z|^2 per row and |e_k|^2 per code: in-order sums of squares
-  if (tid < ROWS) {
-    float s = 0.f;
-    for (int d = 0; d < D; ++d) s = __fadd_rn(s, __fmul_rn(zs[tid * ZP + d], zs[tid * ZP + d]));
-    zzs[tid] = s;
+  for (int i = 0; i < ZPT; ++i) {
+    const int it = tid + i * VQ_THREADS, r = it / NQ, q = it - r * NQ;
+    if (it < ROWS * NQ) put4(zs, r, q, zr[i]);
   }
-  {
-    float s = 0.f;
-#pragma unroll 16
-    for (int d = 0; d < D; ++d) s = __fadd_rn(s, __fmul_rn(es[d * EP + tid], es[d * EP + tid]));
-    ees[tid] = s;
-  }
-  __syncthreads();
+  hist[tid] = 0.f;
 
-  f32x2 acc[RPL][4];               // [row i][code pair jp]: codes 8lc + 2jp, 8lc + 2jp + 1
+  // ---- chunk loop: store chunk dc, barrier, its 8 MFMA steps (two groups of four) and the norms' next 16 terms
+  f32x16 acc[2][2];                // [code tile mi][row tile ni]
 #pragma unroll
-  for (int i = 0; i < RPL; ++i)
+  for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x2{0.f, 0.f};
-  // software-pipelined LDS reads: the z quads of step q + 1 and the code values of the next embedding index are in
-  // flight while the current index's 32 packed FMAs issue (read at their use, the waves waited on LDS half the time)
-  const float* eb = es + w * 64 + 8 * lc;
-  const float* zb = zs + lr * ZP;
-  float4 zc[RPL], zn[RPL];
+    for (int ni = 0; ni < 2; ++ni)
 #pragma unroll
-  for (int i = 0; i < RPL; ++i) zc[i] = *reinterpret_cast<const float4*>(zb + 8 * i * ZP);
-  float4 e0 = *reinterpret_cast<const float4*>(eb), e1 = *reinterpret_cast<const float4*>(eb + 4);
-#pragma unroll 1
-  for (int q = 0; q < NQ; ++q) {
-    const int qn = q + 1 < NQ ? q + 1 : q;   // the last step re-reads its own quads (unused)
+      for (int r = 0; r < 16; ++r) acc[mi][ni][r] = 0.f;
+  float ee = 0.f, zz = 0.f;        // in-order sums of squares: code tid, and row lane (wave 7)
+  auto sumsq16 = [&](const float* img, int c, int dc, float s) {   // dims 16 dc .. 16 dc + 15 in order
+    const float4 e0 = *reinterpret_cast<const float4*>(img + vq_pos<D>(c, 8 * dc));
+    const float4 e1 = *reinterpret_cast<const float4*>(img + vq_pos<D>(c, 8 * dc + 4));
+    const float4 o0 = *reinterpret_cast<const float4*>(img + vq_pos<D>(c, H2 + 8 * dc));
+    const float4 o1 = *reinterpret_cast<const float4*>(img + vq_pos<D>(c, H2 + 8 * dc + 4));
+    const float ev[8] = {e0.x, e0.y, e0.z, e0.w, e1.x, e1.y, e1.z, e1.w};
+    const float ov[8] = {o0.x, o0.y, o0.z, o0.w, o1.x, o1.y, o1.z, o1.w};
 #pragma unroll
-    for (int dd = 0; dd < 4; ++dd) {
-      const int dn = 4 * q + dd + 1 < D ? 4 * q + dd + 1 : 4 * q + dd;
-      const float4 n0 = *reinterpret_cast<const float4*>(eb + dn * EP);
-      const float4 n1 = *reinterpret_cast<const float4*>(eb + dn * EP + 4);
-      if (dd == 0) {
-        // issued behind the next code values: LDS reads retire in order, so the code values' waits do not wait
-        // for these
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int i = 0; i < RPL; ++i) zn[i] = *reinterpret_cast<const float4*>(zb + 8 * i * ZP + 4 * qn);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      const f32x2 ep[4] = {f32x2{e0.x, e0.y}, f32x2{e0.z, e0.w}, f32x2{e1.x, e1.y}, f32x2{e1.z, e1.w}};
-#pragma unroll
-      for (int i = 0; i < RPL; ++i) {
-        const float zi = dd == 0 ? zc[i].x : dd == 1 ? zc[i].y : dd == 2 ? zc[i].z : zc[i].w;
-        const f32x2 zp = f32x2{zi, zi};
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_elementwise_fma(zp, ep[j], acc[i][j]);
-      }
-      e0 = n0;
-      e1 = n1;
+    for (int i = 0; i < 8; ++i) {
+      s = __fadd_rn(s, __fmul_rn(ev[i], ev[i]));
+      s = __fadd_rn(s, __fmul_rn(ov[i], ov[i]));
     }
+    return s;
+  };
+  const int ca = 64 * w + jr;      // this lane's A row (code) in tile mi: ca + 32 mi; B row (z row): jr + 32 ni
 #pragma unroll
-    for (int i = 0; i < RPL; ++i) zc[i] = zn[i];
+  for (int dc = 0; dc < NCH; ++dc) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) put4(es, 128 * u + (tid >> 2), 4 * dc + (tid & 3), pe[dc][u]);
+    vq_lds_barrier();
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+      const int p = h * H2 + 8 * dc + 4 * g;     // steps 8 dc + 4 g .. + 3 of lane half h
+      float4 a[2], b[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        a[t] = *reinterpret_cast<const float4*>(es + vq_pos<D>(ca + 32 * t, p));
+        b[t] = *reinterpret_cast<const float4*>(zs + vq_pos<D>(jr + 32 * t, p));
+      }
+      const float av[2][4] = {{a[0].x, a[0].y, a[0].z, a[0].w}, {a[1].x, a[1].y, a[1].z, a[1].w}};
+      const float bv[2][4] = {{b[0].x, b[0].y, b[0].z, b[0].w}, {b[1].x, b[1].y, b[1].z, b[1].w}};
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4)
+#pragma unroll
+        for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < 2; ++ni)
+            acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[mi][s4], bv[ni][s4], acc[mi][ni], 0, 0, 0);
+    }
+    ee = sumsq16(es, tid, dc, ee);
+    if (w == 7) zz = sumsq16(zs, lane, dc, zz);
   }
-  // ---- distances and this lane's (d, k) minimum
-  float best[RPL];
-  int bestk[RPL];
-  const float* eet = ees + w * 64 + 8 * lc;
+  ees[tid] = tid < K ? ee : __builtin_nanf("");
+  if (w == 7) zzs[lane] = zz;
+  vq_lds_barrier();
+
+  // ---- distances d = fl(fl(|z|^2 + |e|^2) - 2 dot) as fma(-2, dot, s) (2 dot is exact, so the one rounding is the
+  //      reference's), two codes per packed op; this lane's minimum per row over its 32 codes, visited in ascending
+  //      k (accumulator register r of tile mi holds code 64w + 32mi + 8(r >> 2) + 4h + (r & 3)), so a strict <
+  //      keeps the first index of a tie.  NaN distances (codes >= K, NaN inputs) never compare less; a lane left
+  //      with none reports (+inf, its first code), which the lexicographic merge below ranks behind every finite
+  //      candidate.
+  float best[2];
+  int bestk[2];
 #pragma unroll
-  for (int i = 0; i < RPL; ++i) {
-    best[i] = __builtin_huge_valf();
-    bestk[i] = 0x7fffffff;
-    const float zz = zzs[lr + 8 * i];
+  for (int ni = 0; ni < 2; ++ni) {
+    const float zr2 = zzs[jr + 32 * ni];
+    float bd = __builtin_huge_valf();
+    int bk = 64 * w + 4 * h;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int gk = w * 64 + 8 * lc + j;
-      const float dot = (j & 1) ? acc[i][j >> 1].y : acc[i][j >> 1].x;
-      const float dist = __fsub_rn(__fadd_rn(zz, eet[j]), __fmul_rn(2.f, dot));
-      lex_take(dist, gk, gk < K, best[i], bestk[i]);
+    for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int c0 = 64 * w + 32 * mi + 8 * g + 4 * h;
+        const float4 e4 = *reinterpret_cast<const float4*>(ees + c0);
+        const f32x2 s01 = f32x2{zr2, zr2} + f32x2{e4.x, e4.y}, s23 = f32x2{zr2, zr2} + f32x2{e4.z, e4.w};
+        const f32x2 d01 = __builtin_elementwise_fma(
+            f32x2{-2.f, -2.f}, f32x2{acc[mi][ni][4 * g], acc[mi][ni][4 * g + 1]}, s01);
+        const f32x2 d23 = __builtin_elementwise_fma(
+            f32x2{-2.f, -2.f}, f32x2{acc[mi][ni][4 * g + 2], acc[mi][ni][4 * g + 3]}, s23);
+        const float dv[4] = {d01.x, d01.y, d23.x, d23.y};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const bool t = dv[r] < bd;
+          bd = t ? dv[r] : bd;
+          bk = t ? c0 + r : bk;
+        }
+      }
+    best[ni] = bd;
+    bestk[ni] = bk;
+  }
+  // ---- lexicographic (d, k) merge of the two lane halves (codes 4h apart), then across the 8 waves (LDS)
+#pragma unroll
+  for (int ni = 0; ni < 2; ++ni) {
+    const float d = __shfl_xor(best[ni], 32, 64);
+    const int k = __shfl_xor(bestk[ni], 32, 64);
+    lex_take(d, k, true, best[ni], bestk[ni]);
+  }
+  if (h == 0) {
+#pragma unroll
+    for (int ni = 0; ni < 2; ++ni) {
+      rd[w * ROWS + jr + 32 * ni] = best[ni];
+      rk[w * ROWS + jr + 32 * ni] = bestk[ni];
     }
   }
-  __syncthreads();   // every wave's codebook reads are done: the E area becomes the exchange scratch
-  vq_finish<D, RPL>(best, bestk, es, EF - 16 * ROWS, zs, reinterpret_cast<double*>(ees), E, N, K, row0, zq, idx,
-                    counts, sqerr, zq2, zq2_bf16);
+  vq_lds_barrier();
+  // ---- thread (row r, quad q) resolves its row's winner from the 8 wave candidates (LDS broadcast reads), takes
+  //      e_k's quad from the pinned codebook and writes z_q (+ the operand copy) coalesced; the q == 0 thread of a
+  //      row writes idx and counts the code in LDS
+  double se = 0.0;
+  for (int it = tid; it < ROWS * NQ; it += VQ_THREADS) {
+    const int r = it / NQ, q = it - r * NQ;
+    const int64_t row = row0 + r;
+    if (row >= N) break;   // rows ascend with it
+    float bd = rd[r];
+    int bk = rk[r];
+#pragma unroll
+    for (int v = 1; v < 8; ++v) lex_take(rd[v * ROWS + r], rk[v * ROWS + r], true, bd, bk);
+    if (bk < 0 || bk >= K) bk = 0;  // all-NaN row guard (torch would return the NaN position)
+    if (q == 0) {
+      idx[row] = bk;
+      atomicAdd(hist + bk, 1.0f);
+    }
+    const float2 e02 = *reinterpret_cast<const float2*>(es + vq_pos<D>(bk, 2 * q));
+    const float2 e13 = *reinterpret_cast<const float2*>(es + vq_pos<D>(bk, H2 + 2 * q));
+    const float2 z02 = *reinterpret_cast<const float2*>(zs + vq_pos<D>(r, 2 * q));
+    const float2 z13 = *reinterpret_cast<const float2*>(zs + vq_pos<D>(r, H2 + 2 * q));
+    const float d0 = __fsub_rn(e02.x, z02.x), d1 = __fsub_rn(e13.x, z13.x);
+    const float d2 = __fsub_rn(e02.y, z02.y), d3 = __fsub_rn(e13.y, z13.y);
+    float4 o;
+    o.x = __fadd_rn(z02.x, d0);  // z + (z_q - z).detach()
+    o.y = __fadd_rn(z13.x, d1);
+    o.z = __fadd_rn(z02.y, d2);
+    o.w = __fadd_rn(z13.y, d3);
+    reinterpret_cast<float4*>(zq + row * D)[q] = o;
+    if (zq2) {   // the GEMM operand copy of z_q (the decoder's first conv reads it): no separate cast launch
+      if (zq2_bf16) {
+        typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+        reinterpret_cast<bf16x4*>(zq2)[row * NQ + q] = bf16x4{(bf16)o.x, (bf16)o.y, (bf16)o.z, (bf16)o.w};
+      } else {
+        reinterpret_cast<float4*>(zq2)[row * NQ + q] = o;
+      }
+    }
+    se += (double)(d0 * d0 + d1 * d1 + d2 * d2 + d3 * d3);
+  }
+  se = wave_sum_d(se);
+  if (lane == 0) red[w] = se;
+  vq_lds_barrier();   // LDS only: no wait for this workgroup's z_q stores
+  if (tid < K) {
+    const float c = hist[tid];
+    if (c != 0.f) atomicAdd(counts + tid, c);
+  }
+  if (tid == 0) {
+    double t = 0.0;
+#pragma unroll
+    for (int v = 0; v < 8; ++v) t += red[v];
+    atomicAdd(sqerr, t);
+  }
 }
 
 __global__ void vq_finalize_kernel(const float* counts, const double* sqerr, int64_t N, int K, int D, float beta,
