@@ -411,29 +411,37 @@ def transformer_traffic():
 
 
 def vq_kernel_roofline(dev, N, K, D, iters=10):
-    """aw_vq_forward alone at (N, K, D): HIP events around each launch on its stream; 2*N*K*D FP32 FLOPs against the
-    157.3 TF fp32 vector peak (the north star's "FP32-VALU-bound" kernel), plus its algorithmic HBM bytes
-    (z + E + idx + z_q + counts)."""
+    """aw_vq_forward_ex2 alone at (N, K, D), called as the training step calls it (the bf16 operand copy of z_q and
+    the grouped code counts, arcweld/vqvae.py): HIP events around each launch on its stream; 2*N*K*D FP32 FLOPs
+    against the 157.3 TF fp32 peak (the f32-input MFMA's = the vector peak: the pinned kernel runs the dot products
+    on the MFMA, the streaming one on the VALU), plus its algorithmic HBM bytes (z + E + idx + z_q + counts)."""
     from arcweld import kernels
+    from arcweld.vqvae import VQ_COUNT_GROUPS
     g = torch.Generator(device=dev).manual_seed(5)
     z = torch.randn(N, D, device=dev, generator=g) * 0.08
     E = torch.randn(K, D, device=dev, generator=g) * 0.08
     zq, idx = torch.empty_like(z), torch.empty(N, dtype=torch.int64, device=dev)
-    counts, sq = torch.zeros(K, device=dev), torch.zeros(1, device=dev, dtype=torch.float64)
+    zq2 = torch.empty(N, D, device=dev, dtype=torch.bfloat16)
+    counts, sq = torch.zeros(VQ_COUNT_GROUPS * K, device=dev), torch.zeros(1, device=dev, dtype=torch.float64)
     s = torch.cuda.current_stream()
-    kernels.vq_forward(z, E, zq, idx, counts, sq)
+
+    def launch():
+        kernels.vq_forward(z, E, zq, idx, counts, sq, zq_copy=zq2, count_groups=VQ_COUNT_GROUPS)
+    launch()
     evs = []
     for _ in range(iters):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(s)
-        kernels.vq_forward(z, E, zq, idx, counts, sq)
+        launch()
         e1.record(s)
         evs.append((e0, e1))
     torch.cuda.synchronize()
     us = sum(a.elapsed_time(b) for a, b in evs) * 1e3 / iters
     tf = 2.0 * N * K * D / (us * 1e-6) / 1e12
-    byts = N * D * 4 * 2 + K * D * 4 + N * 8 + K * 4
-    return {"kernel": "vq_fwd_kernel<D> (aw_vq_forward)", "bound": "fp32-valu", "N": N, "K": K, "D": D,
+    byts = N * D * 4 * 2 + N * D * 2 + K * D * 4 + N * 8 + K * 4
+    pinned = K <= 512 and D in (16, 32, 64)
+    return {"kernel": "vq_fwd_pinned_kernel<D> (f32 MFMA)" if pinned else "vq_fwd_kernel<D> (f32 VALU)",
+            "bound": "fp32-mfma" if pinned else "fp32-valu", "N": N, "K": K, "D": D,
             "avg_launch_us": round(us, 2), "achieved": round(tf, 2), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": round(tf / FP32_PEAK_TFLOPS, 4), "algorithmic_bytes": byts,
             "hbm_gbs": round(byts / (us * 1e-6) / 1e9, 1)}

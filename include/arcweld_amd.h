@@ -214,10 +214,20 @@ int aw_vq_forward(const float* z, const float* E, int64_t N, int K, int D,
  * the GEMM operand of the decoder's first conv, without a separate cast launch. */
 int aw_vq_forward_ex(const float* z, const float* E, int64_t N, int K, int D, float* zq, int64_t* idx, float* counts,
                      double* sqerr, void* zq_copy, int copy_dtype, void* stream);
+/* aw_vq_forward_ex with the code counts split over count_groups partial histograms (1..AW_VQ_COUNT_GROUPS_MAX):
+ * counts holds count_groups x K floats, zero on entry; workgroup b adds into partial b % count_groups, so the adds
+ * into any one address are count_groups times fewer (they serialise at the memory-side atomic units).  The partials
+ * sum to the counts; aw_vq_finalize_ex takes them as they are. */
+#define AW_VQ_COUNT_GROUPS_MAX 64
+int aw_vq_forward_ex2(const float* z, const float* E, int64_t N, int K, int D, float* zq, int64_t* idx, float* counts,
+                      int count_groups, double* sqerr, void* zq_copy, int copy_dtype, void* stream);
 /* loss = m + beta*m with m = sqerr/(N*D) (vector_quantizer.py:107-108); perplexity = exp(-sum p log(p+1e-10)),
  * p = counts/N (:114-115).  Each output is one f32 device scalar. */
 int aw_vq_finalize(const float* counts, const double* sqerr, int64_t N, int K, int D, float beta,
                    float* loss, float* perplexity, void* stream);
+/* aw_vq_finalize over count_groups partial histograms (aw_vq_forward_ex2), summed per code in a fixed order. */
+int aw_vq_finalize_ex(const float* counts, int count_groups, const double* sqerr, int64_t N, int K, int D, float beta,
+                      float* loss, float* perplexity, void* stream);
 /* Backward of the STE + loss: dz = g_zq + g_loss*2(z - z_q)/(N*D);  dE[idx] += g_loss*2*beta*(z_q - z)/(N*D).
  * g_zq may be NULL (treated as 0); g_loss is a device scalar.  dE is accumulated (not overwritten). */
 int aw_vq_backward(const float* z, const float* E, const int64_t* idx, const float* g_zq, const float* g_loss,

@@ -294,6 +294,28 @@ def test_vq_operand_copies_match_the_cast_outputs(K, cdt, Kc, D, N):
             assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("Kc,D,N", [(512, 64, 16384), (512, 64, 1000), (64, 16, 1000), (8192, 256, 4096)])
+@pytest.mark.parametrize("G", [2, 8])
+def test_vq_grouped_counts_sum_to_the_counts(K, Kc, D, N, G):
+    """aw_vq_forward_ex2 / aw_vq_finalize_ex: the count_groups partial histograms sum exactly to the count_groups 1
+    counts (both kernels: pinned MFMA at K <= 512, streaming VALU above), every other output is unchanged, and the
+    finalize over the partials gives the same loss and perplexity bits."""
+    z = torch.tensor(gen.normal(311, (N, D), 0.08), device=DEV)
+    E = torch.tensor(gen.normal(312, (Kc, D), 0.08), device=DEV)
+    outs = []
+    for cg in (1, G):
+        zq, idx = torch.empty_like(z), torch.empty(N, dtype=torch.int64, device=DEV)
+        counts, sq = torch.zeros(cg * Kc, device=DEV), torch.zeros(1, dtype=torch.float64, device=DEV)
+        K.vq_forward(z, E, zq, idx, counts, sq, count_groups=cg)
+        fin = torch.empty(2, device=DEV)
+        K.vq_finalize(counts, sq, N, Kc, D, 0.25, fin[0:1], fin[1:2], count_groups=cg)
+        outs.append((zq, idx, counts.view(cg, Kc).sum(0), fin))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    assert torch.equal(outs[0][2], outs[1][2])
+    assert torch.equal(outs[0][2], torch.bincount(outs[0][1], minlength=Kc).float())
+    torch.testing.assert_close(outs[0][3], outs[1][3], rtol=1e-6, atol=0)   # sqerr: f64 atomics, order varies
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("use_ws", [True, False])
 def test_gemm_split_k_accumulate_colmap(K, tile, dtype, use_ws):

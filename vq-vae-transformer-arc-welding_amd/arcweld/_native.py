@@ -108,6 +108,8 @@ SIGNATURES = {
     "aw_vq_forward": [c_p, c_p, c_i64, c_int, c_int, c_p, c_p, c_p, c_p, c_p],
     "aw_vq_forward_ex": [c_p, c_p, c_i64, c_int, c_int, c_p, c_p, c_p, c_p, c_p, c_int, c_p],
     "aw_vq_finalize": [c_p, c_p, c_i64, c_int, c_int, c_f, c_p, c_p, c_p],
+    "aw_vq_forward_ex2": [c_p, c_p, c_i64, c_int, c_int, c_p, c_p, c_p, c_int, c_p, c_p, c_int, c_p],
+    "aw_vq_finalize_ex": [c_p, c_int, c_p, c_i64, c_int, c_int, c_f, c_p, c_p, c_p],
     "aw_vq_backward": [c_p, c_p, c_p, c_p, c_p, c_i64, c_int, c_int, c_f, c_p, c_p, c_p],
     "aw_vq_backward_ex": [c_p, c_p, c_p, c_p, c_p, c_i64, c_int, c_int, c_f, c_p, c_p, c_p, c_int, c_p],
     "aw_vq_onehot": [c_p, c_i64, c_int, c_p, c_p],

@@ -352,20 +352,19 @@ def res_pack_weights(src, fwd=None, bwd=None, taps=1, stream=None):
 
 
 # ------------------------------------------------------------------------------------------------ VQ
-def vq_forward(z2d, E, zq, idx, counts, sqerr, stream=None, zq_copy=None):
-    """zq_copy: optional bf16/f32 tensor that also receives z_q (aw_vq_forward_ex)."""
+def vq_forward(z2d, E, zq, idx, counts, sqerr, stream=None, zq_copy=None, count_groups=1):
+    """zq_copy: optional bf16/f32 tensor that also receives z_q.  count_groups > 1: counts holds that many partial
+    histograms of K floats (aw_vq_forward_ex2; vq_finalize sums them)."""
     N, D = z2d.shape
-    if zq_copy is None:
-        call("aw_vq_forward", ptr(z2d), ptr(E), N, E.shape[0], D, ptr(zq), ptr(idx), ptr(counts), ptr(sqerr),
-             stream_ptr(stream))
-    else:
-        call("aw_vq_forward_ex", ptr(z2d), ptr(E), N, E.shape[0], D, ptr(zq), ptr(idx), ptr(counts), ptr(sqerr),
-             ptr(zq_copy), dtype_code(zq_copy.dtype), stream_ptr(stream))
+    Kc = E.shape[0]
+    assert counts.numel() >= count_groups * Kc, "counts: count_groups x K floats"
+    call("aw_vq_forward_ex2", ptr(z2d), ptr(E), N, Kc, D, ptr(zq), ptr(idx), ptr(counts), int(count_groups),
+         ptr(sqerr), ptr(zq_copy), dtype_code(zq_copy.dtype) if zq_copy is not None else 0, stream_ptr(stream))
 
 
-def vq_finalize(counts, sqerr, N, K, D, beta, loss, perplexity, stream=None):
-    call("aw_vq_finalize", ptr(counts), ptr(sqerr), N, K, D, float(beta), ptr(loss), ptr(perplexity),
-         stream_ptr(stream))
+def vq_finalize(counts, sqerr, N, K, D, beta, loss, perplexity, stream=None, count_groups=1):
+    call("aw_vq_finalize_ex", ptr(counts), int(count_groups), ptr(sqerr), N, K, D, float(beta), ptr(loss),
+         ptr(perplexity), stream_ptr(stream))
 
 
 def vq_backward(z2d, E, idx, g_zq, g_loss, beta, dz, dE, stream=None, dz_copy=None):

@@ -57,21 +57,28 @@ def rng_snapshot(m, dev, p_drop, zero=None):
     return snap
 
 
+# partial code histograms of the VQ forward (aw_vq_forward_ex2): workgroup b adds into partial b % 8, so no more
+# than N / (64 * 8) workgroups add into one address (at 1, every workgroup's adds into the same 2 KB serialised at
+# the memory-side atomic units: 2.5 us of the configs[1] kernel)
+VQ_COUNT_GROUPS = 8
+
+
 def accumulators(m, dev, K, H, zero=True):
     """Device accumulators of one forward, carved from one persistent f64 block (zeroed by ONE launch: here, or by
     rng_snapshot's when zero=False and the caller passes it the "block"): VQ sqerr (f64), MSE sqerr (f64,
-    fused_train_step), BN column statistics (2H f64) and the VQ code counts (K f32).  Each is consumed inside the
-    call that filled it (never across a forward/backward boundary)."""
+    fused_train_step), BN column statistics (2H f64) and the VQ code counts (VQ_COUNT_GROUPS partial histograms of K
+    f32, summed by aw_vq_finalize_ex).  Each is consumed inside the call that filled it (never across a
+    forward/backward boundary)."""
     key = (dev, K, H)
     st = m.__dict__.get("_acc_block")
     if st is None or st[0] != key:
-        st = (key, torch.empty(2 + 4 * H + (K + 1) // 2, dtype=torch.float64, device=dev))
+        st = (key, torch.empty(2 + 4 * H + (VQ_COUNT_GROUPS * K + 1) // 2, dtype=torch.float64, device=dev))
         m.__dict__["_acc_block"] = st
     buf = st[1]
     if zero:
         buf.zero_()
     return dict(block=buf, vq_sq=buf[0:1], mse_sq=buf[1:2], colstats=buf[2:2 + 2 * H], head_gsums=buf[2 + 2 * H:2 + 4 * H],
-                counts=buf[2 + 4 * H:].view(torch.float32)[:K])
+                counts=buf[2 + 4 * H:].view(torch.float32)[:VQ_COUNT_GROUPS * K])
 
 
 def resid_dtype(m, T):
@@ -409,9 +416,10 @@ def forward(m, x, training: bool, need_backward: bool, dtype=None, seed: int = 0
         idx = e(N, dt=torch.int64)
         counts, sq = acc["counts"], acc["vq_sq"]
         zq_T = None if T == F32 else e(N, D, dt=T)    # the operand copy comes out of the VQ kernel itself
-        K.vq_forward(z, pr["E"], zq, idx, counts, sq, zq_copy=zq_T)
+        K.vq_forward(z, pr["E"], zq, idx, counts, sq, zq_copy=zq_T, count_groups=VQ_COUNT_GROUPS)
         emb_loss, perplexity = e(()), e(())
-        K.vq_finalize(counts, sq, N, Kc, D, m.vector_quantization.beta, emb_loss, perplexity)
+        K.vq_finalize(counts, sq, N, Kc, D, m.vector_quantization.beta, emb_loss, perplexity,
+                      count_groups=VQ_COUNT_GROUPS)
     if pr["E"] is None or T == F32:
         zq_T = zq if T == F32 else _cast(zq, T)
 

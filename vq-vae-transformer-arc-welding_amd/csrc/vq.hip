@@ -61,6 +61,7 @@ __device__ __forceinline__ void vq_finish(float (&best)[RPL], int (&bestk)[RPL],
                                           int64_t row0, float* __restrict__ zq, int64_t* __restrict__ idx,
                                           float* __restrict__ counts, double* __restrict__ sqerr, void* __restrict__ zq2,
                                           int zq2_bf16) {
+  // counts: this workgroup's partial histogram (the caller offsets it by blockIdx % count_groups)
   constexpr int ROWS = 8 * RPL, ZP = D + 4;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int lr = lane >> 3, lc = lane & 7;
@@ -161,7 +162,7 @@ template <int D, int RPL>
 __global__ __launch_bounds__(VQ_THREADS, 2) void vq_fwd_kernel(const float* __restrict__ z,
                                                                const float* __restrict__ E, int64_t N, int K,
                                                                float* __restrict__ zq, int64_t* __restrict__ idx,
-                                                               float* __restrict__ counts,
+                                                               float* __restrict__ counts, int cgroups,
                                                                double* __restrict__ sqerr, void* __restrict__ zq2,
                                                                int zq2_bf16) {
   constexpr int ROWS = 8 * RPL;
@@ -296,7 +297,7 @@ __global__ __launch_bounds__(VQ_THREADS, 2) void vq_fwd_kernel(const float* __re
   }
 
   vq_finish<D, RPL>(best, bestk, es, 2 * L::E - 16 * ROWS, zs, reinterpret_cast<double*>(ees), E, N, K, row0, zq,
-                    idx, counts, sqerr, zq2, zq2_bf16);
+                    idx, counts + (int64_t)(blockIdx.x % cgroups) * K, sqerr, zq2, zq2_bf16);
 }
 
 // Codebook-pinned form (K <= 512, D <= 64: the configs[1] codebook, 512 x 64 fp32 = 128 KB): ONE workgroup per CU
@@ -314,7 +315,7 @@ __global__ __launch_bounds__(VQ_THREADS, 2) void vq_fwd_kernel(const float* __re
 template <int D> struct VqPinLds {
   static constexpr int ROWS = 64;
   static constexpr int ES = 0, ZS = ES + VQ_CODES * D, EES = ZS + ROWS * D, ZZS = EES + VQ_CODES;
-  static constexpr int RD = ZZS + ROWS, RK = RD + 8 * ROWS, HIST = RK + 8 * ROWS, RED = HIST + VQ_CODES;
+  static constexpr int RD = ZZS + ROWS, HIST = RD + 16 * ROWS, RED = HIST + VQ_CODES;   // RD: ROWS x 8 int2
   static constexpr int TOTAL = RED + 16;                     // floats (RED: 8 doubles)
   static_assert(TOTAL * 4 <= 160 * 1024, "pinned VQ LDS");
 };
@@ -327,6 +328,40 @@ template <int D> __device__ __forceinline__ int vq_pos(int c, int p) {
   return c * D + ((((p >> 2) ^ c) & (D / 4 - 1)) << 2) + (p & 3);
 }
 
+// Wave sum of a double on the VALU only (no LDS round trips): DPP within 16-lane rows (quad swaps, half-row and row
+// mirrors), then gfx950's v_permlane16_swap / v_permlane32_swap for lanes 16 and 32 apart.  Every lane ends with the
+// total (each step adds the same two values on both partners).
+template <int CTRL> __device__ __forceinline__ double vq_dpp_d(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)b, CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(b >> 32), CTRL, 0xF, 0xF, false);
+  return __longlong_as_double((long long)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo));
+}
+__device__ __forceinline__ double vq_wave_sum_d(double v) {
+  v += vq_dpp_d<0xB1>(v);    // quad_perm [1, 0, 3, 2]
+  v += vq_dpp_d<0x4E>(v);    // quad_perm [2, 3, 0, 1]
+  v += vq_dpp_d<0x141>(v);   // row_half_mirror
+  v += vq_dpp_d<0x140>(v);   // row_mirror
+  const int lane = __lane_id();
+  {
+    const uint64_t b = (uint64_t)__double_as_longlong(v);
+    const auto lo = __builtin_amdgcn_permlane16_swap((uint32_t)b, (uint32_t)b, false, false);
+    const auto hi = __builtin_amdgcn_permlane16_swap((uint32_t)(b >> 32), (uint32_t)(b >> 32), false, false);
+    const bool odd = (lane >> 4) & 1;   // rows 1, 3 received rows 0, 2 in [0]; rows 0, 2 received rows 1, 3 in [1]
+    const uint32_t plo = odd ? lo[0] : lo[1], phi = odd ? hi[0] : hi[1];
+    v += __longlong_as_double((long long)(((uint64_t)phi << 32) | plo));
+  }
+  {
+    const uint64_t b = (uint64_t)__double_as_longlong(v);
+    const auto lo = __builtin_amdgcn_permlane32_swap((uint32_t)b, (uint32_t)b, false, false);
+    const auto hi = __builtin_amdgcn_permlane32_swap((uint32_t)(b >> 32), (uint32_t)(b >> 32), false, false);
+    const bool up = lane >= 32;
+    const uint32_t plo = up ? lo[0] : lo[1], phi = up ? hi[0] : hi[1];
+    v += __longlong_as_double((long long)(((uint64_t)phi << 32) | plo));
+  }
+  return v;
+}
+
 __device__ __forceinline__ void vq_lds_barrier() {   // LDS-only: no wait for the global loads still in flight
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
@@ -337,7 +372,7 @@ template <int D>
 __global__ __launch_bounds__(VQ_THREADS, 1) void vq_fwd_pinned_kernel(const float* __restrict__ z,
                                                                      const float* __restrict__ E, int64_t N, int K,
                                                                      float* __restrict__ zq, int64_t* __restrict__ idx,
-                                                                     float* __restrict__ counts,
+                                                                     float* __restrict__ counts, int cgroups,
                                                                      double* __restrict__ sqerr, void* __restrict__ zq2,
                                                                      int zq2_bf16) {
   typedef __attribute__((ext_vector_type(16))) float f32x16;
@@ -350,8 +385,7 @@ __global__ __launch_bounds__(VQ_THREADS, 1) void vq_fwd_pinned_kernel(const floa
   float* zs = smem + L::ZS;                // [ROWS][D] likewise
   float* ees = smem + L::EES;              // [VQ_CODES]: |e_k|^2, NaN for k >= K
   float* zzs = smem + L::ZZS;              // [ROWS]
-  float* rd = smem + L::RD;                // [8 waves][ROWS] per-wave row minima
-  int* rk = reinterpret_cast<int*>(smem + L::RK);
+  int2* cand = reinterpret_cast<int2*>(smem + L::RD);   // [ROWS][8 waves] per-wave row minima (d bits, k)
   float* hist = smem + L::HIST;            // [VQ_CODES] this workgroup's code counts
   double* red = reinterpret_cast<double*>(smem + L::RED);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -390,7 +424,7 @@ __global__ __launch_bounds__(VQ_THREADS, 1) void vq_fwd_pinned_kernel(const floa
   }
   hist[tid] = 0.f;
 
-  // ---- chunk loop: store chunk dc, barrier, its 8 MFMA steps (two groups of four) and the norms' next 16 terms
+  // ---- chunk loop: per 16-dim chunk, 8 MFMA steps (two groups of four) and the norms' next 16 terms
   f32x16 acc[2][2];                // [code tile mi][row tile ni]
 #pragma unroll
   for (int mi = 0; mi < 2; ++mi)
@@ -414,32 +448,49 @@ __global__ __launch_bounds__(VQ_THREADS, 1) void vq_fwd_pinned_kernel(const floa
     return s;
   };
   const int ca = 64 * w + jr;      // this lane's A row (code) in tile mi: ca + 32 mi; B row (z row): jr + 32 ni
+  auto ops = [&](int dc, int g, float4 (&a)[2], float4 (&b)[2]) {   // steps 8 dc + 4 g .. + 3 of lane half h
+    const int p = h * H2 + 8 * dc + 4 * g;
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      a[t] = *reinterpret_cast<const float4*>(es + vq_pos<D>(ca + 32 * t, p));
+      b[t] = *reinterpret_cast<const float4*>(zs + vq_pos<D>(jr + 32 * t, p));
+    }
+  };
+  auto mma4 = [&](const float4 (&a)[2], const float4 (&b)[2]) {
+    const float av[2][4] = {{a[0].x, a[0].y, a[0].z, a[0].w}, {a[1].x, a[1].y, a[1].z, a[1].w}};
+    const float bv[2][4] = {{b[0].x, b[0].y, b[0].z, b[0].w}, {b[1].x, b[1].y, b[1].z, b[1].w}};
+#pragma unroll
+    for (int s4 = 0; s4 < 4; ++s4)
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni)
+          acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[mi][s4], bv[ni][s4], acc[mi][ni], 0, 0, 0);
+  };
+  // chunk dc + 1 is stored while chunk dc computes, and its barrier sits between chunk dc's two MFMA groups, so the
+  // first operands of chunk dc + 1 are read before the second group issues: the matrix pipe does not wait on LDS
+  // latency at a chunk boundary
+#pragma unroll
+  for (int u = 0; u < 4; ++u) put4(es, 128 * u + (tid >> 2), tid & 3, pe[0][u]);
+  vq_lds_barrier();
+  float4 a0[2], b0[2], a1[2], b1[2];
+  ops(0, 0, a0, b0);
 #pragma unroll
   for (int dc = 0; dc < NCH; ++dc) {
+    if (dc + 1 < NCH) {
 #pragma unroll
-    for (int u = 0; u < 4; ++u) put4(es, 128 * u + (tid >> 2), 4 * dc + (tid & 3), pe[dc][u]);
-    vq_lds_barrier();
-#pragma unroll
-    for (int g = 0; g < 2; ++g) {
-      const int p = h * H2 + 8 * dc + 4 * g;     // steps 8 dc + 4 g .. + 3 of lane half h
-      float4 a[2], b[2];
-#pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        a[t] = *reinterpret_cast<const float4*>(es + vq_pos<D>(ca + 32 * t, p));
-        b[t] = *reinterpret_cast<const float4*>(zs + vq_pos<D>(jr + 32 * t, p));
-      }
-      const float av[2][4] = {{a[0].x, a[0].y, a[0].z, a[0].w}, {a[1].x, a[1].y, a[1].z, a[1].w}};
-      const float bv[2][4] = {{b[0].x, b[0].y, b[0].z, b[0].w}, {b[1].x, b[1].y, b[1].z, b[1].w}};
-#pragma unroll
-      for (int s4 = 0; s4 < 4; ++s4)
-#pragma unroll
-        for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-          for (int ni = 0; ni < 2; ++ni)
-            acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[mi][s4], bv[ni][s4], acc[mi][ni], 0, 0, 0);
+      for (int u = 0; u < 4; ++u) put4(es, 128 * u + (tid >> 2), 4 * (dc + 1) + (tid & 3), pe[dc + 1][u]);
     }
+    ops(dc, 1, a1, b1);
+    mma4(a0, b0);
     ee = sumsq16(es, tid, dc, ee);
     if (w == 7) zz = sumsq16(zs, lane, dc, zz);
+    if (dc + 1 < NCH) {
+      vq_lds_barrier();
+      ops(dc + 1, 0, a0, b0);
+      __builtin_amdgcn_sched_barrier(0);   // keep the reads ahead of the MFMAs below
+    }
+    mma4(a1, b1);
   }
   ees[tid] = tid < K ? ee : __builtin_nanf("");
   if (w == 7) zzs[lane] = zz;
@@ -451,35 +502,41 @@ __global__ __launch_bounds__(VQ_THREADS, 1) void vq_fwd_pinned_kernel(const floa
   //      keeps the first index of a tie.  NaN distances (codes >= K, NaN inputs) never compare less; a lane left
   //      with none reports (+inf, its first code), which the lexicographic merge below ranks behind every finite
   //      candidate.
-  float best[2];
-  int bestk[2];
-#pragma unroll
-  for (int ni = 0; ni < 2; ++ni) {
-    const float zr2 = zzs[jr + 32 * ni];
-    float bd = __builtin_huge_valf();
-    int bk = 64 * w + 4 * h;
+  //      The two rows run interleaved (independent compare chains), and the running index is the register
+  //      position j = 16 mi + 4 g + r, a literal in each select, mapped to its code once at the end.
+  float best[2] = {__builtin_huge_valf(), __builtin_huge_valf()};
+  int bj[2] = {0, 0};
+  {
+    const float zrow[2] = {zzs[jr], zzs[jr + 32]};
 #pragma unroll
     for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        const int c0 = 64 * w + 32 * mi + 8 * g + 4 * h;
-        const float4 e4 = *reinterpret_cast<const float4*>(ees + c0);
-        const f32x2 s01 = f32x2{zr2, zr2} + f32x2{e4.x, e4.y}, s23 = f32x2{zr2, zr2} + f32x2{e4.z, e4.w};
-        const f32x2 d01 = __builtin_elementwise_fma(
-            f32x2{-2.f, -2.f}, f32x2{acc[mi][ni][4 * g], acc[mi][ni][4 * g + 1]}, s01);
-        const f32x2 d23 = __builtin_elementwise_fma(
-            f32x2{-2.f, -2.f}, f32x2{acc[mi][ni][4 * g + 2], acc[mi][ni][4 * g + 3]}, s23);
-        const float dv[4] = {d01.x, d01.y, d23.x, d23.y};
+        const float4 e4 = *reinterpret_cast<const float4*>(ees + 64 * w + 32 * mi + 8 * g + 4 * h);
+        float dv[2][4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const bool t = dv[r] < bd;
-          bd = t ? dv[r] : bd;
-          bk = t ? c0 + r : bk;
+        for (int ni = 0; ni < 2; ++ni) {
+          const f32x2 s01 = f32x2{zrow[ni], zrow[ni]} + f32x2{e4.x, e4.y};
+          const f32x2 s23 = f32x2{zrow[ni], zrow[ni]} + f32x2{e4.z, e4.w};
+          const f32x2 d01 = __builtin_elementwise_fma(
+              f32x2{-2.f, -2.f}, f32x2{acc[mi][ni][4 * g], acc[mi][ni][4 * g + 1]}, s01);
+          const f32x2 d23 = __builtin_elementwise_fma(
+              f32x2{-2.f, -2.f}, f32x2{acc[mi][ni][4 * g + 2], acc[mi][ni][4 * g + 3]}, s23);
+          dv[ni][0] = d01.x, dv[ni][1] = d01.y, dv[ni][2] = d23.x, dv[ni][3] = d23.y;
         }
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int ni = 0; ni < 2; ++ni) {
+            const bool t = dv[ni][r] < best[ni];
+            best[ni] = t ? dv[ni][r] : best[ni];
+            bj[ni] = t ? 16 * mi + 4 * g + r : bj[ni];
+          }
       }
-    best[ni] = bd;
-    bestk[ni] = bk;
   }
+  int bestk[2];
+#pragma unroll
+  for (int ni = 0; ni < 2; ++ni) bestk[ni] = 64 * w + 4 * h + 2 * bj[ni] - (bj[ni] & 3);   // = 32 mi + 8 g + r
   // ---- lexicographic (d, k) merge of the two lane halves (codes 4h apart), then across the 8 waves (LDS)
 #pragma unroll
   for (int ni = 0; ni < 2; ++ni) {
@@ -487,28 +544,35 @@ __global__ __launch_bounds__(VQ_THREADS, 1) void vq_fwd_pinned_kernel(const floa
     const int k = __shfl_xor(bestk[ni], 32, 64);
     lex_take(d, k, true, best[ni], bestk[ni]);
   }
-  if (h == 0) {
+  if (h == 0) {   // candidates as (d bits, k) pairs, [row][wave]: a row's 8 are one 64-B line
 #pragma unroll
-    for (int ni = 0; ni < 2; ++ni) {
-      rd[w * ROWS + jr + 32 * ni] = best[ni];
-      rk[w * ROWS + jr + 32 * ni] = bestk[ni];
-    }
+    for (int ni = 0; ni < 2; ++ni) cand[(jr + 32 * ni) * 8 + w] = make_int2(__float_as_int(best[ni]), bestk[ni]);
   }
   vq_lds_barrier();
-  // ---- thread (row r, quad q) resolves its row's winner from the 8 wave candidates (LDS broadcast reads), takes
-  //      e_k's quad from the pinned codebook and writes z_q (+ the operand copy) coalesced; the q == 0 thread of a
-  //      row writes idx and counts the code in LDS
+  // ---- thread (row r, quad q) resolves its row's winner from the 8 wave candidates (four 16-B LDS broadcast
+  //      reads), takes e_k's quad from the pinned codebook and writes z_q (+ the operand copy) coalesced; the q == 0
+  //      thread of a row writes idx and counts the code in LDS.  The items of a thread are unrolled and only their
+  //      stores predicated, so their LDS chains overlap.
   double se = 0.0;
-  for (int it = tid; it < ROWS * NQ; it += VQ_THREADS) {
+  constexpr int IPT = (ROWS * NQ + VQ_THREADS - 1) / VQ_THREADS;
+#pragma unroll
+  for (int i = 0; i < IPT; ++i) {
+    const int it = min(tid + i * VQ_THREADS, ROWS * NQ - 1);
     const int r = it / NQ, q = it - r * NQ;
     const int64_t row = row0 + r;
-    if (row >= N) break;   // rows ascend with it
-    float bd = rd[r];
-    int bk = rk[r];
+    const bool live = tid + i * VQ_THREADS < ROWS * NQ && row < N;
+    const int4* cp = reinterpret_cast<const int4*>(cand + r * 8);
+    const int4 c[4] = {cp[0], cp[1], cp[2], cp[3]};
+    float bd = __int_as_float(c[0].x);
+    int bk = c[0].y;
+    lex_take(__int_as_float(c[0].z), c[0].w, true, bd, bk);
 #pragma unroll
-    for (int v = 1; v < 8; ++v) lex_take(rd[v * ROWS + r], rk[v * ROWS + r], true, bd, bk);
+    for (int v = 1; v < 4; ++v) {
+      lex_take(__int_as_float(c[v].x), c[v].y, true, bd, bk);
+      lex_take(__int_as_float(c[v].z), c[v].w, true, bd, bk);
+    }
     if (bk < 0 || bk >= K) bk = 0;  // all-NaN row guard (torch would return the NaN position)
-    if (q == 0) {
+    if (live && q == 0) {
       idx[row] = bk;
       atomicAdd(hist + bk, 1.0f);
     }
@@ -523,23 +587,29 @@ __global__ __launch_bounds__(VQ_THREADS, 1) void vq_fwd_pinned_kernel(const floa
     o.y = __fadd_rn(z13.x, d1);
     o.z = __fadd_rn(z02.y, d2);
     o.w = __fadd_rn(z13.y, d3);
-    reinterpret_cast<float4*>(zq + row * D)[q] = o;
-    if (zq2) {   // the GEMM operand copy of z_q (the decoder's first conv reads it): no separate cast launch
-      if (zq2_bf16) {
-        typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
-        reinterpret_cast<bf16x4*>(zq2)[row * NQ + q] = bf16x4{(bf16)o.x, (bf16)o.y, (bf16)o.z, (bf16)o.w};
-      } else {
-        reinterpret_cast<float4*>(zq2)[row * NQ + q] = o;
+    if (live) {
+      // write-through stores: the lines leave L2 now instead of at the end-of-kernel release
+      aw_st_wt(zq + row * D + 4 * q, f32x4{o.x, o.y, o.z, o.w});
+      if (zq2) {   // the GEMM operand copy of z_q (the decoder's first conv reads it): no separate cast launch
+        if (zq2_bf16) {
+          typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+          const bf16x4 v = bf16x4{(bf16)o.x, (bf16)o.y, (bf16)o.z, (bf16)o.w};
+          aw_st_wt(reinterpret_cast<bf16x4*>(zq2) + row * NQ + q, __builtin_bit_cast(u32x2, v));
+        } else {
+          aw_st_wt(reinterpret_cast<float4*>(zq2) + row * NQ + q, f32x4{o.x, o.y, o.z, o.w});
+        }
       }
+      se += (double)(d0 * d0 + d1 * d1 + d2 * d2 + d3 * d3);
     }
-    se += (double)(d0 * d0 + d1 * d1 + d2 * d2 + d3 * d3);
   }
-  se = wave_sum_d(se);
+  se = vq_wave_sum_d(se);
   if (lane == 0) red[w] = se;
   vq_lds_barrier();   // LDS only: no wait for this workgroup's z_q stores
+  // the histogram goes to partial blockIdx % cgroups: the adds into one address stay cgroups times fewer (every
+  // workgroup adding into the same 2 KB serialises at the memory-side atomic units: 2.5 us of drain at cgroups 1)
   if (tid < K) {
     const float c = hist[tid];
-    if (c != 0.f) atomicAdd(counts + tid, c);
+    if (c != 0.f) atomicAdd(counts + (int64_t)(blockIdx.x % cgroups) * K + tid, c);
   }
   if (tid == 0) {
     double t = 0.0;
@@ -549,13 +619,15 @@ __global__ __launch_bounds__(VQ_THREADS, 1) void vq_fwd_pinned_kernel(const floa
   }
 }
 
-__global__ void vq_finalize_kernel(const float* counts, const double* sqerr, int64_t N, int K, int D, float beta,
-                                   float* loss, float* perp) {
+__global__ void vq_finalize_kernel(const float* counts, int cgroups, const double* sqerr, int64_t N, int K, int D,
+                                   float beta, float* loss, float* perp) {
   __shared__ float part[256];
   const float invN = 1.0f / (float)N;
   float s = 0.f;
   for (int k = threadIdx.x; k < K; k += 256) {
-    const float p = counts[k] * invN;
+    float c = counts[k];
+    for (int g = 1; g < cgroups; ++g) c += counts[(int64_t)g * K + k];   // integer-valued: exact in any order
+    const float p = c * invN;
     s += p * logf(p + 1e-10f);
   }
   part[threadIdx.x] = s;
@@ -609,9 +681,12 @@ __global__ void vq_gather_kernel(const float* E, const int64_t* idx, int64_t N, 
 }  // namespace
 
 
-extern "C" int aw_vq_forward_ex(const float* z, const float* E, int64_t N, int K, int D, float* zq, int64_t* idx,
-                                float* counts, double* sqerr, void* zq_copy, int copy_dtype, void* stream) {
+extern "C" int aw_vq_forward_ex2(const float* z, const float* E, int64_t N, int K, int D, float* zq, int64_t* idx,
+                                 float* counts, int count_groups, double* sqerr, void* zq_copy, int copy_dtype,
+                                 void* stream) {
   AW_REQUIRE(z && E && zq && idx && counts && sqerr, "aw_vq_forward: null pointer");
+  AW_REQUIRE(count_groups >= 1 && count_groups <= AW_VQ_COUNT_GROUPS_MAX, "aw_vq_forward_ex2: count_groups 1..%d",
+             AW_VQ_COUNT_GROUPS_MAX);
   AW_REQUIRE(!zq_copy || ((copy_dtype == AW_BF16 || copy_dtype == AW_F32) && ((uintptr_t)zq_copy % 16) == 0),
              "aw_vq_forward_ex: zq_copy must be 16-B aligned bf16 or f32");
   const int cbf = copy_dtype == AW_BF16;
@@ -634,19 +709,19 @@ extern "C" int aw_vq_forward_ex(const float* z, const float* E, int64_t N, int K
   if (!rows_env && K <= VQ_CODES && (D == 16 || D == 32 || D == 64)) {
     const dim3 g64(aw_cdiv(N, 64));
     if (D == 16) hipLaunchKernelGGL((vq_fwd_pinned_kernel<16>), g64, dim3(VQ_THREADS), 0, s, z, E, N, K, zq, idx, counts,
-                                    sqerr, zq_copy, cbf);
+                                    count_groups, sqerr, zq_copy, cbf);
     else if (D == 32) hipLaunchKernelGGL((vq_fwd_pinned_kernel<32>), g64, dim3(VQ_THREADS), 0, s, z, E, N, K, zq, idx,
-                                         counts, sqerr, zq_copy, cbf);
-    else hipLaunchKernelGGL((vq_fwd_pinned_kernel<64>), g64, dim3(VQ_THREADS), 0, s, z, E, N, K, zq, idx, counts, sqerr,
-                            zq_copy, cbf);
+                                         counts, count_groups, sqerr, zq_copy, cbf);
+    else hipLaunchKernelGGL((vq_fwd_pinned_kernel<64>), g64, dim3(VQ_THREADS), 0, s, z, E, N, K, zq, idx, counts, count_groups,
+                            sqerr, zq_copy, cbf);
     return aw::check_launch("aw_vq_forward");
   }
 #define AW_VQ_CASE(DD)                                                                                               \
   case DD:                                                                                                           \
-    if (half) hipLaunchKernelGGL((vq_fwd_kernel<DD, 4>), grid, dim3(VQ_THREADS), 0, s, z, E, N, K, zq, idx, counts, sqerr, \
-                                 zq_copy, cbf);                                                                      \
-    else hipLaunchKernelGGL((vq_fwd_kernel<DD, 8>), grid, dim3(VQ_THREADS), 0, s, z, E, N, K, zq, idx, counts, sqerr,     \
-                            zq_copy, cbf);                                                                           \
+    if (half) hipLaunchKernelGGL((vq_fwd_kernel<DD, 4>), grid, dim3(VQ_THREADS), 0, s, z, E, N, K, zq, idx, counts,   \
+                                 count_groups, sqerr, zq_copy, cbf);                                                 \
+    else hipLaunchKernelGGL((vq_fwd_kernel<DD, 8>), grid, dim3(VQ_THREADS), 0, s, z, E, N, K, zq, idx, counts,        \
+                            count_groups, sqerr, zq_copy, cbf);                                                      \
     break;
   switch (D) {
     AW_VQ_CASE(16)
@@ -660,17 +735,29 @@ extern "C" int aw_vq_forward_ex(const float* z, const float* E, int64_t N, int K
   return aw::check_launch("aw_vq_forward");
 }
 
+extern "C" int aw_vq_forward_ex(const float* z, const float* E, int64_t N, int K, int D, float* zq, int64_t* idx,
+                                float* counts, double* sqerr, void* zq_copy, int copy_dtype, void* stream) {
+  return aw_vq_forward_ex2(z, E, N, K, D, zq, idx, counts, 1, sqerr, zq_copy, copy_dtype, stream);
+}
+
 extern "C" int aw_vq_forward(const float* z, const float* E, int64_t N, int K, int D, float* zq, int64_t* idx,
                              float* counts, double* sqerr, void* stream) {
-  return aw_vq_forward_ex(z, E, N, K, D, zq, idx, counts, sqerr, nullptr, AW_F32, stream);
+  return aw_vq_forward_ex2(z, E, N, K, D, zq, idx, counts, 1, sqerr, nullptr, AW_F32, stream);
+}
+
+extern "C" int aw_vq_finalize_ex(const float* counts, int count_groups, const double* sqerr, int64_t N, int K, int D,
+                                 float beta, float* loss, float* perplexity, void* stream) {
+  AW_REQUIRE(counts && sqerr && loss && perplexity && N > 0 && K > 0 && D > 0, "aw_vq_finalize: bad args");
+  AW_REQUIRE(count_groups >= 1 && count_groups <= AW_VQ_COUNT_GROUPS_MAX, "aw_vq_finalize_ex: count_groups 1..%d",
+             AW_VQ_COUNT_GROUPS_MAX);
+  hipLaunchKernelGGL(vq_finalize_kernel, dim3(1), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), counts,
+                     count_groups, sqerr, N, K, D, beta, loss, perplexity);
+  return aw::check_launch("aw_vq_finalize");
 }
 
 extern "C" int aw_vq_finalize(const float* counts, const double* sqerr, int64_t N, int K, int D, float beta,
                               float* loss, float* perplexity, void* stream) {
-  AW_REQUIRE(counts && sqerr && loss && perplexity && N > 0 && K > 0 && D > 0, "aw_vq_finalize: bad args");
-  hipLaunchKernelGGL(vq_finalize_kernel, dim3(1), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), counts, sqerr,
-                     N, K, D, beta, loss, perplexity);
-  return aw::check_launch("aw_vq_finalize");
+  return aw_vq_finalize_ex(counts, 1, sqerr, N, K, D, beta, loss, perplexity, stream);
 }
 
 extern "C" int aw_vq_backward_ex(const float* z, const float* E, const int64_t* idx, const float* g_zq,
