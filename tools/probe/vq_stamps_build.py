@@ -43,6 +43,10 @@ VARIANTS = {
             "    aw_st_wt(zq + row * D + 4 * q, f32x4{o.x, o.y, o.z, o.w});\n    if (zq2) {")],
     # launch floor: the workgroups exit at once (same LDS allocation and grid)
     "empty": [("  float4 zr[ZPT];", "  if (N > 0) return;\n  float4 zr[ZPT];")],
+    # the same with a 1 KB LDS allocation (the launch floor without the 156 KB workgroup LDS)
+    "emptysmall": [("  float4 zr[ZPT];", "  if (N > 0) return;\n  float4 zr[ZPT];"),
+                   ("  __shared__ __attribute__((aligned(16))) float smem[L::TOTAL];",
+                    "  __shared__ __attribute__((aligned(16))) float smem[256];")],
     # no code-count atomics
     "nohist": [("    if (c != 0.f) atomicAdd(counts + tid, c);", "    if (c == -1.f) atomicAdd(counts + tid, c);")],
 }
