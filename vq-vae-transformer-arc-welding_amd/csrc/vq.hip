@@ -432,8 +432,13 @@ __global__ __launch_bounds__(VQ_THREADS, 1) void vq_fwd_pinned_kernel(const floa
     for (int ni = 0; ni < 2; ++ni)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[mi][ni][r] = 0.f;
-  float ee = 0.f, zz = 0.f;        // in-order sums of squares: code tid, and row lane (wave 7)
-  auto sumsq16 = [&](const float* img, int c, int dc, float s) {   // dims 16 dc .. 16 dc + 15 in order
+  // in-order fmaf chains of squares (s = fma(x_d, x_d, s), d = 0, 1, ...: the kernels' norms since round 1):
+  // |e_k|^2 of code tid and |z|^2 of row lane (every wave computes the rows' sums; wave 7 publishes them).  A chunk's
+  // 16 values are read with the chunk's first operands; the two 16-long dependent chains then run one link per MFMA
+  // pair inside the chunk's MFMA groups (issued as their own block they stalled the wave's issue -- and with it its
+  // next MFMAs -- for ~400 cycles per chunk)
+  float ee = 0.f, zz = 0.f;
+  auto ld16 = [&](const float* img, int c, int dc, float (&v)[16]) {   // dims 16 dc .. 16 dc + 15, in dim order
     const float4 e0 = *reinterpret_cast<const float4*>(img + vq_pos<D>(c, 8 * dc));
     const float4 e1 = *reinterpret_cast<const float4*>(img + vq_pos<D>(c, 8 * dc + 4));
     const float4 o0 = *reinterpret_cast<const float4*>(img + vq_pos<D>(c, H2 + 8 * dc));
@@ -442,10 +447,9 @@ __global__ __launch_bounds__(VQ_THREADS, 1) void vq_fwd_pinned_kernel(const floa
     const float ov[8] = {o0.x, o0.y, o0.z, o0.w, o1.x, o1.y, o1.z, o1.w};
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      s = __fadd_rn(s, __fmul_rn(ev[i], ev[i]));
-      s = __fadd_rn(s, __fmul_rn(ov[i], ov[i]));
+      v[2 * i] = ev[i];
+      v[2 * i + 1] = ov[i];
     }
-    return s;
   };
   const int ca = 64 * w + jr;      // this lane's A row (code) in tile mi: ca + 32 mi; B row (z row): jr + 32 ni
   auto ops = [&](int dc, int g, float4 (&a)[2], float4 (&b)[2]) {   // steps 8 dc + 4 g .. + 3 of lane half h
@@ -456,41 +460,54 @@ __global__ __launch_bounds__(VQ_THREADS, 1) void vq_fwd_pinned_kernel(const floa
       b[t] = *reinterpret_cast<const float4*>(zs + vq_pos<D>(jr + 32 * t, p));
     }
   };
-  auto mma4 = [&](const float4 (&a)[2], const float4 (&b)[2]) {
+  // 16 MFMAs (four steps x 2 x 2 tiles), add i of each norm chain after MFMA 2i + 1
+  auto mma4 = [&](const float4 (&a)[2], const float4 (&b)[2], const float* se, const float* sz) {
     const float av[2][4] = {{a[0].x, a[0].y, a[0].z, a[0].w}, {a[1].x, a[1].y, a[1].z, a[1].w}};
     const float bv[2][4] = {{b[0].x, b[0].y, b[0].z, b[0].w}, {b[1].x, b[1].y, b[1].z, b[1].w}};
 #pragma unroll
     for (int s4 = 0; s4 < 4; ++s4)
 #pragma unroll
-      for (int mi = 0; mi < 2; ++mi)
+      for (int mi = 0; mi < 2; ++mi) {
 #pragma unroll
         for (int ni = 0; ni < 2; ++ni)
           acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[mi][s4], bv[ni][s4], acc[mi][ni], 0, 0, 0);
+        ee = __builtin_fmaf(se[2 * s4 + mi], se[2 * s4 + mi], ee);
+        zz = __builtin_fmaf(sz[2 * s4 + mi], sz[2 * s4 + mi], zz);
+        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);   // the two MFMAs,
+        __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);   // then the two adds
+      }
   };
-  // chunk dc + 1 is stored while chunk dc computes, and its barrier sits between chunk dc's two MFMA groups, so the
-  // first operands of chunk dc + 1 are read before the second group issues: the matrix pipe does not wait on LDS
-  // latency at a chunk boundary
+  // chunk dc + 1 is stored while chunk dc computes (after its first MFMA group), and its barrier sits between chunk
+  // dc's two MFMA groups, so the first operands of chunk dc + 1 are read before the second group issues: the matrix
+  // pipe does not wait on LDS latency at a chunk boundary
 #pragma unroll
   for (int u = 0; u < 4; ++u) put4(es, 128 * u + (tid >> 2), tid & 3, pe[0][u]);
   vq_lds_barrier();
   float4 a0[2], b0[2], a1[2], b1[2];
+  float ev[16], zv[16];
   ops(0, 0, a0, b0);
+  ld16(es, tid, 0, ev);
+  ld16(zs, lane, 0, zv);
 #pragma unroll
   for (int dc = 0; dc < NCH; ++dc) {
-    if (dc + 1 < NCH) {
+    ops(dc, 1, a1, b1);
+    float se[16], sz[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      se[i] = ev[i];
+      sz[i] = zv[i];
+    }
+    mma4(a0, b0, se, sz);
+    if (dc + 1 < NCH) {   // behind the first MFMA group: the chunk's loads get that much longer to land
 #pragma unroll
       for (int u = 0; u < 4; ++u) put4(es, 128 * u + (tid >> 2), 4 * (dc + 1) + (tid & 3), pe[dc + 1][u]);
-    }
-    ops(dc, 1, a1, b1);
-    mma4(a0, b0);
-    ee = sumsq16(es, tid, dc, ee);
-    if (w == 7) zz = sumsq16(zs, lane, dc, zz);
-    if (dc + 1 < NCH) {
       vq_lds_barrier();
       ops(dc + 1, 0, a0, b0);
+      ld16(es, tid, dc + 1, ev);
+      ld16(zs, lane, dc + 1, zv);
       __builtin_amdgcn_sched_barrier(0);   // keep the reads ahead of the MFMAs below
     }
-    mma4(a1, b1);
+    mma4(a1, b1, se + 8, sz + 8);
   }
   ees[tid] = tid < K ? ee : __builtin_nanf("");
   if (w == 7) zzs[lane] = zz;
