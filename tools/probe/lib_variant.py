@@ -15,9 +15,11 @@ CSRC = os.path.join(REPO, "vq-vae-transformer-arc-welding_amd", "csrc")
 # name -> [(file, product text, replacement)]
 VARIANTS = {
     "base": [],
+    # the decoder chain's images with the encoder's swizzle keys (key(u) = u: the round-5 layout before the search)
+    "chain_oldkeys": [("reschain.hip", "0xfdb64fdb98264210ull", "0xfedcba9876543210ull")],
     # the fused un-patch head forward + pass 1 without its per-channel sums' global atomics (7H per workgroup)
-    "head_noatom": [("vqvae.hip", "    if (i < 5 * H) {\n      atomicAdd(gw2 + i, t);",
-                     "    if (t == -1.2345f) {\n      atomicAdd(gw2 + i, t);")],
+    "head_noatom": [("vqvae.hip", "  for (int i0 = threadIdx.x; i0 < 7 * H; i0 += 64 * HFW) {",
+                     "  for (int i0 = threadIdx.x; i0 < 7 * H && gmul < -1e30f; i0 += 64 * HFW) {")],
 }
 
 

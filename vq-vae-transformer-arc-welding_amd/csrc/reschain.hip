@@ -92,6 +92,14 @@ template <int TAPS> struct EcGeo {
   static constexpr int LDS = BIAS + 8 * 256;
   static constexpr uint32_t WBYTES = (uint32_t)EC_H * EC_H * 2 * TAPS;   // one packed weight matrix
   static constexpr int WWAVE = 4 * KS * 1024;                      // a wave's 4 packed block rows
+  // Image swizzle key of token u of a 16-token group: chunk c of the token sits at chunk c ^ key(u).  The encoder
+  // reads only unshifted rows: key = u.  The decoder's shifted taps read rows u - 1 / u + 1 beside u, and with key = u
+  // the 16 lanes of a ds_read_b128 group hit one bank slot twice under either shift (PMC: 38 % of the decoder chain's
+  // LDS cycles were bank conflicts); this table (found by exhaustive search, tools/probe/chain_swizzle.py) makes all
+  // three taps conflict-free and keeps the epilogue's ds_write_b64 at its minimum of two lanes per bank.  The zero
+  // rows ahead of / behind a window (u = -1 / 16) read with keys 15 / 0.
+  static constexpr uint64_t KEYS = TAPS == 1 ? 0xfedcba9876543210ull : 0xfdb64fdb98264210ull;
+  __device__ static int key(int u) { return u < 0 ? 15 : u > 15 ? 0 : (int)((KEYS >> (4 * u)) & 15); }
 };
 static_assert(EcGeo<3>::LDS <= 160 * 1024, "decoder chain LDS");
 
@@ -148,10 +156,10 @@ __device__ __forceinline__ uint4 ec_lds_r16(const char* smem, int off) {
 }
 
 // image [token][k]: 16-B chunk c of token t (16-token group j, t % 16 = u) sits at R0 + j JS + u ROWB, chunk
-// c ^ u.  A fragment read (lane: token u, chunk 4s + g) hits 16 distinct 16-B bank slots in each ds_read_b128 lane
-// group.  The decoder's zero rows (at j JS, j = 0..4) are read by the shifted taps only.
+// c ^ key(u) (EcGeo::key).  A fragment read (lane: token u + tap shift, chunk 4s + g) hits 16 distinct 16-B bank slots
+// in each ds_read_b128 lane group.  The decoder's zero rows (at j JS, j = 0..4) are read by the shifted taps only.
 template <class G> __device__ __forceinline__ int ec_off(int tok, int chunk) {
-  return G::R0 + (tok >> 4) * G::JS + (tok & 15) * EC_ROWB + ((chunk ^ (tok & 15)) << 4);
+  return G::R0 + (tok >> 4) * G::JS + (tok & 15) * EC_ROWB + ((chunk ^ G::key(tok & 15)) << 4);
 }
 
 // The first operand image of a chain: rows [row0, row0 + 64) of a [N][H] bf16 tensor (zeros past N); the decoder
@@ -315,10 +323,10 @@ template <class G, int DIR> struct EcLane {
     wl = w * G::WWAVE + lane * 16;
 #pragma unroll
     for (int t = 0; t < T; ++t) {
-      const int tp = li + (T == 1 ? 0 : DIR * (t - 1)), key = tp & 15;   // tp = -1 / 16: the window's zero rows
+      const int tp = li + (T == 1 ? 0 : DIR * (t - 1)), key = G::key(tp);   // tp = -1 / 16: the zero rows
       rb[t] = G::R0 + tp * EC_ROWB + ((4 * (key >> 2) + (g ^ (key & 3))) << 4);
     }
-    wb0 = G::R0 + li * EC_ROWB + (((8 * w + (g >> 1)) ^ li) << 4) + (g & 1) * 8;
+    wb0 = G::R0 + li * EC_ROWB + (((8 * w + (g >> 1)) ^ G::key(li)) << 4) + (g & 1) * 8;
   }
   __device__ __forceinline__ int wb(int i) const { return wb0 ^ (32 * i); }
 };
@@ -335,7 +343,7 @@ template <class G> struct EcStore {
     const int lane = tid & 63, w = tid >> 6, g = lane >> 4, li = lane & 15;
     const int t8 = lane >> 3, c8 = lane & 7;
 #pragma unroll
-    for (int p = 0; p < 2; ++p) ir[p] = G::R0 + (8 * p + t8) * EC_ROWB + (((8 * w + c8) ^ (8 * p + t8)) << 4);
+    for (int p = 0; p < 2; ++p) ir[p] = G::R0 + (8 * p + t8) * EC_ROWB + (((8 * w + c8) ^ G::key(8 * p + t8)) << 4);
     const int sbase = G::SCR + w * EC_SCR;
 #pragma unroll
     for (int i = 0; i < 4; ++i) sw[i] = sbase + li * 128 + (((2 * i + (g >> 1)) ^ (li & 7)) << 4) + (g & 1) * 8;
