@@ -1,6 +1,7 @@
-"""Probe builds of csrc/reschain.hip (EC_PROBE_FLAGS, see the top of that file): the chain kernels alone at the
-configs[1] shape with parts left out, and per-conv s_memtime stamps.  Results of the probe builds are garbage by
-construction.  Build on the CPU first:  python tools/probe/res_chain_variants.py build
+"""Probe builds of csrc/reschain.hip: the chain kernels alone at the configs[1] shape with parts left out.  Each
+variant is a copy of the product source with text replacements (the product carries no probe switches), compiled
+with runtime.hip into tools/probe/build/ec_<name>.so.  Results of the probe builds are garbage by construction.
+Build on the CPU first:  python tools/probe/res_chain_variants.py build
 usage on the GPU box: python tools/probe/res_chain_variants.py [iters] [taps]   (taps 1: encoder, 3: decoder)"""
 import ctypes
 import os
@@ -10,21 +11,39 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(os.path.dirname(HERE))
 SRC = os.path.join(REPO, "vq-vae-transformer-arc-welding_amd", "csrc")
-# name -> EC_PROBE_FLAGS, or (EC_PROBE_FLAGS, extra -D defines)
-VARIANTS = {"base": 0, "base2": 0, "no_gelu": 16, "scalar": (0, ["-DEC_SCALAR_GELU=1"]),
-            "scalar_noslp": (0, ["-DEC_SCALAR_GELU=1", "-fno-slp-vectorize"]),
-            "noslp": (0, ["-fno-slp-vectorize"])}
+# name -> [(product text, replacement)]
+VARIANTS = {
+    "base": [],
+    # no global stores
+    "nostore": [("  __builtin_amdgcn_raw_buffer_store_b128(u, r, voff, soff, WT ? 16 : 2);\n", "")],
+    # every weight load reads the first 64 KB of its matrix (L1 / L2-resident)
+    "l2weights": [("  const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0);\n  uint4 u;",
+                   "  const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff & 0xFFFF, 0);\n  uint4 u;")],
+    # no slice-flag waits
+    "noflagwait": [("  while (__builtin_amdgcn_readfirstlane(*ec_flag<G>(smem, wv)) < target) __builtin_amdgcn_s_sleep(1);\n",
+                    "")],
+    # GELU / GELU' replaced by the identity / one
+    "nogelu": [("for (int e = 0; e < 4; ++e) y[e] = gelu_erf_fast(v[e]);", "for (int e = 0; e < 4; ++e) y[e] = v[e];"),
+               ("for (int e = 0; e < 4; ++e) y[e] = gelu_erf_grad_fast(v[e]);", "for (int e = 0; e < 4; ++e) y[e] = 1.f;")],
+}
 
 
 def build():
     os.makedirs(os.path.join(HERE, "build"), exist_ok=True)
+    src = open(os.path.join(SRC, "reschain.hip")).read()
     procs = []
-    for name, fl in VARIANTS.items():
-        fl, extra = fl if isinstance(fl, tuple) else (fl, [])
+    for name, reps in VARIANTS.items():
+        text = src
+        for a, b in reps:
+            if text.count(a) != 1:
+                sys.exit(f"{name}: text not found exactly once: {a[:60]!r}")
+            text = text.replace(a, b)
+        path = os.path.join(HERE, "build", f"ec_{name}.hip")
+        open(path, "w").write(text)
         out = os.path.join(HERE, "build", f"ec_{name}.so")
         procs.append(subprocess.Popen(
             ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-fPIC", "-shared", "-std=c++17", "-Wl,-Bsymbolic",
-             f"-DEC_PROBE_FLAGS={fl}", *extra, "-I" + os.path.join(REPO, "include"), os.path.join(SRC, "reschain.hip"),
+             "-munsafe-fp-atomics", "-I" + SRC, "-I" + os.path.join(REPO, "include"), path,
              os.path.join(SRC, "runtime.hip"), "-o", out]))
     for p in procs:
         assert p.wait() == 0
@@ -93,19 +112,6 @@ def main(iters=20, taps=1):
             t1.record()
             torch.cuda.synchronize()
             res.append(t0.elapsed_time(t1) * 1000 / iters)
-            if name.startswith("stamps"):
-                import numpy as np
-                buf = (ctypes.c_uint64 * (256 * 32 * 4))()
-                lib.aw_probe_ec_stamps(buf, 256 * 32 * 4)
-                st = np.frombuffer(buf, dtype=np.uint64).reshape(256, 32, 4).astype(np.int64)[:, :2 * R]
-                loop = np.median(st[:, :, 1] - st[:, :, 0], axis=0)
-                pub = np.median(st[:, :-1, 3] - st[:, :-1, 1], axis=0)
-                epi = np.median(st[:, :-1, 2] - st[:, :-1, 3], axis=0)
-                gap = np.median(st[:, 1:, 0] - st[:, :-1, 2], axis=0)
-                print(f"  {'fwd' if args is fa else 'bwd'} stamps (cycles, median over WGs) k-loop {loop.astype(int).tolist()}")
-                print(f"      k-loop end -> published {pub.astype(int).tolist()}")
-                print(f"      published -> epilogue end {epi.astype(int).tolist()}")
-                print(f"      -> next k-loop  {gap.astype(int).tolist()}")
         print(f"{name:14s} fwd {res[0]:7.1f} us   bwd {res[1]:7.1f} us", flush=True)
 
 

@@ -46,32 +46,9 @@
 
 #pragma clang diagnostic ignored "-Winline-asm"
 
-// Probe builds only (tools/probe/res_chain_variants.py compiles this file alone with -DEC_PROBE_FLAGS=n; the
-// library never sets it): 1 = no global stores, 2 = every weight load reads the first 64 KB of its matrix
-// (L1/L2-resident), 4 = per-conv s_memtime stamps of wave 0 into g_ec_stamps (K loop start, K loop end, epilogue
-// end, slice published), 8 = no slice-flag waits, 16 = GELU / GELU' replaced by the identity / one, 32 = no saved
-// tensor through the scratch (forward).  Results of the probe builds are garbage by construction.
-#ifndef EC_PROBE_FLAGS
-#define EC_PROBE_FLAGS 0
-#endif
-#if EC_PROBE_FLAGS & 4
-__device__ uint64_t g_ec_stamps[1024 * 32 * 4];
-extern "C" int aw_probe_ec_stamps(uint64_t* out, int n) {
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ec_stamps), (size_t)n * 8) == hipSuccess ? n : -1;
-}
-#endif
+// (Probe builds with parts left out are made from text replacements of this file: tools/probe/res_chain_variants.py.)
 
 namespace {
-
-__device__ __forceinline__ void ec_stamp(int conv, int k) {
-#if EC_PROBE_FLAGS & 4
-  if (threadIdx.x == 0 && blockIdx.x < 1024 && conv < 32)
-    g_ec_stamps[(blockIdx.x * 32 + conv) * 4 + k] = __builtin_amdgcn_s_memtime();
-#else
-  (void)conv;
-  (void)k;
-#endif
-}
 
 constexpr int EC_H = 512;                   // channels (the reference's hidden_dim)
 constexpr int EC_ROWS = 64;                 // tokens per workgroup
@@ -117,13 +94,11 @@ __device__ __forceinline__ u32x2 ec_load8(rsrc_t r, uint32_t voff, int soff) {
 // the data registers stay untouched for a few cycles after a store issues: reused at once (the next LDS address
 // computed into them), the stored data's first dword intermittently came out as that address
 template <bool WT> __device__ __forceinline__ void ec_store16(rsrc_t r, uint32_t voff, int soff, uint4 v) {
-  if constexpr ((EC_PROBE_FLAGS & 1) == 0) {
-    aw_v4i32 u;
-    memcpy(&u, &v, 16);
-    // sc1 (write-through) or nt: the lines must not stay in the XCD's L2, which holds the weight stream
-    __builtin_amdgcn_raw_buffer_store_b128(u, r, voff, soff, WT ? 16 : 2);
-    asm volatile("s_nop 4" ::"v"(u));
-  }
+  aw_v4i32 u;
+  memcpy(&u, &v, 16);
+  // sc1 (write-through) or nt: the lines must not stay in the XCD's L2, which holds the weight stream
+  __builtin_amdgcn_raw_buffer_store_b128(u, r, voff, soff, WT ? 16 : 2);
+  asm volatile("s_nop 4" ::"v"(u));
 }
 __device__ __forceinline__ void ec_store8(rsrc_t r, uint32_t voff, u32x2 v) {
   __builtin_amdgcn_raw_buffer_store_b64(v, r, voff, 0, 2);
@@ -144,7 +119,6 @@ __device__ __forceinline__ void ec_unpack(u32x2 u, float (&v)[4]) {
   v[3] = __uint_as_float(u.y & 0xFFFF0000u);
 }
 __device__ __forceinline__ uint4 ec_wload(rsrc_t r, int voff, int soff) {
-  if constexpr ((EC_PROBE_FLAGS & 2) != 0) soff &= 0xFFFF;
   const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0);
   uint4 u;
   memcpy(&u, &v, 16);
@@ -192,13 +166,11 @@ template <class G> __device__ __forceinline__ lds_vint* ec_flag(char* smem, int 
 }
 // wait until wave wv has published `target` epilogues (its slice of the image this conv reads is written)
 template <class G> __device__ __forceinline__ void ec_wait(char* smem, int wv, int target) {
-  if constexpr ((EC_PROBE_FLAGS & 8) != 0) return;
   while (__builtin_amdgcn_readfirstlane(*ec_flag<G>(smem, wv)) < target) __builtin_amdgcn_s_sleep(1);
   asm volatile("" ::: "memory");   // the image reads that follow stay behind the flag read
 }
 // publish this wave's slice of the next image (every LDS write of it performed first)
 template <class G> __device__ __forceinline__ void ec_publish(char* smem, int w, int lane, int count) {
-  ec_stamp(count - 1, 3);
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   if (lane == 0) *ec_flag<G>(smem, w) = count;
 }
@@ -212,20 +184,12 @@ __device__ __forceinline__ void ec_frag_fence(int) { __builtin_amdgcn_sched_barr
 // the same bits as the unfused GEMM epilogues): written per element, the compiler packs only where it pays (the
 // fully packed pair form measured 3 % slower here, MI355X_MICROARCH.md: packed f32 VALU beside MFMAs)
 __device__ __forceinline__ void ec_gelu4(const float (&v)[4], float (&y)[4]) {
-  if constexpr ((EC_PROBE_FLAGS & 16) != 0) {
-    for (int e = 0; e < 4; ++e) y[e] = v[e];
-  } else {
 #pragma unroll
-    for (int e = 0; e < 4; ++e) y[e] = gelu_erf_fast(v[e]);
-  }
+  for (int e = 0; e < 4; ++e) y[e] = gelu_erf_fast(v[e]);
 }
 __device__ __forceinline__ void ec_gelu_grad4(const float (&v)[4], float (&y)[4]) {
-  if constexpr ((EC_PROBE_FLAGS & 16) != 0) {
-    for (int e = 0; e < 4; ++e) y[e] = 1.f;
-  } else {
 #pragma unroll
-    for (int e = 0; e < 4; ++e) y[e] = gelu_erf_grad_fast(v[e]);
-  }
+  for (int e = 0; e < 4; ++e) y[e] = gelu_erf_grad_fast(v[e]);
 }
 
 // Weight fragment (i, s) of wave w (rows 64w + 16i .. +15, k 32s .. 32s + 31) in the fragment-packed layout: block
@@ -419,7 +383,6 @@ __global__ __launch_bounds__(EC_NTH) void res_chain_fwd_kernel(aw_res_chain_fwd_
     const rsrc_t rn = ec_rsrc(has_next ? (second ? P.w1[r + 1] : P.w2[r]) : nullptr, G::WBYTES);
     const int io = (c & 1) * G::IMG, no = ((c + 1) & 1) * G::IMG;
     f32x4 acc[4][4];
-    ec_stamp(c, 0);
     // this conv's bias, one value per lane (the wave's 64 channels), loaded ahead of the K loop and parked in the
     // wave's LDS slot at its end (read in the epilogue as a 16-B broadcast per fragment row: no L2 latency there)
     const float bias_l = (second ? P.b2[r] : P.b1[r])[64 * L.w + L.lane];
@@ -436,7 +399,6 @@ __global__ __launch_bounds__(EC_NTH) void res_chain_fwd_kernel(aw_res_chain_fwd_
     };
     ec_conv<G>(acc, wf, smem, L.rb, io, rc, rn, has_next, L.wl, L.w, c, park, hash);
     const u32x2 keep = {kb[0], kb[1]};
-    ec_stamp(c, 1);
     int nwb[4];   // this lane's write positions in the next image (fragment i; + JS j)
 #pragma unroll
     for (int i = 0; i < 4; ++i) nwb[i] = L.wb(i) + no;
@@ -466,7 +428,7 @@ __global__ __launch_bounds__(EC_NTH) void res_chain_fwd_kernel(aw_res_chain_fwd_
       ec_publish<G>(smem, L.w, L.lane, c + 1);
       const rsrc_t rh = ec_rsrc(P.h[r], nbytes);
 #pragma unroll
-      for (int j = 0; j < ((EC_PROBE_FLAGS & 32) ? 0 : 4); ++j) {
+      for (int j = 0; j < 4; ++j) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           float v[4], bv[4];
@@ -507,7 +469,7 @@ __global__ __launch_bounds__(EC_NTH) void res_chain_fwd_kernel(aw_res_chain_fwd_
         ec_publish<G>(smem, L.w, L.lane, c + 1);
         const rsrc_t rx = ec_rsrc(P.x[r], nbytes);
 #pragma unroll
-        for (int j = 0; j < ((EC_PROBE_FLAGS & 32) ? 0 : 4); ++j) {
+        for (int j = 0; j < 4; ++j) {
 #pragma unroll
           for (int i = 0; i < 4; ++i) ec_lds_w8(smem, S.sw[i], xr[i][j]);
           ec_store_scratch<G, WT>(smem, j, S, rx);
@@ -526,7 +488,6 @@ __global__ __launch_bounds__(EC_NTH) void res_chain_fwd_kernel(aw_res_chain_fwd_
       }
       ec_store_slice<G, WT>(smem, no, S, ec_rsrc(P.a[r], nbytes));
     }
-    ec_stamp(c, 2);
   }
 }
 
@@ -565,7 +526,6 @@ __global__ __launch_bounds__(EC_NTH) void res_chain_bwd_kernel(aw_res_chain_bwd_
     const rsrc_t rn = ec_rsrc(has_next ? (second ? P.w2t[r - 1] : P.w1t[r]) : nullptr, G::WBYTES);
     const int io = (c & 1) * G::IMG, no = ((c + 1) & 1) * G::IMG;
     f32x4 acc[4][4];
-    ec_stamp(c, 0);
     // the epilogue's pre-activation (h_r for conv2's gradient, x_r for conv1's) as whole 128-B lines (the wave's
     // 64-channel slice of 8 tokens per load, as the stores), turned into fragments through the wave's scratch in
     // the epilogue; and, for conv1's, block r - 1's dropout keep bits.  Loaded behind the last K step's weight loads:
@@ -585,7 +545,6 @@ __global__ __launch_bounds__(EC_NTH) void res_chain_bwd_kernel(aw_res_chain_bwd_
       if (DROP && second && r > 0) keep = ec_keep(P.drop_masks, r - 1, tid);
     };
     ec_conv<G>(acc, wf, smem, L.rb, io, rc, rn, has_next, L.wl, L.w, c, load_pre, [](int) {});
-    ec_stamp(c, 1);
     int nwb[4];   // this lane's write positions in the next image (fragment i; + JS j)
 #pragma unroll
     for (int i = 0; i < 4; ++i) nwb[i] = L.wb(i) + no;
@@ -659,7 +618,6 @@ __global__ __launch_bounds__(EC_NTH) void res_chain_bwd_kernel(aw_res_chain_bwd_
       }
       ec_store_slice<G, WT>(smem, no, S, ec_rsrc(P.gxo_out[r], nbytes));
     }
-    ec_stamp(c, 2);
   }
 }
 
