@@ -28,7 +28,7 @@ ANCHORS = [
     ("  ees[tid] = tid < K ? ee", [2], "before"),
     ("  // ---- distances d = fl(", [3], "before"),
     ("  // ---- lexicographic (d, k) merge", [4], "before"),
-    ("  // ---- thread (row r, quad q) resolves", [5], "before"),
+    ("  // ---- thread (row r, quad q) reads its row's winner", [5], "before"),
     ("    atomicAdd(sqerr, t);\n  }\n}", [6, 9], "end"),
 ]
 PHASES = "loads-issue+z chunks(mfma) norms-publish argmin merge+barrier finish"

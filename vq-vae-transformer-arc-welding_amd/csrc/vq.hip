@@ -315,7 +315,7 @@ __global__ __launch_bounds__(VQ_THREADS, 2) void vq_fwd_kernel(const float* __re
 template <int D> struct VqPinLds {
   static constexpr int ROWS = 64;
   static constexpr int ES = 0, ZS = ES + VQ_CODES * D, EES = ZS + ROWS * D, ZZS = EES + VQ_CODES;
-  static constexpr int RD = ZZS + ROWS, HIST = RD + 16 * ROWS, RED = HIST + VQ_CODES;   // RD: ROWS x 8 int2
+  static constexpr int RD = ZZS + ROWS, HIST = RD + 2 * ROWS, RED = HIST + VQ_CODES;   // RD: ROWS u64 keys
   static constexpr int TOTAL = RED + 16;                     // floats (RED: 8 doubles)
   static_assert(TOTAL * 4 <= 160 * 1024, "pinned VQ LDS");
 };
@@ -385,7 +385,8 @@ __global__ __launch_bounds__(VQ_THREADS, 1) void vq_fwd_pinned_kernel(const floa
   float* zs = smem + L::ZS;                // [ROWS][D] likewise
   float* ees = smem + L::EES;              // [VQ_CODES]: |e_k|^2, NaN for k >= K
   float* zzs = smem + L::ZZS;              // [ROWS]
-  int2* cand = reinterpret_cast<int2*>(smem + L::RD);   // [ROWS][8 waves] per-wave row minima (d bits, k)
+  // [ROWS] lexicographic (d, k) row minima as 64-bit keys (order-preserving d bits above k), merged by LDS atomic min
+  unsigned long long* rkey = reinterpret_cast<unsigned long long*>(smem + L::RD);
   float* hist = smem + L::HIST;            // [VQ_CODES] this workgroup's code counts
   double* red = reinterpret_cast<double*>(smem + L::RED);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -423,6 +424,7 @@ __global__ __launch_bounds__(VQ_THREADS, 1) void vq_fwd_pinned_kernel(const floa
     if (it < ROWS * NQ) put4(zs, r, q, zr[i]);
   }
   hist[tid] = 0.f;
+  if (tid < ROWS) rkey[tid] = ~0ull;
 
   // ---- chunk loop: per 16-dim chunk, 8 MFMA steps (two groups of four) and the norms' next 16 terms
   f32x16 acc[2][2];                // [code tile mi][row tile ni]
@@ -554,22 +556,21 @@ __global__ __launch_bounds__(VQ_THREADS, 1) void vq_fwd_pinned_kernel(const floa
   int bestk[2];
 #pragma unroll
   for (int ni = 0; ni < 2; ++ni) bestk[ni] = 64 * w + 4 * h + 2 * bj[ni] - (bj[ni] & 3);   // = 32 mi + 8 g + r
-  // ---- lexicographic (d, k) merge of the two lane halves (codes 4h apart), then across the 8 waves (LDS)
+  // ---- lexicographic (d, k) merge across the 16 lane candidates of a row (2 lane halves x 8 waves): one LDS 64-bit
+  //      atomic min per lane and row on the key (sortable d << 32 | k).  The float -> sortable map (sign set: all
+  //      bits flipped, else the sign bit set) orders the keys as the floats; the candidates are never NaN (a lane
+  //      without a finite distance reports +inf), and -0 cannot occur (a distance is an exact zero only as x - x).
 #pragma unroll
   for (int ni = 0; ni < 2; ++ni) {
-    const float d = __shfl_xor(best[ni], 32, 64);
-    const int k = __shfl_xor(bestk[ni], 32, 64);
-    lex_take(d, k, true, best[ni], bestk[ni]);
-  }
-  if (h == 0) {   // candidates as (d bits, k) pairs, [row][wave]: a row's 8 are one 64-B line
-#pragma unroll
-    for (int ni = 0; ni < 2; ++ni) cand[(jr + 32 * ni) * 8 + w] = make_int2(__float_as_int(best[ni]), bestk[ni]);
+    const uint32_t b = __float_as_uint(best[ni]);
+    const uint32_t u = (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+    atomicMin(rkey + jr + 32 * ni, ((unsigned long long)u << 32) | (uint32_t)bestk[ni]);
   }
   vq_lds_barrier();
-  // ---- thread (row r, quad q) resolves its row's winner from the 8 wave candidates (four 16-B LDS broadcast
-  //      reads), takes e_k's quad from the pinned codebook and writes z_q (+ the operand copy) coalesced; the q == 0
-  //      thread of a row writes idx and counts the code in LDS.  The items of a thread are unrolled and only their
-  //      stores predicated, so their LDS chains overlap.
+  // ---- thread (row r, quad q) reads its row's winner (one LDS broadcast read of the key), takes e_k's quad from
+  //      the pinned codebook and writes z_q (+ the operand copy) coalesced; the q == 0 thread of a row writes idx and
+  //      counts the code in LDS.  The items of a thread are unrolled and only their stores predicated, so their LDS
+  //      chains overlap.
   double se = 0.0;
   constexpr int IPT = (ROWS * NQ + VQ_THREADS - 1) / VQ_THREADS;
 #pragma unroll
@@ -578,16 +579,7 @@ __global__ __launch_bounds__(VQ_THREADS, 1) void vq_fwd_pinned_kernel(const floa
     const int r = it / NQ, q = it - r * NQ;
     const int64_t row = row0 + r;
     const bool live = tid + i * VQ_THREADS < ROWS * NQ && row < N;
-    const int4* cp = reinterpret_cast<const int4*>(cand + r * 8);
-    const int4 c[4] = {cp[0], cp[1], cp[2], cp[3]};
-    float bd = __int_as_float(c[0].x);
-    int bk = c[0].y;
-    lex_take(__int_as_float(c[0].z), c[0].w, true, bd, bk);
-#pragma unroll
-    for (int v = 1; v < 4; ++v) {
-      lex_take(__int_as_float(c[v].x), c[v].y, true, bd, bk);
-      lex_take(__int_as_float(c[v].z), c[v].w, true, bd, bk);
-    }
+    int bk = (int)(uint32_t)rkey[r];
     if (bk < 0 || bk >= K) bk = 0;  // all-NaN row guard (torch would return the NaN position)
     if (live && q == 0) {
       idx[row] = bk;
