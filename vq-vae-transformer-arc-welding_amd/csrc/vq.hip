@@ -547,8 +547,10 @@ __global__ __launch_bounds__(VQ_THREADS, 1) void vq_fwd_pinned_kernel(const floa
         for (int r = 0; r < 4; ++r)
 #pragma unroll
           for (int ni = 0; ni < 2; ++ni) {
+            // the running minimum as v_min (off the compare's VCC: the next compare does not wait for a select);
+            // v_min never takes a NaN over a number, as the strict < never does
             const bool t = dv[ni][r] < best[ni];
-            best[ni] = t ? dv[ni][r] : best[ni];
+            best[ni] = __builtin_fminf(best[ni], dv[ni][r]);
             bj[ni] = t ? 16 * mi + 4 * g + r : bj[ni];
           }
       }
