@@ -1,0 +1,62 @@
+"""The decoder chain's LDS image swizzle (csrc/reschain.hip, EcGeo<3>::KEYS): the keys the kernel is built with make
+every B-fragment ds_read_b128 lane group conflict-free for all three tap shifts, and keep the epilogue's
+ds_write_b64 at two lanes per bank (tools/probe/chain_swizzle.py derived them).  CPU only: reads the constant from
+the source."""
+import os
+import re
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SRC = os.path.join(REPO, "vq-vae-transformer-arc-welding_amd", "csrc", "reschain.hip")
+
+
+def _keys():
+    text = open(SRC).read()
+    m = re.search(r"KEYS = TAPS == 1 \? 0x([0-9a-f]+)ull : 0x([0-9a-f]+)ull", text)
+    assert m, "EcGeo::KEYS not found"
+    enc, dec = int(m.group(1), 16), int(m.group(2), 16)
+
+    def table(v):
+        k = {u: (v >> (4 * u)) & 15 for u in range(16)}
+        k[-1], k[16] = 15, 0          # EcGeo::key of the zero rows
+        return k
+    return table(enc), table(dec)
+
+
+def _bank_slots(key, shift):
+    """16-B bank slot (physical chunk mod 16) hit by each lane of the four ds_read_b128 lane groups of a B-fragment
+    read at K step kk = 0 (the XOR with 4 (kk & 3) and the + 16 (kk >> 2) only permute the slots)."""
+    groups = [list(range(0, 4)) + list(range(12, 16)) + list(range(20, 28)),
+              list(range(4, 12)) + list(range(16, 20)) + list(range(28, 32))]
+    groups += [[l + 32 for l in g] for g in groups]
+    out = []
+    for grp in groups:
+        slots = []
+        for lane in grp:
+            g, li = lane >> 4, lane & 15
+            tp = li + shift
+            slots.append((g ^ key[tp]) & 15)
+        out.append(slots)
+    return out
+
+
+def test_decoder_keys_make_every_tap_read_conflict_free():
+    _, dec = _keys()
+    for shift in (-1, 0, 1):
+        for slots in _bank_slots(dec, shift):
+            assert len(set(slots)) == 16, (shift, slots)
+
+
+def test_encoder_keys_are_the_identity_and_conflict_free_unshifted():
+    enc, _ = _keys()
+    assert [enc[u] for u in range(16)] == list(range(16))
+    for slots in _bank_slots(enc, 0):
+        assert len(set(slots)) == 16
+
+
+def test_decoder_keys_keep_the_epilogue_writes_at_two_lanes_per_bank():
+    _, dec = _keys()
+    # ds_write_b64: 16 contiguous lanes = tokens 0..15 of one g; bank (4 * chunk + 2 (g & 1)) mod 32
+    counts = {}
+    for u in range(16):
+        counts[dec[u] % 8] = counts.get(dec[u] % 8, 0) + 1
+    assert sorted(counts.values()) == [2] * 8
