@@ -175,14 +175,12 @@ def transformer_workload(dev, rank, world, args, seqs, n_cycles, accumulate=1, l
         pel = (time.perf_counter() - t1) / n_prof
         prof = (kernels.PROFILE, n_prof)
         kernels.PROFILE = None
-        traffic, tsrc = transformer_traffic()
+        pmc, tsrc = pmc_traffic("pmc_traffic_transformer.json")
         roof = gemm_roofline(prof, pel, el, args.steps, BF16_PEAK_TFLOPS, "bf16",
-                             traffic if pretokenized else None, tsrc if pretokenized else None)
-        roof["kernel"] = "gemm_kernel<bf16> (aw_gemm / aw_gemm_grouped): the decoder's Linear layers, fwd + dgrad + wgrad"
+                             pmc if pretokenized else None, tsrc if pretokenized else None)
         if not pretokenized and any(e[3] == "gemm_f32" for e in prof[0]):
-            roof["tokenize_gemm_f32"] = {k: v for k, v in gemm_roofline(prof, pel, el, args.steps, FP32_PEAK_TFLOPS,
-                                                                          "f32").items()
-                                         if k in ("achieved", "peak", "frac", "launches_per_step", "gemm_ms_per_step")}
+            r32 = gemm_roofline(prof, pel, el, args.steps, FP32_PEAK_TFLOPS, "f32")
+            roof["tokenize_gemm_f32"] = {"peak": FP32_PEAK_TFLOPS, **r32["family"]}
         attn = attn_roofline(prof)
     return {"value": round(windows / el, 2), "unit": "windows/s", "ms_per_step": round(el * 1e3 / args.steps, 3),
             "steps": args.steps, "roofline": roof, "attention": attn,
@@ -209,21 +207,15 @@ def _newest_profile(name):
     return files[-1] if files else None
 
 
-def gemm_traffic():
-    """HBM bytes of the GEMM family from the newest committed rocprofv3 PMC passes (FETCH_SIZE and WRITE_SIZE in
-    separate runs, FETCH_SIZE doubled on gfx950; tools/pmc_traffic.py) of this same workload: counters cannot be
-    read from inside the timed run.  Since round 3 the family is every kernel an aw_gemm / aw_gemm_grouped call
-    launches (gemm_kernel, wgrad_conv3_kernel, gemm_reduce_kernel) and the file carries its bytes per traced step,
-    which gemm_roofline divides by the calls per step (older files: the per-kernel-launch average)."""
-    newest = _newest_profile("pmc_gemm_traffic.json")
+def pmc_traffic(name):
+    """The newest committed pmc_traffic.py record `name` (profiles/r<round>/<session>/): HBM bytes per launch of
+    every traced kernel of this same workload, FETCH_SIZE (doubled on gfx950) and WRITE_SIZE from separate rocprofv3
+    passes (tools/prof_round.sh, tools/prof_transformer.sh): counters cannot be read from inside the timed run."""
+    newest = _newest_profile(name)
     if newest is None:
         return None, None
     with open(newest) as f:
-        d = json.load(f)
-    src = os.path.relpath(newest, REPO)
-    if d.get("bytes_per_step"):
-        return {"bytes_per_step": d["bytes_per_step"]}, src
-    return round(d["avg_bytes_per_launch"]), src
+        return json.load(f), os.path.relpath(newest, REPO)
 
 
 REFERENCE_CPU = {"value": 85.0, "unit": "windows/s", "cores": 8, "kind": "reference",
@@ -356,26 +348,96 @@ def vqvae_workload(dev, rank, world, args, dtype, steps, warmup, profile=True, K
     return elapsed, prof, prof_el
 
 
-def gemm_roofline(prof, prof_el, elapsed, steps, peak, dtype_name, traffic=None, traffic_src=None):
-    """The GEMM family of one operand dtype over the profiled eager steps (HIP events per launch)."""
+def _ev_ms(e):
+    return e[0].elapsed_time(e[1])
+
+
+def _pmc_bytes(pmc, name, exclude=None):
+    """HBM bytes per launch of the kernel `name` (the profile name: "res_chain_bwd_kernel<3>", "wgrad_conv3_kernel",
+    ...) from a pmc_traffic.py record: every traced kernel whose rocprofv3 name holds the stem (template arguments
+    after the first dropped), the f32 instantiations left out of a bf16 family."""
+    if not pmc:
+        return None
+    stem = name.split(" ")[0]
+    stem = stem[:-1] if stem.endswith(">") else stem
+    tot, n = 0.0, 0
+    for k, v in pmc.get("kernels", {}).items():
+        if stem in k and not (exclude and exclude in k):
+            tot += v["bytes_per_launch"] * v["launches"]
+            n += v["launches"]
+    return round(tot / n) if n else None
+
+
+def kernel_table(prof, tag, peak, pmc=None, exclude=None):
+    """Per kernel of one family (the profile's kernel names): launches per step, average launch duration (HIP events
+    on the launch stream), algorithmic GFLOP per launch, achieved TFLOP/s and fraction of `peak`, algorithmic HBM
+    bytes per launch where the call states them, and the PMC-counted bytes per launch with their ratio to it."""
     lst, n_prof = prof
-    lst = [e for e in lst if e[3] == f"gemm_{dtype_name}"]
-    ms = sum(e0.elapsed_time(e1) for e0, e1, _, _ in lst)
-    flops = sum(e[2] for e in lst)
-    n = len(lst)
-    achieved = flops / (ms * 1e-3) / 1e12
-    if isinstance(traffic, dict):     # family bytes per traced step -> per aw_gemm call
-        traffic = round(traffic["bytes_per_step"] / max(1, n // n_prof))
-    return {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
-            "frac": round(achieved / peak, 4), "traffic": traffic, "traffic_unit": "bytes/launch",
-            "traffic_source": traffic_src, "kernel": f"gemm_kernel<{dtype_name}> (aw_gemm)",
-            "launches_per_step": n // n_prof, "avg_launch_us": round(ms * 1e3 / n, 2),
-            "avg_algorithmic_gflop_per_launch": round(flops / n / 1e9, 4),
-            "gemm_ms_per_step": round(ms / n_prof, 3),
-            "gemm_share_of_step": round(ms / n_prof / (elapsed * 1e3 / steps), 4),
+    by = {}
+    for e in lst:
+        if e[3] == tag:
+            by.setdefault(e[4], []).append(e)
+    out = {}
+    for name, ev in by.items():
+        ms = sum(_ev_ms(e) for e in ev)
+        fl = sum(e[2] for e in ev)
+        tf = fl / (ms * 1e-3) / 1e12
+        row = {"launches_per_step": len(ev) // n_prof, "avg_launch_us": round(ms * 1e3 / len(ev), 2),
+               "ms_per_step": round(ms / n_prof, 3), "gflop_per_launch": round(fl / len(ev) / 1e9, 4),
+               "achieved": round(tf, 2), "frac": round(tf / peak, 4)}
+        if all(e[5] is not None for e in ev):
+            row["algorithmic_bytes_per_launch"] = round(sum(e[5] for e in ev) / len(ev))
+        t = _pmc_bytes(pmc, name, exclude)
+        if t is not None:
+            row["traffic_bytes_per_launch"] = t
+            if row.get("algorithmic_bytes_per_launch"):
+                row["traffic_over_algorithmic"] = round(t / row["algorithmic_bytes_per_launch"], 3)
+        out[name] = row
+    return dict(sorted(out.items(), key=lambda kv: -kv[1]["ms_per_step"]))
+
+
+def gemm_roofline(prof, prof_el, elapsed, steps, peak, dtype_name, pmc=None, traffic_src=None):
+    """The roofline of the DOMINANT kernel of the MFMA family of one operand dtype (the kernel with the most time
+    per step over the profiled eager steps, HIP events per launch on its launch stream): its algorithmic FLOPs per
+    launch / its average launch duration, and its PMC-counted HBM bytes per launch (`pmc`: the pmc_traffic.py
+    record of the same workload, committed under profiles/).  `kernels` holds the same figures for every kernel of
+    the family, `family` the aggregate over all of them."""
+    lst, n_prof = prof
+    tag = f"gemm_{dtype_name}"
+    fam = [e for e in lst if e[3] == tag]
+    ms = sum(_ev_ms(e) for e in fam)
+    flops = sum(e[2] for e in fam)
+    n = len(fam)
+    fam_tf = flops / (ms * 1e-3) / 1e12
+    excl = "<float" if dtype_name == "bf16" else None
+    table = kernel_table(prof, tag, peak, pmc, excl)
+    dom_name, dom = next(iter(table.items()))
+    return {"bound": "mfma", "achieved": dom["achieved"], "peak": peak, "unit": "TFLOP/s", "frac": dom["frac"],
+            "traffic": dom.get("traffic_bytes_per_launch"), "traffic_unit": "bytes/launch",
+            "traffic_source": traffic_src, "kernel": dom_name,
+            "avg_launch_us": dom["avg_launch_us"], "algorithmic_gflop_per_launch": dom["gflop_per_launch"],
+            "algorithmic_bytes_per_launch": dom.get("algorithmic_bytes_per_launch"),
+            "traffic_over_algorithmic": dom.get("traffic_over_algorithmic"),
+            "family": {"achieved": round(fam_tf, 2), "frac": round(fam_tf / peak, 4), "launches_per_step": n // n_prof,
+                       "ms_per_step": round(ms / n_prof, 3),
+                       "share_of_step": round(ms / n_prof / (elapsed * 1e3 / steps), 4),
+                       "kernels": f"every {tag} MFMA launch: " + ", ".join(table)},
+            "kernels": table,
             "measured_over": f"{n_prof} eager steps after the timed region (HIP events per launch, on the launch "
                              "stream)",
             "eager_ms_per_step_with_events": round(prof_el * 1e3, 3)}
+
+
+def vq_in_step(prof):
+    """The VQ forward as the training step runs it (profiled eager steps: its codebook cold behind the encoder)."""
+    lst, n_prof = prof
+    ev = [e for e in lst if e[3] == "vq_fwd"]
+    if not ev:
+        return None
+    us = sum(_ev_ms(e) for e in ev) * 1e3 / len(ev)
+    tf = sum(e[2] for e in ev) / len(ev) / (us * 1e-6) / 1e12
+    return {"kernel": ev[0][4], "avg_launch_us": round(us, 2), "frac": round(tf / FP32_PEAK_TFLOPS, 4),
+            "launches_per_step": len(ev) // n_prof}
 
 
 def attn_roofline(prof):
@@ -387,27 +449,13 @@ def attn_roofline(prof):
         ev = [e for e in lst if e[3] == tag]
         if not ev:
             continue
-        us = sum(e0.elapsed_time(e1) for e0, e1, _, _ in ev) * 1e3 / len(ev)
+        us = sum(_ev_ms(e) for e in ev) * 1e3 / len(ev)
         tf = sum(e[2] for e in ev) / len(ev) / (us * 1e-6) / 1e12
         out[tag] = {"avg_launch_us": round(us, 2), "achieved": round(tf, 2), "peak": BF16_PEAK_TFLOPS,
                     "unit": "TFLOP/s", "frac": round(tf / BF16_PEAK_TFLOPS, 4),
                     "gflop_per_launch": round(sum(e[2] for e in ev) / len(ev) / 1e9, 4),
                     "launches_per_step": len(ev) // n_prof}
     return out
-
-
-def transformer_traffic():
-    """HBM bytes per bf16 GEMM launch of the decoder train step from the committed PMC passes of the
-    transformer_pretokenized workload (tools/prof_transformer.sh; FETCH_SIZE doubled per the gfx950 note)."""
-    newest = _newest_profile("pmc_transformer_gemm_traffic.json")
-    if newest is None:
-        return None, None
-    with open(newest) as f:
-        d = json.load(f)
-    src = os.path.relpath(newest, REPO)
-    if d.get("bytes_per_step"):
-        return {"bytes_per_step": d["bytes_per_step"]}, src
-    return round(d["avg_bytes_per_launch"]), src
 
 
 def vq_kernel_roofline(dev, N, K, D, iters=10):
@@ -486,11 +534,20 @@ def _transformer_lines(extra, dev, rank, world, args):
 
 
 _ROOF_KEYS = ("bound", "achieved", "peak", "unit", "frac", "traffic", "traffic_unit", "traffic_source", "kernel",
-              "launches_per_step", "avg_launch_us", "avg_algorithmic_gflop_per_launch", "gemm_ms_per_step")
+              "avg_launch_us", "algorithmic_gflop_per_launch", "algorithmic_bytes_per_launch",
+              "traffic_over_algorithmic")
 
 
 def _compact_roof(r, keys=_ROOF_KEYS):
-    return None if r is None else {k: r[k] for k in keys if k in r}
+    """The dominant kernel's roofline, the family aggregate, and per kernel of the family its launch time, fraction
+    of the peak and counted / algorithmic HBM bytes."""
+    if r is None:
+        return None
+    out = {k: r[k] for k in keys if k in r}
+    out["family"] = {k: r["family"][k] for k in ("achieved", "frac", "launches_per_step", "ms_per_step")}
+    out["per_kernel"] = {n: {k: v[k] for k in ("avg_launch_us", "launches_per_step", "frac", "traffic_over_algorithmic")
+                             if k in v} for n, v in r["kernels"].items()}
+    return out
 
 
 def _sub(d):
@@ -498,7 +555,7 @@ def _sub(d):
     out = {"value": d["value"], "unit": d["unit"], "ms_per_step": d["ms_per_step"]}
     r = d.get("roofline")
     if r:
-        out["gemm_frac"] = r["frac"]
+        out["gemm_frac"] = r["family"]["frac"]
         if "tokenize_gemm_f32" in r:
             out["tokenize_gemm_f32_frac"] = r["tokenize_gemm_f32"]["frac"]
     for tag, a in (d.get("attention") or {}).items():
@@ -523,15 +580,19 @@ def compact_line(line, detail):
     if "vq_kernel" in line:
         v = line["vq_kernel"]
         lines["vq_kernel"] = {"us": v["avg_launch_us"], "frac": v["frac"], "bound": v["bound"]}
+        if v.get("in_step"):
+            lines["vq_kernel"]["in_step_us"] = v["in_step"]["avg_launch_us"]
+            lines["vq_kernel"]["in_step_frac"] = v["in_step"]["frac"]
     if "fp32" in line:
         f = line["fp32"]
         lines["fp32"] = {"value": f["value"], "unit": f["unit"], "ms_per_step": f["ms_per_step"],
-                         "gemm_frac_of_fp32_peak": f["roofline"]["frac"] if f.get("roofline") else None}
+                         "gemm_frac_of_fp32_peak": f["roofline"]["family"]["frac"] if f.get("roofline") else None}
     st = line.get("stress")
     if st:
         lines["stress_vqvae"] = {"value": st["vqvae"]["value"], "unit": "windows/s",
                                  "ms_per_step": st["vqvae"]["ms_per_step"],
-                                 "gemm_frac": st["vqvae"]["roofline"]["frac"] if st["vqvae"].get("roofline") else None,
+                                 "gemm_frac": st["vqvae"]["roofline"]["family"]["frac"] if st["vqvae"].get("roofline")
+                                 else None,
                                  "vq_kernel_frac": st["vqvae"]["vq_kernel"]["frac"]}
         lines["stress_transformer"] = _sub(st["transformer"])
     for k in ("transformer", "transformer_b16_acc5", "transformer_t257", "transformer_pretokenized"):
@@ -577,11 +638,13 @@ def main():
     elapsed, prof, prof_el = vqvae_workload(dev, rank, world, args, torch.bfloat16, args.steps, args.warmup,
                                             profile=not args.no_profile)
     value = world * args.batch * args.steps / elapsed
-    traffic, traffic_src = gemm_traffic()
-    roofline = gemm_roofline(prof, prof_el, elapsed, args.steps, BF16_PEAK_TFLOPS, "bf16", traffic,
+    pmc, traffic_src = pmc_traffic("pmc_traffic_vqvae.json")
+    roofline = gemm_roofline(prof, prof_el, elapsed, args.steps, BF16_PEAK_TFLOPS, "bf16", pmc,
                              traffic_src) if prof else None
 
     extra = {"vq_kernel": vq_kernel_roofline(dev, args.batch * 16, 512, 64)}
+    if prof:
+        extra["vq_kernel"]["in_step"] = vq_in_step(prof)
     if not args.no_fp32:
         # the same step with exact-fp32 operands (the default numerics, the reference's): priced against the
         # 157.3 TF fp32 MFMA roof

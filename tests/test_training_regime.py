@@ -67,6 +67,43 @@ def test_accumulate5_clip08_two_stage_trajectory_matches_reference(graphs):
                                            err_msg=f"stage {si} {n}")
 
 
+@pytest.mark.parametrize("n_batches", [13, 11])
+def test_graphed_fit_with_short_last_group_matches_eager(n_batches):
+    """An epoch whose length is not a multiple of accumulate_grad_batches ends on a short group (Lightning steps on
+    the epoch's last batch): 13 micro-batches = 5 + 5 + 3, 11 = 5 + 5 + 1.  The captured step replays groups of five
+    as one batch (arcweld/graphs.py), so the short group must run eagerly on the same gradients and optimizer state,
+    in every epoch, before and after the capture, and must never become the captured group size.  Three epochs of a
+    graphed fit (steps 1-2 warm up, epoch 1's short group eager before any capture, epoch 2 captures, replays and
+    steps its short group eagerly, epoch 3 replays after an eager step) against the same fit without graphs; fp32
+    operands, no dropout: only the weight-gradient reduction order differs."""
+    from arcweld.precision import operands
+    from arcweld.trainer import Trainer
+    from model.transformer_decoder import MyTransformerDecoder
+    kw = dict(d_model=128, n_classes=40, seq_len=33, n_blocks=2, n_head=4, res_dropout=0.0, att_dropout=0.0)
+    g = torch.Generator(device="cpu").manual_seed(11)
+    batches = []
+    for j in range(n_batches):
+        x = torch.randint(0, 38, (6, 33), generator=g)
+        y = torch.randint(0, 38, (6, 33), generator=g)
+        batches.append((x.cuda(), torch.zeros(6, dtype=torch.long).cuda(), y.cuda()))
+    params, steps = [], []
+    for graphs in (False, True):
+        torch.manual_seed(0)
+        m = MyTransformerDecoder(**kw).cuda().train()
+        m.switch_to_generate()
+        tr = Trainer(gradient_clip_val=0.8, accumulate_grad_batches=5, max_epochs=3, log_every_n_steps=1,
+                     hip_graphs=graphs)
+        with operands(torch.float32):
+            tr.fit(m, train_dataloaders=batches)
+        torch.cuda.synchronize()
+        steps.append(tr.global_step)
+        params.append({n: p.detach().clone() for n, p in m.named_parameters()})
+    assert steps == [9, 9]
+    assert tr._graphs.G == 5 and tr._graphs.static is not None
+    for n, p0 in params[0].items():
+        torch.testing.assert_close(params[1][n], p0, rtol=1e-4, atol=1e-6, msg=n)
+
+
 @pytest.mark.parametrize("task", ["generate", "classification"])
 def test_grouped_accumulation_equals_micro_batch_sum(task):
     """fused_train_step(groups=5) on the five micro-batches side by side (arcweld/decoder.py fused_step, what the

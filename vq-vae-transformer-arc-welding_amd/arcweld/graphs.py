@@ -159,28 +159,37 @@ class StepGraphs:
         with torch.cuda.graph(self.g2, pool=pool, capture_error_mode=_MODE):
             self.trainer._update(self.model)
 
+    def _eager(self, batches):
+        """One optimizer step over the micro-batches without the graphs (warm-up calls, groups the capture cannot
+        take): each micro-batch's forward/backward, the all-reduce of every live gradient, the update."""
+        for j, b in enumerate(batches):
+            loss = self.trainer.micro_step(self.model, b, j, self.scale)
+        for w in self.allreduce("all"):
+            w.wait()
+        self.trainer._update(self.model)
+        self.trainer.global_step += 1
+        return loss
+
     def run(self, batch):
         """One optimizer step over `batch`, or over a list of micro-batches (accumulate_grad_batches > 1: the
         forward/backward graph is replayed once per micro-batch, gradients accumulating in the flat buffer; the
         all-reduce runs once, split around the last micro-batch's backward -- DDP's no_sync accumulation)."""
         batches = batch if isinstance(batch, list) else [batch]
         G = len(batches) if len(batches) > 1 and self.group_accum and _same_shapes(batches) else 1
-        if self.fuse_update and len(batches) > 1 and G == 1:
-            raise ValueError("StepGraphs: the update is captured with the backward; one micro-batch per step")
         self.calls += 1
         if self.calls <= self.warmup:
-            for j, b in enumerate(batches):
-                loss = self.trainer.micro_step(self.model, b, j, self.scale)
-            for w in self.allreduce("all"):
-                w.wait()
-            self.trainer._update(self.model)
-            self.trainer.global_step += 1
-            return loss
+            return self._eager(batches)
+        # A group the captured step cannot replay runs eagerly on the same gradients and optimizer state: the short
+        # last group of an epoch (Lightning steps on the epoch's last batch whatever the group size), micro-batches
+        # of different shapes, or more than one micro-batch where the update is captured with the backward.  The
+        # graphs are captured on the first full group only, so a short group never fixes the captured size.
+        full = getattr(self.trainer, "accumulate", 1) if self.group_accum else 1
+        if (self.group_accum and G != full) or (self.fuse_update and G == 1 and len(batches) > 1) or \
+                (self.static is not None and G != self.G):
+            return self._eager(batches)
         if self.static is None:
             self.G = G
             self._capture(_concat(batches) if G > 1 else batches[0], G)
-        if G != self.G:
-            raise ValueError(f"StepGraphs: captured for groups of {self.G} micro-batches, got {len(batches)}")
         if G > 1:
             _copy_group_into(self.static, batches)
             batches = [None]      # one replay of the group's forward/backward

@@ -118,14 +118,16 @@ def _gemm_args(A, B, M, N, K, *, a_trans=False, b_trans=False, conv=None, alpha=
     return a
 
 
-def _timed(s, fn, flops, tag):
+def _timed(s, fn, flops, tag, name=None, nbytes=None):
     """Bench profiling (PROFILE is a list): HIP events around one launch on its stream, with the launch's
-    algorithmic FLOPs and a kernel-family tag ("gemm_bf16", "gemm_f32", "attn_fwd", "attn_bwd")."""
+    algorithmic FLOPs, a kernel-family tag ("gemm_bf16", "gemm_f32", "attn_fwd", "attn_bwd", "vq_fwd"), the name of
+    the kernel it runs (the rocprofv3 kernel name's stem, for the per-kernel roofline) and its algorithmic HBM bytes
+    (None where not stated)."""
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(s)
     fn(s.cuda_stream)
     e1.record(s)
-    PROFILE.append((e0, e1, flops, tag))
+    PROFILE.append((e0, e1, flops, tag, name or tag, nbytes))
 
 
 def _gemm_tag(A):
@@ -145,7 +147,7 @@ def gemm(A, B, M, N, K, *, stream=None, flops=None, **kw):
         return kw.get("C")
     s = stream if stream is not None else torch.cuda.current_stream()
     _timed(s, lambda sp: call("aw_gemm_ws", ctypes.byref(a), ptr(ws), wsn, sp),
-           _algorithmic_flops(M, N, K, kw.get("conv"), flops), _gemm_tag(A))
+           _algorithmic_flops(M, N, K, kw.get("conv"), flops), _gemm_tag(A), "gemm_kernel")
     return kw.get("C")
 
 
@@ -163,7 +165,11 @@ def gemm_grouped(problems, stream=None):
             continue
         s = stream if stream is not None else torch.cuda.current_stream()
         fl = sum(_algorithmic_flops(M, N, K, kw.get("conv"), None) for (_, _, M, N, K, kw) in chunk)
-        _timed(s, lambda sp: call("aw_gemm_grouped", arr, len(chunk), sp), fl, _gemm_tag(chunk[0][0]))
+        c0_ = chunk[0]
+        # the grouped decoder k = 3 weight gradients run wgrad_conv3_kernel (csrc/wgrad.hip wgrad_conv3_try)
+        nm = "wgrad_conv3_kernel" if (c0_[5].get("conv") is not None and c0_[0].dtype == torch.bfloat16) \
+            else "gemm_kernel (grouped)"
+        _timed(s, lambda sp: call("aw_gemm_grouped", arr, len(chunk), sp), fl, _gemm_tag(chunk[0][0]), nm)
 
 
 WGRAD_BATCH_MAX = 32     # aw_wgrad_batch problems per launch (include/arcweld_amd.h AW_WGRAD_BATCH_MAX)
@@ -201,7 +207,8 @@ def wgrad_batch(problems, stream=None):
         return
     s = stream if stream is not None else torch.cuda.current_stream()
     fl = sum(_algorithmic_flops(M, N, K, None, None) for (_, _, M, N, K, _) in problems)
-    _timed(s, lambda sp: call("aw_wgrad_batch", arr, len(problems), ptr(ws), wsb, sp), fl, _gemm_tag(problems[0][0]))
+    _timed(s, lambda sp: call("aw_wgrad_batch", arr, len(problems), ptr(ws), wsb, sp), fl, _gemm_tag(problems[0][0]),
+           "wgrad_tt_kernel")
 
 
 def wgrad_issue(problems, stream=None):
@@ -275,6 +282,17 @@ def res_dropout_masks(N, drop, seed_ptr=None, stream=None):
     return out
 
 
+def _nbytes(ts):
+    """Algorithmic HBM bytes of a launch: every operand read once and every output written once (distinct tensors;
+    None entries are absent operands)."""
+    seen, n = set(), 0
+    for t in ts:
+        if t is not None and t.data_ptr() not in seen:
+            seen.add(t.data_ptr())
+            n += t.numel() * t.element_size()
+    return n
+
+
 def _chain_flops(R, N, H, taps, seg):
     """Algorithmic flops of one chain launch: 2R convs of 2 N H (taps H) -- for taps 3 only the taps that touch a
     real row (the window edges lose one tap each, as _algorithmic_flops counts the implicit conv GEMMs)."""
@@ -307,7 +325,9 @@ def res_chain_fwd(a0, x0, w1, w2, b1, b2, h, a1, x, a, drop=(0.0, None), seed_pt
     g.store_policy = _chain_store_policy()
     g.drop_masks = ptr(masks)
     _maybe_timed(stream, "gemm_bf16", _chain_flops(R, N, H, taps, seg),
-                 lambda sp: call("aw_res_chain_fwd", ctypes.byref(g), sp))
+                 lambda sp: call("aw_res_chain_fwd", ctypes.byref(g), sp), f"res_chain_fwd_kernel<{int(taps)}>",
+                 _nbytes([a0, x0, masks] + list(w1) + list(w2) + list(b1) + list(b2) + list(h) + list(a1) +
+                         list(x)[:-1] + list(a)))
 
 
 def res_chain_bwd(gx, gxo, w1t, w2t, h, x, gh, gxo_out, drop_p=0.0, masks=None, taps=1, seg=16, stream=None):
@@ -329,7 +349,8 @@ def res_chain_bwd(gx, gxo, w1t, w2t, h, x, gh, gxo_out, drop_p=0.0, masks=None, 
     g.store_policy = _chain_store_policy()
     g.drop_masks = ptr(masks)
     _maybe_timed(stream, "gemm_bf16", _chain_flops(R, N, H, taps, seg),
-                 lambda sp: call("aw_res_chain_bwd", ctypes.byref(g), sp))
+                 lambda sp: call("aw_res_chain_bwd", ctypes.byref(g), sp), f"res_chain_bwd_kernel<{int(taps)}>",
+                 _nbytes([gx, gxo, masks] + list(w1t) + list(w2t) + list(h) + list(x) + list(gh) + list(gxo_out)))
 
 
 def res_pack_weights(src, fwd=None, bwd=None, taps=1, stream=None):
@@ -358,8 +379,12 @@ def vq_forward(z2d, E, zq, idx, counts, sqerr, stream=None, zq_copy=None, count_
     N, D = z2d.shape
     Kc = E.shape[0]
     assert counts.numel() >= count_groups * Kc, "counts: count_groups x K floats"
-    call("aw_vq_forward_ex2", ptr(z2d), ptr(E), N, Kc, D, ptr(zq), ptr(idx), ptr(counts), int(count_groups),
-         ptr(sqerr), ptr(zq_copy), dtype_code(zq_copy.dtype) if zq_copy is not None else 0, stream_ptr(stream))
+    # the pinned kernel (codebook in LDS, f32-input MFMA) serves K <= 512, D in {16, 32, 64} (csrc/vq.hip)
+    name = "vq_fwd_pinned_kernel" if Kc <= 512 and D in (16, 32, 64) else "vq_fwd_kernel"
+    _maybe_timed(stream, "vq_fwd", 2.0 * N * Kc * D, lambda sp: call(
+        "aw_vq_forward_ex2", ptr(z2d), ptr(E), N, Kc, D, ptr(zq), ptr(idx), ptr(counts), int(count_groups),
+        ptr(sqerr), ptr(zq_copy), dtype_code(zq_copy.dtype) if zq_copy is not None else 0, sp), name,
+        _nbytes([z2d, E, zq, idx, zq_copy]) + 4 * Kc * count_groups)
 
 
 def vq_finalize(counts, sqerr, N, K, D, beta, loss, perplexity, stream=None, count_groups=1):
@@ -613,12 +638,12 @@ def attn_flops(B, T, n_head, d):
     return 4.0 * B * n_head * (T * (T + 1) / 2) * (d // n_head)
 
 
-def _maybe_timed(stream, tag, flops, fn):
+def _maybe_timed(stream, tag, flops, fn, name=None, nbytes=None):
     if PROFILE is None:
         fn(stream_ptr(stream))
         return
     s = stream if stream is not None else torch.cuda.current_stream()
-    _timed(s, fn, flops, tag)
+    _timed(s, fn, flops, tag, name, nbytes)
 
 
 def attn_fwd(qkv, B, T, n_head, d, y, lse, drop=(0.0, 0), seed_ptr=None, stream=None):
