@@ -45,7 +45,7 @@ def main(iters=20, taps=1, N=16384):
                         taps=taps)
 
     def chain_bwd():
-        K.res_chain_bwd(gx, gxo, wt[:R], wt[R:], h, xs, gh, go, drop_p=p, masks=masks, taps=taps)
+        K.res_chain_bwd(gx, gxo, wt[:R], wt[R:], h, x0, [None] + x[:R - 1], gh, go, drop_p=p, masks=masks, taps=taps)
 
     def pack():
         K.res_pack_weights(w1 + w2, pk, wt, taps=taps)

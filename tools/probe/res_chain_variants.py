@@ -14,16 +14,13 @@ SRC = os.path.join(REPO, "vq-vae-transformer-arc-welding_amd", "csrc")
 # name -> [(product text, replacement)]
 VARIANTS = {
     "base": [],
-    # no global stores
-    "nostore": [("  __builtin_amdgcn_raw_buffer_store_b128(u, r, voff, soff, WT ? 16 : 2);\n", "")],
     # every weight load reads the first 64 KB of its matrix (L1 / L2-resident)
     "l2weights": [("  const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0);\n  uint4 u;",
                    "  const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff & 0xFFFF, 0);\n  uint4 u;")],
-    # no slice-flag waits
-    "noflagwait": [("  while (__builtin_amdgcn_readfirstlane(*ec_flag<G>(smem, wv)) < target) __builtin_amdgcn_s_sleep(1);\n",
-                    "")],
-    # GELU / GELU' replaced by the identity / one
-    "nogelu": [("for (int e = 0; e < 4; ++e) y[e] = gelu_erf_fast(v[e]);", "for (int e = 0; e < 4; ++e) y[e] = v[e];"),
+    # no wait for the partner workgroup's flag (the exchange's latency; the partner's slice may be stale)
+    "nopartnerwait": [("        ec_wait_partner(sync, E, c);\n", "")],
+    # the forward's GELU / GELU' replaced by the identity / one, the backward's GELU'(x_0) by one
+    "nogelu": [("    const float phi = aw_phi_e(v[e], ex);", "    const float phi = 1.f;\n    ex = 0.f;"),
                ("for (int e = 0; e < 4; ++e) y[e] = gelu_erf_grad_fast(v[e]);", "for (int e = 0; e < 4; ++e) y[e] = 1.f;")],
 }
 
@@ -73,19 +70,22 @@ def main(iters=20, taps=1):
     TH = taps * H
     gx, gxo = rnd(N, H, sc=0.01), rnd(N, H, sc=0.01)
     keep += [gx, gxo]
-    ba.gx, ba.gxo = gx.data_ptr(), gxo.data_ptr()
+    ba.gx, ba.gxo, ba.x0 = gx.data_ptr(), gxo.data_ptr(), x0.data_ptr()
     for r in range(R):
         ts = [rnd(H, TH, sc=TH ** -0.5), rnd(H, TH, sc=TH ** -0.5), rnd(H, sc=0.1, dt=torch.float32),
               rnd(H, sc=0.1, dt=torch.float32), e(), e(), e(), e(), rnd(H, TH, sc=TH ** -0.5),
               rnd(H, TH, sc=TH ** -0.5), e(), e()]
         keep += ts
         fa.w1[r], fa.w2[r], fa.b1[r], fa.b2[r] = (t.data_ptr() for t in ts[:4])
-        fa.h[r], fa.a1[r], fa.a[r] = ts[4].data_ptr(), ts[5].data_ptr(), ts[7].data_ptr()
-        fa.x[r] = ts[6].data_ptr() if r < R - 1 else None
+        fa.dgelu_h[r], fa.a1[r], fa.a[r] = ts[4].data_ptr(), ts[5].data_ptr(), ts[7].data_ptr()
+        fa.dgelu_x[r] = ts[6].data_ptr() if r < R - 1 else None
         fa.drop_seed[r] = r + 1
         ba.w1t[r], ba.w2t[r] = ts[8].data_ptr(), ts[9].data_ptr()
-        ba.h[r], ba.x[r], ba.gh[r], ba.gxo_out[r] = ts[4].data_ptr(), ts[6].data_ptr(), ts[10].data_ptr(), \
+        ba.dgelu_h[r], ba.dgelu_x[r], ba.gh[r], ba.gxo_out[r] = ts[4].data_ptr(), ts[6].data_ptr(), ts[10].data_ptr(), \
             ts[11].data_ptr()
+    sync = torch.zeros(int(nat.load().aw_res_chain_sync_words(N)) + 64, device="cuda", dtype=torch.int32)
+    keep.append(sync)
+    fa.sync = ba.sync = sync.data_ptr()
     s = torch.cuda.current_stream().cuda_stream
     masks = torch.empty(R * (N // 64) * 512 * 8, device="cuda", dtype=torch.uint8)
     keep.append(masks)
