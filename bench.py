@@ -121,10 +121,15 @@ def transformer_workload(dev, rank, world, args, seqs, n_cycles, accumulate=1, l
     cond = torch.zeros(seqs, dtype=torch.long, device=dev)
     use_graph = not args.no_graph
 
+    assert dec.task == "generate"   # the synthetic condition is unread by the generation loss
+
     def train(w):
+        # w: one micro-batch of windows, or the captured group's micro-batches side by side (arcweld/graphs.py): the
+        # condition rows follow the windows (each micro-batch's synthetic condition is zeros)
         ids = tokenize.encode_ids(vq, w)
         x, y, _ = tokenize.autoregressive_pairs(ids, start_token=K)
-        return (x, cond if w.shape[0] == seqs else torch.zeros(w.shape[0], dtype=torch.long, device=dev), y)
+        c = cond if w.shape[0] == seqs else torch.cat([cond] * (w.shape[0] // seqs))
+        return (x, c, y)
 
     batches = [train(w) for w in wins] if pretokenized else None
 

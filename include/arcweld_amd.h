@@ -134,16 +134,18 @@ int aw_wgrad_batch(const aw_gemm_args* args, int n, void* ws, int64_t ws_bytes, 
  * Forward, per block r (x_0 = x0, a_0 = a0 = GELU(x_0)), conv(W, v)[t] = sum_j W_j v[t + j - 1] (taps = 3) or W v[t]:
  *   h_r = conv(W1_r, a_r) + b1_r,  a1_r = GELU(h_r),  x_{r+1} = x_r + Dropout(conv(W2_r, a1_r) + b2_r; drop_seed[r],
  *   group row*H + c as aw_gemm's epilogue),  a_{r+1} = GELU(x_{r+1}) for r < R-1 and x_R for r = R-1.
- *   Stored: h[r] = h_r, a1[r] = a1_r, x[r] = x_{r+1} (r < R-1), a[r] = a_{r+1}; h / a1 / x may be NULL (not stored:
- *   eval forwards).  Weights w1 / w2 are the forward copies of aw_res_pack_weights, biases f32.  With drop_p > 0
+ *   Stored: dgelu_h[r] = GELU'(h_r), a1[r] = a1_r, dgelu_x[r] = GELU'(x_{r+1}) (r < R-1), a[r] = a_{r+1} (GELU' of
+ *   the f32 values, rounded to bf16: the backward's multipliers, in place of the unfused path's saved h_r / x_{r+1});
+ *   dgelu_h / a1 / dgelu_x may be NULL (not stored: eval forwards).  Weights w1 / w2 are the forward copies of aw_res_pack_weights, biases f32.  With drop_p > 0
  *   and drop_masks != NULL the launch also writes the keep bits of every block there (aw_res_dropout_masks_bytes;
  *   the masks aw_res_dropout_masks makes), for the backward.
  * Backward, per block r = R-1 .. 0, from gx = dL/dx_R (bf16) and gxo = gx * mask_{R-1} (bf16), with
  * convT(W, v)[t] = sum_j W_j^T v[t - j + 1] (taps = 3) or W^T v[t]:
  *   gh_r = convT(W2_r, go_r) * GELU'(h_r),  gx_r = gx_{r+1} + convT(W1_r, gh_r) * GELU'(x_r),
  *   gxo_out[r] = gx_r * mask_{r-1} (r > 0: block r-1's conv2 operand) or gx_0 (r = 0); gh[r] = gh_r.
- *   w1t / w2t are the backward copies of aw_res_pack_weights; h / x are the forward's saved tensors with x[0] = x_0
- *   and x[r] = the forward's x[r-1]; drop_masks (drop_p > 0) = what the forward wrote.
+ *   w1t / w2t are the backward copies of aw_res_pack_weights; dgelu_h[r] = the forward's dgelu_h[r], dgelu_x[r] =
+ *   the forward's dgelu_x[r-1] (r >= 1; dgelu_x[0] unused), x0 = x_0 (block 0's GELU'(x_0) is evaluated here, the
+ *   erf form of aw_gemm's bf16 epilogues); drop_masks (drop_p > 0) = what the forward wrote.
  * All activations are [N][H] bf16 with row stride H, 16-B aligned; N * H * 2 < 2^31; 1 <= R <= AW_RES_CHAIN_MAX;
  * taps = 3 needs seg = 16 and N % 16 == 0.  drop_seed / seed_ptr select the masks (forward); store_policy AW_STORE_WT
  * (sc1) or AW_STORE_NT for every global store. */
@@ -158,9 +160,9 @@ typedef struct {
   const void* w2[AW_RES_CHAIN_MAX];
   const float* b1[AW_RES_CHAIN_MAX];
   const float* b2[AW_RES_CHAIN_MAX];
-  void* h[AW_RES_CHAIN_MAX];
+  void* dgelu_h[AW_RES_CHAIN_MAX];
   void* a1[AW_RES_CHAIN_MAX];
-  void* x[AW_RES_CHAIN_MAX];
+  void* dgelu_x[AW_RES_CHAIN_MAX];
   void* a[AW_RES_CHAIN_MAX];
   float drop_p;
   uint64_t drop_seed[AW_RES_CHAIN_MAX];
@@ -174,10 +176,11 @@ typedef struct {
   int taps, seg;
   const void* gx;
   const void* gxo;
+  const void* x0;
   const void* w1t[AW_RES_CHAIN_MAX];
   const void* w2t[AW_RES_CHAIN_MAX];
-  const void* h[AW_RES_CHAIN_MAX];
-  const void* x[AW_RES_CHAIN_MAX];
+  const void* dgelu_h[AW_RES_CHAIN_MAX];
+  const void* dgelu_x[AW_RES_CHAIN_MAX];
   void* gh[AW_RES_CHAIN_MAX];
   void* gxo_out[AW_RES_CHAIN_MAX];
   float drop_p;

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-6 pair-chain check on one GPU box: the chain tests, the chain probes (product library and the variants), and a
+# Chain check on one GPU box: the chain tests, the chain probes (product library and the variants), and a
 # same-box A/B of the VQ-VAE step against ./ab_base.  Stops at the first GPU fault / timeout (rc not in {0, 1}).
 set -o pipefail
 export TMPDIR=/tmp

@@ -76,7 +76,7 @@ class ResChainFwdArgs(ctypes.Structure):
     """aw_res_chain_fwd_args (include/arcweld_amd.h)."""
     _fields_ = [("N", c_i64), ("H", c_int), ("R", c_int), ("taps", c_int), ("seg", c_int), ("a0", c_p), ("x0", c_p),
                 ("w1", c_p * _E), ("w2", c_p * _E), ("b1", c_p * _E), ("b2", c_p * _E),
-                ("h", c_p * _E), ("a1", c_p * _E), ("x", c_p * _E), ("a", c_p * _E),
+                ("dgelu_h", c_p * _E), ("a1", c_p * _E), ("dgelu_x", c_p * _E), ("a", c_p * _E),
                 ("drop_p", c_f), ("drop_seed", ctypes.c_uint64 * _E), ("seed_ptr", c_p), ("store_policy", c_int),
                 ("drop_masks", c_p)]
 
@@ -84,7 +84,7 @@ class ResChainFwdArgs(ctypes.Structure):
 class ResChainBwdArgs(ctypes.Structure):
     """aw_res_chain_bwd_args (include/arcweld_amd.h)."""
     _fields_ = [("N", c_i64), ("H", c_int), ("R", c_int), ("taps", c_int), ("seg", c_int), ("gx", c_p), ("gxo", c_p),
-                ("w1t", c_p * _E), ("w2t", c_p * _E), ("h", c_p * _E), ("x", c_p * _E),
+                ("x0", c_p), ("w1t", c_p * _E), ("w2t", c_p * _E), ("dgelu_h", c_p * _E), ("dgelu_x", c_p * _E),
                 ("gh", c_p * _E), ("gxo_out", c_p * _E),
                 ("drop_p", c_f), ("store_policy", c_int), ("drop_masks", c_p)]
 

@@ -312,7 +312,10 @@ def fused_step(m, batch, scale, slot, mid_hook=None, groups=1):
     sequences (accumulate_grad_batches, train_transformer_mtasks.py:32): each micro-batch's loss is its own mean
     over its own valid tokens (one cross-entropy reduction per group), so the summed gradient is Lightning's sum of
     the G micro-batch gradients; the returned loss is the mean of the G losses.  Every row draws its own dropout
-    mask from the one counter range of this forward."""
+    mask from the one counter range of this forward.  RNG stream: the G eager micro-steps draw G seeds (one
+    _next_seed() each), the grouped step one, so with dropout > 0 an eager and a graphed run of the same seed draw
+    different (equally distributed, independent per row) masks; runs are reproducible within either path, and the
+    eager-vs-grouped equivalence tests run at dropout 0 (tests/test_training_regime.py)."""
     x, cond, y = batch
     generate = m.task == "generate"
     dev = x.device

@@ -301,24 +301,25 @@ def _chain_flops(R, N, H, taps, seg):
     return 4.0 * R * N * H * H * (3 - 2.0 / seg)
 
 
-def res_chain_fwd(a0, x0, w1, w2, b1, b2, h, a1, x, a, drop=(0.0, None), seed_ptr=None, masks=None, taps=1, seg=16,
+def res_chain_fwd(a0, x0, w1, w2, b1, b2, dh, a1, dx, a, drop=(0.0, None), seed_ptr=None, masks=None, taps=1, seg=16,
                   stream=None):
     """One aw_res_chain_fwd launch over the R = len(w1) ResBlocks (see include/arcweld_amd.h).
 
-    a0 / x0: (N, H) bf16; w1 / w2: R packed weight copies (res_pack_weights); b1 / b2: R f32 biases; h / a1 / x / a: R
-    output tensors each (h, a1, x entries may be None: not stored; x[R-1] is never stored); drop = (p, R seeds); masks:
-    None or a res_dropout_masks_empty(N, R) buffer the launch fills with the keep bits (for res_chain_bwd)."""
+    a0 / x0: (N, H) bf16; w1 / w2: R packed weight copies (res_pack_weights); b1 / b2: R f32 biases; dh / a1 / dx / a:
+    R output tensors each -- dh[r] = GELU'(h_r), a1[r], dx[r] = GELU'(x_{r+1}) (the backward's multipliers), a[r]
+    (dh, a1, dx entries may be None: not stored; dx[R-1] is never stored); drop = (p, R seeds); masks: None or a
+    res_dropout_masks_empty(N, R) buffer the launch fills with the keep bits (for res_chain_bwd)."""
     N, H = a0.shape
     R = len(w1)
-    if not (1 <= R <= RES_CHAIN_MAX) or not all(len(v) == R for v in (w2, b1, b2, h, a1, x, a)):
+    if not (1 <= R <= RES_CHAIN_MAX) or not all(len(v) == R for v in (w2, b1, b2, dh, a1, dx, a)):
         raise nat.NativeError("res_chain_fwd: need R (1..16) entries in every per-block list")
-    _chk_rows([a0, x0] + list(h) + list(a1) + list(x) + list(a), N, H, "res_chain_fwd")
+    _chk_rows([a0, x0] + list(dh) + list(a1) + list(dx) + list(a), N, H, "res_chain_fwd")
     g = nat.ResChainFwdArgs()
     g.N, g.H, g.R, g.taps, g.seg = N, H, R, int(taps), int(seg)
     g.a0, g.x0 = ptr(a0), ptr(x0)
     for r in range(R):
         g.w1[r], g.w2[r], g.b1[r], g.b2[r] = ptr(w1[r]), ptr(w2[r]), ptr(b1[r]), ptr(b2[r])
-        g.h[r], g.a1[r], g.x[r], g.a[r] = ptr(h[r]), ptr(a1[r]), ptr(x[r]), ptr(a[r])
+        g.dgelu_h[r], g.a1[r], g.dgelu_x[r], g.a[r] = ptr(dh[r]), ptr(a1[r]), ptr(dx[r]), ptr(a[r])
         g.drop_seed[r] = int(drop[1][r]) & 0xFFFFFFFFFFFFFFFF if drop[0] > 0 else 0
     g.drop_p = float(drop[0])
     g.seed_ptr = ptr(seed_ptr)
@@ -326,31 +327,34 @@ def res_chain_fwd(a0, x0, w1, w2, b1, b2, h, a1, x, a, drop=(0.0, None), seed_pt
     g.drop_masks = ptr(masks)
     _maybe_timed(stream, "gemm_bf16", _chain_flops(R, N, H, taps, seg),
                  lambda sp: call("aw_res_chain_fwd", ctypes.byref(g), sp), f"res_chain_fwd_kernel<{int(taps)}>",
-                 _nbytes([a0, x0, masks] + list(w1) + list(w2) + list(b1) + list(b2) + list(h) + list(a1) +
-                         list(x)[:-1] + list(a)))
+                 _nbytes([a0, x0, masks] + list(w1) + list(w2) + list(b1) + list(b2) + list(dh) + list(a1) +
+                         list(dx)[:-1] + list(a)))
 
 
-def res_chain_bwd(gx, gxo, w1t, w2t, h, x, gh, gxo_out, drop_p=0.0, masks=None, taps=1, seg=16, stream=None):
-    """One aw_res_chain_bwd launch (see include/arcweld_amd.h): w1t / w2t are the packed backward copies, h / x
-    the forward's saved pre-activations and residual streams (x[0] = x_0), gh / gxo_out the R outputs each; masks
-    (drop_p > 0, R > 1): the keep bits res_chain_fwd wrote (or res_dropout_masks made)."""
+def res_chain_bwd(gx, gxo, w1t, w2t, dh, x0, dx, gh, gxo_out, drop_p=0.0, masks=None, taps=1, seg=16, stream=None):
+    """One aw_res_chain_bwd launch (see include/arcweld_amd.h): w1t / w2t are the packed backward copies, dh the
+    forward's saved GELU'(h_r), x0 the stack input x_0 and dx[r] (r >= 1) the forward's GELU'(x_r) (dx[0] is not read:
+    GELU'(x_0) is evaluated in the launch), gh / gxo_out the R outputs each; masks (drop_p > 0, R > 1): the keep bits
+    res_chain_fwd wrote (or res_dropout_masks made)."""
     N, H = gx.shape
     R = len(w1t)
-    if not (1 <= R <= RES_CHAIN_MAX) or not all(len(v) == R for v in (w2t, h, x, gh, gxo_out)):
+    if not (1 <= R <= RES_CHAIN_MAX) or not all(len(v) == R for v in (w2t, dh, dx, gh, gxo_out)):
         raise nat.NativeError("res_chain_bwd: need R (1..16) entries in every per-block list")
-    _chk_rows([gx, gxo] + list(h) + list(x) + list(gh) + list(gxo_out), N, H, "res_chain_bwd")
+    _chk_rows([gx, gxo, x0] + list(dh) + list(dx[1:]) + list(gh) + list(gxo_out), N, H, "res_chain_bwd")
     g = nat.ResChainBwdArgs()
     g.N, g.H, g.R, g.taps, g.seg = N, H, R, int(taps), int(seg)
-    g.gx, g.gxo = ptr(gx), ptr(gxo)
+    g.gx, g.gxo, g.x0 = ptr(gx), ptr(gxo), ptr(x0)
     for r in range(R):
-        g.w1t[r], g.w2t[r], g.h[r], g.x[r] = ptr(w1t[r]), ptr(w2t[r]), ptr(h[r]), ptr(x[r])
+        g.w1t[r], g.w2t[r], g.dgelu_h[r] = ptr(w1t[r]), ptr(w2t[r]), ptr(dh[r])
+        g.dgelu_x[r] = ptr(dx[r]) if r > 0 else None
         g.gh[r], g.gxo_out[r] = ptr(gh[r]), ptr(gxo_out[r])
     g.drop_p = float(drop_p)
     g.store_policy = _chain_store_policy()
     g.drop_masks = ptr(masks)
     _maybe_timed(stream, "gemm_bf16", _chain_flops(R, N, H, taps, seg),
                  lambda sp: call("aw_res_chain_bwd", ctypes.byref(g), sp), f"res_chain_bwd_kernel<{int(taps)}>",
-                 _nbytes([gx, gxo, masks] + list(w1t) + list(w2t) + list(h) + list(x) + list(gh) + list(gxo_out)))
+                 _nbytes([gx, gxo, x0, masks] + list(w1t) + list(w2t) + list(dh) + list(dx[1:]) + list(gh) +
+                         list(gxo_out)))
 
 
 def res_pack_weights(src, fwd=None, bwd=None, taps=1, stream=None):

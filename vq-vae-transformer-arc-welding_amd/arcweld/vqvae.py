@@ -265,9 +265,10 @@ def _bn_block_bwd(gy, x, a0, bs, w1d, w2d, Kd, dgemm_kw, wg, c1, c2, bns, G, tra
 
 def _chain_fwd(ws, convs, a0, x0, N, H, T, RT, p_drop, seeds, ctr, need_backward, taps, seg):
     """Forward of a ResBlock stack through aw_res_chain_fwd (encoder: taps 1, decoder: taps 3).  ws: the R pairs of
-    optimizer-maintained operand copies ([O][I] or [O][3I]); convs: the R (conv1, conv2) modules.  Returns (h, a1, x,
-    a lists as the per-conv loop makes them -- h / a1 / x None without a backward --, the packed backward weight
-    copies or None, the dropout keep bits for the backward or None)."""
+    optimizer-maintained operand copies ([O][I] or [O][3I]); convs: the R (conv1, conv2) modules.  Returns (GELU'(h),
+    a1, GELU'(x), a lists -- a1 and a as the per-conv loop makes them, the saved derivatives in place of its h and x
+    (the chain's backward multiplies by them), None without a backward --, the packed backward weight copies or None,
+    the dropout keep bits for the backward or None)."""
     R = len(ws)
     dev = a0.device
     e = lambda dt: torch.empty(N, H, device=dev, dtype=dt)  # noqa: E731
@@ -297,8 +298,9 @@ def _chain_bwd(sv, convs, gx, gxo, hs, xs, a0s, a1s, pk_bwd, masks, wgrad_target
     T = gxo.dtype
     gh = [torch.empty(N, H, device=dev, dtype=T) for _ in range(R)]
     go = [torch.empty(N, H, device=dev, dtype=T) for _ in range(R)]
-    K.res_chain_bwd(gx, gxo, pk_bwd[0::2], pk_bwd[1::2], hs, xs[:R], gh, go, drop_p=sv.p_drop, masks=masks, taps=taps,
-                    seg=seg)
+    # hs / xs[1:]: the forward chain's saved GELU'(h_r) / GELU'(x_r); xs[0] = x_0, the stack input
+    K.res_chain_bwd(gx, gxo, pk_bwd[0::2], pk_bwd[1::2], hs, xs[0], [None] + list(xs[1:R]), gh, go, drop_p=sv.p_drop,
+                    masks=masks, taps=taps, seg=seg)
     extra = dict(conv=(H, seg, 1, 1)) if taps == 3 else {}
     wgrads = []
     for r in reversed(range(R)):

@@ -2,6 +2,9 @@
 // (model/vq_vae_patch_embedd.py:60-74 ResBlock inside CNNBlock :103-110), each as ONE persistent launch per direction.
 //   forward   h = conv1(a) + b1,  a1 = GELU(h),  x' = x + Dropout(conv2(a1) + b2),  a' = GELU(x')      (a = GELU(x))
 //   backward  gh = conv2^T(go) * GELU'(h),  gx = gx' + conv1^T(gh) * GELU'(x),  go = gx * mask(block r-1)
+// The forward saves GELU'(h) and GELU'(x') (bf16) for the backward, evaluated from the same Phi / exp as the GELU it
+// computes anyway (two VALU operations more per element); the backward multiplies by them and evaluates no
+// transcendental (only GELU'(x_0) of the stack input, for block 0's conv1, is its own).  Same-bytes as saving h and x'.
 // Encoder (CNNBlock(seperate=True)): each conv sees a length-1 token slice, so it is its centre tap, a [H][H]
 // contraction per token (TAPS = 1).  Decoder (seperate=False): k = 3, padding-1 convs along each 16-token window
 // (TAPS = 3, K = 3H: tap j reads token t + j - 1 forward, t - j + 1 backward, zero outside the window).  Either way a
@@ -36,13 +39,17 @@
 //    the output that is also the next operand from the wave's own slice of the next image, the other one through a
 //    2 KB per-wave scratch.  Stored straight from the accumulator layout (32-B pieces per token) they cost 20 k
 //    cycles per epilogue (probe stamps);
-//  * the residual stream (x forward, gx backward) stays in registers as bf16 (the bf16 mode's resid dtype), and
-//    the saved tensors of the unfused path are still written (h, a1, x, a for the weight gradients and GELU';
-//    gh and the masked gx for the weight gradients), so the rest of the step is unchanged.
+//  * the residual stream (x forward, gx backward) stays in registers as bf16 (the bf16 mode's resid dtype); the
+//    weight gradients' operands are written as the unfused path writes them (a1, a forward; gh and the masked gx
+//    backward), and in place of the unfused path's h and x the forward saves GELU'(h), GELU'(x') for the backward.
 // Per element the epilogues run the unfused GEMM epilogue's operations in its order (gemm_core.h), and each
 // accumulator sees the same MFMA sequence (K ascending in 32-deep steps, tap-major as the implicit conv GEMM), so
-// the outputs are the unfused path's bit for bit (tests/test_res_chain.py).
+// the forward's outputs a1 / a / keep bits are the unfused path's bit for bit; the saved derivatives are GELU' of the
+// f32 pre-activation (the unfused backward: of its bf16 copy) rounded to bf16, so the backward tracks the unfused one
+// to bf16 rounding (tests/test_res_chain.py).
 #include "common.h"
+
+#include <type_traits>
 
 #pragma clang diagnostic ignored "-Winline-asm"
 
@@ -91,18 +98,26 @@ __device__ __forceinline__ rsrc_t ec_rsrc(const void* p, uint32_t nbytes) {
 __device__ __forceinline__ u32x2 ec_load8(rsrc_t r, uint32_t voff, int soff) {
   return __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0);
 }
-// the data registers stay untouched for a few cycles after a store issues: reused at once (the next LDS address
-// computed into them), the stored data's first dword intermittently came out as that address
+// Store-data hazard: a VMEM store of more than 64 bits of data reads its data VGPRs after issue, so a VALU write of
+// those VGPRs needs 2 wait states behind it on gfx94x / gfx950 (LLVM GCNHazardRecognizer: VALUWaitStates = 2;
+// cdna_hip_programming.md 5.7 item 1).  ROCm 7.2's hazard recognizer pads it for every form EXCEPT a MUBUF / MTBUF
+// store whose soffset is a register (createsVALUHazard skips those, the SI-era premise that the hazard needs an
+// immediate soffset), and these stores pass the tile offset in an SGPR soffset.  Without a pad the compiler emitted
+//   buffer_store_dwordx4 v[34:37], v217, s[24:27], s65 offen sc1
+//   v_add_u32_e32 v34, 0xc008, v222          ; the next LDS address, 0 wait states later
+// and on the GPU the stored line's first dword intermittently came out as that address (round 5).  The pad: one
+// s_nop 1 (2 wait states) that names the data registers, so none of them is reused before it.  Audited over the
+// whole library's ISA by tests/test_isa_hazards.py.
 template <bool WT> __device__ __forceinline__ void ec_store16(rsrc_t r, uint32_t voff, int soff, uint4 v) {
   aw_v4i32 u;
   memcpy(&u, &v, 16);
   // sc1 (write-through) or nt: the lines must not stay in the XCD's L2, which holds the weight stream
   __builtin_amdgcn_raw_buffer_store_b128(u, r, voff, soff, WT ? 16 : 2);
-  asm volatile("s_nop 4" ::"v"(u));
+  asm volatile("s_nop 1" ::"v"(u));
 }
+// 64-bit data: outside the hazard (and soffset 0, which the compiler pads anyway)
 __device__ __forceinline__ void ec_store8(rsrc_t r, uint32_t voff, u32x2 v) {
   __builtin_amdgcn_raw_buffer_store_b64(v, r, voff, 0, 2);
-  asm volatile("s_nop 4" ::"v"(v));
 }
 typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
 // 4 floats -> 4 bf16 (round to nearest even, as the unfused epilogue's (bf16) casts): two v_cvt_pk_bf16_f32 (the
@@ -183,13 +198,19 @@ __device__ __forceinline__ void ec_frag_fence(int) { __builtin_amdgcn_sched_barr
 // GELU / GELU' of a fragment's 4 values, element by element (the same operations as aw_gelu4 / aw_gelu_grad4, so
 // the same bits as the unfused GEMM epilogues): written per element, the compiler packs only where it pays (the
 // fully packed pair form measured 3 % slower here, MI355X_MICROARCH.md: packed f32 VALU beside MFMAs)
-__device__ __forceinline__ void ec_gelu4(const float (&v)[4], float (&y)[4]) {
-#pragma unroll
-  for (int e = 0; e < 4; ++e) y[e] = gelu_erf_fast(v[e]);
-}
 __device__ __forceinline__ void ec_gelu_grad4(const float (&v)[4], float (&y)[4]) {
 #pragma unroll
   for (int e = 0; e < 4; ++e) y[e] = gelu_erf_grad_fast(v[e]);
+}
+// both from one Phi / exp evaluation: y = GELU(v) with ec_gelu4's bits, d = GELU'(v) with ec_gelu_grad4's
+__device__ __forceinline__ void ec_gelu_and_grad4(const float (&v)[4], float (&y)[4], float (&d)[4]) {
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    float ex;
+    const float phi = aw_phi_e(v[e], ex);
+    y[e] = v[e] * phi;
+    d[e] = fmaf(v[e] * AW_INV_SQRT2PI, ex, phi);
+  }
 }
 
 // Weight fragment (i, s) of wave w (rows 64w + 16i .. +15, k 32s .. 32s + 31) in the fragment-packed layout: block
@@ -411,39 +432,31 @@ __global__ __launch_bounds__(EC_NTH) void res_chain_fwd_kernel(aw_res_chain_fwd_
     // The slice is published as soon as the next operand image holds it (the other waves' next K loops wait for
     // it); the saved tensor that goes through the scratch (h, x') follows the publish.
     if (!second) {
-      // a1 = GELU(h), h = conv1 + b1: a1 into the next operand image (stored from there once published), then h
-      // (the saved pre-activation) recomputed from the accumulators through the scratch
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          float v[4], y[4], bv[4];
-          bias(i, bv);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = acc[i][j][e] + bv[e];
-          ec_gelu4(v, y);
-          ec_lds_w8(smem, nwb[i] + G::JS * j, ec_pack(y));
-          ec_frag_fence(4 * j + i);
-        }
-      ec_publish<G>(smem, L.w, L.lane, c + 1);
-      const rsrc_t rh = ec_rsrc(P.h[r], nbytes);
+      // a1 = GELU(h), h = conv1 + b1: a1 into the next operand image (stored from there once published); GELU'(h)
+      // from the same Phi into the scratch, saved 16 tokens at a time (held in registers until after the publish, the
+      // 32 VGPRs made the kernel spill 145-175)
+      const rsrc_t rh = ec_rsrc(P.dgelu_h[r], nbytes);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          float v[4], bv[4];
+          float v[4], y[4], d[4], bv[4];
           bias(i, bv);
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[e] = acc[i][j][e] + bv[e];
-          ec_lds_w8(smem, S.sw[i], ec_pack(v));
+          ec_gelu_and_grad4(v, y, d);
+          ec_lds_w8(smem, nwb[i] + G::JS * j, ec_pack(y));
+          ec_lds_w8(smem, S.sw[i], ec_pack(d));
+          ec_frag_fence(4 * j + i);
         }
         ec_store_scratch<G, WT>(smem, j, S, rh);
         __builtin_amdgcn_sched_barrier(0);
       }
+      ec_publish<G>(smem, L.w, L.lane, c + 1);
       ec_store_slice<G, WT>(smem, no, S, ec_rsrc(P.a1[r], nbytes));
     } else {
-      // x' = x + Dropout(conv2 + b2): x' (saved for GELU', via the scratch) and a' = GELU(x') (the next operand
-      // image); the last block stores x_R itself (the next stage's operand), staged in the image
+      // x' = x + Dropout(conv2 + b2) (kept in registers) and a' = GELU(x') (the next operand image), GELU'(x') saved
+      // through the scratch; the last block stores x_R itself (the next stage's operand), staged in the image
       const bool last = r == R - 1;
       const float dk = DROP ? 1.f / (1.f - P.drop_p) : 1.f;
       auto resid = [&](int i, int j, float (&v)[4]) {
@@ -456,25 +469,22 @@ __global__ __launch_bounds__(EC_NTH) void res_chain_fwd_kernel(aw_res_chain_fwd_
         xr[i][j] = ec_pack(v);
       };
       if (!last) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            float v[4], y[4];
-            resid(i, j, v);
-            ec_gelu4(v, y);
-            ec_lds_w8(smem, nwb[i] + G::JS * j, ec_pack(y));
-            ec_frag_fence(4 * j + i);
-          }
-        ec_publish<G>(smem, L.w, L.lane, c + 1);
-        const rsrc_t rx = ec_rsrc(P.x[r], nbytes);
+        const rsrc_t rx = ec_rsrc(P.dgelu_x[r], nbytes);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
 #pragma unroll
-          for (int i = 0; i < 4; ++i) ec_lds_w8(smem, S.sw[i], xr[i][j]);
+          for (int i = 0; i < 4; ++i) {
+            float v[4], y[4], d[4];
+            resid(i, j, v);
+            ec_gelu_and_grad4(v, y, d);
+            ec_lds_w8(smem, nwb[i] + G::JS * j, ec_pack(y));
+            ec_lds_w8(smem, S.sw[i], ec_pack(d));
+            ec_frag_fence(4 * j + i);
+          }
           ec_store_scratch<G, WT>(smem, j, S, rx);
           __builtin_amdgcn_sched_barrier(0);
         }
+        ec_publish<G>(smem, L.w, L.lane, c + 1);
       } else {
 #pragma unroll
         for (int i = 0; i < 4; ++i)
@@ -526,16 +536,17 @@ __global__ __launch_bounds__(EC_NTH) void res_chain_bwd_kernel(aw_res_chain_bwd_
     const rsrc_t rn = ec_rsrc(has_next ? (second ? P.w2t[r - 1] : P.w1t[r]) : nullptr, G::WBYTES);
     const int io = (c & 1) * G::IMG, no = ((c + 1) & 1) * G::IMG;
     f32x4 acc[4][4];
-    // the epilogue's pre-activation (h_r for conv2's gradient, x_r for conv1's) as whole 128-B lines (the wave's
-    // 64-channel slice of 8 tokens per load, as the stores), turned into fragments through the wave's scratch in
-    // the epilogue; and, for conv1's, block r - 1's dropout keep bits.  Loaded behind the last K step's weight loads:
+    // the epilogue's GELU' (the forward's GELU'(h_r) for conv2's gradient, GELU'(x_r) for conv1's; for block 0's
+    // conv1 the stack input x_0 itself, whose GELU' is evaluated here) as whole 128-B lines (the wave's 64-channel
+    // slice of 8 tokens per load, as the stores), turned into fragments through the wave's scratch in the epilogue;
+    // and, for conv1's, block r - 1's dropout keep bits.  Loaded behind the last K step's weight loads:
     // issued earlier, a load would hold up (in vmcnt order) the weight loads issued after it.  Loaded in the
     // fragment layout (16 rows x 32 B per instruction, every line touched by four instructions) the backward ran
     // 40 % slower than with the pre-activations left out (probe), against 7 % for the forward's GELU alone.
     uint4 pl[8];
     u32x2 keep = {0u, 0u};
     auto load_pre = [&] {
-      const rsrc_t rp = ec_rsrc(second ? P.x[r] : P.h[r], nbytes);
+      const rsrc_t rp = ec_rsrc(second ? (r > 0 ? P.dgelu_x[r] : P.x0) : P.dgelu_h[r], nbytes);
       const uint32_t gs = (uint32_t)(((row0 + (L.lane >> 3)) * EC_H + 64 * L.w + 8 * (L.lane & 7)) * 2);
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
@@ -563,9 +574,8 @@ __global__ __launch_bounds__(EC_NTH) void res_chain_bwd_kernel(aw_res_chain_bwd_
         stage_pre(j);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          float pv[4], v[4], ag[4];
-          pre_frag(i, pv);
-          ec_gelu_grad4(pv, ag);
+          float ag[4], v[4];
+          pre_frag(i, ag);
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[e] = aw_epi_mad(acc[i][j][e], ag[e], true, 0.f, false);
           ec_lds_w8(smem, nwb[i] + G::JS * j, ec_pack(v));
@@ -577,11 +587,17 @@ __global__ __launch_bounds__(EC_NTH) void res_chain_bwd_kernel(aw_res_chain_bwd_
     } else {
       // gx = gx' + (W1^T gh) * GELU'(x); go = gx * mask(block r - 1) (block r - 1's conv2 operand: the next operand
       // image) or, for r = 0, gx itself (the previous stage's weight-gradient operand, staged in the image)
-      auto grad = [&](int i, int j, float (&v)[4]) {
+      // raw (block 0): the scratch holds x_0, whose GELU' is evaluated here; otherwise the saved GELU'(x_r)
+      auto grad = [&](int i, int j, float (&v)[4], auto raw) {
         float pv[4], gv[4], ag[4];
         pre_frag(i, pv);
         ec_unpack(gr[i][j], gv);
-        ec_gelu_grad4(pv, ag);
+        if constexpr (decltype(raw)::value) {
+          ec_gelu_grad4(pv, ag);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) ag[e] = pv[e];
+        }
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] = aw_epi_mad(acc[i][j][e], ag[e], true, gv[e], true);
         gr[i][j] = ec_pack(v);
@@ -594,7 +610,7 @@ __global__ __launch_bounds__(EC_NTH) void res_chain_bwd_kernel(aw_res_chain_bwd_
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             float v[4], ds[4] = {1.f, 1.f, 1.f, 1.f}, o[4];
-            grad(i, j, v);
+            grad(i, j, v, std::false_type{});
             if constexpr (DROP) ec_scales(keep, i, j, dk, ds);
 #pragma unroll
             for (int e = 0; e < 4; ++e) o[e] = v[e] * ds[e];
@@ -610,7 +626,7 @@ __global__ __launch_bounds__(EC_NTH) void res_chain_bwd_kernel(aw_res_chain_bwd_
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             float v[4];
-            grad(i, j, v);
+            grad(i, j, v, std::true_type{});
             ec_lds_w8(smem, nwb[i] + G::JS * j, gr[i][j]);
             ec_frag_fence(4 * j + i);
           }
@@ -743,7 +759,7 @@ extern "C" int aw_res_chain_fwd(const aw_res_chain_fwd_args* a, void* stream) {
     AW_REQUIRE(a->w1[r] && a->w2[r] && a->b1[r] && a->b2[r] && aligned16(a->w1[r]) && aligned16(a->w2[r]) &&
                aligned16(a->b1[r]) && aligned16(a->b2[r]), "aw_res_chain_fwd: block %d weights missing or unaligned", r);
     AW_REQUIRE(a->a[r] && aligned16(a->a[r]), "aw_res_chain_fwd: block %d output a missing or unaligned", r);
-    AW_REQUIRE(aligned16(a->h[r]) && aligned16(a->a1[r]) && aligned16(a->x[r]),
+    AW_REQUIRE(aligned16(a->dgelu_h[r]) && aligned16(a->a1[r]) && aligned16(a->dgelu_x[r]),
                "aw_res_chain_fwd: block %d saved outputs unaligned", r);
   }
   AW_REQUIRE(aligned16(a->drop_masks), "aw_res_chain_fwd: drop_masks unaligned");
@@ -757,12 +773,13 @@ extern "C" int aw_res_chain_fwd(const aw_res_chain_fwd_args* a, void* stream) {
 
 extern "C" int aw_res_chain_bwd(const aw_res_chain_bwd_args* a, void* stream) {
   CHAIN_SHAPE_CHECKS("aw_res_chain_bwd");
-  AW_REQUIRE(a->gx && a->gxo && aligned16(a->gx) && aligned16(a->gxo), "aw_res_chain_bwd: gx / gxo missing or unaligned");
+  AW_REQUIRE(a->gx && a->gxo && a->x0 && aligned16(a->gx) && aligned16(a->gxo) && aligned16(a->x0),
+             "aw_res_chain_bwd: gx / gxo / x0 missing or unaligned");
   for (int r = 0; r < a->R; ++r) {
     AW_REQUIRE(a->w1t[r] && a->w2t[r] && aligned16(a->w1t[r]) && aligned16(a->w2t[r]),
                "aw_res_chain_bwd: block %d weights missing or unaligned", r);
-    AW_REQUIRE(a->h[r] && a->x[r] && aligned16(a->h[r]) && aligned16(a->x[r]),
-               "aw_res_chain_bwd: block %d saved h / x missing or unaligned", r);
+    AW_REQUIRE(a->dgelu_h[r] && aligned16(a->dgelu_h[r]) && (r == 0 || (a->dgelu_x[r] && aligned16(a->dgelu_x[r]))),
+               "aw_res_chain_bwd: block %d saved GELU' missing or unaligned", r);
     AW_REQUIRE(a->gh[r] && a->gxo_out[r] && aligned16(a->gh[r]) && aligned16(a->gxo_out[r]),
                "aw_res_chain_bwd: block %d outputs missing or unaligned", r);
   }
