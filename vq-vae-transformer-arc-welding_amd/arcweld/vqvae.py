@@ -267,8 +267,8 @@ def _chain_fwd(ws, convs, a0, x0, N, H, T, RT, p_drop, seeds, ctr, need_backward
     """Forward of a ResBlock stack through aw_res_chain_fwd (encoder: taps 1, decoder: taps 3).  ws: the R pairs of
     optimizer-maintained operand copies ([O][I] or [O][3I]); convs: the R (conv1, conv2) modules.  Returns (GELU'(h),
     a1, GELU'(x), a lists -- a1 and a as the per-conv loop makes them, the saved derivatives in place of its h and x
-    (the chain's backward multiplies by them), None without a backward --, the packed backward weight copies or None,
-    the dropout keep bits for the backward or None)."""
+    (the chain's backward multiplies by them), None without a backward --, the operand copies the backward packs its
+    weights from or None, the dropout keep bits for the backward or None)."""
     R = len(ws)
     dev = a0.device
     e = lambda dt: torch.empty(N, H, device=dev, dtype=dt)  # noqa: E731
@@ -277,11 +277,13 @@ def _chain_fwd(ws, convs, a0, x0, N, H, T, RT, p_drop, seeds, ctr, need_backward
     a1s = [e(T) if sb else None for _ in range(R)]
     xo = [e(RT) if sb and r < R - 1 else None for r in range(R)]
     ao = [e(T) for _ in range(R)]
-    # fragment-packed weight copies, from the operand copies (one launch; the backward's come out of the same launch)
+    # fragment-packed weight copies, from the operand copies, packed right before the chain that streams them (the
+    # backward's by _chain_bwd, right before the backward chain): the pack's writes are still in the caches when the
+    # chain starts reading
     wsrc = [w for pair in ws for w in pair]
     pk = [torch.empty(H, taps * H, device=dev, dtype=T) for _ in wsrc]
-    pk_bwd = [torch.empty(H, taps * H, device=dev, dtype=T) for _ in wsrc] if sb else None
-    K.res_pack_weights(wsrc, pk, pk_bwd, taps=taps)
+    K.res_pack_weights(wsrc, pk, None, taps=taps)
+    pk_bwd = wsrc if sb else None      # the sources of the backward's packed copies
     masks = K.res_dropout_masks_empty(N, R, dev) if sb and p_drop > 0 and R > 1 else None
     K.res_chain_fwd(a0, x0, pk[0::2], pk[1::2], [c1.bias for c1, _ in convs], [c2.bias for _, c2 in convs], hs, a1s,
                     xo, ao, drop=(p_drop, seeds), seed_ptr=ctr, masks=masks, taps=taps, seg=seg)
@@ -298,6 +300,8 @@ def _chain_bwd(sv, convs, gx, gxo, hs, xs, a0s, a1s, pk_bwd, masks, wgrad_target
     T = gxo.dtype
     gh = [torch.empty(N, H, device=dev, dtype=T) for _ in range(R)]
     go = [torch.empty(N, H, device=dev, dtype=T) for _ in range(R)]
+    wsrc, pk_bwd = pk_bwd, [torch.empty(H, taps * H, device=dev, dtype=T) for _ in pk_bwd]
+    K.res_pack_weights(wsrc, None, pk_bwd, taps=taps)
     # hs / xs[1:]: the forward chain's saved GELU'(h_r) / GELU'(x_r); xs[0] = x_0, the stack input
     K.res_chain_bwd(gx, gxo, pk_bwd[0::2], pk_bwd[1::2], hs, xs[0], [None] + list(xs[1:R]), gh, go, drop_p=sv.p_drop,
                     masks=masks, taps=taps, seg=seg)
