@@ -218,6 +218,17 @@ static bool is_ragged(const aw_gemm_args& a) {
 #define AW_SPLIT_MIN_KSTEPS 12
 #endif
 
+// fewest K steps of one split of a launch with at most 16 output tiles (the VQ-VAE's small weight gradients: M x N =
+// 512 x 25 / 64 x 512 / 512 x 64 over K = 16384 tokens): 6 (tools/probe/small_wgrad_probe.py, same box: 24.1 / 18.7 /
+// 19.7 us at 12, 24.2 / 17.0 / 17.8 at 6, 29.1 / 18.0 / 19.2 at 4); AW_SPLIT_MIN_KSTEPS_SMALL: tuning override
+static int min_ksteps_small() {
+  static const int v = [] {
+    const char* e = getenv("AW_SPLIT_MIN_KSTEPS_SMALL");
+    return e && atoi(e) > 0 ? atoi(e) : 6;
+  }();
+  return v;
+}
+
 static int g_tile_override = 0;   // aw_gemm_set_tile: 0 = automatic, 128 / 256 = force (tests, tuning)
 
 extern "C" int aw_gemm_set_tile(int bm) {
@@ -280,7 +291,7 @@ static void plan(const aw_gemm_args& a, int ngroups, bool grouped, GemmP& P) {
     if (plain && nb < 384 && a.K >= 24 * BK) {
       // two co-resident blocks per CU (256 CUs); keep >= 12 K-steps per split so the slab write + reduce is small
       splits = 512 / nb;
-      const int max_splits = a.K / (AW_SPLIT_MIN_KSTEPS * BK);
+      const int max_splits = a.K / ((nb <= 16 ? min_ksteps_small() : AW_SPLIT_MIN_KSTEPS) * BK);
       if (splits > max_splits) splits = max_splits;
       if (grouped && splits > AW_GROUPED_MAXSPLIT) splits = AW_GROUPED_MAXSPLIT;
       if (splits < 1) splits = 1;
