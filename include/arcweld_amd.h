@@ -21,7 +21,9 @@ extern "C" {
 
 enum { AW_OK = 0, AW_ERR_ARG = -1, AW_ERR_LAUNCH = -2 };
 enum { AW_F32 = 0, AW_BF16 = 1 };
-enum { AW_ACT_GELU_ERF = 0, AW_ACT_GELU_TANH = 1 };
+/* act: the activation of C2 modes 1 / 4 and of the epilogue's act'; AW_ACT_DERIV (with pre): pre already holds the
+ * activation's derivative (saved by a c2_mode 4 forward), the epilogue multiplies by it as it is */
+enum { AW_ACT_GELU_ERF = 0, AW_ACT_GELU_TANH = 1, AW_ACT_DERIV = 2 };
 
 const char* aw_last_error(void);
 int aw_version(void);
@@ -44,7 +46,9 @@ int aw_version(void);
  * Epilogue, per element (row r, col c), in this order:
  *   v = alpha*acc;  v += bias[c] (bias[c % bias_mod] if bias_mod > 0);  v *= act'(pre[r*ld_pre + c]) (pre f32/bf16);  v *= dropout(drop_seed, r*N+c, drop_p);
  *   v += resid[r*ld_resid + c] (resid f32/bf16);  v += beta * C_old (C must be f32 when beta != 0);  C[r*ldc + c] = v (c_dtype)
- *   C2 (c2_mode): 1 = act(v), 2 = v, 3 = v * dropout(drop2_seed, r*N+c, drop2_p); stored as c2_dtype
+ *   C2 (c2_mode): 1 = act(v), 2 = v, 3 = v * dropout(drop2_seed, r*N+c, drop2_p); stored as c2_dtype;
+ *   c2_mode 4: C = act(v) and C2 = act'(v) instead (from one exponential: the backward multiplies by the saved
+ *   derivative, act = AW_ACT_DERIV, rather than evaluating act' of a saved pre-activation)
  *   colstats (f64, 2*stats_mod): += v and v*v into slot (c % stats_mod)      (BatchNorm batch statistics)
  *   a_rowsum (f32, M): += sum_k A[m][k]                                      (bias gradients, fused)
  */
@@ -56,7 +60,7 @@ typedef struct {
   int conv_cin, conv_seg, conv_dir, conv_operand;
   float alpha, beta;
   const float* bias;
-  int act;                       /* AW_ACT_GELU_ERF or AW_ACT_GELU_TANH, for act' and C2 mode 1 */
+  int act;                       /* AW_ACT_GELU_ERF / _TANH (act' and C2 modes 1, 4) or AW_ACT_DERIV (pre = act') */
   const float* pre; int64_t ld_pre;
   const float* resid; int64_t ld_resid;
   float drop_p; uint64_t drop_seed;

@@ -17,7 +17,7 @@ LIB_PATH = os.environ.get("ARCWELD_LIB") or os.path.join(PKG_DIR, "lib", "libarc
 HEADER = os.path.join(os.path.dirname(PKG_DIR), "include", "arcweld_amd.h")
 
 AW_F32, AW_BF16 = 0, 1
-AW_ACT_GELU_ERF, AW_ACT_GELU_TANH = 0, 1
+AW_ACT_GELU_ERF, AW_ACT_GELU_TANH, AW_ACT_DERIV = 0, 1, 2
 AW_STORE_NT, AW_STORE_WT = 0, 1   # aw_gemm_args.store_policy
 
 c_i64 = ctypes.c_int64

@@ -8,7 +8,8 @@ Rows are the R = B*T tokens of a batch, row = b*T + t.  Per block:
   y   = causal attention(qkv)        aw_attn_fwd (flash-style, lse saved; the T x T matrix never exists)
   x1  = x + drop(y . Wo^T + bo)      aw_gemm (bias + dropout + residual fused)
   a2  = LN2(x1)
-  h   = a2 . Wfc^T + bfc             aw_gemm, C = h (f32, for GELU') and C2 = GELU_tanh(h) (operand dtype)
+  h   = a2 . Wfc^T + bfc             aw_gemm, C = h (f32, for GELU') and C2 = GELU_tanh(h) (f32 operands); bf16:
+                                     C = GELU_tanh(h) and C2 = GELU_tanh'(h) (c2_mode 4, the backward's multiplier)
   x2  = x1 + drop(g . Wp^T + bp)     aw_gemm
 
 Heads: lm_head (logits [R][V], ld padded to 8) + cross-entropy(ignore_index=-1), or the classification head
@@ -119,8 +120,14 @@ def forward(m, ids, generate: bool, training: bool, need_backward: bool, seed: i
                seed_ptr=sv.ctr)
         a2, mu2, rs2 = e(R, d, dt=T_), e(R), e(R)
         K.layernorm_fwd(x1, blk.ln_2.weight, blk.ln_2.bias, blk.ln_2.eps, a2, mu2, rs2)
-        h, g = e(R, 4 * d, dt=T_), e(R, 4 * d, dt=T_)   # pre-activation in the operand dtype
-        K.gemm(a2, Wfc, R, 4 * d, d, bias=mlp.c_fc.bias, act=K.AW_ACT_GELU_TANH, C=h, C2=g, c2_mode=1)
+        if T_ == F32:   # exact mode: the pre-activation h, the backward evaluates GELU'(h) (h: f32)
+            h, g = e(R, 4 * d, dt=T_), e(R, 4 * d, dt=T_)
+            K.gemm(a2, Wfc, R, 4 * d, d, bias=mlp.c_fc.bias, act=K.AW_ACT_GELU_TANH, C=h, C2=g, c2_mode=1)
+        else:
+            # bf16: g = GELU(h) and GELU'(h) from one exponential (c2_mode 4), the derivative saved in place of h
+            # (same bytes); the backward multiplies by it instead of evaluating GELU' of the bf16 pre-activation
+            g, h = e(R, 4 * d, dt=T_), e(R, 4 * d, dt=T_)
+            K.gemm(a2, Wfc, R, 4 * d, d, bias=mlp.c_fc.bias, act=K.AW_ACT_GELU_TANH, C=g, C2=h, c2_mode=4)
         x2 = e(R, d)
         K.gemm(g, Wp, R, d, 4 * d, bias=mlp.c_proj.bias, drop=(p_drop, sv.seed_mlp[i]), resid=x1, C=x2,
                seed_ptr=sv.ctr)
@@ -207,7 +214,9 @@ def backward(m, sv, g_out, slot, mid_hook=None):
         c = sv.blocks[i]
         # ---- MLP
         gh = e(R, 4 * d, dt=T_)
-        K.gemm(go, c["Wp"], R, 4 * d, d, b_trans=True, act=K.AW_ACT_GELU_TANH, pre=c["h"], C=gh)
+        # c["h"]: the pre-activation (f32 mode) or its saved GELU' (bf16 mode, forward c2_mode 4)
+        K.gemm(go, c["Wp"], R, 4 * d, d, b_trans=True, act=K.AW_ACT_GELU_TANH if T_ == F32 else K.AW_ACT_DERIV,
+               pre=c["h"], C=gh)
         wg["fc2"].append((go, c["g"], d, 4 * d, R, dict(a_trans=True, b_trans=True, C=slot(mlp.c_proj.weight),
                                                          accumulate=True, a_rowsum=slot(mlp.c_proj.bias))))
         ga2 = e(R, d)

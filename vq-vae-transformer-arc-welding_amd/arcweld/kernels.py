@@ -11,9 +11,9 @@ import ctypes
 import torch
 
 from . import _native as nat
-from ._native import AW_ACT_GELU_ERF, AW_ACT_GELU_TANH, AW_BF16, AW_F32, GemmArgs, call, dtype_code, ptr, stream_ptr
+from ._native import AW_ACT_DERIV, AW_ACT_GELU_ERF, AW_ACT_GELU_TANH, AW_BF16, AW_F32, GemmArgs, call, dtype_code, ptr, stream_ptr
 
-__all__ = ["gemm", "AW_ACT_GELU_ERF", "AW_ACT_GELU_TANH", "AW_BF16", "AW_F32"]
+__all__ = ["gemm", "AW_ACT_DERIV", "AW_ACT_GELU_ERF", "AW_ACT_GELU_TANH", "AW_BF16", "AW_F32"]
 
 
 def _ld(t):

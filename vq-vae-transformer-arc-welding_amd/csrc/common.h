@@ -175,6 +175,27 @@ __device__ __forceinline__ float gelu_tanh_grad(float x) {
   const float du = AW_SQRT_2_OVER_PI * (1.0f + 3.0f * 0.044715f * x * x);
   return s + 2.0f * x * s * (1.0f - s) * du;
 }
+// a pair of them as packed f32 (v_pk_mul_f32 / v_pk_fma_f32 / v_pk_add_f32; exp and rcp stay scalar): the same
+// operations per element up to FMA contraction
+__device__ __forceinline__ void gelu_tanh_and_grad2(f32x2 x, f32x2& g, f32x2& dg) {
+  const f32x2 x2 = x * x;
+  const f32x2 u = aw_splat2(AW_SQRT_2_OVER_PI) * __builtin_elementwise_fma(aw_splat2(0.044715f) * x2, x, x);
+  const f32x2 a = aw_splat2(-2.0f * 1.44269504088896340736f) * u;
+  const f32x2 s = {__builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(a.x)),
+                   __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(a.y))};
+  const f32x2 du = aw_splat2(AW_SQRT_2_OVER_PI) * __builtin_elementwise_fma(aw_splat2(3.0f * 0.044715f), x2,
+                                                                             aw_splat2(1.0f));
+  g = x * s;
+  dg = __builtin_elementwise_fma((x + x) * s * (aw_splat2(1.0f) - s), du, s);
+}
+// both from one exponential: g = gelu_tanh(x), dg = gelu_tanh_grad(x), the same operations as the two above
+__device__ __forceinline__ void gelu_tanh_and_grad(float x, float& g, float& dg) {
+  const float u = AW_SQRT_2_OVER_PI * (x + 0.044715f * x * x * x);
+  const float s = __builtin_amdgcn_rcpf(1.0f + __expf(-2.0f * u));
+  const float du = AW_SQRT_2_OVER_PI * (1.0f + 3.0f * 0.044715f * x * x);
+  g = x * s;
+  dg = s + 2.0f * x * s * (1.0f - s) * du;
+}
 
 // The GEMM epilogue's  x * m + r  (m = the last of act' / dropout scale, r = the residual): fused when both are
 // present, so the rounding does not depend on the compiler's contraction choices (gemm_core.h and the fused encoder

@@ -31,7 +31,8 @@ uint32_t epi_code(const aw_gemm_args& a, const GemmP& P, bool ragged) {
   if (a.bias) c |= EP_BIAS;
   if (a.bias && a.bias_mod > 0) c |= EP_BIASMOD;
   if (a.pre) c |= EP_PRE | (a.pre_dtype == AW_BF16 ? EP_PREBF : 0u);
-  if ((a.pre || a.c2_mode == 1) && a.act == AW_ACT_GELU_TANH) c |= EP_TANH;
+  if ((a.pre || a.c2_mode == 1 || a.c2_mode == 4) && a.act == AW_ACT_GELU_TANH) c |= EP_TANH;
+  if (a.pre && a.act == AW_ACT_DERIV) c |= EP_DERIV;
   if (a.drop_p > 0.f) c |= EP_DROP;
   if (a.resid) c |= EP_RESID | (a.resid_dtype == AW_BF16 ? EP_RESIDBF : 0u);
   if (a.beta != 0.f) c |= EP_BETA;
@@ -39,6 +40,7 @@ uint32_t epi_code(const aw_gemm_args& a, const GemmP& P, bool ragged) {
   if (a.c2_mode == 1) c |= EP_C2ACT;
   else if (a.c2_mode == 2 || (a.c2_mode == 3 && a.drop2_p <= 0.f)) c |= EP_C2COPY;
   else if (a.c2_mode == 3) c |= EP_C2DROP;
+  else if (a.c2_mode == 4) c |= EP_C2DACT;
   if (a.c2_mode && a.c2_dtype == AW_BF16) c |= EP_C2BF;
   if (a.colstats) c |= EP_STATS;
   return c;
@@ -176,6 +178,10 @@ static int validate(const aw_gemm_args& a) {
   }
   AW_REQUIRE(!(a.beta != 0.f && a.c_dtype != AW_F32), "aw_gemm: beta != 0 needs an f32 C");
   AW_REQUIRE(!(a.c2_mode && !a.C2), "aw_gemm: c2_mode without C2");
+  AW_REQUIRE(a.c2_mode >= 0 && a.c2_mode <= 4 && a.act >= AW_ACT_GELU_ERF && a.act <= AW_ACT_DERIV,
+             "aw_gemm: bad c2_mode %d / act %d", a.c2_mode, a.act);
+  AW_REQUIRE(!(a.act == AW_ACT_DERIV && (a.c2_mode == 1 || a.c2_mode == 4)),
+             "aw_gemm: AW_ACT_DERIV names no activation for C2 modes 1 / 4");
   AW_REQUIRE(!(a.colstats && a.stats_mod <= 0), "aw_gemm: colstats needs stats_mod > 0");
   AW_REQUIRE(a.pre_dtype == AW_F32 || a.pre_dtype == AW_BF16, "aw_gemm: bad pre_dtype %d", a.pre_dtype);
   AW_REQUIRE(a.resid_dtype == AW_F32 || a.resid_dtype == AW_BF16, "aw_gemm: bad resid_dtype %d", a.resid_dtype);

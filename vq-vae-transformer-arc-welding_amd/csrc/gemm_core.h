@@ -94,7 +94,7 @@ enum EpiBits : uint32_t {
   EP_BIAS = 1u << 0, EP_BIASMOD = 1u << 1, EP_PRE = 1u << 2, EP_TANH = 1u << 3, EP_DROP = 1u << 4,
   EP_RESID = 1u << 5, EP_BETA = 1u << 6, EP_C = 1u << 7, EP_CBF = 1u << 8, EP_C2ACT = 1u << 9,
   EP_C2COPY = 1u << 10, EP_C2DROP = 1u << 11, EP_C2BF = 1u << 12, EP_STATS = 1u << 13, EP_ACCUM = 1u << 14,
-  EP_PREBF = 1u << 15, EP_RESIDBF = 1u << 16, EP_GENERIC = 1u << 31
+  EP_PREBF = 1u << 15, EP_RESIDBF = 1u << 16, EP_DERIV = 1u << 17, EP_C2DACT = 1u << 18, EP_GENERIC = 1u << 31
 };
 
 // Diagnostic phase stamps (tools/probe only: defined there before this file is included; never in the library).
@@ -709,13 +709,15 @@ __global__ __launch_bounds__(Cfg<BMT>::NTH, RAGGED ? 1 : Cfg<BMT>::MINB) void ge
   const bool f_pre = EPF(EP_PRE, p.pre != nullptr);
   const bool f_prebf = EPF(EP_PREBF, p.pre_dtype == AW_BF16);
   const bool f_tanh = EPF(EP_TANH, p.act == AW_ACT_GELU_TANH);
+  const bool f_deriv = EPF(EP_DERIV, p.act == AW_ACT_DERIV);   // pre holds act' itself
   const bool f_drop = EPF(EP_DROP, p.drop_p > 0.f);
   const bool f_resid = EPF(EP_RESID, p.resid != nullptr);
   const bool f_residbf = EPF(EP_RESIDBF, p.resid_dtype == AW_BF16);
   const bool f_beta = EPF(EP_BETA, p.beta != 0.f);
   const bool f_c = EPF(EP_C, Cptr != nullptr);
   const bool f_cbf = EPF(EP_CBF, p.c_dtype == AW_BF16);
-  const int c2m = GEN ? p.c2_mode : ((EPI & EP_C2ACT) ? 1 : (EPI & EP_C2COPY) ? 2 : (EPI & EP_C2DROP) ? 3 : 0);
+  const int c2m = GEN ? p.c2_mode
+                      : ((EPI & EP_C2ACT) ? 1 : (EPI & EP_C2COPY) ? 2 : (EPI & EP_C2DROP) ? 3 : (EPI & EP_C2DACT) ? 4 : 0);
   const bool f_c2bf = EPF(EP_C2BF, p.c2_dtype == AW_BF16);
   const bool f_stats = EPF(EP_STATS, p.colstats != nullptr);
   const float alpha = GEN ? p.alpha : 1.f;       // specialised codes are issued for alpha == 1 only
@@ -792,7 +794,7 @@ __global__ __launch_bounds__(Cfg<BMT>::NTH, RAGGED ? 1 : Cfg<BMT>::MINB) void ge
         if (c2m == 3) aw_dropout_scale4(dseed2, e0, p.drop2_p, ds2);
         float v[4], w[4], ag[4];
         // bf16 operands: GELU and GELU' in packed pairs (aw_gelu4 / aw_gelu_grad4, shared with the encoder chain)
-        if (FASTGELU && f_pre && !f_tanh) aw_gelu_grad4(pv, ag);
+        if (FASTGELU && f_pre && !f_tanh && !f_deriv) aw_gelu_grad4(pv, ag);
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           float x = alpha * av[e] + bias[e];
@@ -801,7 +803,7 @@ __global__ __launch_bounds__(Cfg<BMT>::NTH, RAGGED ? 1 : Cfg<BMT>::MINB) void ge
           float m = 1.f;
           bool has_m = false;
           if (f_pre) {
-            const float a = f_tanh ? gelu_tanh_grad(pv[e]) : (FASTGELU ? ag[e] : gelu_erf_grad(pv[e]));
+            const float a = f_deriv ? pv[e] : f_tanh ? gelu_tanh_grad(pv[e]) : (FASTGELU ? ag[e] : gelu_erf_grad(pv[e]));
             if (f_drop) x *= a;
             else m = a, has_m = true;
           }
@@ -819,6 +821,29 @@ __global__ __launch_bounds__(Cfg<BMT>::NTH, RAGGED ? 1 : Cfg<BMT>::MINB) void ge
           }
         }
         if (FASTGELU && c2m == 1 && !f_tanh) aw_gelu4(v, w);
+        if (c2m == 4 && f_tanh && FASTGELU) {   // C = act(v), C2 = act'(v) from one exponential, packed pairs
+#pragma unroll
+          for (int e = 0; e < 4; e += 2) {
+            f32x2 g, dg;
+            gelu_tanh_and_grad2((f32x2){v[e], v[e + 1]}, g, dg);
+            v[e] = g.x, v[e + 1] = g.y, w[e] = dg.x, w[e + 1] = dg.y;
+          }
+        } else if (c2m == 4) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            float g, dg;
+            if (f_tanh) {
+              gelu_tanh_and_grad(v[e], g, dg);
+            } else {
+              float ex;
+              const float phi = FASTGELU ? aw_phi_e(v[e], ex) : 0.f;
+              g = FASTGELU ? v[e] * phi : gelu_erf(v[e]);
+              dg = FASTGELU ? fmaf(v[e] * AW_INV_SQRT2PI, ex, phi) : gelu_erf_grad(v[e]);
+            }
+            v[e] = g;
+            w[e] = dg;
+          }
+        }
         if (vec) {
           if (f_c) store4(Cptr, f_cbf, row * p.ldc + col, v, wt);
           if (c2m) store4(p.C2, f_c2bf, row * p.ldc2 + col, w, wt);

@@ -6,7 +6,7 @@
 // forward layouts (A row-major [M][K], B [N][K]; plain and implicit-conv A):
 //   VQ-VAE:  conv/ResBlock pre-activation + GELU operand, residual + dropout, sep conv, ConvT + BN statistics
 //            (model/vq_vae_patch_embedd.py:11,65,68,87,143,27), exact-f32 tokenization forms;
-//   Transformer: c_attn, c_proj/MLP projection + dropout + residual, c_fc + tanh-GELU, lm_head
+//   Transformer: c_attn, c_proj/MLP projection + dropout + residual, c_fc + tanh-GELU (and its derivative), lm_head
 //            (model/transformer_block.py:30,32,78-79; model/transformer_decoder.py:29).
 #define AW_FWD_CODES(X, T, LY)                                              \
   X(T, LY, EP_BIAS | EP_C | EP_C2ACT | EP_C2BF)                             \
@@ -31,6 +31,7 @@
   X(T, LY, EP_BIAS | EP_RESID | EP_C)                                       \
   X(T, LY, EP_BIAS | EP_TANH | EP_C | EP_C2ACT | EP_C2BF)                   \
   X(T, LY, EP_BIAS | EP_TANH | EP_C | EP_CBF | EP_C2ACT | EP_C2BF)          \
+  X(T, LY, EP_BIAS | EP_TANH | EP_C | EP_CBF | EP_C2DACT | EP_C2BF)         \
   X(T, LY, EP_C)                                                            \
   X(T, LY, EP_C | EP_CBF)
 
@@ -59,4 +60,5 @@
   X(T, LY, EP_C)                                                            \
   X(T, LY, EP_C | EP_CBF)                                                   \
   X(T, LY, EP_PRE | EP_TANH | EP_C | EP_CBF)                               \
-  X(T, LY, EP_PRE | EP_PREBF | EP_TANH | EP_C | EP_CBF)
+  X(T, LY, EP_PRE | EP_PREBF | EP_TANH | EP_C | EP_CBF)                    \
+  X(T, LY, EP_PRE | EP_PREBF | EP_DERIV | EP_C | EP_CBF)
