@@ -1,9 +1,11 @@
-"""The decoder chain's LDS image swizzle (csrc/reschain.hip, EcGeo<3>::KEYS): the keys the kernel is built with make
-every B-fragment ds_read_b128 lane group conflict-free for all three tap shifts, and keep the epilogue's
-ds_write_b64 at two lanes per bank (tools/probe/chain_swizzle.py derived them).  CPU only: reads the constant from
-the source."""
+"""The chains' LDS image swizzle (csrc/reschain.hip, EcGeo::KEYS): the keys the kernels are built with make every
+B-fragment ds_read_b128 lane group conflict-free (the decoder for all three tap shifts), keep the epilogue's
+ds_write_b64 at two lanes per bank, and make the store path's slice reads (EcStore::ir) conflict-free
+(tools/probe/chain_swizzle.py derived them).  CPU only: reads the constants from the source."""
 import os
 import re
+
+import pytest
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRC = os.path.join(REPO, "vq-vae-transformer-arc-welding_amd", "csrc", "reschain.hip")
@@ -46,11 +48,44 @@ def test_decoder_keys_make_every_tap_read_conflict_free():
             assert len(set(slots)) == 16, (shift, slots)
 
 
-def test_encoder_keys_are_the_identity_and_conflict_free_unshifted():
+def test_encoder_keys_are_conflict_free_unshifted():
     enc, _ = _keys()
-    assert [enc[u] for u in range(16)] == list(range(16))
+    assert sorted(enc[u] for u in range(16)) == list(range(16))
     for slots in _bank_slots(enc, 0):
         assert len(set(slots)) == 16
+
+
+@pytest.mark.parametrize("which", [0, 1])
+def test_store_slice_reads_are_conflict_free(which):
+    """EcStore::ir: lane l reads token 8 p + (l >> 3), logical chunk 8 w + (l & 7) of the wave's slice; per ds_read_b128
+    lane group the physical chunks mod 16 must be distinct for p = 0, 1 and either parity of w."""
+    key = _keys()[which]
+    groups = [list(range(0, 4)) + list(range(12, 16)) + list(range(20, 28)),
+              list(range(4, 12)) + list(range(16, 20)) + list(range(28, 32))]
+    groups += [[lane + 32 for lane in g] for g in groups]
+    for grp in groups:
+        for p in (0, 1):
+            for wb in (0, 1):
+                slots = [((8 * wb + (lane & 7)) ^ key[8 * p + (lane >> 3)]) & 15 for lane in grp]
+                assert len(set(slots)) == 16, (which, p, wb, slots)
+
+
+@pytest.mark.parametrize("which", [0, 1])
+def test_keys_keep_the_epilogue_writes_at_two_lanes_per_bank(which):
+    key = _keys()[which]
+    counts = {}
+    for u in range(16):
+        counts[key[u] % 8] = counts.get(key[u] % 8, 0) + 1
+    assert sorted(counts.values()) == [2] * 8
+
+
+def test_search_tool_reproduces_the_built_keys():
+    import sys
+    sys.path.insert(0, os.path.join(REPO, "tools", "probe"))
+    import chain_swizzle as cs
+    enc, dec = _keys()
+    assert cs.packed(cs.search((0,))) == sum(enc[u] << (4 * u) for u in range(16))
+    assert cs.packed(cs.search((-1, 0, 1))) == sum(dec[u] << (4 * u) for u in range(16))
 
 
 def test_decoder_keys_keep_the_epilogue_writes_at_two_lanes_per_bank():

@@ -76,13 +76,15 @@ template <int TAPS> struct EcGeo {
   static constexpr int LDS = BIAS + 8 * 256;
   static constexpr uint32_t WBYTES = (uint32_t)EC_H * EC_H * 2 * TAPS;   // one packed weight matrix
   static constexpr int WWAVE = 4 * KS * 1024;                      // a wave's 4 packed block rows
-  // Image swizzle key of token u of a 16-token group: chunk c of the token sits at chunk c ^ key(u).  The encoder
-  // reads only unshifted rows: key = u.  The decoder's shifted taps read rows u - 1 / u + 1 beside u, and with key = u
-  // the 16 lanes of a ds_read_b128 group hit one bank slot twice under either shift (PMC: 38 % of the decoder chain's
-  // LDS cycles were bank conflicts); this table (found by exhaustive search, tools/probe/chain_swizzle.py) makes all
-  // three taps conflict-free and keeps the epilogue's ds_write_b64 at its minimum of two lanes per bank.  The zero
-  // rows ahead of / behind a window (u = -1 / 16) read with keys 15 / 0.
-  static constexpr uint64_t KEYS = TAPS == 1 ? 0xfedcba9876543210ull : 0xfdb64fdb98264210ull;
+  // Image swizzle key of token u of a 16-token group: chunk c of the token sits at chunk c ^ key(u).  Three kinds of
+  // LDS access see the keys: the B-fragment reads of the K loop (the decoder's shifted taps read rows u - 1 / u + 1
+  // beside u: with key = u the 16 lanes of a ds_read_b128 group hit one bank slot twice under either shift, 38 % of
+  // the decoder chain's LDS cycles were bank conflicts), the epilogue's ds_write_b64 (at best two lanes per bank) and
+  // the store path's whole-line slice reads (EcStore::ir, eight tokens x eight chunks per instruction: the identity and
+  // the round-5 decoder keys put two lanes of a group on one slot there, 21-23 % conflicts in the encoder chains).
+  // Both tables come from an exhaustive search over all three (tools/probe/chain_swizzle.py; the encoder's only for the
+  // unshifted reads it makes).  The zero rows ahead of / behind a window (u = -1 / 16) read with keys 15 / 0.
+  static constexpr uint64_t KEYS = TAPS == 1 ? 0xfe76dc54ba329810ull : 0xf53ac739685ace10ull;
   __device__ static int key(int u) { return u < 0 ? 15 : u > 15 ? 0 : (int)((KEYS >> (4 * u)) & 15); }
 };
 static_assert(EcGeo<3>::LDS <= 160 * 1024, "decoder chain LDS");
@@ -318,11 +320,14 @@ template <class G, int DIR> struct EcLane {
 // The store side, derived in the epilogue (not held across the K loop).  Global stores write a wave's 64-channel
 // slice (128 B per token) of 8 tokens per instruction, lane -> (token lane >> 3, 16-B chunk lane & 7), at gs + 8192 q
 // for tokens 8q .. 8q + 7.  The slice comes from the wave's own chunks of the next image (ir[q & 1] + JS (q >> 1))
-// or from its scratch (16 tokens at a time: written at sw[i], read at sr + 1024 q; chunk XOR-swizzled by token & 7).
+// or from its scratch (16 tokens at a time: written at sw[i], read at sr[q]; the 16-B chunk of token t XOR-swizzled
+// by t >> 1, so that a ds_write_b64 of the fragment layout puts each lane on a bank of its own -- with t & 7 tokens t
+// and t + 8 met on one bank -- and the line-layout ds_read_b128 / ds_write_b128 groups stay conflict-free).
 template <class G> struct EcStore {
   int ir[2];     // image own-slice read bases (q parity), without the image offset
   int sw[4];     // scratch write bases per i
-  int sr;        // scratch read base
+  int sr;        // scratch line base of tokens lane >> 3; tokens 8 + (lane >> 3) at srq(1) = (sr ^ 64) + 1024
+  __device__ __forceinline__ int srq(int q) const { return q ? (sr ^ 64) + 1024 : sr; }
   uint32_t gs;   // global byte offset of this lane's store piece for tokens 0..7
   __device__ __forceinline__ EcStore(int tid, int64_t row0) {
     const int lane = tid & 63, w = tid >> 6, g = lane >> 4, li = lane & 15;
@@ -331,8 +336,8 @@ template <class G> struct EcStore {
     for (int p = 0; p < 2; ++p) ir[p] = G::R0 + (8 * p + t8) * EC_ROWB + (((8 * w + c8) ^ G::key(8 * p + t8)) << 4);
     const int sbase = G::SCR + w * EC_SCR;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) sw[i] = sbase + li * 128 + (((2 * i + (g >> 1)) ^ (li & 7)) << 4) + (g & 1) * 8;
-    sr = sbase + t8 * 128 + ((c8 ^ t8) << 4);
+    for (int i = 0; i < 4; ++i) sw[i] = sbase + li * 128 + (((2 * i + (g >> 1)) ^ (li >> 1)) << 4) + (g & 1) * 8;
+    sr = sbase + t8 * 128 + ((c8 ^ (t8 >> 1)) << 4);   // (t8 + 8) >> 1 = (t8 >> 1) ^ 4: chunk bit 2, byte bit 6
     gs = (uint32_t)(((row0 + t8) * EC_H + 64 * w + 8 * c8) * 2);
   }
 };
@@ -359,7 +364,7 @@ __device__ __forceinline__ void ec_store_slice(const char* smem, int img, const 
 template <class G, bool WT>
 __device__ __forceinline__ void ec_store_scratch(const char* smem, int j, const EcStore<G>& S, rsrc_t r) {
 #pragma unroll
-  for (int q = 0; q < 2; ++q) ec_store16<WT>(r, S.gs, 8192 * (2 * j + q), ec_lds_r16(smem, S.sr + 1024 * q));
+  for (int q = 0; q < 2; ++q) ec_store16<WT>(r, S.gs, 8192 * (2 * j + q), ec_lds_r16(smem, S.srq(q)));
 }
 
 template <class G> __device__ __forceinline__ void ec_init(char* smem, int tid) {
@@ -562,8 +567,8 @@ __global__ __launch_bounds__(EC_NTH) void res_chain_bwd_kernel(aw_res_chain_bwd_
     const EcStore<G> S(tid, row0);
     // tokens 16 j .. 16 j + 15 of the pre lines into the scratch (read back below as this lane's fragments (i, j))
     auto stage_pre = [&](int j) {
-      *reinterpret_cast<uint4*>(smem + S.sr) = pl[2 * j];
-      *reinterpret_cast<uint4*>(smem + S.sr + 1024) = pl[2 * j + 1];
+      *reinterpret_cast<uint4*>(smem + S.srq(0)) = pl[2 * j];
+      *reinterpret_cast<uint4*>(smem + S.srq(1)) = pl[2 * j + 1];
     };
     auto pre_frag = [&](int i, float (&pv)[4]) { ec_unpack(*reinterpret_cast<const u32x2*>(smem + S.sw[i]), pv); };
 
