@@ -125,6 +125,11 @@ int aw_gemm_set_wgrad_policy(int mode);
 #define AW_WGRAD_BATCH_MAX 32
 int64_t aw_wgrad_batch_workspace(const aw_gemm_args* args, int n);
 int aw_wgrad_batch(const aw_gemm_args* args, int n, void* ws, int64_t ws_bytes, void* stream);
+/* Bound of the fix-up's poll for its sibling pieces (default 2^26 polls; a piece that runs out of it poisons its tile
+ * with NaN instead of summing unpublished partials).  0 forces that path on every split tile: a test hook, after
+ * which the per-tile hand-off counters of this process are stale (tests/test_gpu_kernels.py runs it in a child
+ * process). */
+int aw_wgrad_set_spin_limit(int polls);
 
 /* Fused ResBlock chain, bf16 operands, H = 512, no BatchNorm: the whole ResBlock stack of the encoder or of the
  * decoder (model/vq_vae_patch_embedd.py:60-74 ResBlock, :103-110 CNNBlock) as ONE persistent launch of N / 64

@@ -591,6 +591,43 @@ def test_wgrad_batch_split_k_vs_fp32_reference(case):
         torch.testing.assert_close(b, bw2, rtol=1e-4, atol=4e-5 * float(bw2.abs().max()))
 
 
+def test_wgrad_batch_broken_handoff_poisons_the_tile():
+    """The split-K fix-up of aw_wgrad_batch waits a bounded number of polls for its sibling pieces (csrc/wgrad.hip: the
+    sc1 hand-off carries no acquire / release); a piece that runs out of them must poison its tile with NaN rather
+    than sum partials that were never published.  aw_wgrad_set_spin_limit(0) forces that path on the one-tile case
+    (four pieces meet in one fix-up).  In a child process: afterwards the per-tile hand-off counters of the process
+    are stale, which would break the next launch of this one."""
+    import os
+    import subprocess
+    import sys
+    import textwrap
+    pkg = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "vq-vae-transformer-arc-welding_amd")
+    code = textwrap.dedent(f"""
+        import sys
+        sys.path.insert(0, {pkg!r})
+        import torch
+        from arcweld import _native
+        from arcweld import kernels as K
+        g = torch.Generator(device="cuda").manual_seed(1)
+        A = torch.randn(8200, 256, device="cuda", generator=g).to(torch.bfloat16)
+        x = torch.randn(8200, 256, device="cuda", generator=g).to(torch.bfloat16)
+        prob = lambda C: (A, x, 256, 256, 8200, dict(a_trans=True, b_trans=True, accumulate=True, C=C))
+        ok = torch.zeros(256, 256, device="cuda")
+        K.wgrad_batch([prob(ok)])
+        bad = torch.zeros(256, 256, device="cuda")
+        _native.call("aw_wgrad_set_spin_limit", 0)
+        K.wgrad_batch([prob(bad)])
+        torch.cuda.synchronize()
+        print("RESULT", int(torch.isnan(ok).sum()), int(torch.isnan(bad).sum()))
+    """)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=180)
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("RESULT")]
+    assert r.returncode == 0 and line, r.stdout + r.stderr
+    n_ok, n_bad = (int(v) for v in line[0].split()[1:])
+    assert n_ok == 0          # the default bound: a normal hand-off
+    assert n_bad > 0          # the forced timeout: the tile is poisoned, loudly
+
+
 @pytest.mark.parametrize("training", [True, False])
 def test_unpatch_head_bf16_y_equals_f32_y(training):
     """aw_unpatch_head_*_ex with the ConvT output in bf16 (the bf16 operand mode, model/vq_vae_patch_embedd.py:24-31)

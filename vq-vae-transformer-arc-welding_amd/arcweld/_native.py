@@ -99,6 +99,7 @@ SIGNATURES = {
     "aw_gemm_set_wgrad_policy": [c_int],
     "aw_wgrad_batch_workspace": [ctypes.POINTER(GemmArgs), c_int],
     "aw_wgrad_batch": [ctypes.POINTER(GemmArgs), c_int, c_p, c_i64, c_p],
+    "aw_wgrad_set_spin_limit": [c_int],
     "aw_res_chain_fwd": [ctypes.POINTER(ResChainFwdArgs), c_p],
     "aw_res_chain_bwd": [ctypes.POINTER(ResChainBwdArgs), c_p],
     "aw_res_pack_weights": [ctypes.POINTER(c_p), ctypes.POINTER(c_p), ctypes.POINTER(c_p), c_int, c_int, c_p],

@@ -346,6 +346,7 @@ struct WTParams {
   int nprob, K, nk, G, total_tiles, S, units;
   float alpha;
   float* ws;          // one slot of WT_SLAB floats per unit
+  int spin;           // poll bound of the fix-up (aw_wgrad_set_spin_limit; 0 forces the broken-hand-off path)
 };
 
 // per-tile counters of arrived and of published pieces; the last arriver resets both of its tile to 0
@@ -523,13 +524,13 @@ __global__ __launch_bounds__(WT_NTH, 1) void wgrad_tt_kernel(WTParams P) {
           // resident and only store, drain and count); running out of it means a broken hand-off, which must not
           // turn into a silently wrong gradient: trap
           int it = 0;   // relaxed agent loads = sc1 loads: past this CU's L1
-          for (; it < (1 << 26); ++it) {
+          for (; it < P.spin; ++it) {
             if (__hip_atomic_load(&g_wt_pub[tile], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= P.S - 1) break;
             __builtin_amdgcn_s_sleep(1);
           }
           // a broken hand-off poisons the tile (NaN: loud in the loss, the clip norm and every check) instead of
           // summing unwritten slots silently
-          if (it == (1 << 26)) acc[0][0] = f32x4{__builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""), 0.f};
+          if (it == P.spin) acc[0][0] = f32x4{__builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""), 0.f};
           __hip_atomic_store(&g_wt_pub[tile], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           __hip_atomic_store(&g_wt_arrive[tile], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
@@ -608,6 +609,7 @@ __global__ __launch_bounds__(WT_NTH, 1) void wgrad_tt_kernel(WTParams P) {
 
 // ---- host side of the batch
 int g_cus = 0;
+int g_wt_spin = 1 << 26;   // the fix-up's poll bound (aw_wgrad_set_spin_limit)
 
 int wt_cus() {
   if (g_cus == 0) {
@@ -769,7 +771,14 @@ extern "C" int aw_wgrad_batch(const aw_gemm_args* args, int n, void* ws, int64_t
                  ws_bytes >= (P.S > 1 ? (int64_t)P.units * WT_SLAB * (int64_t)sizeof(float) : 16),
              "aw_wgrad_batch: workspace must be 16-B aligned and hold aw_wgrad_batch_workspace() bytes");
   P.ws = reinterpret_cast<float*>(ws);
+  P.spin = g_wt_spin;
   hipLaunchKernelGGL(wgrad_tt_kernel, dim3(P.G), dim3(WT_NTH), 0, reinterpret_cast<hipStream_t>(stream), P);
   return aw::check_launch("aw_wgrad_batch");
+}
+
+extern "C" int aw_wgrad_set_spin_limit(int polls) {
+  AW_REQUIRE(polls >= 0, "aw_wgrad_set_spin_limit: polls must be >= 0");
+  g_wt_spin = polls;
+  return AW_OK;
 }
 
