@@ -134,7 +134,9 @@ int aw_wgrad_set_spin_limit(int polls);
 /* Fused ResBlock chain, bf16 operands, H = 512, no BatchNorm: the whole ResBlock stack of the encoder or of the
  * decoder (model/vq_vae_patch_embedd.py:60-74 ResBlock, :103-110 CNNBlock) as ONE persistent launch of N / 64
  * workgroups, each walking a 64-token row block through the 2R convs with its activations resident in LDS; it
- * replaces the 2R aw_gemm launches of either direction and produces the same tensors bit for bit.
+ * replaces the 2R aw_gemm launches of either direction.  The forward's operands a1 / a and keep bits are theirs bit for
+ * bit; in place of their saved pre-activations h / x it saves GELU'(h) / GELU'(x) (f32 values rounded to bf16), and
+ * the backward multiplies by those: its gh / gxo_out track the unfused backward to bf16 rounding.
  *   taps = 1: the encoder (CNNBlock(seperate=True)): every conv sees a length-1 token slice, so it is its centre tap,
  *             a [H][H] contraction per token; weights are [H][H] (packed).
  *   taps = 3: the decoder (CNNBlock(seperate=False)): k = 3, padding 1 convs along windows of seg = 16 consecutive
