@@ -23,6 +23,8 @@
 //    (the image is lane-linear per DMA instruction).
 #include "gemm_core.h"
 
+#include <stdlib.h>
+
 #include <algorithm>
 
 #pragma clang diagnostic ignored "-Winline-asm"
@@ -344,6 +346,7 @@ struct WTProb {
 struct WTParams {
   WTProb p[AW_WGRAD_BATCH_MAX];   // 32 x 88 B: the kernel-argument block stays under 3 KB
   int nprob, K, nk, G, total_tiles, S, units;
+  int big;            // tiles [0, big) run unsplit (one full-K unit each), the rest in S k-aligned pieces
   float alpha;
   float* ws;          // one slot of WT_SLAB floats per unit
   int spin;           // poll bound of the fix-up (aw_wgrad_set_spin_limit; 0 forces the broken-hand-off path)
@@ -390,8 +393,18 @@ __global__ __launch_bounds__(WT_NTH, 1) void wgrad_tt_kernel(WTParams P) {
   }
 
   for (int unit = c; unit < P.units; unit += P.G) {
-    const int sp = unit / P.total_tiles, tile = unit - sp * P.total_tiles;
-    const int k0 = (int)((int64_t)sp * P.nk / P.S), k1 = (int)((int64_t)(sp + 1) * P.nk / P.S);
+    // units [0, big): tile = unit, full K; then the split tiles' pieces, split-major: piece sp of split tile t is unit
+    // big + sp * nsplit + (t - big) = sp * nsplit + t (big = 0: the uniform plan)
+    const int nsplit = P.total_tiles - P.big;
+    int tile, sp, St;
+    if (unit < P.big) {
+      tile = unit, sp = 0, St = 1;
+    } else {
+      sp = (unit - P.big) / nsplit;
+      tile = unit - sp * nsplit;
+      St = P.S;
+    }
+    const int k0 = (int)((int64_t)sp * P.nk / St), k1 = (int)((int64_t)(sp + 1) * P.nk / St);
     int pi = 0;
     while (pi + 1 < P.nprob && tile >= P.p[pi + 1].tile0) ++pi;
     const WTProb& pr = P.p[pi];
@@ -497,12 +510,12 @@ __global__ __launch_bounds__(WT_NTH, 1) void wgrad_tt_kernel(WTParams P) {
         }
     }
     bool write = true;
-    if (P.S > 1) {
+    if (St > 1) {
       // ---- one piece of S: take an arrival ticket first; the last to arrive sums the other pieces once they have
       //      published (they took their tickets before it, so they are resident and only store, drain and count: the
       //      wait is bounded whatever the residency), the others publish their accumulators and leave
       if (tid == 0) s_last = __hip_atomic_fetch_add(&g_wt_arrive[tile], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-                             P.S - 1;
+                             St - 1;
       __syncthreads();
       write = s_last != 0;
       if (!write) {
@@ -525,7 +538,7 @@ __global__ __launch_bounds__(WT_NTH, 1) void wgrad_tt_kernel(WTParams P) {
           // turn into a silently wrong gradient: trap
           int it = 0;   // relaxed agent loads = sc1 loads: past this CU's L1
           for (; it < P.spin; ++it) {
-            if (__hip_atomic_load(&g_wt_pub[tile], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= P.S - 1) break;
+            if (__hip_atomic_load(&g_wt_pub[tile], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= St - 1) break;
             __builtin_amdgcn_s_sleep(1);
           }
           // a broken hand-off poisons the tile (NaN: loud in the loss, the clip norm and every check) instead of
@@ -535,9 +548,9 @@ __global__ __launch_bounds__(WT_NTH, 1) void wgrad_tt_kernel(WTParams P) {
           __hip_atomic_store(&g_wt_arrive[tile], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         __syncthreads();   // the polling wave joins: every wave's slot loads (all sc1) come after the poll matched
-        for (int o = 0; o < P.S; ++o) {
+        for (int o = 0; o < St; ++o) {
           if (o == sp) continue;
-          const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(P.ws + ((int64_t)o * P.total_tiles + tile) * WT_SLAB,
+          const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(P.ws + ((int64_t)o * nsplit + tile) * WT_SLAB,
                                                               (short)0, WT_SLAB * 4, 0x00020000);
 #pragma unroll
           for (int i = 0; i < 8; ++i)
@@ -696,7 +709,13 @@ int wt_plan(const aw_gemm_args* args, int n, WTParams* P) {
     }
   }
   P->S = best;
-  P->units = tiles * best;
+  // Mixed plan: with S = 2 and more tiles than CUs, the first `cus` tiles run unsplit (one full-K unit each) and only
+  // the rest in two pieces, when those pieces fit one per workgroup: every workgroup then runs one full unit and at
+  // most one half -- the uniform plan's three halves -- with a third of its fix-ups (the split tiles' slabs written and
+  // read back).  The 8-block decoder batch: 384 tiles = 256 unsplit + 128 split.  AW_WGRAD_MIXED=0: uniform plan.
+  static const bool mixed = [] { const char* e = getenv("AW_WGRAD_MIXED"); return !(e && atoi(e) == 0); }();
+  P->big = (mixed && best == 2 && tiles > cus && 2 * (tiles - cus) <= cus) ? cus : 0;
+  P->units = P->big + (tiles - P->big) * best;
   P->G = std::min(cus, P->units);
   P->alpha = a0.alpha;
   return AW_OK;
