@@ -465,6 +465,11 @@ int aw_class_head_bwd(const float* xf, const float* s, const float* dout, int64_
 /* Token embedding + sinusoidal PE (model/embedding.py:57-59): x[b,t,:] = Wtok[ids[b,t]] + pe[t] */
 int aw_embed_fwd(const int64_t* ids, int64_t B, int T, int D, const float* wtok, const float* pe, float* x,
                  void* stream);
+/* aw_embed_fwd followed by aw_layernorm_fwd(x, B*T, D, w, b, eps, y, y_dtype, mean, rstd) in one launch, bit-identical
+   to the pair (the first block's ln_1, model/transformer_block.py:84); D = 256, 512, 768 or 1024, 16-B aligned rows */
+int aw_embed_ln_fwd(const int64_t* ids, int64_t B, int T, int D, const float* wtok, const float* pe, float* x,
+                    const float* w, const float* b, float eps, void* y, int y_dtype, float* mean, float* rstd,
+                    void* stream);
 int aw_embed_bwd(const int64_t* ids, int64_t B, int T, int D, const float* dx, float* dwtok, void* stream);
 /* Causal self-attention core (model/transformer_block.py:44-60) on the packed qkv projection
  * (B*T, 3*d, dtype), heads of hs = d/n_head: y (B*T, d, dtype) = softmax(q k^T / sqrt(hs), causal) v;

@@ -688,3 +688,27 @@ def test_embedding_forward_backward_vs_torch(B, T, V, D):
     want = prior.clone().index_add_(0, ids.reshape(-1), dx)
     torch.testing.assert_close(dw, want, rtol=1e-5, atol=1e-4)
     assert torch.equal(dw[V - 1], prior[V - 1])
+
+
+@pytest.mark.parametrize("B,T,V,D,dt", [(51, 321, 514, 512, torch.bfloat16), (3, 17, 30, 256, torch.float32),
+                                        (2, 9, 11, 768, torch.bfloat16), (2, 5, 7, 1024, torch.float32)])
+def test_embed_ln_fused_matches_the_two_launches(B, T, V, D, dt):
+    """aw_embed_ln_fwd (the decoder's embedding with block 0's ln_1 fused) against aw_embed_fwd followed by
+    aw_layernorm_fwd on the same inputs: x, y, mean and rstd bit-identical (the same per-element add and the vector
+    LayerNorm's order of operations), at every d_model the fused form accepts and both operand dtypes."""
+    from arcweld import kernels as K
+    g = torch.Generator(device="cuda").manual_seed(B * T + D)
+    ids = torch.randint(0, V, (B, T), device="cuda", generator=g)
+    W = torch.randn(V, D, device="cuda", generator=g)
+    pe = torch.randn(T + 3, D, device="cuda", generator=g)          # a longer table: rows t < T are read
+    w = 1 + 0.1 * torch.randn(D, device="cuda", generator=g)
+    b = 0.1 * torch.randn(D, device="cuda", generator=g)
+    R = B * T
+    x0, y0, m0, r0 = torch.empty(R, D, device="cuda"), torch.empty(R, D, device="cuda", dtype=dt), \
+        torch.empty(R, device="cuda"), torch.empty(R, device="cuda")
+    K.embed_fwd(ids, W, pe, x0)
+    K.layernorm_fwd(x0, w, b, 1e-5, y0, m0, r0)
+    x1, y1, m1, r1 = (torch.full_like(t, float("nan")) for t in (x0, y0, m0, r0))
+    K.embed_ln_fwd(ids, W, pe, x1, w, b, 1e-5, y1, m1, r1)
+    for got, want in ((x1, x0), (y1, y0), (m1, m0), (r1, r0)):
+        assert torch.equal(got, want)

@@ -154,6 +154,7 @@ SIGNATURES = {
     "aw_class_head_fwd": [c_p, c_i64, c_int, c_int, c_p, c_p, c_p, c_p, c_p, c_p, c_p],
     "aw_class_head_bwd": [c_p, c_p, c_p, c_i64, c_int, c_int, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p],
     "aw_embed_fwd": [c_p, c_i64, c_int, c_int, c_p, c_p, c_p, c_p],
+    "aw_embed_ln_fwd": [c_p, c_i64, c_int, c_int, c_p, c_p, c_p, c_p, c_p, c_f, c_p, c_int, c_p, c_p, c_p],
     "aw_embed_bwd": [c_p, c_i64, c_int, c_int, c_p, c_p, c_p],
     "aw_attn_fwd": [c_p, c_i64, c_int, c_int, c_int, c_int, c_p, c_p, c_p],
     "aw_attn_bwd": [c_p, c_p, c_p, c_p, c_i64, c_int, c_int, c_int, c_int, c_p, c_p, c_p],

@@ -98,7 +98,15 @@ def forward(m, ids, generate: bool, training: bool, need_backward: bool, seed: i
     ids = ids.contiguous()
 
     x = e(R, d)
-    K.embed_fwd(ids, m.embedding.latent_embedding.weight, pe[0], x)
+    # the first block's ln_1 runs inside the embedding launch when the vector LayerNorm form applies (d_model
+    # 256..1024): the same arithmetic, without re-reading x
+    ln0 = None
+    if nb and d in (256, 512, 768, 1024):
+        l1 = m.transformer.h[0].ln_1
+        ln0 = (e(R, d, dt=T_), e(R), e(R))
+        K.embed_ln_fwd(ids, m.embedding.latent_embedding.weight, pe[0], x, l1.weight, l1.bias, l1.eps, *ln0)
+    else:
+        K.embed_fwd(ids, m.embedding.latent_embedding.weight, pe[0], x)
     # operand copies of every block's Linear weights and the padded lm head (f32 Linear operands are used as they
     # are): persistent, re-cast only when a weight changed outside the optimizer (arcweld/operands.py)
     ops = operands.get(m, ("decoder", T_), lambda: _operand_jobs(m, T_))
@@ -109,8 +117,11 @@ def forward(m, ids, generate: bool, training: bool, need_backward: bool, seed: i
     for i, blk in enumerate(m.transformer.h):
         at, mlp = blk.attn, blk.mlp
         Wqkv, Wo, Wfc, Wp = wops[i]
-        a, mu1, rs1 = e(R, d, dt=T_), e(R), e(R)
-        K.layernorm_fwd(x, blk.ln_1.weight, blk.ln_1.bias, blk.ln_1.eps, a, mu1, rs1)
+        if i == 0 and ln0 is not None:
+            a, mu1, rs1 = ln0
+        else:
+            a, mu1, rs1 = e(R, d, dt=T_), e(R), e(R)
+            K.layernorm_fwd(x, blk.ln_1.weight, blk.ln_1.bias, blk.ln_1.eps, a, mu1, rs1)
         qkv = e(R, 3 * d, dt=T_)
         K.gemm(a, Wqkv, R, 3 * d, d, bias=at.c_attn.bias, C=qkv)
         y, lse = e(R, d, dt=T_), e(B * nh * T)

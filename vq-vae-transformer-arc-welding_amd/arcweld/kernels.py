@@ -632,6 +632,13 @@ def embed_fwd(ids, wtok, pe, x, stream=None):
     call("aw_embed_fwd", ptr(ids), B, T, wtok.shape[1], ptr(wtok), ptr(pe), ptr(x), stream_ptr(stream))
 
 
+def embed_ln_fwd(ids, wtok, pe, x, w, b, eps, y, mean, rstd, stream=None):
+    """embed_fwd followed by layernorm_fwd(x, ...) in one launch (d_model 256/512/768/1024), bit-identical to the pair."""
+    B, T = ids.shape
+    call("aw_embed_ln_fwd", ptr(ids), B, T, wtok.shape[1], ptr(wtok), ptr(pe), ptr(x), ptr(w), ptr(b), float(eps),
+         ptr(y), dtype_code(y.dtype), ptr(mean), ptr(rstd), stream_ptr(stream))
+
+
 def embed_bwd(ids, dx, dwtok, stream=None):
     B, T = ids.shape
     call("aw_embed_bwd", ptr(ids), B, T, dwtok.shape[1], ptr(dx), ptr(dwtok), stream_ptr(stream))

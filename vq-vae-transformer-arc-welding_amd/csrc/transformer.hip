@@ -300,6 +300,64 @@ __global__ __launch_bounds__(256) void embed_fwd_rows_kernel(const int64_t* __re
   }
 }
 
+// The embedding with the first block's ln_1 fused (D = 256 NV, one wave per row): x = wtok[id] + pe[t] as
+// embed_fwd_rows_kernel, then LayerNorm(x) from the same registers, in ln_fwd_vec_kernel's order of operations
+// (bit-identical to the two launches; the LayerNorm's read of x is saved)
+template <typename T, int NV>
+__global__ __launch_bounds__(256) void embed_ln_fwd_kernel(const int64_t* __restrict__ ids, int64_t R, int Tn, int D,
+                                                           const float* __restrict__ wtok, const float* __restrict__ pe,
+                                                           float* __restrict__ x, const float* __restrict__ w,
+                                                           const float* __restrict__ b, float eps, T* __restrict__ y,
+                                                           float* __restrict__ mean, float* __restrict__ rstd) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  if (r >= R) return;
+  const float* a = wtok + ids[r] * D;
+  const float* p = pe + (r % Tn) * D;
+  float4 v[NV], w4[NV], b4[NV];
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const float4 u = *reinterpret_cast<const float4*>(a + 4 * lane + 256 * j);
+    const float4 q = *reinterpret_cast<const float4*>(p + 4 * lane + 256 * j);
+    v[j] = make_float4(u.x + q.x, u.y + q.y, u.z + q.z, u.w + q.w);
+  }
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    w4[j] = *reinterpret_cast<const float4*>(w + 4 * lane + 256 * j);
+    b4[j] = *reinterpret_cast<const float4*>(b + 4 * lane + 256 * j);
+    *reinterpret_cast<float4*>(x + r * D + 4 * lane + 256 * j) = v[j];
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < NV; ++j) s += (v[j].x + v[j].y) + (v[j].z + v[j].w);
+  const float mu = wave_sum(s) / (float)D;
+  float q = 0.f;
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const float a0 = v[j].x - mu, a1 = v[j].y - mu, a2 = v[j].z - mu, a3 = v[j].w - mu;
+    q += (a0 * a0 + a1 * a1) + (a2 * a2 + a3 * a3);
+  }
+  const float rs = rsqrtf(wave_sum(q) / (float)D + eps);
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const int c = 4 * lane + 256 * j;
+    const float o[4] = {(v[j].x - mu) * rs * w4[j].x + b4[j].x, (v[j].y - mu) * rs * w4[j].y + b4[j].y,
+                        (v[j].z - mu) * rs * w4[j].z + b4[j].z, (v[j].w - mu) * rs * w4[j].w + b4[j].w};
+    if constexpr (sizeof(T) == 2) {
+      bf16 h[4] = {(bf16)o[0], (bf16)o[1], (bf16)o[2], (bf16)o[3]};
+      uint2 u;
+      memcpy(&u, h, 8);
+      *reinterpret_cast<uint2*>(y + r * D + c) = u;
+    } else {
+      *reinterpret_cast<float4*>(y + r * D + c) = make_float4(o[0], o[1], o[2], o[3]);
+    }
+  }
+  if (lane == 0) {
+    mean[r] = mu;
+    rstd[r] = rs;
+  }
+}
+
 __global__ void embed_bwd_kernel(const int64_t* __restrict__ ids, int64_t B, int T, int D, const float* __restrict__ dx,
                                  float* __restrict__ dw) {
   const int64_t n = B * T * D;
@@ -912,6 +970,32 @@ extern "C" int aw_embed_fwd(const int64_t* ids, int64_t B, int T, int D, const f
   hipLaunchKernelGGL(embed_fwd_kernel, dim3(gridcap(B * T * D)), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
                      ids, B, T, D, wtok, pe, x);
   return aw::check_launch("aw_embed_fwd");
+}
+
+extern "C" int aw_embed_ln_fwd(const int64_t* ids, int64_t B, int T, int D, const float* wtok, const float* pe, float* x,
+                               const float* w, const float* b, float eps, void* y, int y_dtype, float* mean,
+                               float* rstd, void* stream) {
+  AW_REQUIRE(ids && wtok && pe && x && w && b && y && mean && rstd && B >= 0 && T > 0 &&
+                 (D == 256 || D == 512 || D == 768 || D == 1024) && (y_dtype == AW_BF16 || y_dtype == AW_F32) &&
+                 (((uintptr_t)wtok | (uintptr_t)pe | (uintptr_t)x | (uintptr_t)w | (uintptr_t)b | (uintptr_t)y) & 15) == 0,
+             "aw_embed_ln_fwd: bad args (D must be 256, 512, 768 or 1024; 16-B aligned tensors)");
+  if (B == 0) return AW_OK;
+  const int64_t R = B * T;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const dim3 grid(aw_cdiv(R, 4));
+#define AW_ELN(NV)                                                                                                   \
+  if (y_dtype == AW_BF16)                                                                                            \
+    hipLaunchKernelGGL((embed_ln_fwd_kernel<bf16, NV>), grid, dim3(256), 0, s, ids, R, T, D, wtok, pe, x, w, b, eps, \
+                       (bf16*)y, mean, rstd);                                                                        \
+  else                                                                                                               \
+    hipLaunchKernelGGL((embed_ln_fwd_kernel<float, NV>), grid, dim3(256), 0, s, ids, R, T, D, wtok, pe, x, w, b, eps,\
+                       (float*)y, mean, rstd);                                                                       \
+  return aw::check_launch("aw_embed_ln_fwd");
+  if (D == 256) { AW_ELN(1) }
+  if (D == 512) { AW_ELN(2) }
+  if (D == 768) { AW_ELN(3) }
+  AW_ELN(4)
+#undef AW_ELN
 }
 
 extern "C" int aw_embed_bwd(const int64_t* ids, int64_t B, int T, int D, const float* dx, float* dwtok, void* stream) {
