@@ -4,6 +4,7 @@ variants live here.  Results of a variant are not the product's (it leaves work 
 usage (CPU side): python tools/probe/lib_variant.py <name>"""
 import glob
 import os
+import re
 import shutil
 import subprocess
 import sys
@@ -23,8 +24,26 @@ VARIANTS = {
 }
 
 
+# a bounds guard: an index compared with a limit (`i0 < 7 * H`, `row < nrows`), up to the clause's end
+GUARD = re.compile(r"\b[A-Za-z_]\w*(?:\[[^\]]*\])?\s*(?:<=|>=|<|>)\s*[\w\s*+\-()]+?(?=\s*(?:;|&&|\|\||\)\s*[{;]|$))")
+
+
+def kept_guards(a, b):
+    """The guards of the product text `a` that its replacement `b` drops (a variant may add conditions to a guard,
+    never remove or rewrite one: round 5's first head_noatom replaced `i < 5 * H` and indexed below its array)."""
+    return [g.strip() for g in GUARD.findall(a) if g.strip() not in b]
+
+
+def check(name):
+    for fn, a, b in VARIANTS[name]:
+        lost = kept_guards(a, b)
+        if lost:
+            sys.exit(f"{name}: the replacement in {fn} drops bounds guard(s) {lost}")
+
+
 def main():
     name = sys.argv[1]
+    check(name)
     work = os.path.join(HERE, "build", "src_" + name)
     shutil.rmtree(work, ignore_errors=True)
     os.makedirs(work)
