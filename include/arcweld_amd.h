@@ -471,6 +471,15 @@ int aw_embed_ln_fwd(const int64_t* ids, int64_t B, int T, int D, const float* wt
                     const float* w, const float* b, float eps, void* y, int y_dtype, float* mean, float* rstd,
                     void* stream);
 int aw_embed_bwd(const int64_t* ids, int64_t B, int T, int D, const float* dx, float* dwtok, void* stream);
+/* aw_embed_bwd for a table of V rows without global atomics: a counting sort of the rows by id, then one owner per
+   table element (ids outside [0, V) are skipped).  work: V + 1 + B*T ints of device scratch.  Falls back to
+   aw_embed_bwd when V > 15360, D is not 256 / 512 / 768 / 1024 or dx / dwtok are not 16-B aligned. */
+int aw_embed_bwd_sorted(const int64_t* ids, int64_t B, int T, int D, int V, const float* dx, float* dwtok, int* work,
+                        void* stream);
+/* Its two halves, for a caller that sorts early (the ids are known at the forward): aw_embed_sort fills work (V + 1 + R ints; V <= 15360) from the R ids,
+   aw_embed_bwd_segsum adds the rows of dx (R x D, D = 256/512/768/1024, 16-B aligned) into dwtok from it. */
+int aw_embed_sort(const int64_t* ids, int64_t R, int V, int* work, void* stream);
+int aw_embed_bwd_segsum(const int* work, int V, int D, const float* dx, float* dwtok, void* stream);
 /* Causal self-attention core (model/transformer_block.py:44-60) on the packed qkv projection
  * (B*T, 3*d, dtype), heads of hs = d/n_head: y (B*T, d, dtype) = softmax(q k^T / sqrt(hs), causal) v;
  * lse (B*n_head*T f32) saved for the backward (flash-style, T x T never materialised). */

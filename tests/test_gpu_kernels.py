@@ -664,14 +664,16 @@ def test_unpatch_head_bf16_y_equals_f32_y(training):
     torch.testing.assert_close(outs[1][7], outs[0][7], rtol=1e-4, atol=1e-5 * float(outs[0][7].abs().max()))
 
 
+@pytest.mark.parametrize("sort", [True, False])
 @pytest.mark.parametrize("B,T,V,D", [(51, 321, 514, 512), (2, 7, 9, 64), (3, 40, 8194, 512), (4, 33, 30, 36),
-                                     (2, 5, 7, 6)])
-def test_embedding_forward_backward_vs_torch(B, T, V, D):
+                                     (2, 5, 7, 6), (2, 9, 40000, 64), (5, 50, 3, 256), (2, 70, 5, 1024)])
+def test_embedding_forward_backward_vs_torch(B, T, V, D, sort):
     """aw_embed_fwd / aw_embed_bwd (model/embedding.py:57-59) against torch: the forward bit-exact (one f32 add per
     element; the row-vectorised kernel at D % 4 == 0, the element-wise one at D = 6), the table gradient as
     index_add_ of the row gradients.  Cases: the decoder's 51 x 321 rows into 514 table rows (~32 rows per table
-    row), a tiny table with many repeats, the stress table of 8194 rows, D = 36 and D = 6.  Ids leave one table row
-    unused, which must stay unchanged."""
+    row), a tiny table with many repeats, the stress table of 8194 rows, D = 36 and D = 6, a 40000-row table (past the
+    sorted form's LDS bins: its atomic fallback).  Both table-gradient forms: the counting sort (aw_embed_bwd_sorted;
+    D = 6 / 36 / 64 take its fallback) and the atomic one.  Ids leave one table row unused, which must stay unchanged."""
     from arcweld import kernels as K
     g = torch.Generator(device="cuda").manual_seed(V + D)
     ids = torch.randint(0, V - 1, (B, T), device="cuda", generator=g)       # row V-1 is never used
@@ -684,7 +686,7 @@ def test_embedding_forward_backward_vs_torch(B, T, V, D):
     dx = torch.randn(B * T, D, device="cuda", generator=g)
     prior = torch.randn(V, D, device="cuda", generator=g)
     dw = prior.clone()
-    K.embed_bwd(ids, dx, dw)
+    K.embed_bwd(ids, dx, dw, sort=sort)
     want = prior.clone().index_add_(0, ids.reshape(-1), dx)
     torch.testing.assert_close(dw, want, rtol=1e-5, atol=1e-4)
     assert torch.equal(dw[V - 1], prior[V - 1])
@@ -712,3 +714,29 @@ def test_embed_ln_fused_matches_the_two_launches(B, T, V, D, dt):
     K.embed_ln_fwd(ids, W, pe, x1, w, b, 1e-5, y1, m1, r1)
     for got, want in ((x1, x0), (y1, y0), (m1, m0), (r1, r0)):
         assert torch.equal(got, want)
+
+
+@pytest.mark.parametrize("R,V,D", [(16371, 514, 512), (300, 3, 256), (4000, 8194, 1024), (7, 15360, 768)])
+def test_embed_sort_segsum_halves(R, V, D):
+    """aw_embed_sort + aw_embed_bwd_segsum (the two halves of aw_embed_bwd_sorted, callable apart) against index_add_: the offsets are the exclusive prefix sums of the id counts, every row index
+    lands in its id's segment exactly once, and the table gradient matches; cases: the decoder's 16371 x 514, a
+    3-row table with ~100-row segments (several 64-entry batches per segment), the 8194-row stress table at D 1024,
+    the largest table the LDS bins take."""
+    from arcweld import kernels as K
+    g = torch.Generator(device="cuda").manual_seed(R + V)
+    ids = torch.randint(0, V, (R,), device="cuda", generator=g)
+    work = torch.full((V + 1 + R,), -7, device="cuda", dtype=torch.int32)
+    K.embed_sort(ids, V, work)
+    cnt = torch.bincount(ids, minlength=V)
+    off = torch.zeros(V + 1, dtype=torch.int64, device="cuda")
+    off[1:] = torch.cumsum(cnt, 0)
+    assert torch.equal(work[:V + 1].long(), off)
+    ord_ = work[V + 1:].long()
+    assert torch.equal(torch.sort(ord_).values, torch.arange(R, device="cuda"))
+    seg = torch.repeat_interleave(torch.arange(V, device="cuda"), cnt)
+    assert torch.equal(ids[ord_], seg)
+    dx = torch.randn(R, D, device="cuda", generator=g)
+    prior = torch.randn(V, D, device="cuda", generator=g)
+    dw = prior.clone()
+    K.embed_bwd_segsum(work, dx, dw)
+    torch.testing.assert_close(dw, prior.clone().index_add_(0, ids, dx), rtol=1e-5, atol=1e-4)

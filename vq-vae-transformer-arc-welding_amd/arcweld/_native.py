@@ -156,6 +156,9 @@ SIGNATURES = {
     "aw_embed_fwd": [c_p, c_i64, c_int, c_int, c_p, c_p, c_p, c_p],
     "aw_embed_ln_fwd": [c_p, c_i64, c_int, c_int, c_p, c_p, c_p, c_p, c_p, c_f, c_p, c_int, c_p, c_p, c_p],
     "aw_embed_bwd": [c_p, c_i64, c_int, c_int, c_p, c_p, c_p],
+    "aw_embed_bwd_sorted": [c_p, c_i64, c_int, c_int, c_int, c_p, c_p, c_p, c_p],
+    "aw_embed_sort": [c_p, c_i64, c_int, c_p, c_p],
+    "aw_embed_bwd_segsum": [c_p, c_int, c_int, c_p, c_p, c_p],
     "aw_attn_fwd": [c_p, c_i64, c_int, c_int, c_int, c_int, c_p, c_p, c_p],
     "aw_attn_bwd": [c_p, c_p, c_p, c_p, c_i64, c_int, c_int, c_int, c_int, c_p, c_p, c_p],
     "aw_attn_fwd_dropout": [c_p, c_i64, c_int, c_int, c_int, c_int, c_p, c_p, c_f, ctypes.c_uint64, c_p, c_p],

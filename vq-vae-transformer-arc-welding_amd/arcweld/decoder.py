@@ -264,6 +264,8 @@ def backward(m, sv, g_out, slot, mid_hook=None):
     K.wgrad_issue([pb for kind in wg for pb in wg[kind]])
     if nb == 0 and mid_hook is not None:
         mid_hook()
+    # the table gradient by counting sort + one owner per element (aw_embed_bwd_sorted: 18 + 25 us against 48 us of
+    # contended atomics at 16371 rows into 514; a side-stream sort at the forward measured slower, step +0.4 %)
     K.embed_bwd(sv_ids(sv), gx, slot(m.embedding.latent_embedding.weight))
 
 

@@ -639,9 +639,30 @@ def embed_ln_fwd(ids, wtok, pe, x, w, b, eps, y, mean, rstd, stream=None):
          ptr(y), dtype_code(y.dtype), ptr(mean), ptr(rstd), stream_ptr(stream))
 
 
-def embed_bwd(ids, dx, dwtok, stream=None):
+def embed_bwd(ids, dx, dwtok, stream=None, sort=True):
+    """dwtok[ids[r]] += dx[r].  sort: the counting-sort form (aw_embed_bwd_sorted; scratch allocated here), else the
+    atomic form."""
     B, T = ids.shape
-    call("aw_embed_bwd", ptr(ids), B, T, dwtok.shape[1], ptr(dx), ptr(dwtok), stream_ptr(stream))
+    if not sort:
+        call("aw_embed_bwd", ptr(ids), B, T, dwtok.shape[1], ptr(dx), ptr(dwtok), stream_ptr(stream))
+        return
+    V = dwtok.shape[0]
+    work = torch.empty(V + 1 + B * T, device=dx.device, dtype=torch.int32)
+    call("aw_embed_bwd_sorted", ptr(ids), B, T, dwtok.shape[1], V, ptr(dx), ptr(dwtok), ptr(work),
+         stream_ptr(stream))
+
+
+EMBED_SORT_MAX_V = 15360
+
+
+def embed_sort(ids, V, work, stream=None):
+    """The counting sort half of embed_bwd (work: V + 1 + ids.numel() int32)."""
+    call("aw_embed_sort", ptr(ids), ids.numel(), V, ptr(work), stream_ptr(stream))
+
+
+def embed_bwd_segsum(work, dx, dwtok, stream=None):
+    """The table-row sums half of embed_bwd, from embed_sort's work."""
+    call("aw_embed_bwd_segsum", ptr(work), dwtok.shape[0], dwtok.shape[1], ptr(dx), ptr(dwtok), stream_ptr(stream))
 
 
 def attn_flops(B, T, n_head, d):

@@ -378,6 +378,129 @@ __global__ __launch_bounds__(256) void embed_bwd_rows_kernel(const int64_t* __re
   }
 }
 
+// The table gradient without global atomics (the decoder's ~32 rows per table row made the atomic form contend on the
+// same addresses: 46.7 us per decoder step for 16371 x 512).  (1) One workgroup counting-sorts the row indices by
+// id in LDS: off[v] .. off[v + 1] - 1 are the slots of ord holding the rows of table row v (ids outside [0, V) are
+// dropped).  (2) One workgroup per table row sums its rows' gradients in registers and adds the sum to the table row with
+// one plain read-modify-write (each element has one owner).  The order of a row's terms follows the
+// sort's LDS atomics, so -- as with the atomic form -- the f32 summation order is not fixed from run to run.
+constexpr int ESORT_THREADS = 1024;
+constexpr int ESORT_MAX_V = 15360;   // LDS: (V + 1024) ints, within 64 KB of dynamic LDS
+constexpr int ESORT_U = 8;           // ids in flight per thread (the loads go out before the LDS atomics)
+
+__global__ __launch_bounds__(ESORT_THREADS) void embed_sort_kernel(const int64_t* __restrict__ ids, int R, int V,
+                                                                   int* __restrict__ off, int* __restrict__ ord) {
+  extern __shared__ int esh[];
+  int* cnt = esh;
+  int* part = esh + V;
+  const int tid = threadIdx.x;
+  for (int i = tid; i < V; i += ESORT_THREADS) cnt[i] = 0;
+  __syncthreads();
+  for (int r0 = tid; r0 < R; r0 += ESORT_U * ESORT_THREADS) {
+    int64_t v[ESORT_U];
+#pragma unroll
+    for (int u = 0; u < ESORT_U; ++u) {   // clamped address, then a select: no branch (and wait) per load
+      const int r = r0 + u * ESORT_THREADS;
+      const int64_t x = ids[min(r, R - 1)];
+      v[u] = r < R ? x : -1;
+    }
+#pragma unroll
+    for (int u = 0; u < ESORT_U; ++u)
+      if ((uint64_t)v[u] < (uint64_t)V) atomicAdd(&cnt[v[u]], 1);
+  }
+  __syncthreads();
+  // exclusive scan of the counts: a serial chunk per thread, then the 1024 chunk sums
+  const int per = (V + ESORT_THREADS - 1) / ESORT_THREADS, b0 = min(V, tid * per), b1 = min(V, b0 + per);
+  int s = 0;
+  for (int i = b0; i < b1; ++i) s += cnt[i];
+  part[tid] = s;
+  __syncthreads();
+  for (int o = 1; o < ESORT_THREADS; o <<= 1) {
+    const int add = tid >= o ? part[tid - o] : 0;
+    __syncthreads();
+    part[tid] += add;
+    __syncthreads();
+  }
+  int run = part[tid] - s;
+  for (int i = b0; i < b1; ++i) {
+    const int c = cnt[i];
+    off[i] = run;
+    cnt[i] = run;   // becomes the row's fill cursor
+    run += c;
+  }
+  if (tid == ESORT_THREADS - 1) off[V] = part[ESORT_THREADS - 1];
+  __syncthreads();
+  for (int r0 = tid; r0 < R; r0 += ESORT_U * ESORT_THREADS) {
+    int64_t v[ESORT_U];
+#pragma unroll
+    for (int u = 0; u < ESORT_U; ++u) {   // clamped address, then a select: no branch (and wait) per load
+      const int r = r0 + u * ESORT_THREADS;
+      const int64_t x = ids[min(r, R - 1)];
+      v[u] = r < R ? x : -1;
+    }
+#pragma unroll
+    for (int u = 0; u < ESORT_U; ++u)
+      if ((uint64_t)v[u] < (uint64_t)V) ord[atomicAdd(&cnt[v[u]], 1)] = r0 + u * ESORT_THREADS;
+  }
+}
+
+// One workgroup (4 waves) per table row v, D = 256 NV: wave w sums the row's entries w, w + 4, ... (8 at a time; lane: float4
+// columns 4 lane + 256 j); the segment's row indices come 64 at a time in one load and are read per entry from a
+// lane (no dependent index load per entry); the 4 partial sums meet in LDS and one read-modify-write adds them.
+constexpr int ESEG_U = 8;   // entries in flight per wave (the decoder's ~32 rows per table row: one round per wave)
+template <int NV>
+__global__ __launch_bounds__(256) void embed_segsum_kernel(const int* __restrict__ off, const int* __restrict__ ord,
+                                                           int D, const float* __restrict__ dx,
+                                                           float* __restrict__ dw) {
+  __shared__ float4 red[3][64 * NV];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int v = blockIdx.x;
+  const int i0 = off[v], i1 = off[v + 1];
+  if (i0 == i1) return;   // workgroup-uniform
+  float4 a[NV];
+#pragma unroll
+  for (int j = 0; j < NV; ++j) a[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int b0 = i0; b0 < i1; b0 += 64) {
+    const int n = min(64, i1 - b0);
+    const int myr = lane < n ? ord[b0 + lane] : 0;
+    for (int e = w; e < n; e += 4 * ESEG_U) {
+      float4 u[ESEG_U][NV];
+#pragma unroll
+      for (int k = 0; k < ESEG_U; ++k) {
+        const int ek = e + 4 * k;
+        // past the segment: the entry's own row again, its value dropped by a select (a branch around each load
+        // made every load wait for the one before)
+        const int r = __shfl(myr, ek < n ? ek : e, 64);
+        const float m = ek < n ? 1.f : 0.f;
+#pragma unroll
+        for (int j = 0; j < NV; ++j) {
+          const float4 x = *reinterpret_cast<const float4*>(dx + (int64_t)r * D + 4 * lane + 256 * j);
+          u[k][j] = make_float4(x.x * m, x.y * m, x.z * m, x.w * m);
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < ESEG_U; ++k)
+#pragma unroll
+        for (int j = 0; j < NV; ++j)
+          a[j] = make_float4(a[j].x + u[k][j].x, a[j].y + u[k][j].y, a[j].z + u[k][j].z, a[j].w + u[k][j].w);
+    }
+  }
+  if (w > 0)
+#pragma unroll
+    for (int j = 0; j < NV; ++j) red[w - 1][64 * j + lane] = a[j];
+  __syncthreads();
+  if (w == 0) {
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      const float4 p1 = red[0][64 * j + lane], p2 = red[1][64 * j + lane], p3 = red[2][64 * j + lane];
+      float4* o = reinterpret_cast<float4*>(dw + (int64_t)v * D + 4 * lane + 256 * j);
+      const float4 p = *o;
+      *o = make_float4(p.x + ((a[j].x + p1.x) + (p2.x + p3.x)), p.y + ((a[j].y + p1.y) + (p2.y + p3.y)),
+                       p.z + ((a[j].z + p1.z) + (p2.z + p3.z)), p.w + ((a[j].w + p1.w) + (p2.w + p3.w)));
+    }
+  }
+}
+
 // ---------------------------------------------------------------- causal attention
 // Two lanes per query (or key) row, each holding half of the head dimension; partial dot products are combined
 // with one xor-1 shuffle.  Key/value (resp. query) tiles of 32 rows are staged in LDS and read as broadcasts.
@@ -996,6 +1119,38 @@ extern "C" int aw_embed_ln_fwd(const int64_t* ids, int64_t B, int T, int D, cons
   if (D == 768) { AW_ELN(3) }
   AW_ELN(4)
 #undef AW_ELN
+}
+
+extern "C" int aw_embed_sort(const int64_t* ids, int64_t R, int V, int* work, void* stream) {
+  AW_REQUIRE(ids && work && R >= 0 && R < (int64_t)1 << 31 && V > 0 && V <= ESORT_MAX_V,
+             "aw_embed_sort: bad args (V must be 1..15360)");
+  hipLaunchKernelGGL(embed_sort_kernel, dim3(1), dim3(ESORT_THREADS), (V + ESORT_THREADS) * sizeof(int),
+                     reinterpret_cast<hipStream_t>(stream), ids, (int)R, V, work, work + V + 1);
+  return aw::check_launch("aw_embed_sort");
+}
+
+extern "C" int aw_embed_bwd_segsum(const int* work, int V, int D, const float* dx, float* dwtok, void* stream) {
+  AW_REQUIRE(work && dx && dwtok && V > 0 && V <= ESORT_MAX_V && (D == 256 || D == 512 || D == 768 || D == 1024) &&
+                 (((uintptr_t)dx | (uintptr_t)dwtok) & 15) == 0,
+             "aw_embed_bwd_segsum: bad args (D must be 256, 512, 768 or 1024; 16-B aligned dx / dwtok)");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const int* off = work;
+  const int* ord = work + V + 1;
+#define AW_SEG(NV) hipLaunchKernelGGL(embed_segsum_kernel<NV>, dim3(V), dim3(256), 0, s, off, ord, D, dx, dwtok);
+  if (D == 256) AW_SEG(1) else if (D == 512) AW_SEG(2) else if (D == 768) AW_SEG(3) else AW_SEG(4)
+#undef AW_SEG
+  return aw::check_launch("aw_embed_bwd_segsum");
+}
+
+extern "C" int aw_embed_bwd_sorted(const int64_t* ids, int64_t B, int T, int D, int V, const float* dx, float* dwtok,
+                                   int* work, void* stream) {
+  AW_REQUIRE(ids && dx && dwtok && work && B >= 0 && T > 0 && D > 0 && V > 0 && B * T < (int64_t)1 << 31,
+             "aw_embed_bwd_sorted: bad args");
+  if (B == 0) return AW_OK;
+  if (V > ESORT_MAX_V || (D != 256 && D != 512 && D != 768 && D != 1024) || (((uintptr_t)dx | (uintptr_t)dwtok) & 15))
+    return aw_embed_bwd(ids, B, T, D, dx, dwtok, stream);
+  const int rc = aw_embed_sort(ids, B * T, V, work, stream);
+  return rc != AW_OK ? rc : aw_embed_bwd_segsum(work, V, D, dx, dwtok, stream);
 }
 
 extern "C" int aw_embed_bwd(const int64_t* ids, int64_t B, int T, int D, const float* dx, float* dwtok, void* stream) {
